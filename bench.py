@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident WebSocket receive (header parse + unmask) on MI355X.
+
+One step = one pass of the hot path over one synthetic batch already resident
+in HBM: k_scan (frame discovery + FIN/opcode/mask/length parse) + k_unmask
+(in-place rotating-key XOR), through the C ABI of libhv_amd/libhvws.so.
+Default workload: BASELINE.json configs[2] (1M x 64 KiB masked binary frames,
+68.7 GB on one GPU), delivered as --segments connections in one contiguous
+rx buffer.  N GPUs: one process per GPU, disjoint batches (distinct seeds),
+no collectives on the data path (weak scaling); gloo carries only the
+barrier and the max-over-ranks time.
+
+Also reported (not `value`): a STREAM-style in-place ceiling on the same
+buffer, the host-memory-inclusive rate (pinned H2D -> scan -> unmask -> D2H,
+hvws_pipeline), and the reference CPU path (oracle/_ref: libhv's own
+websocket_parser.c driven through a restatement of WebSocketParser.cpp,
+8 KiB chunks) timed on this host on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+CONFIGS = {
+    "c2": ("1M x 1 KiB masked binary frames (BASELINE configs[1])", "c2"),
+    "c3": ("1M x 64 KiB masked binary frames (BASELINE configs[2])", "c3"),
+    "c4": ("mixed 128 B-1 MiB masked frames incl. FIN=0 fragments, ~4 GiB (BASELINE configs[3])", "c4"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--segments", type=int, default=4096,
+                    help="connections the batch is cut into (1 = one stream)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget for the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-sample-mib", type=int, default=256)
+    ap.add_argument("--host-gib", type=float, default=4.0, help="host-inclusive sample size (0: skip)")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sample: np.ndarray, seconds: float, threads: int):
+    """Reference CPU path on `sample` (whole frames): WebSocketParser semantics
+    fed in 8 KiB chunks (event/hevent.h:16).  Each pass re-XORs the payload,
+    which is the same work.  Returns (GiB/s of payload, kind, passes)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wsharness as H
+
+    if H.have_ref():
+        L, kind = H.ref(), "reference"
+    else:
+        L, kind = H.oracle(), "port"
+    out = (ctypes.c_uint64 * 4)()
+    bufs = [sample.copy() for _ in range(threads)]
+    # one pass to learn the payload bytes per pass
+    rc = L.msgp_bench_feed(bufs[0].ctypes.data, bufs[0].nbytes, 8192, out)
+    assert rc == 0
+    payload = int(out[1])
+    t0 = time.perf_counter()
+    L.msgp_bench_feed(bufs[0].ctypes.data, bufs[0].nbytes, 8192, out)
+    one = max(time.perf_counter() - t0, 1e-6)
+    passes = max(1, int(seconds / one))
+    counts = [0] * threads
+
+    def work(i):
+        o = (ctypes.c_uint64 * 4)()
+        for _ in range(passes):
+            L.msgp_bench_feed(bufs[i].ctypes.data, bufs[i].nbytes, 8192, o)
+            counts[i] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    return payload * sum(counts) / dt / 2**30, kind, passes, payload * sum(counts)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+
+    import libhv_amd
+    from libhv_amd import synth
+
+    def barrier():
+        eng.sync()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local)
+        if dist is not None:
+            dist.barrier()
+
+    desc, cfg = CONFIGS[args.config]
+    eng = libhv_amd.Engine(local)
+    t = time.perf_counter()
+    plan = synth.config_plan(cfg, seed=1000 + rank).split(args.segments)
+    dp = libhv_amd.DevicePlan(eng, plan)
+    rx = eng.alloc(plan.total + 64)
+    eng.synth(rx, plan.total, plan.seed, dp, 0)
+    eng.sync()
+    log(rank, f"[bench] {plan.n} frames, {plan.total / 1e9:.2f} GB rx, {len(plan.segments)} segments, "
+              f"built in {time.perf_counter() - t:.2f}s")
+    P = plan.masked_payload_bytes()
+    HB = plan.header_bytes
+    segs = plan.segments
+
+    for _ in range(args.warmup):
+        eng.step(rx, plan.total, segs)
+    barrier()
+    scan_ms, unmask_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step(rx, plan.total, segs)
+        s_ms, u_ms = eng.last_times()
+        scan_ms.append(s_ms)
+        unmask_ms.append(u_ms)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # Correctness after the timed region: an odd number of passes leaves the
+    # payload unmasked, an even number masked again (XOR is an involution).
+    passes = args.warmup + args.steps
+    bad = eng.synth(rx, plan.total, plan.seed, dp, 2 if passes % 2 else 1)
+    if bad:
+        raise SystemExit(f"rank {rank}: {bad} bytes differ from the expected batch after {passes} passes")
+
+    value = world * plan.payload_bytes * args.steps / elapsed / 2**30
+    mean_unmask = float(np.mean(unmask_ms))
+    alg_bytes = 2 * P + HB
+    achieved = alg_bytes / (mean_unmask * 1e-3) / 1e9
+
+    extra = {}
+    sample = None
+    if rank == 0:
+        # STREAM-style in-place ceiling (read+write every byte) on the same buffer
+        eng.sync()
+        t = time.perf_counter()
+        reps = 4
+        for _ in range(reps):
+            eng.stream_xor(rx, plan.total & ~15, 0x5A5A5A5A)
+        eng.sync()
+        ceiling = 2 * (plan.total & ~15) * reps / (time.perf_counter() - t) / 1e9
+        extra["stream_ceiling_GBps"] = round(ceiling, 1)
+        extra["scan_ms_mean"] = round(float(np.mean(scan_ms)), 3)
+        extra["unmask_ms_mean"] = round(mean_unmask, 3)
+
+        # host-inclusive: pinned host rx -> device -> scan+unmask -> host
+        if args.host_gib > 0:
+            sizes = synth.frame_size(plan.flags, plan.length)
+            ends = np.cumsum(sizes)
+            m = int(np.searchsorted(ends, int(args.host_gib * 2**30), side="right"))
+            m = max(1, min(m, plan.n))
+            hbytes = int(ends[m - 1])
+            eng.synth(rx, plan.total, plan.seed, dp, 0)
+            L = libhv_amd.lib()
+            pinned = L.hvws_host_alloc(eng.ctx, hbytes)
+            host = np.ctypeslib.as_array((ctypes.c_uint8 * hbytes).from_address(pinned))
+            libhv_amd._check(L.hvws_d2h(eng.ctx, pinned, rx.ptr, hbytes), "d2h")
+            eng.sync()
+            # CPU baseline sample = the first whole frames of the same (masked) batch
+            sample = None
+            if args.cpu_seconds > 0:
+                ms = max(1, int(np.searchsorted(ends, args.cpu_sample_mib << 20, side="right")))
+                sample = np.array(host[: int(ends[ms - 1])], copy=True)
+            carry = libhv_amd.WsParser()
+            L.websocket_parser_init(ctypes.byref(carry))
+            t = time.perf_counter()
+            libhv_amd._check(L.hvws_pipeline(eng.ctx, pinned, hbytes, 64 << 20, ctypes.byref(carry)), "pipeline")
+            dt = time.perf_counter() - t
+            extra["host_inclusive"] = {
+                "GiBps_payload": round(float(plan.length[:m].sum()) / dt / 2**30, 2),
+                "GBps_wire": round(hbytes / dt / 1e9, 2),
+                "bytes": hbytes, "chunk": 64 << 20,
+                "note": "pinned H2D + scan + unmask + D2H, 3-slot ring, PCIe-bound",
+            }
+            L.hvws_host_free(eng.ctx, pinned)
+
+    dp.free()
+    rx.free()
+
+    if rank == 0:
+        cpu = None
+        if sample is not None:
+            v1, kind, passes1, _ = cpu_baseline(sample, args.cpu_seconds, 1)
+            nthr = min(16, os.cpu_count() or 1)
+            vn, _, _, _ = cpu_baseline(sample, args.cpu_seconds / 2, nthr)
+            cpu = {
+                "value": round(v1, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+                "sample": f"{sample.nbytes} B of the same batch ({args.config} frames) x {passes1} passes, "
+                          "WebSocketParser semantics (header parse + in-place unmask + message append), 8 KiB chunks",
+                "multi_thread": {"value": round(vn, 3), "threads": nthr},
+            }
+        out = {
+            "metric": "device-resident WS unmask GiB/s, 64 KiB masked frames, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (websocket_build_frame layout, splitmix64 payloads/keys, distinct seed per rank)",
+            "config": {
+                "workload": desc,
+                "frames_per_gpu": plan.n,
+                "rx_bytes_per_gpu": plan.total,
+                "payload_bytes_per_gpu": plan.payload_bytes,
+                "segments_per_gpu": len(segs),
+                "parallelism": f"replicas{world} (disjoint batches, no collectives)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_unmask",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        out.update(extra)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,53 @@
+/*
+ * WebSocketParser.h -- drop-in for libhv's WebSocket message reassembler
+ * (reference: http/WebSocketParser.h:10-33, http/WebSocketParser.cpp:8-75).
+ *
+ * Same public members, constructor/destructor and FeedRecvData signature, so
+ * http/server/HttpHandler.cpp:168-217,757-763 and
+ * http/client/WebSocketClient.cpp:187-193 compile and link unchanged.
+ * FeedRecvData runs frame discovery/header parse and the XOR unmask as HIP
+ * kernels on MI355X, rewrites the caller's buffer in place exactly as the
+ * reference does (payload unmasked, header bytes untouched), and fires
+ * onMessage(opcode, message) for every FIN frame in order.
+ */
+#ifndef HVWS_WEBSOCKET_PARSER_HPP
+#define HVWS_WEBSOCKET_PARSER_HPP
+
+#include <stddef.h>
+
+#include <functional>
+#include <memory>
+#include <string>
+
+#ifndef HV_EXPORT
+#define HV_EXPORT __attribute__((visibility("default")))
+#endif
+
+enum websocket_parser_state {
+    WS_FRAME_BEGIN,
+    WS_FRAME_HEADER,
+    WS_FRAME_BODY,
+    WS_FRAME_END,
+    WS_FRAME_FIN,
+};
+
+struct websocket_parser;
+
+class HV_EXPORT WebSocketParser {
+public:
+    websocket_parser*                                       parser;
+    websocket_parser_state                                  state;
+    int                                                     opcode;
+    std::string                                             message;
+    std::function<void(int opcode, const std::string& msg)> onMessage;
+
+    WebSocketParser();
+    ~WebSocketParser();
+
+    /* Returns len (as int, like the reference) once every byte is consumed. */
+    int FeedRecvData(const char* data, size_t len);
+};
+
+typedef std::shared_ptr<WebSocketParser> WebSocketParserPtr;
+
+#endif

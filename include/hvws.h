@@ -1,0 +1,146 @@
+/*
+ * hvws.h -- batch / device-resident C ABI of the MI355X WebSocket receive
+ * engine (libhv_amd/libhvws.so).  New entry points; the reference has no
+ * batch API.  What each one stands in for:
+ *
+ *   hvws_scan    websocket_parser_execute's header state machine
+ *                (reference http/websocket_parser.c:53-171) run over many
+ *                segments (= connections' rx bytes) at once: frame
+ *                discovery + FIN/opcode/mask/length extraction on the GPU.
+ *   hvws_unmask  the per-byte XOR of websocket_parser_decode
+ *                (http/websocket_parser.c:173-180) as called in place by
+ *                WebSocketParser's on_frame_body (http/WebSocketParser.cpp:32-34),
+ *                applied to every masked payload span the last scan found.
+ *   hvws_step    scan + unmask: one pass of the hot path over a batch.
+ *   hvws_rx_batch  the same from/to host memory (H2D, step, D2H).
+ *   hvws_wsp_*   C handle over the WebSocketParser class
+ *                (http/WebSocketParser.h:19-31) for FFI callers.
+ *
+ * A batch is a buffer holding `nseg` segments; segment s is the byte range
+ * [segs[s].off, segs[s].off + segs[s].len) and continues the stream whose
+ * parser state is carry[s] (a `struct websocket_parser`).  Segments must be
+ * sorted by offset and must not overlap.  Contexts are per (thread, device):
+ * several event-loop threads may each own one; there is no global lock.
+ * Device buffers passed in must be 16-byte aligned.
+ */
+#ifndef HVWS_H
+#define HVWS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "websocket_parser.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    HVWS_OK = 0,
+    HVWS_ENODEV = -1,   /* no HIP device / runtime */
+    HVWS_EINVAL = -2,
+    HVWS_ENOMEM = -3,
+    HVWS_EHIP = -4      /* a HIP call failed; see hvws_last_error() */
+};
+
+/* hvws_frame.info bits */
+#define HVWS_I_FLAGS       0xFFu      /* websocket_flags of the frame          */
+#define HVWS_I_PHASE_SHIFT 8          /* 2-bit mask phase at pay_off           */
+#define HVWS_I_HDR         (1u << 10) /* header completed here (on_frame_header fires) */
+#define HVWS_I_BODY        (1u << 11) /* >= 1 payload byte here (on_frame_body fires)   */
+#define HVWS_I_END         (1u << 12) /* frame completed here (on_frame_end fires)      */
+#define HVWS_I_START       (1u << 13) /* first header byte is inside this segment       */
+
+typedef struct hvws_ctx hvws_ctx;
+
+typedef struct hvws_segment {
+    uint64_t off;
+    uint64_t len;
+} hvws_segment;
+
+/* One frame as seen by one batch (40 bytes). Offsets are absolute in the
+ * batch buffer. */
+typedef struct hvws_frame {
+    int64_t  hdr_off;   /* first header byte, -1 if it was in an earlier batch */
+    uint64_t pay_off;   /* first payload byte of this frame in the batch       */
+    uint64_t pay_len;   /* payload bytes of this frame inside the batch        */
+    uint64_t length;    /* full payload length (parser->length)                */
+    uint32_t key;       /* masking key, mask[0] in bits 0-7 (0 if unmasked)    */
+    uint32_t info;      /* HVWS_I_* */
+} hvws_frame;
+
+/* ---- context / memory ---------------------------------------------- */
+int         hvws_device_count(void);
+hvws_ctx*   hvws_ctx_create(int device);          /* NULL on failure */
+void        hvws_ctx_destroy(hvws_ctx* ctx);
+const char* hvws_last_error(void);                /* thread-local */
+void*       hvws_ctx_stream(hvws_ctx* ctx);       /* hipStream_t */
+int         hvws_ctx_device(hvws_ctx* ctx);
+
+void* hvws_dev_alloc(hvws_ctx* ctx, uint64_t bytes);
+void  hvws_dev_free(hvws_ctx* ctx, void* p);
+void* hvws_host_alloc(hvws_ctx* ctx, uint64_t bytes); /* pinned */
+void  hvws_host_free(hvws_ctx* ctx, void* p);
+int   hvws_h2d(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async, ctx stream */
+int   hvws_d2h(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async, ctx stream */
+int   hvws_memset(hvws_ctx* ctx, void* dst, int v, uint64_t n);
+int   hvws_sync(hvws_ctx* ctx);
+
+/* ---- the hot path, device resident ---------------------------------- */
+/* Frame discovery + header parse for every segment.  Synchronises once (to
+ * size the frame table).  Results stay on the device in `ctx`. */
+int hvws_scan(hvws_ctx* ctx, const uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+              const websocket_parser* carry_in, uint32_t nseg);
+/* Unmask, in place, every masked payload span found by the last scan.
+ * Asynchronous on the ctx stream. */
+int hvws_unmask(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len);
+/* scan + unmask */
+int hvws_step(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+              const websocket_parser* carry_in, uint32_t nseg);
+
+int64_t hvws_frame_count(hvws_ctx* ctx);
+int     hvws_get_frames(hvws_ctx* ctx, hvws_frame* out, uint64_t first, uint64_t n);
+/* first frame index and frame count of every segment of the last scan */
+int     hvws_get_segment_frames(hvws_ctx* ctx, uint64_t* first, uint64_t* count);
+/* parser state after each segment (WebSocketParser semantics: mask_offset
+ * advanced over unmasked bytes).  started[s] = 1 when the pending frame's
+ * first header byte lay inside segment s. */
+int     hvws_get_carry(hvws_ctx* ctx, websocket_parser* out, int* started);
+
+/* Device time (ms, HIP events on the ctx stream) of the last scan and
+ * unmask: out[0] = scan kernels (count + offsets + emit + tile index),
+ * out[1] = unmask kernel. */
+int hvws_last_times(hvws_ctx* ctx, float out[2]);
+
+/* STREAM-style in-place ceiling: d[i] ^= pattern over n bytes (16-B aligned). */
+int hvws_stream_xor(hvws_ctx* ctx, uint8_t* d, uint64_t n, uint32_t pattern);
+
+/* ---- host memory in, host memory out -------------------------------- */
+/* Copies h_rx to the device, runs scan (+ unmask if `unmask`), copies the
+ * bytes back in place and updates carry[].  Frames of the batch are then
+ * available through hvws_get_frames(). */
+int hvws_rx_batch(hvws_ctx* ctx, uint8_t* h_rx, uint64_t len, const hvws_segment* segs,
+                  websocket_parser* carry, uint32_t nseg, int unmask);
+
+/* Host-inclusive streaming unmask of a large pinned host buffer holding
+ * frames back to back from one stream: chunked H2D -> scan -> unmask -> D2H,
+ * double-buffered over two streams.  carry is in/out. */
+int hvws_pipeline(hvws_ctx* ctx, uint8_t* h_rx, uint64_t len, uint64_t chunk,
+                  websocket_parser* carry);
+
+/* ---- WebSocketParser handle for FFI ------------------------------------ */
+typedef void (*hvws_msg_cb)(void* user, int opcode, const char* data, size_t len);
+void* hvws_wsp_new(void);
+void  hvws_wsp_free(void* h);
+void  hvws_wsp_set_sink(void* h, hvws_msg_cb cb, void* user);
+int   hvws_wsp_feed(void* h, const char* data, size_t len);
+void  hvws_wsp_state(void* h, uint64_t out[8]);
+
+/* Device used by the reference-API entry points on the calling thread
+ * (default: $HVWS_DEVICE or 0). */
+int hvws_set_thread_device(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HVWS_H */

@@ -1,0 +1,719 @@
+// hvws_engine.cpp -- host side of the MI355X WebSocket receive engine:
+// per-(thread, device) contexts, frame-table management, kernel sequencing,
+// and the C ABI declared in include/hvws.h and include/hvws_synth.h.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "hvws.h"
+#include "hvws_internal.h"
+#include "hvws_synth.h"
+
+using namespace hvws;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_OR(expr, code)                                                              \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return set_err((code), "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                           __LINE__);                                                   \
+    } while (0)
+
+// Grow-only device allocation.
+struct dbuf {
+    void* p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t want = std::max<uint64_t>(bytes + bytes / 2, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct hbuf {   // grow-only pinned host allocation
+    void* p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t want = std::max<uint64_t>(bytes + bytes / 2, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+}  // namespace
+
+struct hvws_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;    // compute
+    hipStream_t copy_in = nullptr;   // pipeline H2D
+    hipStream_t copy_out = nullptr;  // pipeline D2H
+    // per-batch tables
+    dbuf segs, carry_in, carry_out, counts, bases, total;
+    dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
+    dbuf tile_first;
+    uint64_t frame_cap = 0;
+    hbuf h_segs, h_carry, h_total;
+    // staging for host-memory entry points
+    dbuf stage;
+    dbuf xor_stage;
+    dbuf synth_sizes, synth_tiles, synth_bad;
+    // last scan
+    uint32_t nseg = 0;
+    uint64_t nfr = 0;
+    uint64_t rx_len = 0;
+    const uint8_t* rx = nullptr;
+    bool have_scan = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool ev_unmask = false;
+};
+
+namespace {
+
+dframes frames_of(hvws_ctx* c) {
+    dframes f;
+    f.hdr_off = c->f_hdr.as<int64_t>();
+    f.pay_off = c->f_off.as<uint64_t>();
+    f.pay_len = c->f_len.as<uint64_t>();
+    f.length = c->f_length.as<uint64_t>();
+    f.key = c->f_key.as<uint32_t>();
+    f.keyrot = c->f_keyrot.as<uint32_t>();
+    f.info = c->f_info.as<uint32_t>();
+    return f;
+}
+
+hipError_t ensure_frames(hvws_ctx* c, uint64_t n) {
+    if (n <= c->frame_cap && c->f_off.p) return hipSuccess;
+    uint64_t want = std::max<uint64_t>(n + n / 4, 1024);
+    hipError_t e;
+    if ((e = c->f_hdr.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->f_off.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->f_len.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->f_length.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->f_key.ensure(want * 4)) != hipSuccess) return e;
+    if ((e = c->f_keyrot.ensure(want * 4)) != hipSuccess) return e;
+    if ((e = c->f_info.ensure(want * 4)) != hipSuccess) return e;
+    c->frame_cap = want;
+    return hipSuccess;
+}
+
+void to_dcarry(const websocket_parser& p, dcarry& d) {
+    d.state = p.state;
+    d.flags = (uint32_t)p.flags;
+    memcpy(&d.mask, p.mask, 4);
+    d.mask_offset = p.mask_offset;
+    d.length = p.length;
+    d.require = p.require;
+    d.offset = p.offset;
+    d.started = 0;
+    d.pad = 0;
+}
+
+void from_dcarry(const dcarry& d, websocket_parser& p) {
+    p.state = d.state;
+    p.flags = (websocket_flags)d.flags;
+    memcpy(p.mask, &d.mask, 4);
+    p.mask_offset = (uint8_t)d.mask_offset;
+    p.length = d.length;
+    p.require = d.require;
+    p.offset = d.offset;
+}
+
+int check_ctx(hvws_ctx* c) {
+    if (!c) return set_err(HVWS_EINVAL, "null context");
+    HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+// Scan with the carry-in already resident in c->carry_in (device).
+int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_t nseg) {
+    HIP_OR(c->counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->total.ensure(8), HVWS_ENOMEM);
+    HIP_OR(c->carry_out.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    HIP_OR(c->h_total.ensure(8), HVWS_ENOMEM);
+    HIP_OR(ensure_frames(c, 1), HVWS_ENOMEM);
+    const dseg* segs = c->segs.as<dseg>();
+    const dcarry* cin = c->carry_in.as<dcarry>();
+    HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
+    HIP_OR(launch_scan(false, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
+                       nullptr, frames_of(c), c->stream),
+           HVWS_EHIP);
+    HIP_OR(launch_offsets(c->counts.as<uint64_t>(), c->bases.as<uint64_t>(), nseg, c->total.as<uint64_t>(),
+                          c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    const uint64_t nfr = *c->h_total.as<uint64_t>();
+    if (nfr >= 0xFFFFFFF0ull) return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)",
+                                             (unsigned long long)nfr);
+    HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
+    HIP_OR(launch_scan(true, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
+                       c->bases.as<uint64_t>(), frames_of(c), c->stream),
+           HVWS_EHIP);
+    const uint64_t ntiles = (rx_len + UNMASK_TILE - 1) / UNMASK_TILE;
+    HIP_OR(c->tile_first.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(launch_tile_index(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), nfr, c->tile_first.as<uint32_t>(),
+                             ntiles, UNMASK_TILE, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
+    c->nseg = nseg;
+    c->nfr = nfr;
+    c->rx = d_rx;
+    c->rx_len = rx_len;
+    c->have_scan = true;
+    c->ev_unmask = false;
+    return HVWS_OK;
+}
+
+int upload_segments(hvws_ctx* c, const hvws_segment* segs, const websocket_parser* carry, uint32_t nseg,
+                    uint64_t rx_len) {
+    for (uint32_t s = 0; s < nseg; ++s) {
+        if (segs[s].off > rx_len || segs[s].len > rx_len - segs[s].off)
+            return set_err(HVWS_EINVAL, "segment %u [%llu,+%llu) outside the %llu-byte buffer", s,
+                           (unsigned long long)segs[s].off, (unsigned long long)segs[s].len,
+                           (unsigned long long)rx_len);
+        if (s && segs[s].off < segs[s - 1].off + segs[s - 1].len)
+            return set_err(HVWS_EINVAL, "segments must be sorted and disjoint (segment %u)", s);
+    }
+    HIP_OR(c->segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
+    HIP_OR(c->carry_in.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    HIP_OR(c->h_segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
+    HIP_OR(c->h_carry.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    // The pinned staging may still be the source of an in-flight copy.
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    dseg* hs = c->h_segs.as<dseg>();
+    dcarry* hc = c->h_carry.as<dcarry>();
+    for (uint32_t s = 0; s < nseg; ++s) {
+        hs[s].off = segs[s].off;
+        hs[s].len = segs[s].len;
+        if (carry) {
+            to_dcarry(carry[s], hc[s]);
+        } else {
+            memset(&hc[s], 0, sizeof(dcarry));
+        }
+    }
+    HIP_OR(hipMemcpyAsync(c->segs.p, hs, (uint64_t)nseg * sizeof(dseg), hipMemcpyHostToDevice, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(c->carry_in.p, hc, (uint64_t)nseg * sizeof(dcarry), hipMemcpyHostToDevice, c->stream),
+           HVWS_EHIP);
+    return HVWS_OK;
+}
+
+thread_local int t_device = -1;
+thread_local hvws_ctx* t_ctx = nullptr;
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+const char* hvws_last_error(void) { return g_err; }
+
+int hvws_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+hvws_ctx* hvws_ctx_create(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        set_err(HVWS_ENODEV, "no HIP device available (%s)", e != hipSuccess ? hipGetErrorString(e) : "count 0");
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        set_err(HVWS_EINVAL, "device %d out of range (have %d)", device, n);
+        return nullptr;
+    }
+    if ((e = hipSetDevice(device)) != hipSuccess) {
+        set_err(HVWS_EHIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+        return nullptr;
+    }
+    hvws_ctx* c = new hvws_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess) {
+        set_err(HVWS_EHIP, "stream creation failed");
+        hvws_ctx_destroy(c);
+        return nullptr;
+    }
+    for (auto& ev : c->ev) {
+        if (hipEventCreate(&ev) != hipSuccess) {
+            set_err(HVWS_EHIP, "event creation failed");
+            hvws_ctx_destroy(c);
+            return nullptr;
+        }
+    }
+    return c;
+}
+
+void hvws_ctx_destroy(hvws_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (dbuf* b : {&c->segs, &c->carry_in, &c->carry_out, &c->counts, &c->bases, &c->total, &c->f_hdr, &c->f_off,
+                    &c->f_len, &c->f_length, &c->f_key, &c->f_keyrot, &c->f_info, &c->tile_first, &c->stage,
+                    &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad})
+        b->release();
+    c->h_segs.release();
+    c->h_carry.release();
+    c->h_total.release();
+    for (auto& ev : c->ev)
+        if (ev) hipEventDestroy(ev);
+    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->copy_in) hipStreamDestroy(c->copy_in);
+    if (c->copy_out) hipStreamDestroy(c->copy_out);
+    delete c;
+}
+
+void* hvws_ctx_stream(hvws_ctx* c) { return c ? (void*)c->stream : nullptr; }
+int hvws_ctx_device(hvws_ctx* c) { return c ? c->device : -1; }
+
+void* hvws_dev_alloc(hvws_ctx* c, uint64_t bytes) {
+    if (check_ctx(c) != HVWS_OK) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+        set_err(HVWS_ENOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+void hvws_dev_free(hvws_ctx* c, void* p) {
+    if (!c || !p) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    hipFree(p);
+}
+
+void* hvws_host_alloc(hvws_ctx* c, uint64_t bytes) {
+    if (check_ctx(c) != HVWS_OK) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_err(HVWS_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+void hvws_host_free(hvws_ctx* c, void* p) {
+    if (!c || !p) return;
+    hipSetDevice(c->device);
+    hipHostFree(p);
+}
+
+int hvws_h2d(hvws_ctx* c, void* dst, const void* src, uint64_t n) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_d2h(hvws_ctx* c, void* dst, const void* src, uint64_t n) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_memset(hvws_ctx* c, void* dst, int v, uint64_t n) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(hipMemsetAsync(dst, v, n, c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_sync(hvws_ctx* c) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_scan(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+              const websocket_parser* carry_in, uint32_t nseg) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
+    if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
+    if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
+    return scan_device_carry(c, d_rx, rx_len, nseg);
+}
+
+int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->have_scan) return set_err(HVWS_EINVAL, "hvws_unmask without a preceding hvws_scan");
+    if (d_rx != c->rx || rx_len != c->rx_len)
+        return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
+    HIP_OR(hipEventRecord(c->ev[2], c->stream), HVWS_EHIP);
+    HIP_OR(launch_unmask(d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(), c->nfr, c->stream), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[3], c->stream), HVWS_EHIP);
+    c->ev_unmask = true;
+    return HVWS_OK;
+}
+
+int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+              const websocket_parser* carry_in, uint32_t nseg) {
+    int rc = hvws_scan(c, d_rx, rx_len, segs, carry_in, nseg);
+    if (rc) return rc;
+    return hvws_unmask(c, d_rx, rx_len);
+}
+
+int64_t hvws_frame_count(hvws_ctx* c) {
+    if (!c || !c->have_scan) return -1;
+    return (int64_t)c->nfr;
+}
+
+int hvws_get_frames(hvws_ctx* c, hvws_frame* out, uint64_t first, uint64_t n) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    if (first > c->nfr || n > c->nfr - first) return set_err(HVWS_EINVAL, "frame range out of bounds");
+    if (n == 0) return HVWS_OK;
+    std::vector<int64_t> hdr(n);
+    std::vector<uint64_t> off(n), len(n), length(n);
+    std::vector<uint32_t> key(n), info(n);
+    HIP_OR(hipMemcpyAsync(hdr.data(), c->f_hdr.as<int64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(off.data(), c->f_off.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(len.data(), c->f_len.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(length.data(), c->f_length.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost,
+                          c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(key.data(), c->f_key.as<uint32_t>() + first, n * 4, hipMemcpyDeviceToHost, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(info.data(), c->f_info.as<uint32_t>() + first, n * 4, hipMemcpyDeviceToHost, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    for (uint64_t i = 0; i < n; ++i) {
+        out[i].hdr_off = hdr[i];
+        out[i].pay_off = off[i];
+        out[i].pay_len = len[i];
+        out[i].length = length[i];
+        out[i].key = key[i];
+        out[i].info = info[i];
+    }
+    return HVWS_OK;
+}
+
+int hvws_get_segment_frames(hvws_ctx* c, uint64_t* first, uint64_t* count) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    if (first)
+        HIP_OR(hipMemcpyAsync(first, c->bases.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
+               HVWS_EHIP);
+    if (count)
+        HIP_OR(hipMemcpyAsync(count, c->counts.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
+               HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_get_carry(hvws_ctx* c, websocket_parser* out, int* started) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    std::vector<dcarry> h(c->nseg);
+    if (c->nseg)
+        HIP_OR(hipMemcpyAsync(h.data(), c->carry_out.p, (uint64_t)c->nseg * sizeof(dcarry),
+                              hipMemcpyDeviceToHost, c->stream),
+               HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    for (uint32_t s = 0; s < c->nseg; ++s) {
+        if (out) from_dcarry(h[s], out[s]);
+        if (started) started[s] = (int)h[s].started;
+    }
+    return HVWS_OK;
+}
+
+int hvws_last_times(hvws_ctx* c, float out[2]) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    out[0] = out[1] = -1.0f;
+    if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    HIP_OR(hipEventSynchronize(c->ev[1]), HVWS_EHIP);
+    HIP_OR(hipEventElapsedTime(&out[0], c->ev[0], c->ev[1]), HVWS_EHIP);
+    if (c->ev_unmask) {
+        HIP_OR(hipEventSynchronize(c->ev[3]), HVWS_EHIP);
+        HIP_OR(hipEventElapsedTime(&out[1], c->ev[2], c->ev[3]), HVWS_EHIP);
+    }
+    return HVWS_OK;
+}
+
+int hvws_stream_xor(hvws_ctx* c, uint8_t* d, uint64_t n, uint32_t pattern) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (((uintptr_t)d & 15u) != 0) return set_err(HVWS_EINVAL, "buffer must be 16-byte aligned");
+    HIP_OR(launch_stream_xor(d, n, pattern, c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_rx_batch(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* segs, websocket_parser* carry,
+                  uint32_t nseg, int unmask) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(c->stage.ensure(len + 64), HVWS_ENOMEM);
+    uint8_t* d = c->stage.as<uint8_t>();
+    if ((rc = upload_segments(c, segs, carry, nseg, len)) != HVWS_OK) return rc;
+    if (len) HIP_OR(hipMemcpyAsync(d, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
+    if ((rc = scan_device_carry(c, d, len, nseg)) != HVWS_OK) return rc;
+    if (unmask) {
+        if ((rc = hvws_unmask(c, d, len)) != HVWS_OK) return rc;
+        if (len) HIP_OR(hipMemcpyAsync(h_rx, d, len, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    }
+    std::vector<void*> keep(nseg);
+    for (uint32_t s = 0; s < nseg; ++s) keep[s] = carry ? carry[s].data : nullptr;
+    if (carry) {
+        if ((rc = hvws_get_carry(c, carry, nullptr)) != HVWS_OK) return rc;
+        for (uint32_t s = 0; s < nseg; ++s) carry[s].data = keep[s];
+    } else {
+        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    }
+    return HVWS_OK;
+}
+
+int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, websocket_parser* carry) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!carry) return set_err(HVWS_EINVAL, "carry required");
+    if (chunk < 4096) chunk = 4096;
+    chunk = (chunk + 15) & ~15ull;
+    const uint64_t nchunks = (len + chunk - 1) / chunk;
+    if (nchunks == 0) return HVWS_OK;
+    // Three device slots: H2D(k+1) and D2H(k-1) overlap compute(k).
+    dbuf slot[3];
+    hipEvent_t in_done[3], comp_done[3], out_done[3];
+    for (int i = 0; i < 3; ++i) {
+        HIP_OR(slot[i].ensure(chunk + 64), HVWS_ENOMEM);
+        hipEventCreateWithFlags(&in_done[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&comp_done[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&out_done[i], hipEventDisableTiming);
+    }
+    hvws_segment seg0 = {0, 0};
+    void* keep = carry->data;
+    int out_rc = HVWS_OK;
+    auto issue_in = [&](uint64_t k) -> hipError_t {
+        const int s = (int)(k % 3);
+        const uint64_t off = k * chunk;
+        const uint64_t n = std::min(chunk, len - off);
+        hipError_t e = hipStreamWaitEvent(c->copy_in, out_done[s], 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(slot[s].p, h_rx + off, n, hipMemcpyHostToDevice, c->copy_in);
+        if (e == hipSuccess) e = hipEventRecord(in_done[s], c->copy_in);
+        return e;
+    };
+    // out_done events start "complete"
+    for (int i = 0; i < 3; ++i) hipEventRecord(out_done[i], c->copy_out);
+    hipError_t e = issue_in(0);
+    for (uint64_t k = 0; k < nchunks && e == hipSuccess && out_rc == HVWS_OK; ++k) {
+        const int s = (int)(k % 3);
+        const uint64_t off = k * chunk;
+        const uint64_t n = std::min(chunk, len - off);
+        if (k + 1 < nchunks) e = issue_in(k + 1);
+        if (e != hipSuccess) break;
+        e = hipStreamWaitEvent(c->stream, in_done[s], 0);
+        if (e != hipSuccess) break;
+        seg0.len = n;
+        if (k == 0) {
+            out_rc = upload_segments(c, &seg0, carry, 1, n);
+        } else {
+            // The carry chains on the device: chunk k-1's carry-out is chunk
+            // k's carry-in (a frame may straddle the chunk boundary).
+            const dseg ds = {0, n};
+            e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) break;
+            memcpy(c->h_segs.p, &ds, sizeof(ds));
+            e = hipMemcpyAsync(c->segs.p, c->h_segs.p, sizeof(ds), hipMemcpyHostToDevice, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(c->carry_in.p, c->carry_out.p, sizeof(dcarry), hipMemcpyDeviceToDevice,
+                                   c->stream);
+            if (e != hipSuccess) break;
+        }
+        if (out_rc != HVWS_OK) break;
+        out_rc = scan_device_carry(c, slot[s].as<uint8_t>(), n, 1);
+        if (out_rc != HVWS_OK) break;
+        out_rc = hvws_unmask(c, slot[s].as<uint8_t>(), n);
+        if (out_rc != HVWS_OK) break;
+        e = hipEventRecord(comp_done[s], c->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->copy_out, comp_done[s], 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(h_rx + off, slot[s].p, n, hipMemcpyDeviceToHost, c->copy_out);
+        if (e == hipSuccess) e = hipEventRecord(out_done[s], c->copy_out);
+    }
+    if (e == hipSuccess && out_rc == HVWS_OK) {
+        e = hipStreamSynchronize(c->copy_out);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) out_rc = hvws_get_carry(c, carry, nullptr);
+    }
+    hipStreamSynchronize(c->copy_in);
+    hipStreamSynchronize(c->copy_out);
+    hipStreamSynchronize(c->stream);
+    for (int i = 0; i < 3; ++i) {
+        hipEventDestroy(in_done[i]);
+        hipEventDestroy(comp_done[i]);
+        hipEventDestroy(out_done[i]);
+        slot[i].release();
+    }
+    carry->data = keep;
+    // The slots are gone: forget the scan that referenced them.
+    c->have_scan = false;
+    if (e != hipSuccess) return set_err(HVWS_EHIP, "pipeline: %s", hipGetErrorString(e));
+    return out_rc;
+}
+
+// ------------------------------------------------------------------ synth
+int hvws_synth(hvws_ctx* c, uint8_t* d_buf, uint64_t buf_len, uint64_t seed, uint64_t nframes,
+               const uint64_t* d_frame_off, const uint8_t* d_flags, const uint32_t* d_mask,
+               const uint64_t* d_length, const uint8_t* d_text, int mode, uint64_t* mismatches) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (mode < 0 || mode > 2) return set_err(HVWS_EINVAL, "bad synth mode %d", mode);
+    const uint64_t tile = synth_tile();
+    const uint64_t ntiles = (buf_len + tile - 1) / tile;
+    HIP_OR(c->synth_sizes.ensure(nframes * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->synth_tiles.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(c->synth_bad.ensure(8), HVWS_ENOMEM);
+    HIP_OR(launch_frame_sizes(d_flags, d_length, nframes, c->synth_sizes.as<uint64_t>(), c->stream), HVWS_EHIP);
+    HIP_OR(launch_tile_index(d_frame_off, c->synth_sizes.as<uint64_t>(), nframes, c->synth_tiles.as<uint32_t>(),
+                             ntiles, tile, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipMemsetAsync(c->synth_bad.p, 0, 8, c->stream), HVWS_EHIP);
+    HIP_OR(launch_synth(d_buf, buf_len, seed, nframes, d_frame_off, d_flags, d_mask, d_length, d_text,
+                        c->synth_sizes.as<uint64_t>(), c->synth_tiles.as<uint32_t>(), mode,
+                        c->synth_bad.as<unsigned long long>(), c->stream),
+           HVWS_EHIP);
+    if (mode != HVWS_SYNTH_WRITE) {
+        uint64_t bad = 0;
+        HIP_OR(hipMemcpyAsync(&bad, c->synth_bad.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+        if (mismatches) *mismatches = bad;
+    }
+    return HVWS_OK;
+}
+
+int hvws_digest(hvws_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* out) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(c->synth_bad.ensure(8), HVWS_ENOMEM);
+    HIP_OR(hipMemsetAsync(c->synth_bad.p, 0, 8, c->stream), HVWS_EHIP);
+    HIP_OR(launch_digest(d_buf, len, c->synth_bad.as<unsigned long long>(), c->stream), HVWS_EHIP);
+    uint64_t v = 0;
+    HIP_OR(hipMemcpyAsync(&v, c->synth_bad.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    if (out) *out = v;
+    return HVWS_OK;
+}
+
+int hvws_set_thread_device(int device) {
+    if (t_ctx && t_ctx->device != device) {
+        hvws_ctx_destroy(t_ctx);
+        t_ctx = nullptr;
+    }
+    t_device = device;
+    return HVWS_OK;
+}
+
+}  // extern "C"
+
+// ----------------------------------------------- internal helpers for the drop-in
+namespace hvws {
+
+[[noreturn]] void fatal(const char* what) {
+    fprintf(stderr, "libhvws: %s: %s -- the MI355X WebSocket path has no CPU fallback\n", what, g_err);
+    fflush(stderr);
+    abort();
+}
+
+hvws_ctx* thread_ctx() {
+    if (t_ctx) return t_ctx;
+    int dev = t_device;
+    if (dev < 0) {
+        const char* e = getenv("HVWS_DEVICE");
+        dev = e ? atoi(e) : 0;
+    }
+    t_ctx = hvws_ctx_create(dev);
+    if (!t_ctx) fatal("cannot open a HIP device context");
+    return t_ctx;
+}
+
+// XOR `n` host bytes at src into dst with key/phase on the GPU.
+void gpu_xor_host(char* dst, const char* src, size_t n, uint32_t key, uint32_t phase) {
+    if (n == 0) return;
+    hvws_ctx* c = thread_ctx();
+    if (hipSetDevice(c->device) != hipSuccess) fatal("hipSetDevice");
+    if (c->xor_stage.ensure(n + 64) != hipSuccess) fatal("device staging allocation");
+    uint8_t* d = c->xor_stage.as<uint8_t>();
+    if (hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        launch_xor_span(d, n, key, phase, c->stream) != hipSuccess ||
+        hipMemcpyAsync(dst, d, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        set_err(HVWS_EHIP, "xor span failed");
+        fatal("websocket_decode on the GPU");
+    }
+}
+
+// One-segment batch from host memory for the streaming drop-in.
+// Returns frames and the carry-out (WebSocketParser semantics).
+void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
+              websocket_parser& carry_out, int& started) {
+    hvws_ctx* c = thread_ctx();
+    hvws_segment seg = {0, (uint64_t)len};
+    websocket_parser cin = carry;
+    if (hvws_rx_batch(c, (uint8_t*)buf, len, &seg, &cin, 1, unmask ? 1 : 0) != HVWS_OK) fatal("hvws_rx_batch");
+    const int64_t n = hvws_frame_count(c);
+    frames.resize((size_t)n);
+    if (n > 0 && hvws_get_frames(c, frames.data(), 0, (uint64_t)n) != HVWS_OK) fatal("hvws_get_frames");
+    int st = 0;
+    if (hvws_get_carry(c, nullptr, &st) != HVWS_OK) fatal("hvws_get_carry");
+    carry_out = cin;
+    started = st;
+}
+
+}  // namespace hvws

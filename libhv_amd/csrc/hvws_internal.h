@@ -1,0 +1,76 @@
+// hvws_internal.h -- shared between the HIP kernels and the host engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hvws {
+
+// Parser states (reference enum at http/websocket_parser.c:34-40).
+enum : uint32_t { S_START = 0, S_HEAD = 1, S_LENGTH = 2, S_MASK = 3, S_BODY = 4 };
+enum : uint32_t { F_OPMASK = 0x0Fu, F_FIN = 0x10u, F_MASK = 0x20u };
+enum : uint32_t {
+    I_HDR = 1u << 10, I_BODY = 1u << 11, I_END = 1u << 12, I_START = 1u << 13
+};
+
+// Device-side carry (the websocket_parser fields the walk needs), 48 bytes.
+struct dcarry {
+    uint32_t state;
+    uint32_t flags;
+    uint32_t mask;         // mask[0] in bits 0-7
+    uint32_t mask_offset;
+    uint64_t length;
+    uint64_t require;
+    uint64_t offset;
+    uint32_t started;      // first header byte of the pending frame was in this segment
+    uint32_t pad;
+};
+
+struct dseg {
+    uint64_t off;
+    uint64_t len;
+};
+
+// Frame table, structure of arrays in HBM (one entry per frame per batch).
+struct dframes {
+    int64_t*  hdr_off;   // absolute, -1 = header began in an earlier batch
+    uint64_t* pay_off;   // absolute
+    uint64_t* pay_len;
+    uint64_t* length;
+    uint32_t* key;       // raw key
+    uint32_t* keyrot;    // key rotated for 4-byte aligned words (0 if not masked)
+    uint32_t* info;
+};
+
+constexpr int SCAN_THREADS = 256;           // 4 waves, one segment per wave
+constexpr int SCAN_U = 4;                   // predicted frames per lane per round
+constexpr int UNMASK_THREADS = 256;
+constexpr int UNMASK_UNROLL = 8;            // 16-B chunks per thread per tile
+constexpr uint64_t UNMASK_TILE = (uint64_t)UNMASK_THREADS * 16u * UNMASK_UNROLL;  // 32 KiB
+constexpr int UNMASK_MAXF = 512;            // frames staged in LDS per tile
+
+// Kernel launchers (hvws_kernels.hip).
+hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
+                       const dcarry* carry_in, dcarry* carry_out, uint64_t* counts,
+                       const uint64_t* bases, dframes fr, hipStream_t st);
+hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
+                          hipStream_t st);
+hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
+                             uint64_t ntiles, uint64_t tile, hipStream_t st);
+hipError_t launch_unmask(uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
+                         uint64_t nfr, hipStream_t st);
+hipError_t launch_stream_xor(uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
+hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st);
+
+// Synthetic data (hvws_synth.hip).
+hipError_t launch_synth(uint8_t* buf, uint64_t buf_len, uint64_t seed, uint64_t nframes,
+                        const uint64_t* frame_off, const uint8_t* flags, const uint32_t* mask,
+                        const uint64_t* length, const uint8_t* text, const uint64_t* frame_size,
+                        const uint32_t* tile_first, int mode, unsigned long long* mismatches,
+                        hipStream_t st);
+hipError_t launch_digest(const uint8_t* buf, uint64_t len, unsigned long long* out, hipStream_t st);
+hipError_t launch_frame_sizes(const uint8_t* flags, const uint64_t* length, uint64_t nframes,
+                              uint64_t* out, hipStream_t st);
+uint64_t synth_tile();
+
+}  // namespace hvws

@@ -1,0 +1,689 @@
+// hvws_kernels.hip -- HIP kernels of the MI355X WebSocket receive path (gfx950).
+//
+//   k_scan        frame discovery + header parse (FIN/opcode/mask/length/key)
+//                 for every segment of a batch: one wavefront per segment,
+//                 speculative stride walk verified with a 64-lane ballot.
+//                 Replaces the per-byte switch of websocket_parser_execute
+//                 (reference http/websocket_parser.c:53-171).
+//   k_offsets     exclusive scan of per-segment frame counts.
+//   k_tile_index  first frame touching each 32 KiB tile of the rx buffer.
+//   k_unmask      rotating 32-bit XOR of every masked payload byte, in place,
+//                 16-B coalesced loads/stores, tile frame table staged in LDS.
+//                 Replaces websocket_parser_decode's byte loop
+//                 (http/websocket_parser.c:173-180) as called by
+//                 WebSocketParser::on_frame_body (http/WebSocketParser.cpp:32-34).
+//   k_stream_xor  STREAM-style in-place read+write ceiling for the roofline.
+//
+// All work is integer; there is no contraction, so no MFMA.  The unmask is
+// HBM-bound: 2 x payload + headers bytes per pass.
+#include "hvws_internal.h"
+
+namespace hvws {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- helpers
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
+    r &= 31u;
+    return r ? (x >> r) | (x << (32u - r)) : x;
+}
+
+// Key word for 4-byte aligned words of a payload whose first byte sits at
+// absolute offset `pay_off` with mask phase `phase`: byte at address a uses
+// mask[(a - pay_off + phase) & 3] (http/websocket_parser.c:175).
+__device__ __forceinline__ uint32_t key_for_aligned(uint32_t key, uint64_t pay_off, uint32_t phase) {
+    uint32_t rot = (phase - (uint32_t)pay_off) & 3u;
+    return rotr32(key, 8u * rot);
+}
+
+__device__ __forceinline__ uint64_t ld64_guard(const uint8_t* rx, uint64_t rx_len, uint64_t a) {
+    if (a + 8 <= rx_len) return *reinterpret_cast<const uint64_t*>(rx + a);
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (a + k < rx_len) v |= (uint64_t)rx[a + k] << (8 * k);
+    return v;
+}
+
+// 16 bytes starting at arbitrary absolute offset q (bytes past rx_len read 0).
+__device__ __forceinline__ void ld16(const uint8_t* rx, uint64_t rx_len, uint64_t q, uint64_t& lo,
+                                     uint64_t& hi) {
+    uint64_t a = q & ~7ull;
+    uint32_t sh = (uint32_t)(q & 7u) * 8u;
+    uint64_t w0 = ld64_guard(rx, rx_len, a);
+    uint64_t w1 = ld64_guard(rx, rx_len, a + 8);
+    if (sh == 0) {
+        lo = w0;
+        hi = w1;
+        return;
+    }
+    uint64_t w2 = ld64_guard(rx, rx_len, a + 16);
+    lo = (w0 >> sh) | (w1 << (64u - sh));
+    hi = (w1 >> sh) | (w2 << (64u - sh));
+}
+
+struct hdr {
+    uint64_t length;
+    uint32_t hlen;
+    uint32_t flags;
+    uint32_t key;
+};
+
+// Fixed-format header decode from its first 16 bytes (lo = bytes 0..7 LE).
+// Layout per websocket_build_frame (http/websocket_parser.c:207-256):
+// b0 = FIN<<7 | opcode, b1 = MASK<<7 | len7, then 0/2/8 big-endian length
+// bytes, then the 4 key bytes if MASK.  RSV bits are dropped (Q1).
+__device__ __forceinline__ hdr parse_hdr(uint64_t lo, uint64_t hi) {
+    hdr h;
+    uint32_t b0 = (uint32_t)lo & 0xFFu;
+    uint32_t b1 = (uint32_t)(lo >> 8) & 0xFFu;
+    uint32_t len7 = b1 & 0x7Fu;
+    bool m = (b1 & 0x80u) != 0;
+    h.flags = (b0 & F_OPMASK) | ((b0 & 0x80u) ? F_FIN : 0u) | (m ? F_MASK : 0u);
+    uint32_t ext = len7 == 126 ? 2u : (len7 == 127 ? 8u : 0u);
+    h.hlen = 2u + ext + (m ? 4u : 0u);
+    uint64_t len16 = (((lo >> 16) & 0xFFu) << 8) | ((lo >> 24) & 0xFFu);
+    uint64_t len64 = __builtin_bswap64((lo >> 16) | (hi << 48));
+    h.length = len7 < 126 ? (uint64_t)len7 : (len7 == 126 ? len16 : len64);
+    uint32_t k0 = (uint32_t)(lo >> 16), k2 = (uint32_t)(lo >> 32), k8 = (uint32_t)(hi >> 16);
+    h.key = m ? (ext == 0 ? k0 : (ext == 2 ? k2 : k8)) : 0u;
+    return h;
+}
+
+struct frec {
+    int64_t  hdr_off;   // segment-relative here; made absolute on store
+    uint64_t pay_off;   // segment-relative
+    uint64_t pay_len;
+    uint64_t length;
+    uint32_t key;
+    uint32_t info;
+};
+
+__device__ __forceinline__ void store_frame(const dframes& fr, uint64_t idx, uint64_t seg_off, const frec& r) {
+    uint32_t phase = (r.info >> 8) & 3u;
+    bool masked = (r.info & F_MASK) != 0;
+    uint64_t abs_pay = seg_off + r.pay_off;
+    fr.hdr_off[idx] = r.hdr_off < 0 ? -1 : (int64_t)(seg_off + (uint64_t)r.hdr_off);
+    fr.pay_off[idx] = abs_pay;
+    fr.pay_len[idx] = r.pay_len;
+    fr.length[idx] = r.length;
+    fr.key[idx] = r.key;
+    fr.keyrot[idx] = masked ? key_for_aligned(r.key, abs_pay, phase) : 0u;
+    fr.info[idx] = r.info;
+}
+
+__device__ __forceinline__ void hdr_complete(frec& r, const dcarry& st, uint64_t pay_off) {
+    r.info = (r.info & ~0xFFu & ~(3u << 8)) | (st.flags & 0xFFu) | I_HDR;
+    r.pay_off = pay_off;
+    r.pay_len = 0;
+    r.length = st.length;
+    r.key = (st.flags & F_MASK) ? st.mask : 0u;
+}
+
+// Exact byte-level state machine for one frame episode starting from `st` at
+// segment-relative `pos`: used for the carry-in frame and for the incomplete
+// frame at the segment end (the speculative walk handles everything whole in
+// between).  Mirrors http/websocket_parser.c:60-164 state by state, with the
+// payload decoded by WebSocketParser (mask_offset advanced over masked bytes).
+// Returns true when any callback of the reference would fire for this frame
+// inside the segment (then `r` holds its record).  All lanes run it
+// redundantly on the same bytes, so control flow stays wave-uniform.
+__device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_t& pos, frec& r) {
+    r.hdr_off = -1;
+    r.pay_off = 0;
+    r.pay_len = 0;
+    r.length = 0;
+    r.key = 0;
+    r.info = 0;
+    bool have = false;
+    if (st.state == S_START) {
+        if (pos >= L) return false;
+        uint32_t b0 = seg[pos];
+        st.offset = 0;
+        st.length = 0;
+        st.mask_offset = 0;
+        st.flags = (b0 & F_OPMASK) | ((b0 & 0x80u) ? F_FIN : 0u);
+        st.state = S_HEAD;
+        st.started = 1;
+        r.hdr_off = (int64_t)pos;
+        r.info |= I_START;
+        ++pos;
+    }
+    if (st.state == S_HEAD) {
+        if (pos >= L) return false;
+        uint32_t b1 = seg[pos];
+        ++pos;
+        st.length = b1 & 0x7Fu;
+        if (b1 & 0x80u) st.flags |= F_MASK;
+        if (st.length >= 126) {
+            st.require = st.length == 127 ? 8 : 2;
+            st.length = 0;
+            st.state = S_LENGTH;
+        } else if (st.flags & F_MASK) {
+            st.state = S_MASK;
+            st.require = 4;
+        } else if (st.length) {
+            st.state = S_BODY;
+            st.require = st.length;
+            hdr_complete(r, st, pos);
+            have = true;
+        } else {
+            st.state = S_START;
+            hdr_complete(r, st, pos);
+            r.info |= I_END;
+            return true;
+        }
+    }
+    if (st.state == S_LENGTH) {
+        while (pos < L && st.require) {
+            st.length = (st.length << 8) | seg[pos];
+            --st.require;
+            ++pos;
+        }
+        if (st.require) return false;
+        if (st.flags & F_MASK) {
+            st.state = S_MASK;
+            st.require = 4;
+        } else if (st.length) {
+            st.state = S_BODY;
+            st.require = st.length;
+            hdr_complete(r, st, pos);
+            have = true;
+        } else {
+            st.state = S_START;
+            hdr_complete(r, st, pos);
+            r.info |= I_END;
+            return true;
+        }
+    }
+    if (st.state == S_MASK) {
+        while (pos < L && st.require) {
+            uint32_t sh = 8u * (uint32_t)(4 - st.require);
+            st.mask = (st.mask & ~(0xFFu << sh)) | ((uint32_t)seg[pos] << sh);
+            --st.require;
+            ++pos;
+        }
+        if (st.require) return false;
+        if (st.length) {
+            st.state = S_BODY;
+            st.require = st.length;
+            hdr_complete(r, st, pos);
+            have = true;
+        } else {
+            st.state = S_START;
+            hdr_complete(r, st, pos);
+            r.info |= I_END;
+            return true;
+        }
+    }
+    if (st.state == S_BODY) {
+        if (st.require == 0) {
+            // Unreachable through the reference API (body states are entered
+            // with require > 0); mirrored: end the frame, skip one byte.
+            if (pos >= L) return have;
+            if (!have) {
+                r.info = (st.flags & 0xFFu) | ((st.mask_offset & 3u) << 8);
+                r.length = st.length;
+                r.key = (st.flags & F_MASK) ? st.mask : 0u;
+                r.pay_off = pos;
+            }
+            st.state = S_START;
+            r.info |= I_END;
+            ++pos;
+            return true;
+        }
+        if (pos >= L) return have;
+        if (!have) {   // continuing frame: header was in an earlier batch
+            r.info = (st.flags & 0xFFu) | ((st.mask_offset & 3u) << 8);
+            r.length = st.length;
+            r.key = (st.flags & F_MASK) ? st.mask : 0u;
+        }
+        uint64_t avail = L - pos;
+        uint64_t nb = st.require < avail ? st.require : avail;
+        r.pay_off = pos;
+        r.pay_len = nb;
+        r.info |= I_BODY;
+        if (st.flags & F_MASK) st.mask_offset = (uint32_t)((st.mask_offset + nb) & 3u);
+        st.require -= nb;
+        pos += nb;
+        if (st.require == 0) {
+            st.state = S_START;
+            r.info |= I_END;
+        } else {
+            st.offset += L - r.pay_off;   // http/websocket_parser.c:153
+        }
+        return true;
+    }
+    return have;
+}
+
+// ---------------------------------------------------------------- k_scan
+//
+// One wavefront per segment.  After finishing any carried-in frame, the wave
+// walks whole frames speculatively: with stride s (bytes of the last frame),
+// lane l predicts frames j = u*64 + l at pos + j*s, parses each predicted
+// header from HBM (all 64*SCAN_U loads in flight at once), and a ballot finds
+// the first prediction whose parsed size breaks the chain.  Every prediction
+// before it is a verified frame (induction from the known header at pos), so
+// uniform streams advance 256 frames per HBM round trip and mixed ones at
+// least one.  COUNT mode only counts; EMIT mode writes the frame table at
+// bases[segment].
+
+template <bool EMIT>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                       const dseg* __restrict__ segs, uint32_t nseg,
+                                                       const dcarry* __restrict__ carry_in,
+                                                       dcarry* __restrict__ carry_out,
+                                                       uint64_t* __restrict__ counts,
+                                                       const uint64_t* __restrict__ bases, dframes fr) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves_per_block = SCAN_THREADS / 64;
+    const uint32_t gw = blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * waves_per_block;
+    constexpr uint32_t NPRED = 64u * SCAN_U;
+
+    for (uint32_t s = gw; s < nseg; s += nw) {
+        const uint64_t sb = segs[s].off;
+        const uint64_t L = segs[s].len;
+        const uint8_t* seg = rx + sb;
+        dcarry st = carry_in[s];
+        st.started = 0;
+        uint64_t pos = 0;
+        uint64_t n = 0;
+        const uint64_t obase = EMIT ? bases[s] : 0;
+        frec r;
+
+        // Phase A: the frame carried in from the previous batch.
+        if (st.state != S_START) {
+            if (scalar_frame(seg, L, st, pos, r)) {
+                if (EMIT && lane == 0) store_frame(fr, obase + n, sb, r);
+                ++n;
+            }
+        }
+
+        // Phase B: whole frames, speculative stride walk.
+        uint64_t stride = 0;
+        while (st.state == S_START && pos < L) {
+            const uint64_t rem = L - pos;
+            if (stride == 0) {
+                uint64_t lo, hi;
+                ld16(rx, rx_len, sb + pos, lo, hi);
+                if (rem < 2) break;
+                hdr h = parse_hdr(lo, hi);
+                if (h.hlen > rem || h.length > rem - h.hlen) break;   // incomplete: tail
+                stride = h.hlen + h.length;
+            }
+            uint64_t lo[SCAN_U], hi[SCAN_U];
+            bool inr[SCAN_U];
+#pragma unroll
+            for (int u = 0; u < SCAN_U; ++u) {
+                const uint32_t j = (uint32_t)u * 64u + lane;
+                inr[u] = rem >= 2 && (j == 0 || stride <= (rem - 2) / j);
+                lo[u] = hi[u] = 0;
+                if (inr[u]) ld16(rx, rx_len, sb + pos + (uint64_t)j * stride, lo[u], hi[u]);
+            }
+            hdr h[SCAN_U];
+            bool whole[SCAN_U];
+            uint32_t f = NPRED;
+#pragma unroll
+            for (int u = 0; u < SCAN_U; ++u) {
+                const uint32_t j = (uint32_t)u * 64u + lane;
+                const uint64_t q = pos + (uint64_t)j * stride;
+                h[u] = parse_hdr(lo[u], hi[u]);
+                const uint64_t rq = inr[u] ? L - q : 0;
+                whole[u] = inr[u] && h[u].hlen <= rq && h[u].length <= rq - h[u].hlen;
+                const bool ok = whole[u] && (uint64_t)h[u].hlen + h[u].length == stride;
+                const unsigned long long bad = __ballot(!ok);
+                if (f == NPRED && bad) f = (uint32_t)u * 64u + (uint32_t)(__ffsll((long long)bad) - 1);
+            }
+            // Verified frames j < f: every callback fires for them here.
+            uint32_t last_flags = 0, last_key = 0;
+            uint64_t last_len = 0;
+            bool any_masked = false;
+#pragma unroll
+            for (int u = 0; u < SCAN_U; ++u) {
+                const uint32_t j = (uint32_t)u * 64u + lane;
+                const bool mine = j < f;
+                if (EMIT && mine) {
+                    frec v;
+                    const uint64_t q = pos + (uint64_t)j * stride;
+                    v.hdr_off = (int64_t)q;
+                    v.pay_off = q + h[u].hlen;
+                    v.pay_len = h[u].length;
+                    v.length = h[u].length;
+                    v.key = h[u].key;
+                    v.info = h[u].flags | I_HDR | I_START | I_END | (h[u].length ? I_BODY : 0u);
+                    store_frame(fr, obase + n + j, sb, v);
+                }
+                const unsigned long long mm = __ballot(mine && (h[u].flags & F_MASK));
+                if (mm) {
+                    const int src = 63 - __clzll((long long)mm);
+                    last_key = __shfl(h[u].key, src);
+                    any_masked = true;
+                }
+                if (f > (uint32_t)u * 64u && f <= (uint32_t)u * 64u + 64u) {
+                    const int src = (int)(f - 1 - (uint32_t)u * 64u);
+                    last_flags = __shfl(h[u].flags, src);
+                    last_len = __shfl(h[u].length, src);
+                }
+            }
+            if (f > 0) {
+                // Q14: fields keep the last frame's values after it ends.
+                st.flags = last_flags;
+                st.length = last_len;
+                st.require = 0;
+                st.offset = 0;
+                st.mask_offset = (last_flags & F_MASK) ? (uint32_t)(last_len & 3u) : 0u;
+                st.started = 0;
+                if (any_masked) st.mask = last_key;
+            }
+            n += f;
+            pos += (uint64_t)f * stride;
+            if (f == NPRED) continue;   // chain unbroken: same stride
+            if (pos >= L) break;
+            // Frame f sits at pos (a true header).  Take its real size.
+            bool wf = false;
+            uint64_t sf = 0;
+            const uint32_t uf = f >> 6, lf = f & 63u;
+#pragma unroll
+            for (int u = 0; u < SCAN_U; ++u) {
+                const bool w = __shfl((int)whole[u], (int)lf) != 0;
+                const uint64_t sz = __shfl((uint64_t)h[u].hlen + h[u].length, (int)lf);
+                if ((uint32_t)u == uf) {
+                    wf = w;
+                    sf = sz;
+                }
+            }
+            if (!wf) break;   // incomplete: tail
+            stride = sf;
+        }
+
+        // Tail: a frame cut by the segment end (partial header or body).
+        if (st.state == S_START && pos < L) {
+            if (scalar_frame(seg, L, st, pos, r)) {
+                if (EMIT && lane == 0) store_frame(fr, obase + n, sb, r);
+                ++n;
+            }
+        }
+        if (lane == 0) {
+            if (!EMIT) counts[s] = n;
+            else carry_out[s] = st;
+        }
+    }
+}
+
+// ------------------------------------------------------------- k_offsets
+// Exclusive scan of counts[0..nseg) into bases[], total into *total.  One
+// block of 1024 threads; each thread owns a contiguous run.
+__global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ counts,
+                                                  uint64_t* __restrict__ bases, uint32_t nseg,
+                                                  uint64_t* __restrict__ total) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nseg + 1023u) / 1024u;
+    const uint32_t b = t * per;
+    const uint32_t e = min(nseg, b + per);
+    uint64_t sum = 0;
+    for (uint32_t i = b; i < e; ++i) sum += counts[i];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+        uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint32_t i = b; i < e; ++i) {
+        bases[i] = run;
+        run += counts[i];
+    }
+    if (t == 1023u) *total = part[1023];
+}
+
+// ---------------------------------------------------------- k_tile_index
+// tile_first[t] = first frame k with off[k] + len[k] > t*tile (t <= ntiles).
+__global__ void k_tile_index(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                             uint64_t nfr, uint32_t* __restrict__ tile_first, uint64_t ntiles,
+                             uint64_t tile) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t x = t * tile;
+    uint64_t lo = 0, hi = nfr;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (off[mid] + len[mid] > x) hi = mid;
+        else lo = mid + 1;
+    }
+    tile_first[t] = (uint32_t)lo;
+}
+
+// -------------------------------------------------------------- k_unmask
+//
+// One workgroup per 32 KiB tile.  Each thread owns 8 16-byte chunks spaced
+// 4 KiB apart (lane-contiguous, so every wave instruction moves 1 KiB).  Data
+// loads are issued first; meanwhile the tile's frames (from the tile index)
+// are staged in LDS as [pay_off, pay_end, key].  A chunk wholly inside one
+// masked payload is XORed with 4 copies of that frame's aligned key word; a
+// chunk touching a header or a frame boundary is merged byte by byte; chunks
+// with no masked byte are not written back.
+
+struct tile_frames {
+    const uint64_t* off;
+    const uint64_t* end;
+    const uint32_t* key;
+};
+
+template <typename OFF, typename END>
+__device__ __forceinline__ uint32_t first_end_after(OFF, END endf, uint32_t n, uint64_t c) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (endf(mid) > c) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+template <typename OFF, typename END, typename KEY>
+__device__ __forceinline__ bool xor_chunk(u32x4& v, uint64_t c, uint32_t nf, OFF offf, END endf, KEY keyf) {
+    uint32_t k = first_end_after(offf, endf, nf, c);
+    if (k >= nf) return false;
+    const uint64_t o = offf(k), e = endf(k);
+    if (o >= c + 16) return false;               // only header/gap bytes here
+    if (o <= c && c + 16 <= e) {                 // fast path: one payload
+        const uint32_t kw = keyf(k);
+        v.x ^= kw;
+        v.y ^= kw;
+        v.z ^= kw;
+        v.w ^= kw;
+        return true;
+    }
+    uint32_t m[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        const uint64_t a = c + (uint64_t)b;
+        while (k < nf && endf(k) <= a) ++k;
+        if (k < nf && offf(k) <= a) m[b >> 2] |= ((keyf(k) >> (8 * (b & 3))) & 0xFFu) << (8 * (b & 3));
+    }
+    v.x ^= m[0];
+    v.y ^= m[1];
+    v.z ^= m[2];
+    v.w ^= m[3];
+    return true;
+}
+
+__global__ __launch_bounds__(UNMASK_THREADS) void k_unmask(uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                           const uint64_t* __restrict__ pay_off,
+                                                           const uint64_t* __restrict__ pay_len,
+                                                           const uint32_t* __restrict__ keyrot,
+                                                           const uint32_t* __restrict__ tile_first,
+                                                           uint64_t nfr) {
+    __shared__ uint64_t s_off[UNMASK_MAXF];
+    __shared__ uint64_t s_end[UNMASK_MAXF];
+    __shared__ uint32_t s_key[UNMASK_MAXF];
+
+    const uint64_t t = blockIdx.x;
+    const uint64_t base = t * UNMASK_TILE;
+    const uint32_t tid = threadIdx.x;
+
+    u32x4 v[UNMASK_UNROLL];
+#pragma unroll
+    for (int i = 0; i < UNMASK_UNROLL; ++i) {
+        const uint64_t c = base + ((uint64_t)i * UNMASK_THREADS + tid) * 16u;
+        if (c + 16 <= rx_len) {
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rx + c));
+        } else {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int b = 0; b < 16; ++b)
+                if (c + b < rx_len) w[b >> 2] |= (uint32_t)rx[c + b] << (8 * (b & 3));
+            v[i] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+    }
+
+    const uint32_t k0 = tile_first[t];
+    const uint32_t k1r = tile_first[t + 1];
+    const uint32_t k1 = (uint64_t)k1r + 1 < nfr ? k1r + 1 : (uint32_t)nfr;
+    const uint32_t nf = k1 > k0 ? k1 - k0 : 0u;
+    const bool staged = nf <= (uint32_t)UNMASK_MAXF;
+
+    if (staged) {
+        for (uint32_t i = tid; i < nf; i += UNMASK_THREADS) {
+            const uint64_t o = pay_off[k0 + i];
+            const uint32_t kw = keyrot[k0 + i];
+            s_off[i] = o;
+            // A zero key word (unmasked frame, or a masked one whose key is
+            // 0) changes nothing: stage it as an empty span so its bytes are
+            // neither XORed nor written back.  Ends stay non-decreasing.
+            s_end[i] = kw ? o + pay_len[k0 + i] : o;
+            s_key[i] = kw;
+        }
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int i = 0; i < UNMASK_UNROLL; ++i) {
+        const uint64_t c = base + ((uint64_t)i * UNMASK_THREADS + tid) * 16u;
+        if (c >= rx_len) continue;
+        bool dirty;
+        if (staged) {
+            dirty = xor_chunk(
+                v[i], c, nf, [&](uint32_t k) { return s_off[k]; }, [&](uint32_t k) { return s_end[k]; },
+                [&](uint32_t k) { return s_key[k]; });
+        } else {
+            dirty = xor_chunk(
+                v[i], c, nf, [&](uint32_t k) { return pay_off[k0 + k]; },
+                [&](uint32_t k) { return keyrot[k0 + k] ? pay_off[k0 + k] + pay_len[k0 + k] : pay_off[k0 + k]; },
+                [&](uint32_t k) { return keyrot[k0 + k]; });
+        }
+        if (!dirty) continue;
+        if (c + 16 <= rx_len) {
+            __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(rx + c));
+        } else {
+            const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            for (int b = 0; b < 16; ++b)
+                if (c + b < rx_len) rx[c + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+// ---------------------------------------------------------- k_stream_xor
+__global__ __launch_bounds__(256) void k_stream_xor(uint8_t* __restrict__ d, uint64_t n, uint32_t pat) {
+    const uint64_t base = (uint64_t)blockIdx.x * UNMASK_TILE;
+    u32x4 v[UNMASK_UNROLL];
+#pragma unroll
+    for (int i = 0; i < UNMASK_UNROLL; ++i) {
+        const uint64_t c = base + ((uint64_t)i * 256u + threadIdx.x) * 16u;
+        if (c + 16 <= n) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(d + c));
+    }
+#pragma unroll
+    for (int i = 0; i < UNMASK_UNROLL; ++i) {
+        const uint64_t c = base + ((uint64_t)i * 256u + threadIdx.x) * 16u;
+        if (c + 16 <= n) {
+            v[i].x ^= pat;
+            v[i].y ^= pat;
+            v[i].z ^= pat;
+            v[i].w ^= pat;
+            __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(d + c));
+        }
+    }
+}
+
+// XOR one span with a key and phase (websocket_decode on device).
+__global__ void k_xor_span(uint8_t* __restrict__ d, uint64_t n, uint32_t key, uint32_t phase) {
+    // d is 16-B aligned; byte a uses key byte (a + phase) & 3.
+    const uint32_t kw = rotr32(key, 8u * (phase & 3u));
+    for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16u; c < n;
+         c += (uint64_t)gridDim.x * blockDim.x * 16u) {
+        if (c + 16 <= n) {
+            uint4 v = *reinterpret_cast<const uint4*>(d + c);
+            v.x ^= kw;
+            v.y ^= kw;
+            v.z ^= kw;
+            v.w ^= kw;
+            *reinterpret_cast<uint4*>(d + c) = v;
+        } else {
+            for (uint64_t a = c; a < n; ++a) d[a] ^= (uint8_t)(kw >> (8 * (a & 3u)));
+        }
+    }
+}
+
+// --------------------------------------------------------------- launchers
+
+hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
+                       const dcarry* carry_in, dcarry* carry_out, uint64_t* counts,
+                       const uint64_t* bases, dframes fr, hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    const uint32_t wpb = SCAN_THREADS / 64;
+    uint32_t blocks = (nseg + wpb - 1) / wpb;
+    if (blocks > 65536u) blocks = 65536u;
+    if (emit)
+        hipLaunchKernelGGL(k_scan<true>, dim3(blocks), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg,
+                           carry_in, carry_out, counts, bases, fr);
+    else
+        hipLaunchKernelGGL(k_scan<false>, dim3(blocks), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg,
+                           carry_in, carry_out, counts, bases, fr);
+    return hipGetLastError();
+}
+
+hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
+                             uint64_t ntiles, uint64_t tile, hipStream_t st) {
+    const uint64_t n = ntiles + 1;
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_tile_index, dim3(blocks), dim3(256), 0, st, off, len, nfr, tile_first, ntiles, tile);
+    return hipGetLastError();
+}
+
+hipError_t launch_unmask(uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first, uint64_t nfr,
+                         hipStream_t st) {
+    if (rx_len == 0 || nfr == 0) return hipSuccess;
+    const uint64_t ntiles = (rx_len + UNMASK_TILE - 1) / UNMASK_TILE;
+    hipLaunchKernelGGL(k_unmask, dim3((uint32_t)ntiles), dim3(UNMASK_THREADS), 0, st, rx, rx_len, fr.pay_off,
+                       fr.pay_len, fr.keyrot, tile_first, nfr);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_xor(uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st) {
+    const uint64_t ntiles = (n + UNMASK_TILE - 1) / UNMASK_TILE;
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_stream_xor, dim3((uint32_t)ntiles), dim3(256), 0, st, d, n, pattern);
+    return hipGetLastError();
+}
+
+hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    uint64_t chunks = (n + 15) / 16;
+    uint32_t blocks = (uint32_t)((chunks + 255) / 256);
+    if (blocks > 8192u) blocks = 8192u;
+    hipLaunchKernelGGL(k_xor_span, dim3(blocks), dim3(256), 0, st, d, n, key, phase);
+    return hipGetLastError();
+}
+
+}  // namespace hvws

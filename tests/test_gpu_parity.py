@@ -1,0 +1,256 @@
+"""GPU parity: the product (libhv_amd/libhvws.so, HIP kernels on MI355X)
+against the CPU oracle on the same seeded inputs.  Integer/byte work, so the
+bar is bit-exact everywhere."""
+from __future__ import annotations
+
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import libhv_amd
+import streams as S
+import wsharness as H
+from libhv_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------ reference frame-layer ABI
+@pytest.mark.parametrize("name,data", S.quirk_streams(), ids=[n for n, _ in S.quirk_streams()])
+@pytest.mark.parametrize("mode", ["one", "bytes", "small"])
+@pytest.mark.parametrize("decode", [False, True])
+def test_execute_quirks(name, data, mode, decode):
+    rng = random.Random(hash((name, mode)) & 0xFFFF)
+    if mode == "bytes" and len(data) > 400:
+        mode = "small"
+    chunks = S.rand_chunks(rng, len(data), mode)
+    assert H.run_evlog("gpu", data, chunks, -1, decode) == H.run_evlog("oracle", data, chunks, -1, decode)
+
+
+def test_execute_random_streams():
+    rng = random.Random(1234)
+    for t in range(60):
+        data = S.rand_stream(rng, rng.randint(1, 10), max_len=rng.choice([40, 300, 3000]))
+        mode = "small" if len(data) > 600 else None
+        chunks = S.rand_chunks(rng, len(data), mode)
+        decode = rng.random() < 0.5
+        got = H.run_evlog("gpu", data, chunks, -1, decode)
+        exp = H.run_evlog("oracle", data, chunks, -1, decode)
+        assert got == exp, f"stream {t}"
+
+
+def test_execute_early_return():
+    """A callback returning non-zero stops the parse at the reference's cursor
+    (http/websocket_parser.c:14-32); the caller re-feeds from there."""
+    rng = random.Random(77)
+    for t in range(40):
+        data = S.rand_stream(rng, rng.randint(2, 6), max_len=200)
+        chunks = S.rand_chunks(rng, len(data), "rand")
+        abort_at = rng.randint(0, 12)
+        decode = rng.random() < 0.5
+        assert H.run_evlog("gpu", data, chunks, abort_at, decode) == \
+            H.run_evlog("oracle", data, chunks, abort_at, decode), f"stream {t} abort {abort_at}"
+
+
+def test_decode_helpers():
+    L = libhv_amd.lib()
+    O = H.oracle()
+    rng = random.Random(5)
+    for n in [0, 1, 3, 4, 15, 16, 17, 1000, 65536 + 7]:
+        src = rng.randbytes(n)
+        key = rng.randbytes(4)
+        for ph in range(6):
+            a = ctypes.create_string_buffer(max(n, 1))
+            b = ctypes.create_string_buffer(max(n, 1))
+            ra = L.websocket_decode(a, src, n, key, ph)
+            rb = O.ows_decode(b, src, n, key, ph)
+            assert ra == rb and a.raw[:n] == b.raw[:n]
+
+
+def test_build_frame_matches_reference_layout():
+    L = libhv_amd.lib()
+    rng = random.Random(9)
+    for n in S.EDGE_LENS + [1000, 70000]:
+        data = rng.randbytes(n)
+        key = rng.randbytes(4)
+        for fl in (0x1 | 0x10 | 0x20, 0x2 | 0x20, 0x9 | 0x10, 0x0):
+            buf = ctypes.create_string_buffer(n + 16)
+            m = L.websocket_build_frame(buf, fl, key, data, n)
+            exp = H.build_frames_ref([(fl, data, key)])
+            assert buf.raw[:m] == exp
+            assert L.websocket_calc_frame_size(fl, n) == len(exp)
+
+
+# ----------------------------------------------------- message layer drop-in
+@pytest.mark.parametrize("name,data", S.quirk_streams(), ids=[n for n, _ in S.quirk_streams()])
+def test_messages_quirks(name, data):
+    for mode in ("one", "small"):
+        chunks = S.rand_chunks(random.Random(3), len(data), mode)
+        assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks)
+
+
+def test_messages_known_answers():
+    """SURVEY.md Appendix A, probed with the compiled reference."""
+    q = dict(S.quirk_streams())
+    msgs, _, _, buf = H.run_messages("gpu", q["q5_control_between_fragments"], [1 << 20])
+    assert msgs == [(9, b"ABPING"), (9, b"CD")]
+    msgs, _, _, _ = H.run_messages("gpu", q["q6_lone_continue"], [1 << 20])
+    assert msgs == [(8, b"orphan")]
+    msgs, _, _, buf = H.run_messages("gpu", q["q10_inplace"], [1 << 20])
+    assert buf == bytes.fromhex("81851122334448656c6c6f") and msgs == [(1, b"Hello")]
+    msgs, _, _, _ = H.run_messages("gpu", q["rfc_hello_masked"], [3, 3, 5])
+    assert msgs == [(1, b"Hello")]
+
+
+def test_messages_random_chunked():
+    rng = random.Random(4321)
+    for t in range(25):
+        data = S.rand_stream(rng, rng.randint(1, 12), max_len=rng.choice([100, 5000, 70000]))
+        chunks = S.rand_chunks(rng, len(data), "rand")
+        assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks), f"stream {t}"
+
+
+# ------------------------------------------------------------ batch engine
+def _oracle_batch(buf: np.ndarray, segs, carries):
+    exp = buf.copy()
+    recs, outs, starts = [], [], []
+    for i, (off, n) in enumerate(segs):
+        r, st, started, out = H.scan_segment(buf[off:off + n].tobytes(), carries[i] if carries else None)
+        r = r.copy()
+        r["pay_off"] += np.uint64(off)
+        r["hdr_off"] = np.where(r["hdr_off"] >= 0, r["hdr_off"] + off, -1)
+        recs.append(r)
+        outs.append(st)
+        starts.append(started)
+        exp[off:off + n] = np.frombuffer(out, np.uint8)
+    return np.concatenate(recs) if recs else np.zeros(0, libhv_amd.FRAME_DTYPE), outs, starts, exp
+
+
+def _compare_batch(eng, buf: np.ndarray, segs, carries=None):
+    rx = eng.to_device(buf)
+    eng.step(rx, len(buf), segs, carries)
+    got = rx.download(len(buf))
+    frames = eng.frames()
+    cout, started = eng.carry(len(segs))
+    rx.free()
+    exp_recs, exp_carry, exp_started, exp = _oracle_batch(buf, segs, carries)
+    assert len(frames) == len(exp_recs)
+    for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
+        assert np.array_equal(frames[f], exp_recs[f]), f
+    assert np.array_equal(got, exp)
+    for s in range(len(segs)):
+        assert cout[s].fields() == exp_carry[s].fields(), s
+        assert started[s] == exp_started[s], s
+
+
+def test_batch_segments_with_carry(eng):
+    """Many connections in one batch, each continuing mid-stream (cut at
+    arbitrary bytes, including inside headers) from its carried parser state."""
+    rng = random.Random(99)
+    for trial in range(6):
+        parts, segs, carries = [], [], []
+        at = 0
+        for c in range(rng.randint(1, 40)):
+            data = S.rand_stream(rng, rng.randint(1, 20), max_len=rng.choice([50, 400, 70000]))
+            a = rng.randint(0, len(data))
+            b = rng.randint(a, len(data))
+            # carry-in = oracle state after [0, a)
+            _, st, _, _ = H.scan_segment(data[:a])
+            gap = rng.choice([0, 0, 3, 16])
+            parts.append(bytes(gap))
+            at += gap
+            parts.append(data[a:b])
+            segs.append((at, b - a))
+            carries.append(st)
+            at += b - a
+        buf = np.frombuffer(b"".join(parts), np.uint8).copy()
+        _compare_batch(eng, buf, segs, carries)
+
+
+def test_batch_every_cut_point(eng):
+    """One frame of each header size cut at every byte: segment 1 ends there,
+    segment 2 (same connection, next batch) resumes from its carry."""
+    k = b"\x01\x02\x03\x04"
+    for L in (5, 300, 70000):
+        data = H.build_frames_ref([(2 | 0x10 | 0x20, bytes(range(256)) * (L // 256) + bytes(L % 256), k),
+                                   (1 | 0x10 | 0x20, b"tail", k)])
+        cuts = list(range(0, 20)) + [len(data) // 2, len(data) - 5, len(data) - 1, len(data)]
+        for cut in cuts:
+            _compare_batch(eng, np.frombuffer(data[:cut], np.uint8).copy(), [(0, cut)])
+            _, st, _, _ = H.scan_segment(data[:cut])
+            rest = np.frombuffer(data[cut:], np.uint8).copy()
+            _compare_batch(eng, rest, [(0, len(rest))], [st])
+
+
+def test_batch_empty_and_tiny(eng):
+    _compare_batch(eng, np.zeros(0, np.uint8), [(0, 0)])
+    _compare_batch(eng, np.frombuffer(bytes([0x82]), np.uint8).copy(), [(0, 1)])
+    _compare_batch(eng, np.frombuffer(bytes([0x82, 0x80]), np.uint8).copy(), [(0, 2)])
+    _compare_batch(eng, np.frombuffer(bytes([0x82, 0x00, 0x82, 0x00]), np.uint8).copy(), [(0, 2), (2, 2)])
+
+
+def test_synth_matches_oracle(eng):
+    for plan in (synth.uniform_plan(300, 1024, 5, opcode=1, text=True),
+                 synth.uniform_plan(20, 70000, 6),
+                 synth.mixed_plan(8 << 20, 7, hi=1 << 19)):
+        host = H.synth_cpu(plan)
+        dp = libhv_amd.DevicePlan(eng, plan)
+        rx = eng.alloc(plan.total + 64)
+        eng.synth(rx, plan.total, plan.seed, dp, 0)
+        assert np.array_equal(rx.download(plan.total), host)
+        assert eng.synth(rx, plan.total, plan.seed, dp, 1) == 0
+        assert eng.digest(rx, plan.total) == H.digest_np(host)
+        dp.free()
+        rx.free()
+
+
+@pytest.mark.parametrize("nseg", [1, 7, 256])
+@pytest.mark.parametrize("kind", ["u1k", "u64k", "mixed"])
+def test_batch_configs_small(eng, kind, nseg):
+    plan = {"u1k": lambda: synth.uniform_plan(4000, 1024, 11),
+            "u64k": lambda: synth.uniform_plan(300, 65536, 12),
+            "mixed": lambda: synth.mixed_plan(24 << 20, 13)}[kind]().split(nseg)
+    host = H.synth_cpu(plan)
+    _compare_batch(eng, host, plan.segments)
+
+
+def test_rx_batch_host_roundtrip(eng):
+    plan = synth.mixed_plan(4 << 20, 21, hi=1 << 18).split(5)
+    host = H.synth_cpu(plan)
+    _, _, _, exp = _oracle_batch(host, plan.segments, None)
+    buf = host.copy()
+    eng.rx_batch(buf, plan.segments, None, True)
+    assert np.array_equal(buf, exp)
+
+
+def test_pipeline_host_inclusive(eng):
+    """Chunked H2D -> scan -> unmask -> D2H with the carry chained across chunk
+    boundaries (frames straddle chunks)."""
+    plan = synth.mixed_plan(12 << 20, 31, hi=1 << 19)
+    host = H.synth_cpu(plan)
+    _, _, _, exp = _oracle_batch(host, [(0, plan.total)], None)
+    L = libhv_amd.lib()
+    pinned = L.hvws_host_alloc(eng.ctx, plan.total)
+    try:
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * plan.total).from_address(pinned))
+        arr[:] = host
+        carry = libhv_amd.WsParser()
+        L.websocket_parser_init(ctypes.byref(carry))
+        rc = L.hvws_pipeline(eng.ctx, pinned, plan.total, 1 << 20, ctypes.byref(carry))
+        assert rc == 0, L.hvws_last_error()
+        assert np.array_equal(arr, exp)
+        assert carry.state == 0
+    finally:
+        L.hvws_host_free(eng.ctx, pinned)
+
+
+def test_stream_xor_roundtrip(eng):
+    rng = np.random.default_rng(1)
+    a = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    b = eng.to_device(a)
+    eng.stream_xor(b, len(a), 0xA5A5A5A5)
+    x = b.download(len(a))
+    assert np.array_equal(x, a ^ np.uint8(0xA5))
+    b.free()
