@@ -99,8 +99,9 @@ def cpu_baseline(sample: np.ndarray, seconds: float, threads: int):
     return payload * sum(counts) / dt / 2**30, kind, passes, payload * sum(counts)
 
 
-def main():
-    args = parse()
+def init_dist():
+    """(rank, world, local_rank, dist-or-None).  One process per GPU; gloo
+    carries only the barrier and the timing reduction (no data collectives)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -110,6 +111,29 @@ def main():
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    return rank, world, local, dist
+
+
+def rank_plan(cfg: str, rank: int, segments: int):
+    """This rank's disjoint batch: same shape on every rank, distinct seed."""
+    from libhv_amd import synth
+
+    return synth.config_plan(cfg, seed=1000 + rank).split(segments)
+
+
+def max_over_ranks(dist, seconds: float) -> float:
+    if dist is None:
+        return seconds
+    import torch
+
+    t = torch.tensor([seconds], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def main():
+    args = parse()
+    rank, world, local, dist = init_dist()
     import torch
 
     import libhv_amd
@@ -125,7 +149,7 @@ def main():
     desc, cfg = CONFIGS[args.config]
     eng = libhv_amd.Engine(local)
     t = time.perf_counter()
-    plan = synth.config_plan(cfg, seed=1000 + rank).split(args.segments)
+    plan = rank_plan(cfg, rank, args.segments)
     dp = libhv_amd.DevicePlan(eng, plan)
     rx = eng.alloc(plan.total + 64)
     eng.synth(rx, plan.total, plan.seed, dp, 0)
@@ -147,11 +171,7 @@ def main():
         scan_ms.append(s_ms)
         unmask_ms.append(u_ms)
     barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
 
     # Correctness after the timed region: an odd number of passes leaves the
     # payload unmasked, an even number masked again (XOR is an involution).

@@ -70,7 +70,7 @@ def quirk_streams() -> List[Tuple[str, bytes]]:
          B([(1 | MASK, b"AB", k), (9 | FIN | MASK, b"PING", k), (0 | FIN | MASK, b"CD", k)])),
         ("q6_lone_continue", B([(0 | FIN | MASK, b"orphan", k)])),
         ("q7_zero_length", B([(1 | FIN | MASK, b"", k), (2 | FIN, b"", None), (2 | FIN | MASK, b"x", k)])),
-        ("q10_inplace", bytes.fromhex("818511223344") + bytes(a ^ b for a, b in zip(b"Hello", bytes.fromhex("11223344")))),
+        ("q10_inplace", bytes.fromhex("818511223344") + bytes(a ^ b for a, b in zip(b"Hello", bytes.fromhex("1122334411")))),
         ("q14_unmasked_after_masked", B([(1 | FIN | MASK, b"one", k), (2 | FIN, b"two", None), (1 | FIN, b"", None)])),
         ("fragments", B([(1 | MASK, b"He", k), (0 | MASK, b"ll", k), (0 | FIN | MASK, b"o!", k)])),
         ("zero_key", B([(2 | FIN | MASK, b"\x00" * 40, b"\x00\x00\x00\x00")])),

@@ -1,0 +1,53 @@
+"""CPU, world_size 2 over gloo: the multi-GPU control path of bench.py
+(one process per GPU, disjoint batches, barrier + max-over-ranks timing, no
+data-path collective)."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import bench
+
+    r, w, local, dist = bench.init_dist()
+    plan = bench.rank_plan("c1", r, 8)
+    dist.barrier()
+    t = bench.max_over_ranks(dist, 1.0 + r)
+    q.put((r, w, local, t, int(plan.mask[:16].astype(np.uint64).sum()), plan.total, len(plan.segments)))
+    dist.destroy_process_group()
+
+
+def test_two_ranks_gloo():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o[0] for o in out] == [0, 1] and all(o[1] == 2 for o in out)
+    assert all(o[3] == 2.0 for o in out)              # max over ranks
+    assert out[0][4] != out[1][4]                      # disjoint batches (distinct seeds)
+    assert out[0][5] == out[1][5] and out[0][6] == 8   # same shape per rank

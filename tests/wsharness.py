@@ -174,8 +174,8 @@ def run_messages(impl: str, data: bytes, chunks: Sequence[int]):
 
         L = libhv_amd.lib()
         h = L.hvws_wsp_new()
-        L.hvws_wsp_set_sink(h, libhv_amd.MSG_CB(sink._on), None)
-        sink._keep = L  # noqa
+        sink.gpu_cb = libhv_amd.MSG_CB(sink._on)   # keep the thunk alive while the handle may call it
+        L.hvws_wsp_set_sink(h, sink.gpu_cb, None)
         feed = lambda p, n: L.hvws_wsp_feed(h, p, n)
         state = lambda: L.hvws_wsp_state(h, st)
         free = lambda: L.hvws_wsp_free(h)
