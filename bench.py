@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--host-gib", type=float, default=4.0, help="host-inclusive sample size (0: skip)")
-    ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--sweep-unmask", action="store_true",
+                    help="rank 0: time every k_unmask geometry on the same batch (design record)")
     return ap.parse_args()
 
 
@@ -198,6 +199,20 @@ def main():
         ceiling = 2 * (plan.total & ~15) * reps / (time.perf_counter() - t) / 1e9
         extra["stream_ceiling_GBps"] = round(ceiling, 1)
         extra["scan_ms_mean"] = round(float(np.mean(scan_ms)), 3)
+        if args.sweep_unmask:
+            L = libhv_amd.lib()
+            sweep = {}
+            for v in range(16):
+                if L.hvws_set_unmask_variant(v) != 0:
+                    break
+                ts = []
+                for _ in range(4):
+                    eng.step(rx, plan.total, segs)
+                    ts.append(eng.last_times()[1])
+                name = L.hvws_unmask_kernel_name().decode()
+                sweep[name] = round(alg_bytes / (float(np.median(ts[1:])) * 1e-3) / 1e9, 1)
+            L.hvws_set_unmask_variant(0)
+            extra["unmask_sweep_GBps"] = sweep
         extra["unmask_ms_mean"] = round(mean_unmask, 3)
 
         # host-inclusive: pinned host rx -> device -> scan+unmask -> host
@@ -269,7 +284,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_unmask",
+                "kernel": libhv_amd.lib().hvws_unmask_kernel_name().decode(),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

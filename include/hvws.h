@@ -112,6 +112,11 @@ int     hvws_get_carry(hvws_ctx* ctx, websocket_parser* out, int* started);
  * out[1] = unmask kernel. */
 int hvws_last_times(hvws_ctx* ctx, float out[2]);
 
+/* Name of the k_unmask geometry in use (e.g. "k_unmask<256,8,xcd>"). */
+const char* hvws_unmask_kernel_name(void);
+/* Select another k_unmask geometry for later scans (tuning; process-wide). */
+int hvws_set_unmask_variant(int variant);
+
 /* STREAM-style in-place ceiling: d[i] ^= pattern over n bytes (16-B aligned). */
 int hvws_stream_xor(hvws_ctx* ctx, uint8_t* d, uint64_t n, uint32_t pattern);
 

@@ -128,6 +128,8 @@ _SIGS = {
     "hvws_wsp_feed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "hvws_wsp_state": (None, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_thread_device": (ctypes.c_int, [ctypes.c_int]),
+    "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
+    "hvws_set_unmask_variant": (ctypes.c_int, [ctypes.c_int]),
     # reference ABI (include/websocket_parser.h, include/wsdef.h)
     "websocket_parser_init": (None, [ctypes.c_void_p]),
     "websocket_parser_settings_init": (None, [ctypes.c_void_p]),

@@ -106,6 +106,7 @@ struct hvws_ctx {
     bool have_scan = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ev_unmask = false;
+    int variant = 0;   // k_unmask geometry the tile index was built for
 };
 
 namespace {
@@ -191,10 +192,12 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     HIP_OR(launch_scan(true, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
                        c->bases.as<uint64_t>(), frames_of(c), c->stream),
            HVWS_EHIP);
-    const uint64_t ntiles = (rx_len + UNMASK_TILE - 1) / UNMASK_TILE;
+    c->variant = unmask_variant();
+    const uint64_t tile = unmask_tile(c->variant);
+    const uint64_t ntiles = (rx_len + tile - 1) / tile;
     HIP_OR(c->tile_first.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
     HIP_OR(launch_tile_index(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), nfr, c->tile_first.as<uint32_t>(),
-                             ntiles, UNMASK_TILE, c->stream),
+                             ntiles, tile, c->stream),
            HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
     c->nseg = nseg;
@@ -392,7 +395,8 @@ int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     if (d_rx != c->rx || rx_len != c->rx_len)
         return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
     HIP_OR(hipEventRecord(c->ev[2], c->stream), HVWS_EHIP);
-    HIP_OR(launch_unmask(d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(), c->nfr, c->stream), HVWS_EHIP);
+    HIP_OR(launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(), c->nfr, c->stream),
+           HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[3], c->stream), HVWS_EHIP);
     c->ev_unmask = true;
     return HVWS_OK;
@@ -493,7 +497,7 @@ int hvws_stream_xor(hvws_ctx* c, uint8_t* d, uint64_t n, uint32_t pattern) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (((uintptr_t)d & 15u) != 0) return set_err(HVWS_EINVAL, "buffer must be 16-byte aligned");
-    HIP_OR(launch_stream_xor(d, n, pattern, c->stream), HVWS_EHIP);
+    HIP_OR(launch_stream_xor(unmask_variant(), d, n, pattern, c->stream), HVWS_EHIP);
     return HVWS_OK;
 }
 
@@ -648,6 +652,14 @@ int hvws_digest(hvws_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* out) 
     HIP_OR(hipMemcpyAsync(&v, c->synth_bad.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (out) *out = v;
+    return HVWS_OK;
+}
+
+const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant()); }
+
+int hvws_set_unmask_variant(int v) {
+    if (set_unmask_variant(v) < 0) return set_err(HVWS_EINVAL, "unmask variant %d out of range [0,%d)", v,
+                                                  unmask_variant_count());
     return HVWS_OK;
 }
 

@@ -44,9 +44,6 @@ struct dframes {
 
 constexpr int SCAN_THREADS = 256;           // 4 waves, one segment per wave
 constexpr int SCAN_U = 4;                   // predicted frames per lane per round
-constexpr int UNMASK_THREADS = 256;
-constexpr int UNMASK_UNROLL = 8;            // 16-B chunks per thread per tile
-constexpr uint64_t UNMASK_TILE = (uint64_t)UNMASK_THREADS * 16u * UNMASK_UNROLL;  // 32 KiB
 constexpr int UNMASK_MAXF = 512;            // frames staged in LDS per tile
 
 // Kernel launchers (hvws_kernels.hip).
@@ -57,9 +54,15 @@ hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg
                           hipStream_t st);
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
                              uint64_t ntiles, uint64_t tile, hipStream_t st);
-hipError_t launch_unmask(uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
+// k_unmask geometry variants (threads x chunks/thread, XCD-ordered tiles)
+int unmask_variant();                      // process default ($HVWS_UNMASK or 0)
+int set_unmask_variant(int v);             // -1 if out of range
+int unmask_variant_count();
+uint64_t unmask_tile(int variant);         // bytes per workgroup tile
+const char* unmask_name(int variant);
+hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
                          uint64_t nfr, hipStream_t st);
-hipError_t launch_stream_xor(uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
+hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
 hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st);
 
 // Synthetic data (hvws_synth.hip).

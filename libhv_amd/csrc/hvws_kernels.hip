@@ -16,6 +16,9 @@
 //
 // All work is integer; there is no contraction, so no MFMA.  The unmask is
 // HBM-bound: 2 x payload + headers bytes per pass.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "hvws_internal.h"
 
 namespace hvws {
@@ -461,22 +464,22 @@ __global__ void k_tile_index(const uint64_t* __restrict__ off, const uint64_t* _
 
 // -------------------------------------------------------------- k_unmask
 //
-// One workgroup per 32 KiB tile.  Each thread owns 8 16-byte chunks spaced
-// 4 KiB apart (lane-contiguous, so every wave instruction moves 1 KiB).  Data
-// loads are issued first; meanwhile the tile's frames (from the tile index)
-// are staged in LDS as [pay_off, pay_end, key].  A chunk wholly inside one
-// masked payload is XORed with 4 copies of that frame's aligned key word; a
-// chunk touching a header or a frame boundary is merged byte by byte; chunks
-// with no masked byte are not written back.
+// One workgroup per tile of T*U*16 bytes.  Each thread owns U 16-byte chunks
+// spaced T*16 bytes apart (so every wave instruction moves 1 KiB of
+// contiguous bytes).  Geometry from the on-device sweep (scripts/membench2.hip,
+// profiles/): the bounds check is hoisted to the tile so the U loads issue
+// back to back (a per-chunk check makes hipcc wait vmcnt(0) after each), and
+// the tile order is XCD-contiguous -- blocks b, b+8, b+16, ... (which the
+// dispatcher places on one XCD) walk adjacent tiles -- worth 5-8 % of HBM
+// throughput on in-place read+write streams.  Data loads are issued first;
+// meanwhile the tile's frames (from the tile index) are staged in LDS as
+// [pay_off, pay_end, key word].  A chunk wholly inside one masked payload is
+// XORed with 4 copies of that frame's aligned key word; a chunk touching a
+// header or a frame boundary is merged byte by byte; chunks with no masked
+// byte are not written back.
 
-struct tile_frames {
-    const uint64_t* off;
-    const uint64_t* end;
-    const uint32_t* key;
-};
-
-template <typename OFF, typename END>
-__device__ __forceinline__ uint32_t first_end_after(OFF, END endf, uint32_t n, uint64_t c) {
+template <typename END>
+__device__ __forceinline__ uint32_t first_end_after(END endf, uint32_t n, uint64_t c) {
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
         uint32_t mid = (lo + hi) >> 1;
@@ -488,53 +491,66 @@ __device__ __forceinline__ uint32_t first_end_after(OFF, END endf, uint32_t n, u
 
 template <typename OFF, typename END, typename KEY>
 __device__ __forceinline__ bool xor_chunk(u32x4& v, uint64_t c, uint32_t nf, OFF offf, END endf, KEY keyf) {
-    uint32_t k = first_end_after(offf, endf, nf, c);
+    uint32_t k = first_end_after(endf, nf, c);
     if (k >= nf) return false;
     const uint64_t o = offf(k), e = endf(k);
     if (o >= c + 16) return false;               // only header/gap bytes here
     if (o <= c && c + 16 <= e) {                 // fast path: one payload
         const uint32_t kw = keyf(k);
-        v.x ^= kw;
-        v.y ^= kw;
-        v.z ^= kw;
-        v.w ^= kw;
+        v ^= u32x4{kw, kw, kw, kw};
         return true;
     }
-    uint32_t m[4] = {0u, 0u, 0u, 0u};
+    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
         const uint64_t a = c + (uint64_t)b;
         while (k < nf && endf(k) <= a) ++k;
-        if (k < nf && offf(k) <= a) m[b >> 2] |= ((keyf(k) >> (8 * (b & 3))) & 0xFFu) << (8 * (b & 3));
+        if (k < nf && offf(k) <= a) {
+            const uint32_t kb = ((keyf(k) >> (8 * (b & 3))) & 0xFFu) << (8 * (b & 3));
+            if (b < 4) m0 |= kb;
+            else if (b < 8) m1 |= kb;
+            else if (b < 12) m2 |= kb;
+            else m3 |= kb;
+        }
     }
-    v.x ^= m[0];
-    v.y ^= m[1];
-    v.z ^= m[2];
-    v.w ^= m[3];
+    v ^= u32x4{m0, m1, m2, m3};
     return true;
 }
 
-__global__ __launch_bounds__(UNMASK_THREADS) void k_unmask(uint8_t* __restrict__ rx, uint64_t rx_len,
-                                                           const uint64_t* __restrict__ pay_off,
-                                                           const uint64_t* __restrict__ pay_len,
-                                                           const uint32_t* __restrict__ keyrot,
-                                                           const uint32_t* __restrict__ tile_first,
-                                                           uint64_t nfr) {
+// Bijective XCD-contiguous tile order (cdna_hip_programming.md sec. 5, "XCD
+// swizzle must be bijective").  Placement only changes speed, never results.
+__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
+    const uint64_t q = ntiles >> 3, r = ntiles & 7u, x = b & 7u, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+template <int T, int U, bool SWZ>
+__global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t rx_len,
+                                              const uint64_t* __restrict__ pay_off,
+                                              const uint64_t* __restrict__ pay_len,
+                                              const uint32_t* __restrict__ keyrot,
+                                              const uint32_t* __restrict__ tile_first, uint64_t nfr,
+                                              uint64_t ntiles) {
+    constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     __shared__ uint64_t s_off[UNMASK_MAXF];
     __shared__ uint64_t s_end[UNMASK_MAXF];
     __shared__ uint32_t s_key[UNMASK_MAXF];
 
-    const uint64_t t = blockIdx.x;
-    const uint64_t base = t * UNMASK_TILE;
+    const uint64_t t = SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x;
+    const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
+    const bool full = base + TILE <= rx_len;
 
-    u32x4 v[UNMASK_UNROLL];
+    u32x4 v[U];
+    if (full) {
 #pragma unroll
-    for (int i = 0; i < UNMASK_UNROLL; ++i) {
-        const uint64_t c = base + ((uint64_t)i * UNMASK_THREADS + tid) * 16u;
-        if (c + 16 <= rx_len) {
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rx + c));
-        } else {
+        for (int i = 0; i < U; ++i)
+            v[i] = __builtin_nontemporal_load(
+                reinterpret_cast<const u32x4*>(rx + base + ((uint64_t)i * T + tid) * 16u));
+    } else {
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
             uint32_t w[4] = {0u, 0u, 0u, 0u};
             for (int b = 0; b < 16; ++b)
                 if (c + b < rx_len) w[b >> 2] |= (uint32_t)rx[c + b] << (8 * (b & 3));
@@ -547,9 +563,8 @@ __global__ __launch_bounds__(UNMASK_THREADS) void k_unmask(uint8_t* __restrict__
     const uint32_t k1 = (uint64_t)k1r + 1 < nfr ? k1r + 1 : (uint32_t)nfr;
     const uint32_t nf = k1 > k0 ? k1 - k0 : 0u;
     const bool staged = nf <= (uint32_t)UNMASK_MAXF;
-
     if (staged) {
-        for (uint32_t i = tid; i < nf; i += UNMASK_THREADS) {
+        for (uint32_t i = tid; i < nf; i += T) {
             const uint64_t o = pay_off[k0 + i];
             const uint32_t kw = keyrot[k0 + i];
             s_off[i] = o;
@@ -562,25 +577,35 @@ __global__ __launch_bounds__(UNMASK_THREADS) void k_unmask(uint8_t* __restrict__
     }
     __syncthreads();
 
+    bool dirty[U];
 #pragma unroll
-    for (int i = 0; i < UNMASK_UNROLL; ++i) {
-        const uint64_t c = base + ((uint64_t)i * UNMASK_THREADS + tid) * 16u;
-        if (c >= rx_len) continue;
-        bool dirty;
+    for (int i = 0; i < U; ++i) {
+        const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+        if (!full && c >= rx_len) {
+            dirty[i] = false;
+            continue;
+        }
         if (staged) {
-            dirty = xor_chunk(
+            dirty[i] = xor_chunk(
                 v[i], c, nf, [&](uint32_t k) { return s_off[k]; }, [&](uint32_t k) { return s_end[k]; },
                 [&](uint32_t k) { return s_key[k]; });
         } else {
-            dirty = xor_chunk(
+            dirty[i] = xor_chunk(
                 v[i], c, nf, [&](uint32_t k) { return pay_off[k0 + k]; },
                 [&](uint32_t k) { return keyrot[k0 + k] ? pay_off[k0 + k] + pay_len[k0 + k] : pay_off[k0 + k]; },
                 [&](uint32_t k) { return keyrot[k0 + k]; });
         }
-        if (!dirty) continue;
-        if (c + 16 <= rx_len) {
-            __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(rx + c));
-        } else {
+    }
+    if (full) {
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            if (dirty[i])
+                __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(rx + base + ((uint64_t)i * T + tid) * 16u));
+    } else {
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            if (!dirty[i]) continue;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
             const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
             for (int b = 0; b < 16; ++b)
                 if (c + b < rx_len) rx[c + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
@@ -589,23 +614,26 @@ __global__ __launch_bounds__(UNMASK_THREADS) void k_unmask(uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------- k_stream_xor
-__global__ __launch_bounds__(256) void k_stream_xor(uint8_t* __restrict__ d, uint64_t n, uint32_t pat) {
-    const uint64_t base = (uint64_t)blockIdx.x * UNMASK_TILE;
-    u32x4 v[UNMASK_UNROLL];
+// The same geometry with no frame table: the measured in-place ceiling.
+template <int T, int U, bool SWZ>
+__global__ __launch_bounds__(T) void k_stream_xor(uint8_t* __restrict__ d, uint64_t n, uint64_t ntiles, uint32_t pat) {
+    constexpr uint64_t TILE = (uint64_t)T * U * 16u;
+    const uint64_t t = SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x;
+    const uint64_t base = t * TILE;
+    if (base + TILE <= n) {
+        u32x4 v[U];
 #pragma unroll
-    for (int i = 0; i < UNMASK_UNROLL; ++i) {
-        const uint64_t c = base + ((uint64_t)i * 256u + threadIdx.x) * 16u;
-        if (c + 16 <= n) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(d + c));
-    }
+        for (int i = 0; i < U; ++i)
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(d + base + ((uint64_t)i * T + threadIdx.x) * 16u));
 #pragma unroll
-    for (int i = 0; i < UNMASK_UNROLL; ++i) {
-        const uint64_t c = base + ((uint64_t)i * 256u + threadIdx.x) * 16u;
-        if (c + 16 <= n) {
-            v[i].x ^= pat;
-            v[i].y ^= pat;
-            v[i].z ^= pat;
-            v[i].w ^= pat;
-            __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(d + c));
+        for (int i = 0; i < U; ++i)
+            __builtin_nontemporal_store(v[i] ^ u32x4{pat, pat, pat, pat},
+                                        reinterpret_cast<u32x4*>(d + base + ((uint64_t)i * T + threadIdx.x) * 16u));
+    } else {
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * T + threadIdx.x) * 16u;
+            for (int b = 0; b < 16; ++b)
+                if (c + b < n) d[c + b] ^= (uint8_t)(pat >> (8 * (b & 3)));
         }
     }
 }
@@ -661,19 +689,84 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_unmask(uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first, uint64_t nfr,
-                         hipStream_t st) {
+// Unmask geometries (threads, chunks per thread, XCD order).  Default from the
+// on-device sweep; HVWS_UNMASK=<index> selects another for experiments.
+struct unmask_geom {
+    int threads, unroll;
+    bool swz;
+};
+// X(index, threads, chunks per thread, XCD order); index 0 is the default.
+#define HVWS_UNMASK_GEOMS(X)                                                              \
+    X(0, 256, 2, true)                                                                    \
+    X(1, 128, 2, true)                                                                    \
+    X(2, 512, 1, true)                                                                    \
+    X(3, 128, 4, true)                                                                    \
+    X(4, 1024, 1, true)                                                                   \
+    X(5, 256, 4, true)                                                                    \
+    X(6, 256, 8, true)                                                                    \
+    X(7, 256, 8, false)                                                                   \
+    X(8, 64, 8, true)
+#define HVWS_GEOM_ENTRY(i, t, u, s) {t, u, s},
+static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
+static int g_geom = -1;
+
+int unmask_variant() {
+    if (g_geom < 0) {
+        const char* e = getenv("HVWS_UNMASK");
+        int v = e ? atoi(e) : 0;
+        if (v < 0 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) v = 0;
+        g_geom = v;
+    }
+    return g_geom;
+}
+
+int set_unmask_variant(int v) {
+    if (v < 0 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) return -1;
+    g_geom = v;
+    return v;
+}
+
+int unmask_variant_count() { return (int)(sizeof(kGeoms) / sizeof(kGeoms[0])); }
+
+uint64_t unmask_tile(int variant) {
+    const unmask_geom& g = kGeoms[variant];
+    return (uint64_t)g.threads * g.unroll * 16u;
+}
+
+const char* unmask_name(int variant) {
+    static char buf[16][48];
+    const unmask_geom& g = kGeoms[variant];
+    snprintf(buf[variant & 15], sizeof(buf[0]), "k_unmask<%d,%d,%s>", g.threads, g.unroll, g.swz ? "xcd" : "linear");
+    return buf[variant & 15];
+}
+
+#define HVWS_GEOM_CASE(i, t, u, s) \
+    case i: hipLaunchKernelGGL((HVWS_K<t, u, s>), HVWS_ARGS); break;
+hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
+                         uint64_t nfr, hipStream_t st) {
     if (rx_len == 0 || nfr == 0) return hipSuccess;
-    const uint64_t ntiles = (rx_len + UNMASK_TILE - 1) / UNMASK_TILE;
-    hipLaunchKernelGGL(k_unmask, dim3((uint32_t)ntiles), dim3(UNMASK_THREADS), 0, st, rx, rx_len, fr.pay_off,
-                       fr.pay_len, fr.keyrot, tile_first, nfr);
+    const uint64_t tile = unmask_tile(variant);
+    const uint64_t ntiles = (rx_len + tile - 1) / tile;
+    const int threads = kGeoms[variant].threads;
+#define HVWS_K k_unmask
+#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, fr.keyrot, \
+                  tile_first, nfr, ntiles
+    switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
+#undef HVWS_K
+#undef HVWS_ARGS
     return hipGetLastError();
 }
 
-hipError_t launch_stream_xor(uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st) {
-    const uint64_t ntiles = (n + UNMASK_TILE - 1) / UNMASK_TILE;
+hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st) {
+    const uint64_t tile = unmask_tile(variant);
+    const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_stream_xor, dim3((uint32_t)ntiles), dim3(256), 0, st, d, n, pattern);
+    const int threads = kGeoms[variant].threads;
+#define HVWS_K k_stream_xor
+#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, d, n, ntiles, pattern
+    switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
+#undef HVWS_K
+#undef HVWS_ARGS
     return hipGetLastError();
 }
 
