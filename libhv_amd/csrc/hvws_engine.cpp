@@ -90,6 +90,7 @@ struct hvws_ctx {
     hipStream_t copy_out = nullptr;  // pipeline D2H
     // per-batch tables
     dbuf segs, carry_in, carry_out, counts, bases, total;
+    dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total;
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first;
     uint64_t frame_cap = 0;
@@ -174,14 +175,24 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     HIP_OR(c->carry_out.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
     HIP_OR(c->h_total.ensure(8), HVWS_ENOMEM);
     HIP_OR(ensure_frames(c, 1), HVWS_ENOMEM);
+    HIP_OR(c->sc_mid.ensure((uint64_t)nseg * sizeof(dmid) + 64), HVWS_ENOMEM);
+    HIP_OR(c->sc_npred.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->sc_pbase.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->sc_fail.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->sc_masked.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->sc_total.ensure(8), HVWS_ENOMEM);
+    scan_scratch sc;
+    sc.mid = c->sc_mid.as<dmid>();
+    sc.npred = c->sc_npred.as<uint64_t>();
+    sc.pbase = c->sc_pbase.as<uint64_t>();
+    sc.first_fail = c->sc_fail.as<uint64_t>();
+    sc.last_masked = c->sc_masked.as<uint64_t>();
+    sc.total_pred = c->sc_total.as<uint64_t>();
     const dseg* segs = c->segs.as<dseg>();
     const dcarry* cin = c->carry_in.as<dcarry>();
     HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
     HIP_OR(launch_scan(false, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                       nullptr, frames_of(c), c->stream),
-           HVWS_EHIP);
-    HIP_OR(launch_offsets(c->counts.as<uint64_t>(), c->bases.as<uint64_t>(), nseg, c->total.as<uint64_t>(),
-                          c->stream),
+                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->stream),
            HVWS_EHIP);
     HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
@@ -190,7 +201,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                                              (unsigned long long)nfr);
     HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
     HIP_OR(launch_scan(true, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                       c->bases.as<uint64_t>(), frames_of(c), c->stream),
+                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->stream),
            HVWS_EHIP);
     c->variant = unmask_variant();
     const uint64_t tile = unmask_tile(c->variant);
@@ -297,6 +308,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    for (dbuf* b : {&c->sc_mid, &c->sc_npred, &c->sc_pbase, &c->sc_fail, &c->sc_masked, &c->sc_total})
+        b->release();
     for (dbuf* b : {&c->segs, &c->carry_in, &c->carry_out, &c->counts, &c->bases, &c->total, &c->f_hdr, &c->f_off,
                     &c->f_len, &c->f_length, &c->f_key, &c->f_keyrot, &c->f_info, &c->tile_first, &c->stage,
                     &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad})

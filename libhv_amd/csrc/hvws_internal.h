@@ -26,6 +26,15 @@ struct dcarry {
     uint32_t pad;
 };
 
+// Per-segment state between the discovery kernels (k_head -> k_verify -> k_walk).
+struct dmid {
+    dcarry   st;       // parser state after the carried-in frame
+    uint64_t pos;      // segment offset of the first whole frame
+    uint64_t stride;   // its size (speculation stride), 0 if none
+    uint64_t n_a;      // frames recorded before pos (0 or 1)
+    uint64_t pad;
+};
+
 struct dseg {
     uint64_t off;
     uint64_t len;
@@ -46,10 +55,21 @@ constexpr int SCAN_THREADS = 256;           // 4 waves, one segment per wave
 constexpr int SCAN_U = 4;                   // predicted frames per lane per round
 constexpr int UNMASK_MAXF = 512;            // frames staged in LDS per tile
 
+struct scan_scratch {   // per-segment arrays (nseg entries) + one total
+    dmid*     mid;
+    uint64_t* npred;
+    uint64_t* pbase;
+    uint64_t* first_fail;
+    uint64_t* last_masked;   // 1 + index of the last masked verified frame, 0 none
+    uint64_t* total_pred;
+};
+
 // Kernel launchers (hvws_kernels.hip).
+// COUNT pass (emit=false): counts[], bases[] (exclusive scan) and *total.
+// EMIT pass: frame table at bases[], carry_out[].
 hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
-                       const dcarry* carry_in, dcarry* carry_out, uint64_t* counts,
-                       const uint64_t* bases, dframes fr, hipStream_t st);
+                       const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
+                       uint64_t* total, scan_scratch sc, dframes fr, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,

@@ -261,61 +261,209 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
     return have;
 }
 
-// ---------------------------------------------------------------- k_scan
+// ----------------------------------------------------------------- k_head
 //
-// One wavefront per segment.  After finishing any carried-in frame, the wave
-// walks whole frames speculatively: with stride s (bytes of the last frame),
-// lane l predicts frames j = u*64 + l at pos + j*s, parses each predicted
-// header from HBM (all 64*SCAN_U loads in flight at once), and a ballot finds
-// the first prediction whose parsed size breaks the chain.  Every prediction
-// before it is a verified frame (induction from the known header at pos), so
-// uniform streams advance 256 frames per HBM round trip and mixed ones at
-// least one.  COUNT mode only counts; EMIT mode writes the frame table at
-// bases[segment].
+// Discovery runs in three kernels per pass (COUNT, then EMIT):
+//   k_head    one wavefront per segment: finish the frame carried in from the
+//             previous batch (exact byte state machine), then parse the first
+//             whole frame; its size is the speculation stride.  Long segments
+//             (>= SPEC_MIN predicted frames) are handed to k_verify.
+//   k_verify  the whole grid checks the predicted headers of every long
+//             segment at pos + j*stride in parallel (first break per segment
+//             by atomicMin); every prediction before the first break is a
+//             true frame by induction from the known header at pos, so a
+//             uniform stream is verified in one parallel pass whatever its
+//             length.  EMIT writes those frames.
+//   k_walk    one wavefront per segment continues after the verified prefix
+//             with a wave-wide speculative walk (64 x SCAN_U predictions per
+//             HBM round trip, broken chains re-predicted from the true size),
+//             then the exact state machine for the frame cut by the segment
+//             end.  Mixed-size streams advance >= 1 frame per round trip.
+
+constexpr uint64_t SPEC_MIN = 256;   // predicted frames that make a segment "long"
+
+__device__ __forceinline__ bool parse_at(const uint8_t* rx, uint64_t rx_len, uint64_t seg_off, uint64_t L,
+                                         uint64_t q, hdr& h) {
+    // true when the frame at segment offset q is whole inside [0, L)
+    if (q >= L || L - q < 2) return false;
+    uint64_t lo, hi;
+    ld16(rx, rx_len, seg_off + q, lo, hi);
+    h = parse_hdr(lo, hi);
+    const uint64_t rq = L - q;
+    return h.hlen <= rq && h.length <= rq - h.hlen;
+}
+
+__device__ __forceinline__ void whole_frame_rec(frec& v, uint64_t q, const hdr& h) {
+    v.hdr_off = (int64_t)q;
+    v.pay_off = q + h.hlen;
+    v.pay_len = h.length;
+    v.length = h.length;
+    v.key = h.key;
+    v.info = h.flags | I_HDR | I_START | I_END | (h.length ? I_BODY : 0u);
+}
 
 template <bool EMIT>
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict__ rx, uint64_t rx_len,
+__global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                        const dseg* __restrict__ segs, uint32_t nseg,
-                                                       const dcarry* __restrict__ carry_in,
-                                                       dcarry* __restrict__ carry_out,
-                                                       uint64_t* __restrict__ counts,
+                                                       const dcarry* __restrict__ carry_in, dmid* __restrict__ mid,
+                                                       uint64_t* __restrict__ npred, uint64_t* __restrict__ first_fail,
+                                                       uint64_t* __restrict__ last_masked,
                                                        const uint64_t* __restrict__ bases, dframes fr) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t waves_per_block = SCAN_THREADS / 64;
-    const uint32_t gw = blockIdx.x * waves_per_block + (threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * waves_per_block;
+    const uint32_t wpb = SCAN_THREADS / 64;
+    for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
+        const uint64_t sb = segs[s].off, L = segs[s].len;
+        dcarry st = carry_in[s];
+        st.started = 0;
+        uint64_t pos = 0, n = 0;
+        frec r;
+        if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, r)) {
+            if (EMIT && lane == 0) store_frame(fr, bases[s], sb, r);
+            ++n;
+        }
+        uint64_t stride = 0, np = 0;
+        hdr h;
+        if (st.state == S_START && parse_at(rx, rx_len, sb, L, pos, h)) {
+            stride = (uint64_t)h.hlen + h.length;
+            const uint64_t cnt = (L - pos) / stride;
+            if (cnt >= SPEC_MIN) np = cnt;
+        }
+        if (lane == 0) {
+            dmid m;
+            m.st = st;
+            m.pos = pos;
+            m.stride = stride;
+            m.n_a = n;
+            m.pad = 0;
+            mid[s] = m;
+            npred[s] = np;
+            if (!EMIT) first_fail[s] = np;
+            else last_masked[s] = 0;
+        }
+    }
+}
+
+// --------------------------------------------------------------- k_verify
+template <bool EMIT>
+__global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                const dseg* __restrict__ segs, uint32_t nseg,
+                                                const dmid* __restrict__ mid, const uint64_t* __restrict__ pbase,
+                                                const uint64_t* __restrict__ total_pred,
+                                                uint64_t* __restrict__ first_fail,
+                                                uint64_t* __restrict__ last_masked,
+                                                const uint64_t* __restrict__ bases, dframes fr) {
+    const uint64_t total = *total_pred;
+    if (total == 0) return;
+    const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+    const uint64_t g0 = (uint64_t)blockIdx.x * per;
+    const uint64_t g1 = g0 + per < total ? g0 + per : total;
+    if (g0 >= g1) return;
+    // segment holding g0: last s with pbase[s] <= g0 (pbase is non-decreasing)
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (pbase[m] <= g0) lo = m;
+        else hi = m;
+    }
+    uint32_t s = lo;
+    // EMIT tracks the last masked verified frame per segment; it is flushed
+    // with one atomic per wave (a per-frame atomic on one word serialises
+    // the whole grid: 1M frames took 12 ms that way).
+    uint32_t ms = s;
+    uint64_t mmax = 0;
+    for (uint64_t g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
+        while (s + 1 < nseg && pbase[s + 1] <= g) ++s;
+        const uint64_t j = g - pbase[s];
+        const dmid& m = mid[s];
+        const uint64_t q = m.pos + j * m.stride;
+        hdr h;
+        const bool whole = parse_at(rx, rx_len, segs[s].off, segs[s].len, q, h);
+        const bool ok = whole && (uint64_t)h.hlen + h.length == m.stride;
+        if (!EMIT) {
+            if (!ok) atomicMin((unsigned long long*)&first_fail[s], (unsigned long long)j);
+        } else if (j < first_fail[s]) {
+            frec v;
+            whole_frame_rec(v, q, h);
+            store_frame(fr, bases[s] + m.n_a + j, segs[s].off, v);
+            if (h.flags & F_MASK) {
+                if (ms != s && mmax) {
+                    atomicMax((unsigned long long*)&last_masked[ms], (unsigned long long)mmax);
+                    mmax = 0;
+                }
+                ms = s;
+                mmax = j + 1 > mmax ? j + 1 : mmax;
+            }
+        }
+    }
+    if (EMIT) {
+        // wave-uniform segment: reduce in registers, one lane publishes
+        const uint32_t ms0 = __shfl(ms, 0);
+        if (__all(ms == ms0)) {
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t other = __shfl_xor(mmax, o);
+                mmax = other > mmax ? other : mmax;
+            }
+            if ((threadIdx.x & 63u) == 0 && mmax)
+                atomicMax((unsigned long long*)&last_masked[ms0], (unsigned long long)mmax);
+        } else if (mmax) {
+            atomicMax((unsigned long long*)&last_masked[ms], (unsigned long long)mmax);
+        }
+    }
+}
+
+// ----------------------------------------------------------------- k_walk
+template <bool EMIT>
+__global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                       const dseg* __restrict__ segs, uint32_t nseg,
+                                                       const dmid* __restrict__ mid,
+                                                       const uint64_t* __restrict__ npred,
+                                                       const uint64_t* __restrict__ first_fail,
+                                                       const uint64_t* __restrict__ last_masked,
+                                                       dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
+                                                       const uint64_t* __restrict__ bases, dframes fr) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wpb = SCAN_THREADS / 64;
     constexpr uint32_t NPRED = 64u * SCAN_U;
 
-    for (uint32_t s = gw; s < nseg; s += nw) {
+    for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
         const uint64_t sb = segs[s].off;
         const uint64_t L = segs[s].len;
         const uint8_t* seg = rx + sb;
-        dcarry st = carry_in[s];
-        st.started = 0;
-        uint64_t pos = 0;
-        uint64_t n = 0;
+        const dmid m = mid[s];
+        dcarry st = m.st;
+        uint64_t pos = m.pos;
+        uint64_t n = m.n_a;
         const uint64_t obase = EMIT ? bases[s] : 0;
         frec r;
 
-        // Phase A: the frame carried in from the previous batch.
-        if (st.state != S_START) {
-            if (scalar_frame(seg, L, st, pos, r)) {
-                if (EMIT && lane == 0) store_frame(fr, obase + n, sb, r);
-                ++n;
+        // Skip the prefix k_verify proved; restore the fields the reference
+        // leaves behind after its last frame (Q14).
+        const uint64_t f0 = npred[s] ? first_fail[s] : 0;
+        if (f0) {
+            pos += f0 * m.stride;
+            n += f0;
+            hdr h;
+            parse_at(rx, rx_len, sb, L, pos - m.stride, h);
+            st.flags = h.flags;
+            st.length = h.length;
+            st.require = 0;
+            st.offset = 0;
+            st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
+            st.started = 0;
+            if (EMIT && last_masked[s]) {
+                hdr hm;
+                parse_at(rx, rx_len, sb, L, m.pos + (last_masked[s] - 1) * m.stride, hm);
+                st.mask = hm.key;
             }
         }
 
-        // Phase B: whole frames, speculative stride walk.
         uint64_t stride = 0;
         while (st.state == S_START && pos < L) {
             const uint64_t rem = L - pos;
             if (stride == 0) {
-                uint64_t lo, hi;
-                ld16(rx, rx_len, sb + pos, lo, hi);
-                if (rem < 2) break;
-                hdr h = parse_hdr(lo, hi);
-                if (h.hlen > rem || h.length > rem - h.hlen) break;   // incomplete: tail
-                stride = h.hlen + h.length;
+                hdr h0;
+                if (!parse_at(rx, rx_len, sb, L, pos, h0)) break;   // incomplete: tail
+                stride = (uint64_t)h0.hlen + h0.length;
             }
             uint64_t lo[SCAN_U], hi[SCAN_U];
             bool inr[SCAN_U];
@@ -340,7 +488,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict
                 const unsigned long long bad = __ballot(!ok);
                 if (f == NPRED && bad) f = (uint32_t)u * 64u + (uint32_t)(__ffsll((long long)bad) - 1);
             }
-            // Verified frames j < f: every callback fires for them here.
             uint32_t last_flags = 0, last_key = 0;
             uint64_t last_len = 0;
             bool any_masked = false;
@@ -350,13 +497,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict
                 const bool mine = j < f;
                 if (EMIT && mine) {
                     frec v;
-                    const uint64_t q = pos + (uint64_t)j * stride;
-                    v.hdr_off = (int64_t)q;
-                    v.pay_off = q + h[u].hlen;
-                    v.pay_len = h[u].length;
-                    v.length = h[u].length;
-                    v.key = h[u].key;
-                    v.info = h[u].flags | I_HDR | I_START | I_END | (h[u].length ? I_BODY : 0u);
+                    whole_frame_rec(v, pos + (uint64_t)j * stride, h[u]);
                     store_frame(fr, obase + n + j, sb, v);
                 }
                 const unsigned long long mm = __ballot(mine && (h[u].flags & F_MASK));
@@ -372,8 +513,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict
                 }
             }
             if (f > 0) {
-                // Q14: fields keep the last frame's values after it ends.
-                st.flags = last_flags;
+                st.flags = last_flags;   // Q14: the last frame's fields persist
                 st.length = last_len;
                 st.require = 0;
                 st.offset = 0;
@@ -383,9 +523,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict
             }
             n += f;
             pos += (uint64_t)f * stride;
-            if (f == NPRED) continue;   // chain unbroken: same stride
+            if (f == NPRED) continue;
             if (pos >= L) break;
-            // Frame f sits at pos (a true header).  Take its real size.
             bool wf = false;
             uint64_t sf = 0;
             const uint32_t uf = f >> 6, lf = f & 63u;
@@ -398,12 +537,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint8_t* __restrict
                     sf = sz;
                 }
             }
-            if (!wf) break;   // incomplete: tail
+            if (!wf) break;
             stride = sf;
         }
 
-        // Tail: a frame cut by the segment end (partial header or body).
-        if (st.state == S_START && pos < L) {
+        if (st.state == S_START && pos < L) {   // frame cut by the segment end
             if (scalar_frame(seg, L, st, pos, r)) {
                 if (EMIT && lane == 0) store_frame(fr, obase + n, sb, r);
                 ++n;
@@ -500,19 +638,32 @@ __device__ __forceinline__ bool xor_chunk(u32x4& v, uint64_t c, uint32_t nf, OFF
         v ^= u32x4{kw, kw, kw, kw};
         return true;
     }
-    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-#pragma unroll
-    for (int b = 0; b < 16; ++b) {
-        const uint64_t a = c + (uint64_t)b;
-        while (k < nf && endf(k) <= a) ++k;
-        if (k < nf && offf(k) <= a) {
-            const uint32_t kb = ((keyf(k) >> (8 * (b & 3))) & 0xFFu) << (8 * (b & 3));
-            if (b < 4) m0 |= kb;
-            else if (b < 8) m1 |= kb;
-            else if (b < 12) m2 |= kb;
-            else m3 |= kb;
+    // Boundary chunk.  Every frame spends >= 2 header bytes, so at most 9
+    // frames touch 16 bytes.  For each payload piece OR in its key word under
+    // a byte mask of the overlap [lo, hi) -- no per-byte loop.
+    uint64_t mlo = 0, mhi = 0;   // key bytes for chunk bytes 0-7 / 8-15
+#pragma unroll 1
+    for (int p = 0; p < 10; ++p) {
+        if (k >= nf) break;
+        const uint64_t po = offf(k), pe = endf(k);
+        if (po >= c + 16) break;
+        const uint32_t lo = po > c ? (uint32_t)(po - c) : 0u;
+        const uint32_t hi = pe < c + 16 ? (uint32_t)(pe - c) : 16u;
+        if (hi > lo) {
+            const uint64_t kw = keyf(k);
+            const uint64_t kk = kw | (kw << 32);
+            // bytes [lo, hi) of a 16-byte little-endian window
+            const uint64_t lo_keep_lo = lo >= 8 ? 0ull : (~0ull << (8 * lo));
+            const uint64_t hi_keep_lo = hi >= 8 ? ~0ull : ((1ull << (8 * hi)) - 1);
+            const uint64_t lo_keep_hi = lo <= 8 ? ~0ull : (~0ull << (8 * (lo - 8)));
+            const uint64_t hi_keep_hi = hi <= 8 ? 0ull : (hi >= 16 ? ~0ull : ((1ull << (8 * (hi - 8))) - 1));
+            mlo |= kk & lo_keep_lo & hi_keep_lo;
+            mhi |= kk & lo_keep_hi & hi_keep_hi;
         }
+        if (pe > c + 16) break;
+        ++k;
     }
+    const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32), m2 = (uint32_t)mhi, m3 = (uint32_t)(mhi >> 32);
     v ^= u32x4{m0, m1, m2, m3};
     return true;
 }
@@ -530,13 +681,13 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
                                               const uint64_t* __restrict__ pay_len,
                                               const uint32_t* __restrict__ keyrot,
                                               const uint32_t* __restrict__ tile_first, uint64_t nfr,
-                                              uint64_t ntiles) {
+                                              uint64_t tile0, uint64_t ntiles) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     __shared__ uint64_t s_off[UNMASK_MAXF];
     __shared__ uint64_t s_end[UNMASK_MAXF];
     __shared__ uint32_t s_key[UNMASK_MAXF];
 
-    const uint64_t t = SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x;
+    const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
     const bool full = base + TILE <= rx_len;
@@ -616,9 +767,10 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
 // ---------------------------------------------------------- k_stream_xor
 // The same geometry with no frame table: the measured in-place ceiling.
 template <int T, int U, bool SWZ>
-__global__ __launch_bounds__(T) void k_stream_xor(uint8_t* __restrict__ d, uint64_t n, uint64_t ntiles, uint32_t pat) {
+__global__ __launch_bounds__(T) void k_stream_xor(uint8_t* __restrict__ d, uint64_t n, uint64_t tile0, uint64_t ntiles,
+                                                  uint32_t pat) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
-    const uint64_t t = SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x;
+    const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
     const uint64_t base = t * TILE;
     if (base + TILE <= n) {
         u32x4 v[U];
@@ -659,19 +811,35 @@ __global__ void k_xor_span(uint8_t* __restrict__ d, uint64_t n, uint32_t key, ui
 
 // --------------------------------------------------------------- launchers
 
-hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
-                       const dcarry* carry_in, dcarry* carry_out, uint64_t* counts,
-                       const uint64_t* bases, dframes fr, hipStream_t st) {
-    if (nseg == 0) return hipSuccess;
+static uint32_t wave_blocks(uint32_t nseg) {
     const uint32_t wpb = SCAN_THREADS / 64;
     uint32_t blocks = (nseg + wpb - 1) / wpb;
-    if (blocks > 65536u) blocks = 65536u;
-    if (emit)
-        hipLaunchKernelGGL(k_scan<true>, dim3(blocks), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg,
-                           carry_in, carry_out, counts, bases, fr);
-    else
-        hipLaunchKernelGGL(k_scan<false>, dim3(blocks), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg,
-                           carry_in, carry_out, counts, bases, fr);
+    return blocks > 65536u ? 65536u : (blocks ? blocks : 1u);
+}
+
+hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
+                       const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
+                       uint64_t* total, scan_scratch sc, dframes fr, hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    const uint32_t wb = wave_blocks(nseg);
+    const uint32_t vb = 2048;
+    if (!emit) {
+        hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
+        hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
+                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr);
+        hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+    } else {
+        hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr);
+        hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
+                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr);
+        hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr);
+    }
     return hipGetLastError();
 }
 
@@ -742,32 +910,53 @@ const char* unmask_name(int variant) {
 
 #define HVWS_GEOM_CASE(i, t, u, s) \
     case i: hipLaunchKernelGGL((HVWS_K<t, u, s>), HVWS_ARGS); break;
+// A launch may hold at most 2^32-1 work-items (and 2^31-1 workgroups); a
+// larger grid is split into several launches over consecutive tile ranges
+// (each keeps its own XCD order).  Never let the runtime truncate a grid.
+static uint64_t max_tiles_per_launch(int threads) {
+    const uint64_t by_items = 0xFFFFFFFFull / (uint64_t)threads;
+    return by_items < 0x7FFFFFFFull ? by_items : 0x7FFFFFFFull;
+}
+
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
                          uint64_t nfr, hipStream_t st) {
     if (rx_len == 0 || nfr == 0) return hipSuccess;
+    if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
     const uint64_t tile = unmask_tile(variant);
-    const uint64_t ntiles = (rx_len + tile - 1) / tile;
+    const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
     const int threads = kGeoms[variant].threads;
+    const uint64_t cap = max_tiles_per_launch(threads);
+    for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
+        const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
 #define HVWS_K k_unmask
 #define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, fr.keyrot, \
-                  tile_first, nfr, ntiles
-    switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
+                  tile_first, nfr, tile0, ntiles
+        switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
 #undef HVWS_K
 #undef HVWS_ARGS
-    return hipGetLastError();
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st) {
+    if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
     const uint64_t tile = unmask_tile(variant);
-    const uint64_t ntiles = (n + tile - 1) / tile;
-    if (ntiles == 0) return hipSuccess;
+    const uint64_t ntiles_all = (n + tile - 1) / tile;
     const int threads = kGeoms[variant].threads;
+    const uint64_t cap = max_tiles_per_launch(threads);
+    for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
+        const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
 #define HVWS_K k_stream_xor
-#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, d, n, ntiles, pattern
-    switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
+#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, d, n, tile0, ntiles, pattern
+        switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
 #undef HVWS_K
 #undef HVWS_ARGS
-    return hipGetLastError();
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st) {

@@ -58,14 +58,66 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ buf, uint64
     for (int i = 0; i < 4; ++i) {
         const uint64_t c = t * SYN_TILE + ((uint64_t)i * 256u + threadIdx.x) * 16u;
         if (c >= buf_len) break;
+        // first frame ending after c
+        uint64_t k = kfirst;
+        while (k < nframes && frame_off[k] + frame_size[k] <= c) ++k;
+        // Fast path: the 16 bytes lie inside one payload -- three mix64 words
+        // cover them; no per-byte frame walk.
+        if (k < nframes && c + 16 <= buf_len) {
+            const uint32_t fl = flags[k];
+            const uint64_t n = length[k];
+            const uint64_t ps = frame_off[k] + hdr_len_of(fl, n);
+            if (ps <= c && c + 16 <= ps + n) {
+                const uint64_t j0 = c - ps;
+                const uint64_t fs = mix64(seed + k * 0x9E3779B97F4A7C15ull);
+                const uint32_t sh = (uint32_t)(j0 & 7u) * 8u;
+                const uint64_t q = j0 >> 3;
+                const uint64_t w0 = mix64(fs + q), w1 = mix64(fs + q + 1);
+                uint64_t lo = w0, hi = w1;
+                if (sh) {
+                    const uint64_t w2 = mix64(fs + q + 2);
+                    lo = (w0 >> sh) | (w1 << (64u - sh));
+                    hi = (w1 >> sh) | (w2 << (64u - sh));
+                }
+                if (text && text[k]) {
+                    uint64_t tl = 0, th = 0;
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) {
+                        tl |= (uint64_t)(0x20u + ((((uint32_t)(lo >> (8 * b)) & 0xFFu) * 95u) >> 8)) << (8 * b);
+                        th |= (uint64_t)(0x20u + ((((uint32_t)(hi >> (8 * b)) & 0xFFu) * 95u) >> 8)) << (8 * b);
+                    }
+                    lo = tl;
+                    hi = th;
+                }
+                if (mode != 2 && (fl & F_MASK)) {
+                    const uint32_t key = mask[k];
+                    const uint32_t r = (uint32_t)(j0 & 3u) * 8u;
+                    const uint32_t kw = r ? (key >> r) | (key << (32u - r)) : key;
+                    const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                    lo ^= kk;
+                    hi ^= kk;
+                }
+                uint64_t* p = reinterpret_cast<uint64_t*>(buf + c);
+                if (mode == 0) {
+                    p[0] = lo;
+                    p[1] = hi;
+                } else {
+                    const uint64_t d0 = p[0] ^ lo, d1 = p[1] ^ hi;
+                    if (d0 | d1) {
+                        for (int b = 0; b < 8; ++b) {
+                            bad += ((d0 >> (8 * b)) & 0xFFu) ? 1u : 0u;
+                            bad += ((d1 >> (8 * b)) & 0xFFu) ? 1u : 0u;
+                        }
+                    }
+                }
+                continue;
+            }
+        }
         uint8_t cur[16];
         uint8_t exp[16];
         bool cov[16];
         const uint32_t nb = (uint32_t)(buf_len - c < 16 ? buf_len - c : 16);
         for (uint32_t b = 0; b < 16; ++b) cur[b] = b < nb ? buf[c + b] : 0;
-        // first frame ending after c
-        uint64_t k = kfirst;
-        while (k < nframes && frame_off[k] + frame_size[k] <= c) ++k;
         uint64_t wid = ~0ull, w = 0, fseed = 0, fk = ~0ull;
         for (uint32_t b = 0; b < 16; ++b) {
             const uint64_t a = c + b;

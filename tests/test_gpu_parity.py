@@ -254,3 +254,57 @@ def test_stream_xor_roundtrip(eng):
     x = b.download(len(a))
     assert np.array_equal(x, a ^ np.uint8(0xA5))
     b.free()
+
+
+def test_batch_dense_tiny_frames(eng):
+    """Many frames inside one 16-byte chunk (2-byte unmasked empties between
+    masked ones) at every alignment: the unmask kernel's boundary merge must
+    visit each payload piece."""
+    rng = random.Random(2024)
+    k = b"\x9a\x5c\x33\xe1"
+    for pad in range(16):
+        frames = []
+        for _ in range(400):
+            r = rng.random()
+            if r < 0.4:
+                frames.append((0x2 | 0x10, b"", None))                      # 2-byte unmasked empty
+            elif r < 0.6:
+                frames.append((0x2 | 0x10 | 0x20, b"", k))                  # 6-byte masked empty
+            else:
+                frames.append((0x1 | 0x10 | 0x20, rng.randbytes(rng.randint(1, 20)), rng.randbytes(4)))
+        data = bytes(pad) + H.build_frames_ref(frames)
+        buf = np.frombuffer(data, np.uint8).copy()
+        _compare_batch(eng, buf, [(pad, len(data) - pad)])
+
+
+def test_long_segment_speculation_breaks(eng):
+    """Uniform runs verified in parallel, broken by a different size at many
+    positions (the prefix verifier must stop exactly at the first break)."""
+    rng = random.Random(31)
+    for brk in (1, 2, 255, 256, 257, 300, 511, 1000):
+        frames = [(0x2 | 0x10 | 0x20, rng.randbytes(100), rng.randbytes(4)) for _ in range(1200)]
+        frames[brk] = (0x2 | 0x20, rng.randbytes(101), rng.randbytes(4))   # one odd size, FIN=0
+        if brk + 5 < len(frames):
+            frames[brk + 5] = (0x0 | 0x10, rng.randbytes(104), None)       # unmasked, same stride
+        data = H.build_frames_ref(frames)
+        cut = len(data) - rng.randint(0, 150)
+        buf = np.frombuffer(data[:cut], np.uint8).copy()
+        _compare_batch(eng, buf, [(0, cut)])
+        _, st, _, _ = H.scan_segment(data[:cut])
+        rest = np.frombuffer(data[cut:], np.uint8).copy()
+        _compare_batch(eng, rest, [(0, len(rest))], [st])
+
+
+def test_long_segment_last_frame_unmasked(eng):
+    """Verified prefix ending in an unmasked frame of the same stride: the
+    carried mask must be the last *masked* key (Q14, stale mask)."""
+    rng = random.Random(41)
+    for n_frames in (256, 257, 700):
+        frames = [(0x2 | 0x10 | 0x20, rng.randbytes(100), rng.randbytes(4)) for _ in range(n_frames)]
+        frames[-1] = (0x2 | 0x10, rng.randbytes(104), None)
+        frames[-2] = (0x2 | 0x10, rng.randbytes(104), None)
+        data = H.build_frames_ref(frames)
+        _compare_batch(eng, np.frombuffer(data, np.uint8).copy(), [(0, len(data))])
+        # and with a partial header of a next frame after it
+        data2 = data + H.build_frames_ref([(0x1 | 0x20, b"abc", b"wxyz")])[:4]
+        _compare_batch(eng, np.frombuffer(data2, np.uint8).copy(), [(0, len(data2))])
