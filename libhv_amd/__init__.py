@@ -276,10 +276,16 @@ class Engine:
     def unmask(self, rx: DeviceBuffer, rx_len: int) -> None:
         _check(lib().hvws_unmask(self.ctx, rx.ptr, rx_len), "hvws_unmask")
 
+    def prepare(self, segs, carry=None) -> "Prepared":
+        """Build the ctypes segment/carry tables once (for repeated steps)."""
+        return Prepared(self._segs(segs), self._carry(len(segs), carry), len(segs))
+
     def step(self, rx: DeviceBuffer, rx_len: int, segs, carry=None) -> None:
-        s = self._segs(segs)
-        c = self._carry(len(segs), carry)
-        _check(lib().hvws_step(self.ctx, rx.ptr, rx_len, s, c, len(segs)), "hvws_step")
+        if isinstance(segs, Prepared):
+            s, c, n = segs.segs, segs.carry, segs.n
+        else:
+            s, c, n = self._segs(segs), self._carry(len(segs), carry), len(segs)
+        _check(lib().hvws_step(self.ctx, rx.ptr, rx_len, s, c, n), "hvws_step")
 
     def frames(self) -> np.ndarray:
         n = lib().hvws_frame_count(self.ctx)
@@ -328,6 +334,11 @@ class Engine:
         out = ctypes.c_uint64(0)
         _check(lib().hvws_digest(self.ctx, buf.ptr, n, ctypes.byref(out)), "hvws_digest")
         return int(out.value)
+
+
+class Prepared:
+    def __init__(self, segs, carry, n):
+        self.segs, self.carry, self.n = segs, carry, n
 
 
 class DevicePlan:

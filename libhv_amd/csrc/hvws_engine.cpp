@@ -92,7 +92,7 @@ struct hvws_ctx {
     dbuf segs, carry_in, carry_out, counts, bases, total;
     dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total;
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
-    dbuf tile_first;
+    dbuf tile_first, tile_key, tile_kind;
     uint64_t frame_cap = 0;
     hbuf h_segs, h_carry, h_total;
     // staging for host-memory entry points
@@ -207,8 +207,14 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const uint64_t tile = unmask_tile(c->variant);
     const uint64_t ntiles = (rx_len + tile - 1) / tile;
     HIP_OR(c->tile_first.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(c->tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(c->tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
     HIP_OR(launch_tile_index(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), nfr, c->tile_first.as<uint32_t>(),
                              ntiles, tile, c->stream),
+           HVWS_EHIP);
+    HIP_OR(launch_tile_class(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), c->f_keyrot.as<uint32_t>(), nfr,
+                             c->tile_first.as<uint32_t>(), c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(),
+                             ntiles, tile, rx_len, c->stream),
            HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
     c->nseg = nseg;
@@ -311,7 +317,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     for (dbuf* b : {&c->sc_mid, &c->sc_npred, &c->sc_pbase, &c->sc_fail, &c->sc_masked, &c->sc_total})
         b->release();
     for (dbuf* b : {&c->segs, &c->carry_in, &c->carry_out, &c->counts, &c->bases, &c->total, &c->f_hdr, &c->f_off,
-                    &c->f_len, &c->f_length, &c->f_key, &c->f_keyrot, &c->f_info, &c->tile_first, &c->stage,
+                    &c->f_len, &c->f_length, &c->f_key, &c->f_keyrot, &c->f_info, &c->tile_first, &c->tile_key, &c->tile_kind, &c->stage,
                     &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad})
         b->release();
     c->h_segs.release();
@@ -408,7 +414,8 @@ int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     if (d_rx != c->rx || rx_len != c->rx_len)
         return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
     HIP_OR(hipEventRecord(c->ev[2], c->stream), HVWS_EHIP);
-    HIP_OR(launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(), c->nfr, c->stream),
+    HIP_OR(launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(),
+                         c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->nfr, c->stream),
            HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[3], c->stream), HVWS_EHIP);
     c->ev_unmask = true;

@@ -81,7 +81,10 @@ int unmask_variant_count();
 uint64_t unmask_tile(int variant);         // bytes per workgroup tile
 const char* unmask_name(int variant);
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
-                         uint64_t nfr, hipStream_t st);
+                         const uint32_t* tile_key, const uint8_t* tile_kind, uint64_t nfr, hipStream_t st);
+hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, uint64_t nfr,
+                             const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
+                             uint64_t tile, uint64_t rx_len, hipStream_t st);
 hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
 hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st);
 

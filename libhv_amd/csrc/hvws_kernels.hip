@@ -600,6 +600,31 @@ __global__ void k_tile_index(const uint64_t* __restrict__ off, const uint64_t* _
     tile_first[t] = (uint32_t)lo;
 }
 
+// Unmask tile classes.  A tile lying wholly inside one masked payload (7 of 8
+// tiles for 64 KiB frames) needs only that frame's key word: k_unmask then
+// skips the frame-table staging, the LDS search and the barrier.
+enum : uint32_t { TILE_GENERAL = 0, TILE_SINGLE = 1, TILE_NONE = 2 };
+
+__global__ void k_tile_class(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                             const uint32_t* __restrict__ keyrot, uint64_t nfr,
+                             const uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
+                             uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile, uint64_t rx_len) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint64_t x = t * tile;
+    const uint64_t xe = x + tile < rx_len ? x + tile : rx_len;
+    const uint32_t k = tile_first[t];
+    uint32_t kind = TILE_GENERAL, key = 0;
+    if (k >= nfr || off[k] >= xe) {
+        kind = TILE_NONE;                       // no payload byte in the tile
+    } else if (off[k] <= x && xe <= off[k] + len[k] && xe == x + tile) {
+        key = keyrot[k];
+        kind = key ? TILE_SINGLE : TILE_NONE;   // one payload; zero key word = no-op
+    }
+    tile_key[t] = key;
+    tile_kind[t] = (uint8_t)kind;
+}
+
 // -------------------------------------------------------------- k_unmask
 //
 // One workgroup per tile of T*U*16 bytes.  Each thread owns U 16-byte chunks
@@ -680,7 +705,9 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
                                               const uint64_t* __restrict__ pay_off,
                                               const uint64_t* __restrict__ pay_len,
                                               const uint32_t* __restrict__ keyrot,
-                                              const uint32_t* __restrict__ tile_first, uint64_t nfr,
+                                              const uint32_t* __restrict__ tile_first,
+                                              const uint32_t* __restrict__ tile_key,
+                                              const uint8_t* __restrict__ tile_kind, uint64_t nfr,
                                               uint64_t tile0, uint64_t ntiles) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     __shared__ uint64_t s_off[UNMASK_MAXF];
@@ -691,8 +718,22 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
     const bool full = base + TILE <= rx_len;
+    const uint32_t kind = tile_kind[t];
+    if (kind == TILE_NONE) return;
 
     u32x4 v[U];
+    if (kind == TILE_SINGLE) {   // whole tile inside one masked payload
+        const uint32_t kw = tile_key[t];
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            v[i] = __builtin_nontemporal_load(
+                reinterpret_cast<const u32x4*>(rx + base + ((uint64_t)i * T + tid) * 16u));
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            __builtin_nontemporal_store(v[i] ^ u32x4{kw, kw, kw, kw},
+                                        reinterpret_cast<u32x4*>(rx + base + ((uint64_t)i * T + tid) * 16u));
+        return;
+    }
     if (full) {
 #pragma unroll
         for (int i = 0; i < U; ++i)
@@ -857,6 +898,16 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
     return hipGetLastError();
 }
 
+hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, uint64_t nfr,
+                             const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
+                             uint64_t tile, uint64_t rx_len, hipStream_t st) {
+    if (ntiles == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)((ntiles + 255) / 256);
+    hipLaunchKernelGGL(k_tile_class, dim3(blocks), dim3(256), 0, st, off, len, keyrot, nfr, tile_first, tile_key,
+                       tile_kind, ntiles, tile, rx_len);
+    return hipGetLastError();
+}
+
 // Unmask geometries (threads, chunks per thread, XCD order).  Default from the
 // on-device sweep; HVWS_UNMASK=<index> selects another for experiments.
 struct unmask_geom {
@@ -865,12 +916,12 @@ struct unmask_geom {
 };
 // X(index, threads, chunks per thread, XCD order); index 0 is the default.
 #define HVWS_UNMASK_GEOMS(X)                                                              \
-    X(0, 256, 2, true)                                                                    \
+    X(0, 256, 4, true)                                                                    \
     X(1, 128, 2, true)                                                                    \
     X(2, 512, 1, true)                                                                    \
     X(3, 128, 4, true)                                                                    \
     X(4, 1024, 1, true)                                                                   \
-    X(5, 256, 4, true)                                                                    \
+    X(5, 256, 2, true)                                                                    \
     X(6, 256, 8, true)                                                                    \
     X(7, 256, 8, false)                                                                   \
     X(8, 64, 8, true)
@@ -919,7 +970,7 @@ static uint64_t max_tiles_per_launch(int threads) {
 }
 
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
-                         uint64_t nfr, hipStream_t st) {
+                         const uint32_t* tile_key, const uint8_t* tile_kind, uint64_t nfr, hipStream_t st) {
     if (rx_len == 0 || nfr == 0) return hipSuccess;
     if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
     const uint64_t tile = unmask_tile(variant);
@@ -930,7 +981,7 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
 #define HVWS_K k_unmask
 #define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, fr.keyrot, \
-                  tile_first, nfr, tile0, ntiles
+                  tile_first, tile_key, tile_kind, nfr, tile0, ntiles
         switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
 #undef HVWS_K
 #undef HVWS_ARGS

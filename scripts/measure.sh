@@ -13,3 +13,5 @@ $S bench_${TAG}_c4 300 python bench.py --config c4 --segments 1024 --cpu-seconds
 $S prof_${TAG} 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --host-gib 0
 $S pmc_fetch_${TAG} 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- python bench.py --steps 2 --warmup 0 --cpu-seconds 0 --host-gib 0
 $S pmc_write_${TAG} 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- python bench.py --steps 2 --warmup 0 --cpu-seconds 0 --host-gib 0
+$S pmc_fetch_c2_${TAG} 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_c2_$TAG -o run --output-format csv -- python bench.py --config c2 --steps 2 --warmup 0 --cpu-seconds 0 --host-gib 0
+$S pmc_write_c2_${TAG} 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_c2_$TAG -o run --output-format csv -- python bench.py --config c2 --steps 2 --warmup 0 --cpu-seconds 0 --host-gib 0

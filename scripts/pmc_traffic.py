@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of each kernel from two separate rocprofv3 --pmc
+passes (FETCH_SIZE, WRITE_SIZE), corrected as MI355X_MICROARCH.md's HBM
+section prescribes: both counters are in KiB; on gfx950 FETCH_SIZE counts
+exactly half of the bytes of a 16-B-per-lane coalesced streaming read, so
+read bytes = 2 x FETCH_SIZE x 1024, write bytes = WRITE_SIZE x 1024.
+
+  scripts/pmc_traffic.py FETCH_DIR WRITE_DIR --rx-bytes N --config NAME [--out profiles/traffic.json]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+from collections import defaultdict
+
+
+def load(d, counter):
+    out = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r["Counter_Name"] == counter:
+                    out[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("hvws::", "")].append(
+                        float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--rx-bytes", type=int, required=True)
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--out", default="profiles/traffic.json")
+    a = ap.parse_args()
+    fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
+    db = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    for k in sorted(set(fetch) & set(write)):
+        if not (k.startswith("k_unmask") or k.startswith("k_stream_xor")):
+            continue
+        rd = 2 * statistics.median(fetch[k]) * 1024
+        wr = statistics.median(write[k]) * 1024
+        name = k.replace(" ", "").replace("true", "xcd").replace("false", "linear")
+        db.setdefault(name, {})[str(a.rx_bytes)] = {
+            "config": a.config, "read_bytes": int(rd), "write_bytes": int(wr), "hbm_bytes": int(rd + wr),
+            "dispatches": min(len(fetch[k]), len(write[k])),
+            "method": "median per dispatch; read = 2 x FETCH_SIZE x 1024 (gfx950 16-B/lane correction), "
+                      "write = WRITE_SIZE x 1024; separate --pmc passes",
+        }
+        print(name, a.rx_bytes, int(rd + wr))
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    json.dump(db, open(a.out, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
