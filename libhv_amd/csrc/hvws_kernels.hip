@@ -326,7 +326,25 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
         if (st.state == S_START && parse_at(rx, rx_len, sb, L, pos, h)) {
             stride = (uint64_t)h.hlen + h.length;
             const uint64_t cnt = (L - pos) / stride;
-            if (cnt >= SPEC_MIN) np = cnt;
+            if (cnt >= SPEC_MIN) {
+                // Probe before committing the grid: lanes 0-31 check
+                // predictions 2^(l/2) (near the start), lanes 32-63 spread over
+                // the whole range.  Speculation stops at the first probe that
+                // breaks, so a mixed-size stream costs no grid-wide work and
+                // no atomic storm; a uniform one keeps every prediction.
+                uint64_t j = lane < 32 ? (1ull << (lane / 2)) + (lane & 1) * ((1ull << (lane / 2)) >> 1)
+                                       : ((uint64_t)(lane - 31) * cnt) / 33;
+                if (j >= cnt) j = cnt - 1;
+                hdr hp;
+                const uint64_t q = pos + j * stride;
+                const bool ok = parse_at(rx, rx_len, sb, L, q, hp) && (uint64_t)hp.hlen + hp.length == stride;
+                uint64_t jb = ok ? cnt : j;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const uint64_t other = __shfl_xor(jb, o);
+                    jb = other < jb ? other : jb;
+                }
+                np = jb >= SPEC_MIN ? jb : 0;
+            }
         }
         if (lane == 0) {
             dmid m;
@@ -380,7 +398,9 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
         const bool whole = parse_at(rx, rx_len, segs[s].off, segs[s].len, q, h);
         const bool ok = whole && (uint64_t)h.hlen + h.length == m.stride;
         if (!EMIT) {
-            if (!ok) atomicMin((unsigned long long*)&first_fail[s], (unsigned long long)j);
+            // filter on a (possibly stale, never too small) read first
+            if (!ok && j < __hip_atomic_load(&first_fail[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                atomicMin((unsigned long long*)&first_fail[s], (unsigned long long)j);
         } else if (j < first_fail[s]) {
             frec v;
             whole_frame_rec(v, q, h);
