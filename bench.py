@@ -143,12 +143,17 @@ def main():
     def barrier():
         eng.sync()
         if torch.cuda.is_available():
-            torch.cuda.synchronize(local)
+            torch.cuda.synchronize(device)
         if dist is not None:
             dist.barrier()
 
     desc, cfg = CONFIGS[args.config]
-    eng = libhv_amd.Engine(local)
+    # one process per GPU: LOCAL_RANK picks the device (modulo the visible
+    # count, so a launcher that narrows HIP_VISIBLE_DEVICES per rank also
+    # works); HVWS_BENCH_DEVICE pins every rank to one card for rehearsals.
+    ndev = max(1, libhv_amd.device_count())
+    device = int(os.environ.get("HVWS_BENCH_DEVICE", local % ndev))
+    eng = libhv_amd.Engine(device)
     t = time.perf_counter()
     plan = rank_plan(cfg, rank, args.segments)
     dp = libhv_amd.DevicePlan(eng, plan)

@@ -50,4 +50,11 @@ public:
 
 typedef std::shared_ptr<WebSocketParser> WebSocketParserPtr;
 
+/* Batched FeedRecvData for an event loop: n connections' reads in one GPU
+ * round trip (one segment each).  Same effects, per parser, as calling
+ * parsers[i]->FeedRecvData(data[i], len[i]) in order i = 0..n-1; rets[i]
+ * receives each call's return value.  New entry point (no reference twin). */
+HV_EXPORT int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
+                             int* rets);
+
 #endif

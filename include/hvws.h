@@ -140,6 +140,8 @@ void  hvws_wsp_free(void* h);
 void  hvws_wsp_set_sink(void* h, hvws_msg_cb cb, void* user);
 int   hvws_wsp_feed(void* h, const char* data, size_t len);
 void  hvws_wsp_state(void* h, uint64_t out[8]);
+/* n handles fed in one GPU round trip (see hvws_feed_many in WebSocketParser.h) */
+int   hvws_wsp_feed_many(void* const* handles, const char* const* data, const size_t* len, int n, int* rets);
 
 /* Device used by the reference-API entry points on the calling thread
  * (default: $HVWS_DEVICE or 0). */

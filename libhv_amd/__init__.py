@@ -127,6 +127,11 @@ _SIGS = {
     "hvws_wsp_set_sink": (None, [ctypes.c_void_p, MSG_CB, ctypes.c_void_p]),
     "hvws_wsp_feed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "hvws_wsp_state": (None, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_wsp_feed_many": (
+        ctypes.c_int,
+        [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+         ctypes.POINTER(ctypes.c_int)],
+    ),
     "hvws_set_thread_device": (ctypes.c_int, [ctypes.c_int]),
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_unmask_variant": (ctypes.c_int, [ctypes.c_int]),
@@ -148,6 +153,7 @@ _SIGS = {
 
 # C++ drop-in symbols (include/WebSocketParser.h)
 CXX_SYMBOLS = (
+    "_Z14hvws_feed_manyPKP15WebSocketParserPKPKcPKmiPi",
     "_ZN15WebSocketParserC1Ev",
     "_ZN15WebSocketParserD1Ev",
     "_ZN15WebSocketParser12FeedRecvDataEPKcm",

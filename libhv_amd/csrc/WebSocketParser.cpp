@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <unordered_set>
 #include <vector>
 
 #include "hvws.h"
@@ -20,6 +21,8 @@
 
 namespace hvws {
 [[noreturn]] void fatal(const char* what);
+hvws_ctx* thread_ctx();
+char* pinned_stage(uint64_t bytes);
 void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
               websocket_parser& carry_out, int& started);
 }  // namespace hvws
@@ -45,6 +48,49 @@ WebSocketParser::~WebSocketParser() {
     }
 }
 
+namespace {
+
+// The reference's per-frame message logic (http/WebSocketParser.cpp:8-50)
+// over the frame records of one connection; `base` is where offset `base_off`
+// of the batch buffer sits in the caller's (already unmasked) bytes.
+void replay_messages(WebSocketParser* wp, const char* base, uint64_t base_off, const hvws_frame* frames, size_t n,
+                     const websocket_parser& out) {
+    websocket_parser* parser = wp->parser;
+    for (size_t i = 0; i < n; ++i) {
+        const hvws_frame& f = frames[i];
+        const uint32_t fl = f.info & HVWS_I_FLAGS;
+        parser->flags = (websocket_flags)fl;
+        parser->length = f.length;
+        if (f.info & HVWS_I_HDR) {
+            const int op = (int)(fl & WS_OP_MASK);
+            if (op != WS_OP_CONTINUE) wp->opcode = op;
+            const int length = (int)f.length;   // int truncation, as the reference (Q11)
+            const int want = length + 1 < kMaxReserve ? length + 1 : kMaxReserve;
+            // The reference compares int with size_t here; a negative `want`
+            // makes it call reserve(huge) and throw.  Skip the reserve instead.
+            if (want >= 0 && (size_t)want > wp->message.capacity()) wp->message.reserve((size_t)want);
+            if (wp->state == WS_FRAME_BEGIN || wp->state == WS_FRAME_FIN) wp->message.clear();
+            wp->state = WS_FRAME_HEADER;
+        }
+        if (f.info & HVWS_I_BODY) {
+            wp->state = WS_FRAME_BODY;
+            wp->message.append(base + (f.pay_off - base_off), (size_t)f.pay_len);
+        }
+        if (f.info & HVWS_I_END) {
+            wp->state = WS_FRAME_END;
+            if (fl & WS_FIN) {
+                wp->state = WS_FRAME_FIN;
+                if (wp->onMessage) wp->onMessage(wp->opcode, wp->message);
+            }
+        }
+    }
+    void* keep = parser->data;
+    *parser = out;
+    parser->data = keep;
+}
+
+}  // namespace
+
 int WebSocketParser::FeedRecvData(const char* data, size_t len) {
     if (len == 0) return 0;
     std::vector<hvws_frame> frames;
@@ -52,38 +98,62 @@ int WebSocketParser::FeedRecvData(const char* data, size_t len) {
     int started = 0;
     char* buf = const_cast<char*>(data);   // unmasked in place, like the reference
     hvws::gpu_feed(buf, len, *parser, true, frames, out, started);
-
-    for (const hvws_frame& f : frames) {
-        const uint32_t fl = f.info & HVWS_I_FLAGS;
-        parser->flags = (websocket_flags)fl;
-        parser->length = f.length;
-        if (f.info & HVWS_I_HDR) {
-            const int op = (int)(fl & WS_OP_MASK);
-            if (op != WS_OP_CONTINUE) opcode = op;
-            const int length = (int)f.length;   // int truncation, as the reference (Q11)
-            const int want = length + 1 < kMaxReserve ? length + 1 : kMaxReserve;
-            // The reference compares int with size_t here; a negative `want`
-            // makes it call reserve(huge) and throw.  Skip the reserve instead.
-            if (want >= 0 && (size_t)want > message.capacity()) message.reserve((size_t)want);
-            if (state == WS_FRAME_BEGIN || state == WS_FRAME_FIN) message.clear();
-            state = WS_FRAME_HEADER;
-        }
-        if (f.info & HVWS_I_BODY) {
-            state = WS_FRAME_BODY;
-            message.append(buf + f.pay_off, (size_t)f.pay_len);
-        }
-        if (f.info & HVWS_I_END) {
-            state = WS_FRAME_END;
-            if (fl & WS_FIN) {
-                state = WS_FRAME_FIN;
-                if (onMessage) onMessage(opcode, message);
-            }
-        }
-    }
-    void* keep = parser->data;
-    *parser = out;
-    parser->data = keep;
+    replay_messages(this, buf, 0, frames.data(), frames.size(), out);
     return (int)len;
+}
+
+// One GPU round trip for many connections' reads:
+// every chunk becomes one segment of a single batch, so the launch and copy
+// latency is paid once per poll iteration instead of once per connection.
+static int feed_distinct(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
+                         int* rets);
+
+int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n, int* rets) {
+    // A connection's second chunk needs the carry its first chunk leaves, so
+    // cut the batch before any parser that already appears in it.
+    int done = 0;
+    while (done < n) {
+        int end = done;
+        std::unordered_set<WebSocketParser*> seen;
+        while (end < n && seen.insert(parsers[end]).second) ++end;
+        feed_distinct(parsers + done, data + done, len + done, end - done, rets ? rets + done : nullptr);
+        done = end;
+    }
+    return n;
+}
+
+static int feed_distinct(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
+                         int* rets) {
+    if (n <= 0) return 0;
+    std::vector<hvws_segment> segs((size_t)n);
+    std::vector<websocket_parser> carry((size_t)n);
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        segs[i].off = total;
+        segs[i].len = len[i];
+        total += len[i];
+        carry[i] = *parsers[i]->parser;
+    }
+    char* stage = hvws::pinned_stage(total);
+    for (int i = 0; i < n; ++i)
+        if (len[i]) memcpy(stage + segs[i].off, data[i], len[i]);
+    hvws_ctx* c = hvws::thread_ctx();
+    if (hvws_rx_batch(c, (uint8_t*)stage, total, segs.data(), carry.data(), (uint32_t)n, 1) != HVWS_OK)
+        hvws::fatal("hvws_rx_batch");
+    const int64_t nf = hvws_frame_count(c);
+    std::vector<hvws_frame> frames((size_t)(nf > 0 ? nf : 0));
+    std::vector<uint64_t> first((size_t)n), count((size_t)n);
+    if ((nf > 0 && hvws_get_frames(c, frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
+        hvws_get_segment_frames(c, first.data(), count.data()) != HVWS_OK)
+        hvws::fatal("frame table read-back");
+    for (int i = 0; i < n; ++i) {
+        char* dst = const_cast<char*>(data[i]);
+        if (len[i]) memcpy(dst, stage + segs[i].off, len[i]);   // in place, like the reference
+        carry[i].data = parsers[i]->parser->data;
+        replay_messages(parsers[i], dst, segs[i].off, frames.data() + first[i], (size_t)count[i], carry[i]);
+        if (rets) rets[i] = (int)len[i];
+    }
+    return n;
 }
 
 // ---------------------------------------------------------------- C handle
@@ -112,6 +182,12 @@ void hvws_wsp_set_sink(void* h, hvws_msg_cb cb, void* user) {
 }
 
 int hvws_wsp_feed(void* h, const char* data, size_t len) { return ((wsp_handle*)h)->p.FeedRecvData(data, len); }
+
+int hvws_wsp_feed_many(void* const* handles, const char* const* data, const size_t* len, int n, int* rets) {
+    std::vector<WebSocketParser*> ps((size_t)(n > 0 ? n : 0));
+    for (int i = 0; i < n; ++i) ps[i] = &((wsp_handle*)handles[i])->p;
+    return hvws_feed_many(ps.data(), data, len, n, rets);
+}
 
 void hvws_wsp_state(void* h, uint64_t out[8]) {
     wsp_handle* w = (wsp_handle*)h;

@@ -715,6 +715,15 @@ hvws_ctx* thread_ctx() {
     return t_ctx;
 }
 
+// Per-thread pinned staging for batched host entry points.
+char* pinned_stage(uint64_t bytes) {
+    thread_local hbuf stage;
+    hvws_ctx* c = thread_ctx();
+    if (hipSetDevice(c->device) != hipSuccess || stage.ensure(bytes + 64) != hipSuccess)
+        fatal("pinned staging allocation");
+    return stage.as<char>();
+}
+
 // XOR `n` host bytes at src into dst with key/phase on the GPU.
 void gpu_xor_host(char* dst, const char* src, size_t n, uint32_t key, uint32_t phase) {
     if (n == 0) return;

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Event-loop shaped measurement of the drop-in.
+
+n connections each deliver 8 KiB reads (event/hevent.h:16 HLOOP_READ_BUFSIZE)
+of a stream of masked 1 KiB binary frames.  One "poll iteration" hands every
+connection's next read to the parser:
+  * gpu_many : one hvws_wsp_feed_many call (one GPU round trip per iteration);
+  * gpu_each : WebSocketParser::FeedRecvData per connection (a round trip each);
+  * cpu_ref  : the reference frame parser + restated WebSocketParser callbacks
+               (oracle/_ref), per connection, one core.
+Reports per-iteration latency and payload throughput.  Prints JSON lines.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+import libhv_amd  # noqa: E402
+import wsharness as H  # noqa: E402
+from libhv_amd import synth  # noqa: E402
+
+READ = 8192
+
+
+def main():
+    iters = int(os.environ.get("ITERS", "20"))
+    L = libhv_amd.lib()
+    R = H.ref() if H.have_ref() else H.oracle()
+    kind = "reference" if H.have_ref() else "port"
+    for n in (1, 16, 256, 1024, 4096):
+        per_conn = READ * iters
+        frames = per_conn // 1032 + 2
+        plan = synth.uniform_plan(frames * n, 1024, 77).split(n)
+        host = H.synth_cpu(plan)
+        streams = [host[o:o + ln] for o, ln in plan.segments]
+        payload_per_read = READ * 1024 / 1032
+        res = {"connections": n, "read_bytes": READ, "iterations": iters}
+        for mode in ("gpu_many", "gpu_each", "cpu_ref"):
+            if mode == "gpu_each" and n > 256:
+                continue
+            bufs = [np.array(s[:per_conn], copy=True) for s in streams]
+            if mode == "cpu_ref":
+                hs = [R.msgp_new() for _ in range(n)]
+                t0 = time.perf_counter()
+                for it in range(iters):
+                    for i in range(n):
+                        R.msgp_feed(hs[i], bufs[i].ctypes.data + it * READ, READ)
+                dt = time.perf_counter() - t0
+                for h in hs:
+                    R.msgp_free(h)
+            else:
+                hs = [L.hvws_wsp_new() for _ in range(n)]
+                hv = (ctypes.c_void_p * n)(*hs)
+                lens = (ctypes.c_size_t * n)(*([READ] * n))
+                rets = (ctypes.c_int * n)()
+                ds = (ctypes.c_void_p * n)()
+                # warm-up iteration on a scratch copy (allocations, first launch)
+                scratch = [b.copy() for b in bufs]
+                for i in range(n):
+                    ds[i] = scratch[i].ctypes.data
+                warm = [L.hvws_wsp_new() for _ in range(n)]
+                L.hvws_wsp_feed_many((ctypes.c_void_p * n)(*warm), ds, lens, n, rets)
+                for h in warm:
+                    L.hvws_wsp_free(h)
+                t0 = time.perf_counter()
+                for it in range(iters):
+                    for i in range(n):
+                        ds[i] = bufs[i].ctypes.data + it * READ
+                    if mode == "gpu_many":
+                        L.hvws_wsp_feed_many(hv, ds, lens, n, rets)
+                    else:
+                        for i in range(n):
+                            L.hvws_wsp_feed(hs[i], ds[i], READ)
+                dt = time.perf_counter() - t0
+                for h in hs:
+                    L.hvws_wsp_free(h)
+            res[mode] = {
+                "iteration_us": round(dt / iters * 1e6, 1),
+                "GiBps_payload": round(n * iters * payload_per_read / dt / 2**30, 3),
+            }
+        res["cpu_kind"] = kind
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

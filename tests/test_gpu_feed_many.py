@@ -1,0 +1,117 @@
+"""GPU: batched FeedRecvData across connections --
+an event loop's poll iteration hands every ready connection's read to one
+GPU round trip; each connection must see exactly what the reference
+WebSocketParser::FeedRecvData sequence produces."""
+from __future__ import annotations
+
+import ctypes
+import random
+
+import pytest
+
+import libhv_amd
+import streams as S
+import wsharness as H
+
+pytestmark = pytest.mark.gpu
+
+
+class Conn:
+    def __init__(self, data: bytes, chunks):
+        self.data = data
+        self.chunks = list(chunks)
+        self.at = 0
+        self.buf = ctypes.create_string_buffer(data, max(len(data), 1))
+        L = libhv_amd.lib()
+        self.h = L.hvws_wsp_new()
+        self.sink = H.MsgLog()
+        self.cb = libhv_amd.MSG_CB(self.sink._on)
+        L.hvws_wsp_set_sink(self.h, self.cb, None)
+        self.rets = []
+
+
+def _loop(rng, conns, max_batch=None, dup=False):
+    L = libhv_amd.lib()
+    pending = [c for c in conns if c.chunks]
+    while pending:
+        ready = [c for c in pending if rng.random() < 0.7] or pending[:1]
+        if dup:   # a connection may be ready twice in one iteration
+            ready = ready + [c for c in ready if rng.random() < 0.3 and len(c.chunks) > 1]
+        if max_batch:
+            ready = ready[:max_batch]
+        n = len(ready)
+        hs = (ctypes.c_void_p * n)()
+        ds = (ctypes.c_void_p * n)()
+        ls = (ctypes.c_size_t * n)()
+        for i, c in enumerate(ready):
+            k = c.chunks.pop(0)
+            hs[i] = c.h
+            ds[i] = ctypes.addressof(c.buf) + c.at
+            ls[i] = k
+            c.at += k
+        rets = (ctypes.c_int * n)()
+        assert L.hvws_wsp_feed_many(hs, ds, ls, n, rets) == n
+        for i, c in enumerate(ready):
+            c.rets.append(rets[i])
+        pending = [c for c in conns if c.chunks]
+
+
+def _check(conns):
+    L = libhv_amd.lib()
+    for c in conns:
+        chunks = []
+        # chunk sizes actually fed, in order
+        tot, i = 0, 0
+        exp_msgs, exp_rets, exp_state, exp_buf = H.run_messages("oracle", c.data, c.fed)
+        st = (ctypes.c_uint64 * 8)()
+        L.hvws_wsp_state(c.h, st)
+        assert c.sink.msgs == exp_msgs
+        assert c.rets == exp_rets
+        assert tuple(st) == exp_state
+        assert c.buf.raw[:len(c.data)] == exp_buf
+        L.hvws_wsp_free(c.h)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_feed_many_matches_sequential_reference(seed):
+    rng = random.Random(seed)
+    conns = []
+    for _ in range(rng.randint(5, 60)):
+        data = S.rand_stream(rng, rng.randint(1, 15), max_len=rng.choice([60, 600, 70000]))
+        chunks = S.rand_chunks(rng, len(data), rng.choice(["rand", "small", "one"]))
+        c = Conn(data, chunks)
+        c.fed = list(chunks)
+        conns.append(c)
+    _loop(rng, conns)
+    _check(conns)
+
+
+def test_feed_many_repeated_connection_in_batch():
+    rng = random.Random(9)
+    conns = []
+    for _ in range(12):
+        data = S.rand_stream(rng, rng.randint(2, 10), max_len=300)
+        chunks = S.rand_chunks(rng, len(data), "small")
+        c = Conn(data, chunks)
+        c.fed = list(chunks)
+        conns.append(c)
+    _loop(rng, conns, dup=True)
+    _check(conns)
+
+
+def test_feed_many_config1_event_loop():
+    """Config 1 (1000 x 1 KiB text) spread over 16 connections, 8 KiB reads."""
+    from libhv_amd import synth
+
+    plan = synth.config_plan("c1", seed=1).split(16)
+    host = H.synth_cpu(plan)
+    conns = []
+    for off, n in plan.segments:
+        data = host[off:off + n].tobytes()
+        chunks = [8192] * (n // 8192) + ([n % 8192] if n % 8192 else [])
+        c = Conn(data, chunks)
+        c.fed = list(chunks)
+        conns.append(c)
+    _loop(random.Random(4), conns)
+    _check(conns)
+    assert sum(len(c.sink.msgs) for c in conns) == 1000
