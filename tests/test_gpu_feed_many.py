@@ -16,10 +16,23 @@ import wsharness as H
 pytestmark = pytest.mark.gpu
 
 
+def _clamp(chunks, n):
+    """chunk sizes that exactly cover n bytes (rand_chunks may overshoot)"""
+    out, at = [], 0
+    for c in chunks:
+        if at >= n:
+            break
+        c = min(c, n - at)
+        out.append(c)
+        at += c
+    return out
+
+
 class Conn:
     def __init__(self, data: bytes, chunks):
         self.data = data
-        self.chunks = list(chunks)
+        self.chunks = _clamp(chunks, len(data))
+        self.fed = list(self.chunks)
         self.at = 0
         self.buf = ctypes.create_string_buffer(data, max(len(data), 1))
         L = libhv_amd.lib()
@@ -59,9 +72,6 @@ def _loop(rng, conns, max_batch=None, dup=False):
 def _check(conns):
     L = libhv_amd.lib()
     for c in conns:
-        chunks = []
-        # chunk sizes actually fed, in order
-        tot, i = 0, 0
         exp_msgs, exp_rets, exp_state, exp_buf = H.run_messages("oracle", c.data, c.fed)
         st = (ctypes.c_uint64 * 8)()
         L.hvws_wsp_state(c.h, st)
@@ -80,7 +90,6 @@ def test_feed_many_matches_sequential_reference(seed):
         data = S.rand_stream(rng, rng.randint(1, 15), max_len=rng.choice([60, 600, 70000]))
         chunks = S.rand_chunks(rng, len(data), rng.choice(["rand", "small", "one"]))
         c = Conn(data, chunks)
-        c.fed = list(chunks)
         conns.append(c)
     _loop(rng, conns)
     _check(conns)
@@ -93,7 +102,6 @@ def test_feed_many_repeated_connection_in_batch():
         data = S.rand_stream(rng, rng.randint(2, 10), max_len=300)
         chunks = S.rand_chunks(rng, len(data), "small")
         c = Conn(data, chunks)
-        c.fed = list(chunks)
         conns.append(c)
     _loop(rng, conns, dup=True)
     _check(conns)
@@ -110,7 +118,6 @@ def test_feed_many_config1_event_loop():
         data = host[off:off + n].tobytes()
         chunks = [8192] * (n // 8192) + ([n % 8192] if n % 8192 else [])
         c = Conn(data, chunks)
-        c.fed = list(chunks)
         conns.append(c)
     _loop(random.Random(4), conns)
     _check(conns)
