@@ -13,6 +13,11 @@
  *                applied to every masked payload span the last scan found.
  *   hvws_step    scan + unmask: one pass of the hot path over a batch.
  *   hvws_rx_batch  the same from/to host memory (H2D, step, D2H).
+ *   hvws_build_frames  transmit side: websocket_build_frame
+ *                (http/websocket_parser.c:207-256, as called per message by
+ *                WebSocketChannel::sendFrame via ws_build_frame,
+ *                http/WebSocketChannel.cpp:66-79, http/wsdef.c:36-46)
+ *                for a whole batch of outgoing frames at once.
  *   hvws_wsp_*   C handle over the WebSocketParser class
  *                (http/WebSocketParser.h:19-31) for FFI callers.
  *
@@ -120,12 +125,41 @@ int hvws_set_unmask_variant(int variant);
 /* STREAM-style in-place ceiling: d[i] ^= pattern over n bytes (16-B aligned). */
 int hvws_stream_xor(hvws_ctx* ctx, uint8_t* d, uint64_t n, uint32_t pattern);
 
+/* ---- transmit side, device resident ---------------------------------- */
+/* Build n frames back to back into d_out, each byte-identical to
+ * websocket_build_frame(frame, flags[i], mask + i, payload + pay_off[i],
+ * len[i]): header (FIN/opcode, MASK bit, 7/16/64-bit length, key) followed by
+ * the payload XOR-masked from phase 0 when flags[i] has WS_HAS_MASK.
+ * d_mask[i] holds frame i's key with mask[0] in bits 0-7; d_mask may be NULL
+ * only if no frame is masked (the reference would read uninitialised bytes).
+ * d_out_off (n words, optional) receives each frame's offset in d_out.
+ * *out_len = total bytes.  Synchronises once (after sizing/validating the
+ * tables: a payload range outside [0, payload_len) or an output larger than
+ * out_cap is HVWS_EINVAL and nothing is written); the build kernel itself is
+ * asynchronous on the ctx stream.  d_out must be 16-byte aligned and must not
+ * overlap d_payload. */
+int hvws_build_frames(hvws_ctx* ctx, uint8_t* d_out, uint64_t out_cap, const uint8_t* d_payload,
+                      uint64_t payload_len, const uint64_t* d_pay_off, const uint64_t* d_len,
+                      const uint8_t* d_flags, const uint32_t* d_mask, uint64_t n, uint64_t* d_out_off,
+                      uint64_t* out_len);
+/* Device time (ms) of the last build kernel, and its name. */
+int hvws_last_build_ms(hvws_ctx* ctx, float* ms);
+const char* hvws_build_kernel_name(void);
+
 /* ---- host memory in, host memory out -------------------------------- */
 /* Copies h_rx to the device, runs scan (+ unmask if `unmask`), copies the
  * bytes back in place and updates carry[].  Frames of the batch are then
  * available through hvws_get_frames(). */
 int hvws_rx_batch(hvws_ctx* ctx, uint8_t* h_rx, uint64_t len, const hvws_segment* segs,
                   websocket_parser* carry, uint32_t nseg, int unmask);
+
+/* Batches of at most `bytes` (default 64 MiB; each segment <= 1 MiB) take
+ * the single-launch small-batch path inside hvws_rx_batch (and so inside
+ * FeedRecvData / websocket_parser_execute); 0 restores the default, ~0
+ * disables the path.  ctx NULL = the calling thread's context used by the
+ * reference-API entry points.  Returns the previous limit.  Results are identical
+ * either way; only latency differs. */
+uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
 
 /* Host-inclusive streaming unmask of a large pinned host buffer holding
  * frames back to back from one stream: chunked H2D -> scan -> unmask -> D2H,

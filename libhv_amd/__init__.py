@@ -122,6 +122,13 @@ _SIGS = {
          ctypes.POINTER(ctypes.c_uint64)],
     ),
     "hvws_digest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_build_frames": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+         ctypes.POINTER(ctypes.c_uint64)],
+    ),
+    "hvws_last_build_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "hvws_wsp_new": (ctypes.c_void_p, []),
     "hvws_wsp_free": (None, [ctypes.c_void_p]),
     "hvws_wsp_set_sink": (None, [ctypes.c_void_p, MSG_CB, ctypes.c_void_p]),
@@ -134,6 +141,8 @@ _SIGS = {
     ),
     "hvws_set_thread_device": (ctypes.c_int, [ctypes.c_int]),
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
+    "hvws_build_kernel_name": (ctypes.c_char_p, []),
+    "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_set_unmask_variant": (ctypes.c_int, [ctypes.c_int]),
     # reference ABI (include/websocket_parser.h, include/wsdef.h)
     "websocket_parser_init": (None, [ctypes.c_void_p]),
@@ -336,6 +345,25 @@ class Engine:
         )
         return int(bad.value)
 
+    def build_frames(self, out: DeviceBuffer, out_cap: int, payload: Optional[DeviceBuffer], payload_len: int,
+                     tx: "TxPlan", out_off: Optional[DeviceBuffer] = None) -> int:
+        """Transmit side: websocket_build_frame for every frame of `tx` into
+        `out` (back to back).  Returns the bytes written (the kernel runs
+        asynchronously on the ctx stream)."""
+        n = ctypes.c_uint64(0)
+        _check(
+            lib().hvws_build_frames(self.ctx, out.ptr, out_cap, payload.ptr if payload else None, payload_len,
+                                    tx.pay_off.ptr, tx.length.ptr, tx.flags.ptr, tx.mask.ptr if tx.mask else None,
+                                    tx.n, out_off.ptr if out_off else None, ctypes.byref(n)),
+            "hvws_build_frames",
+        )
+        return int(n.value)
+
+    def last_build_ms(self) -> float:
+        out = ctypes.c_float(0)
+        _check(lib().hvws_last_build_ms(self.ctx, ctypes.byref(out)), "hvws_last_build_ms")
+        return float(out.value)
+
     def digest(self, buf: DeviceBuffer, n: int) -> int:
         out = ctypes.c_uint64(0)
         _check(lib().hvws_digest(self.ctx, buf.ptr, n, ctypes.byref(out)), "hvws_digest")
@@ -360,6 +388,23 @@ class DevicePlan:
 
     def free(self):
         for b in (self.off, self.flags, self.mask, self.length, self.text):
+            if b is not None:
+                b.free()
+
+
+class TxPlan:
+    """Outgoing-frame tables on the device for Engine.build_frames: frame i is
+    websocket_build_frame(flags[i], mask[i], payload + pay_off[i], length[i])."""
+
+    def __init__(self, eng: Engine, pay_off, length, flags, mask=None):
+        self.n = len(length)
+        self.pay_off = eng.to_device(np.asarray(pay_off, dtype=np.uint64))
+        self.length = eng.to_device(np.asarray(length, dtype=np.uint64))
+        self.flags = eng.to_device(np.asarray(flags, dtype=np.uint8))
+        self.mask = eng.to_device(np.asarray(mask, dtype=np.uint32)) if mask is not None else None
+
+    def free(self):
+        for b in (self.pay_off, self.length, self.flags, self.mask):
             if b is not None:
                 b.free()
 

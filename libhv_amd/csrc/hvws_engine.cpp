@@ -83,6 +83,13 @@ struct hbuf {   // grow-only pinned host allocation
 
 }  // namespace
 
+namespace hvws {
+hvws_ctx* thread_ctx();
+}
+
+static_assert(sizeof(drec) == sizeof(hvws_frame), "drec mirrors hvws_frame");
+static_assert(sizeof(dsmall_out) == 64, "dsmall_out layout");
+
 struct hvws_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // compute
@@ -99,16 +106,41 @@ struct hvws_ctx {
     dbuf stage;
     dbuf xor_stage;
     dbuf synth_sizes, synth_tiles, synth_bad;
+    // small-batch path (k_small): upload packet, record slots, pinned results
+    hbuf h_small_in, h_small_out;
+    dbuf d_small_in, d_small_slots;
+    uint64_t small_limit = 0;   // bytes; 0 = default
+    // transmit side (hvws_build_frames)
+    dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat;
+    hbuf h_tx;
+    bool ev_build = false;
     // last scan
     uint32_t nseg = 0;
     uint64_t nfr = 0;
     uint64_t rx_len = 0;
     const uint8_t* rx = nullptr;
     bool have_scan = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // scan, unmask, build
     bool ev_unmask = false;
     int variant = 0;   // k_unmask geometry the tile index was built for
+    bool nfr_known = false;   // else c->nfr is an upper bound, the count is on the device
+    // host copy of the last scan's results (readback_all)
+    hbuf h_readback;
+    bool hcache_valid = false;
+    std::vector<hvws_frame> hcache;
+    std::vector<uint64_t> hfirst, hcount;
+    std::vector<dcarry> hcarry;
 };
+
+namespace {
+constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
+constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
+// Small-batch path (k_small): batches up to kSmallBatch bytes whose segments
+// are each at most kSmallSegment bytes run as one launch.
+constexpr uint64_t kSmallBatch = 64ull << 20;
+constexpr uint64_t kSmallSegment = 1ull << 20;
+constexpr uint64_t kSmallHostRecords = 1ull << 20;   // records returned through pinned memory
+}  // namespace
 
 namespace {
 
@@ -194,12 +226,24 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     HIP_OR(launch_scan(false, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
                        c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->stream),
            HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
-    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
-    const uint64_t nfr = *c->h_total.as<uint64_t>();
-    if (nfr >= 0xFFFFFFF0ull) return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)",
-                                             (unsigned long long)nfr);
-    HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
+    // Frame records are bounded: after a segment's first record every frame
+    // spends >= 2 of its bytes.  When the bound fits the table, EMIT follows
+    // COUNT with no host round trip and the count stays on the device (the
+    // tile kernels and k_unmask read it there); otherwise read the count first.
+    const uint64_t bound = rx_len / 2 + 2 * (uint64_t)nseg + 1;
+    uint64_t nfr = bound;
+    c->nfr_known = false;
+    if (bound <= kFastFrameBound) {
+        HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
+    } else {
+        HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+        nfr = *c->h_total.as<uint64_t>();
+        if (nfr >= 0xFFFFFFF0ull)
+            return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)nfr);
+        HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
+        c->nfr_known = true;
+    }
     HIP_OR(launch_scan(true, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
                        c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->stream),
            HVWS_EHIP);
@@ -209,10 +253,11 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     HIP_OR(c->tile_first.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
     HIP_OR(c->tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
     HIP_OR(c->tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
-    HIP_OR(launch_tile_index(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), nfr, c->tile_first.as<uint32_t>(),
-                             ntiles, tile, c->stream),
+    const uint64_t* nfr_dev = c->total.as<uint64_t>();
+    HIP_OR(launch_tile_index(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), 0, nfr_dev,
+                             c->tile_first.as<uint32_t>(), ntiles, tile, c->stream),
            HVWS_EHIP);
-    HIP_OR(launch_tile_class(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), c->f_keyrot.as<uint32_t>(), nfr,
+    HIP_OR(launch_tile_class(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), c->f_keyrot.as<uint32_t>(), nfr_dev,
                              c->tile_first.as<uint32_t>(), c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(),
                              ntiles, tile, rx_len, c->stream),
            HVWS_EHIP);
@@ -223,6 +268,94 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     c->rx_len = rx_len;
     c->have_scan = true;
     c->ev_unmask = false;
+    c->hcache_valid = false;
+    return HVWS_OK;
+}
+
+// The frame count of the last scan on the host (one small read-back when the
+// scan left it on the device).
+int ensure_count(hvws_ctx* c) {
+    if (c->nfr_known) return HVWS_OK;
+    HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    c->nfr = *c->h_total.as<uint64_t>();
+    c->nfr_known = true;
+    return HVWS_OK;
+}
+
+// Everything a host-side replay needs from the last scan, in one round trip:
+// count, per-segment first/count, carry-out, and the frame table up to the
+// record bound (small batches) -- copied into pinned memory, one sync.
+int readback_all(hvws_ctx* c) {
+    const uint32_t nseg = c->nseg;
+    // c->nfr is the exact count or its bound; copy at most a prefix of the
+    // table with the rest, and the remainder after the sync if needed.
+    const uint64_t nrec = c->nfr < kReadbackPrefix ? c->nfr : kReadbackPrefix;
+    const uint64_t cap = c->nfr_known ? c->nfr : nrec;
+    const uint64_t soa = (cap > nrec ? cap : nrec) * (8 + 8 + 8 + 8 + 4 + 4);
+    const uint64_t need = 64 + (uint64_t)nseg * (16 + sizeof(dcarry)) + soa + 64;
+    HIP_OR(c->h_readback.ensure(need), HVWS_ENOMEM);
+    uint8_t* h = c->h_readback.as<uint8_t>();
+    uint64_t* total = (uint64_t*)h;
+    uint64_t* first = (uint64_t*)(h + 64);
+    uint64_t* count = first + nseg;
+    dcarry* carry = (dcarry*)(count + nseg);
+    hipStream_t s = c->stream;
+    HIP_OR(hipMemcpyAsync(total, c->total.p, 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
+    if (nseg) {
+        HIP_OR(hipMemcpyAsync(first, c->bases.p, (uint64_t)nseg * 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
+        HIP_OR(hipMemcpyAsync(count, c->counts.p, (uint64_t)nseg * 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
+        HIP_OR(hipMemcpyAsync(carry, c->carry_out.p, (uint64_t)nseg * sizeof(dcarry), hipMemcpyDeviceToHost, s),
+               HVWS_EHIP);
+    }
+    // SoA staging sized for `cap` records (exact count known) or the prefix
+    uint64_t room = cap > nrec ? cap : nrec;
+    uint8_t* f = (uint8_t*)(carry + nseg);
+    int64_t* f_hdr = (int64_t*)f;
+    uint64_t* f_off = (uint64_t*)(f_hdr + room);
+    uint64_t* f_len = f_off + room;
+    uint64_t* f_length = f_len + room;
+    uint32_t* f_key = (uint32_t*)(f_length + room);
+    uint32_t* f_info = f_key + room;
+    auto copy_range = [&](uint64_t a, uint64_t b) -> hipError_t {
+        if (b <= a) return hipSuccess;
+        const uint64_t n = b - a;
+        hipError_t e2;
+        if ((e2 = hipMemcpyAsync(f_hdr + a, c->f_hdr.as<int64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
+        if ((e2 = hipMemcpyAsync(f_off + a, c->f_off.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
+        if ((e2 = hipMemcpyAsync(f_len + a, c->f_len.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
+        if ((e2 = hipMemcpyAsync(f_length + a, c->f_length.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s)))
+            return e2;
+        if ((e2 = hipMemcpyAsync(f_key + a, c->f_key.as<uint32_t>() + a, n * 4, hipMemcpyDeviceToHost, s))) return e2;
+        return hipMemcpyAsync(f_info + a, c->f_info.as<uint32_t>() + a, n * 4, hipMemcpyDeviceToHost, s);
+    };
+    HIP_OR(copy_range(0, c->nfr_known ? c->nfr : nrec), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(s), HVWS_EHIP);
+    const uint64_t got = c->nfr_known ? c->nfr : nrec;
+    if (*total > got) {
+        // more records than the speculative prefix: the exact count is known
+        // now, so one more round trip copies the whole table
+        c->nfr = *total;
+        c->nfr_known = true;
+        return readback_all(c);
+    }
+    const uint64_t n = *total;
+    c->nfr = n;
+    c->nfr_known = true;
+    c->hcache.resize(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        hvws_frame& o = c->hcache[i];
+        o.hdr_off = f_hdr[i];
+        o.pay_off = f_off[i];
+        o.pay_len = f_len[i];
+        o.length = f_length[i];
+        o.key = f_key[i];
+        o.info = f_info[i];
+    }
+    c->hfirst.assign(first, first + nseg);
+    c->hcount.assign(count, count + nseg);
+    c->hcarry.assign(carry, carry + nseg);
+    c->hcache_valid = true;
     return HVWS_OK;
 }
 
@@ -257,6 +390,134 @@ int upload_segments(hvws_ctx* c, const hvws_segment* segs, const websocket_parse
            HVWS_EHIP);
     HIP_OR(hipMemcpyAsync(c->carry_in.p, hc, (uint64_t)nseg * sizeof(dcarry), hipMemcpyHostToDevice, c->stream),
            HVWS_EHIP);
+    return HVWS_OK;
+}
+
+// Device-visible address of pinned host memory (nullptr if `p` is not
+// pinned/registered host memory).
+uint8_t* host_mapped(void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return (uint8_t*)a.devicePointer + ((uint8_t*)p - (uint8_t*)a.hostPointer);
+}
+
+template <typename T>
+T* mapped(hbuf& b) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, b.p, 0) != hipSuccess) return nullptr;
+    return reinterpret_cast<T*>(d);
+}
+
+bool small_eligible(hvws_ctx* c, uint64_t len, const hvws_segment* segs, uint32_t nseg) {
+    const uint64_t limit = c->small_limit ? c->small_limit : kSmallBatch;
+    if (c->small_limit == ~0ull || len > limit || nseg == 0) return false;
+    for (uint32_t s = 0; s < nseg; ++s)
+        if (segs[s].len > kSmallSegment) return false;
+    return true;
+}
+
+// hvws_rx_batch for small batches: one H2D copy, k_small, one sync.
+int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* segs, websocket_parser* carry,
+                   uint32_t nseg, int unmask) {
+    for (uint32_t s = 0; s < nseg; ++s) {
+        if (segs[s].off > len || segs[s].len > len - segs[s].off)
+            return set_err(HVWS_EINVAL, "segment %u [%llu,+%llu) outside the %llu-byte buffer", s,
+                           (unsigned long long)segs[s].off, (unsigned long long)segs[s].len, (unsigned long long)len);
+        if (s && segs[s].off < segs[s - 1].off + segs[s - 1].len)
+            return set_err(HVWS_EINVAL, "segments must be sorted and disjoint (segment %u)", s);
+    }
+    // packet: [counter | segs | carry | slot_base | data (256-aligned)]
+    const uint64_t o_segs = 64;
+    const uint64_t o_carry = o_segs + (uint64_t)nseg * sizeof(dseg);
+    const uint64_t o_slot = o_carry + (uint64_t)nseg * sizeof(dcarry);
+    const uint64_t o_data = (o_slot + (uint64_t)nseg * 8 + 255) & ~255ull;
+    uint8_t* user_mapped = host_mapped(h_rx);   // pinned caller buffer: read and write it directly
+    const uint64_t pkt = user_mapped ? o_data : o_data + len;
+    // The pinned packet may still be the source of an in-flight copy.
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    HIP_OR(c->h_small_in.ensure(o_data + len + 64), HVWS_ENOMEM);
+    HIP_OR(c->d_small_in.ensure(o_data + len + 64), HVWS_ENOMEM);
+    uint8_t* hp = c->h_small_in.as<uint8_t>();
+    memset(hp, 0, 64);
+    dseg* hs = (dseg*)(hp + o_segs);
+    dcarry* hc = (dcarry*)(hp + o_carry);
+    uint64_t* hb = (uint64_t*)(hp + o_slot);
+    uint64_t nslots = 0;
+    for (uint32_t s = 0; s < nseg; ++s) {
+        hs[s].off = segs[s].off;
+        hs[s].len = segs[s].len;
+        if (carry) to_dcarry(carry[s], hc[s]);
+        else memset(&hc[s], 0, sizeof(dcarry));
+        hb[s] = nslots;
+        nslots += segs[s].len / 2 + 3;   // carried-in frame + >= 2 bytes per frame + tail
+    }
+    if (!user_mapped && len) memcpy(hp + o_data, h_rx, len);
+    const uint64_t hcap = std::min<uint64_t>(nslots, kSmallHostRecords);
+    HIP_OR(c->d_small_slots.ensure(nslots * sizeof(drec) + 64), HVWS_ENOMEM);
+    HIP_OR(c->h_small_out.ensure((uint64_t)nseg * sizeof(dsmall_out) + hcap * sizeof(drec) + 64), HVWS_ENOMEM);
+    dsmall_out* ho = c->h_small_out.as<dsmall_out>();
+    drec* hr = (drec*)(ho + nseg);
+    dsmall_out* ho_d = mapped<dsmall_out>(c->h_small_out);
+    uint8_t* hp_d = mapped<uint8_t>(c->h_small_in);
+    if (!ho_d || !hp_d) return set_err(HVWS_EHIP, "pinned buffers not device-mapped");
+    uint8_t* d = c->d_small_in.as<uint8_t>();
+    HIP_OR(hipMemcpyAsync(d, hp, pkt, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
+    if (user_mapped && len) HIP_OR(hipMemcpyAsync(d + o_data, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
+    HIP_OR(launch_small(d + o_data, len, (const dseg*)(d + o_segs), (const dcarry*)(d + o_carry), nseg,
+                        (const uint64_t*)(d + o_slot), c->d_small_slots.as<drec>(), (unsigned long long*)d,
+                        (drec*)(ho_d + nseg), hcap, ho_d, user_mapped ? user_mapped : hp_d + o_data, unmask,
+                        c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    if (!user_mapped && unmask && len) memcpy(h_rx, hp + o_data, len);
+    // host cache in segment order
+    uint64_t total = 0;
+    for (uint32_t s = 0; s < nseg; ++s) total += ho[s].count;
+    c->hcache.resize(total);
+    c->hfirst.resize(nseg);
+    c->hcount.resize(nseg);
+    c->hcarry.resize(nseg);
+    const bool on_host = total <= hcap;
+    const drec* slots_base = c->d_small_slots.as<drec>();
+    uint64_t k = 0;
+    for (uint32_t s = 0; s < nseg; ++s) {
+        const uint64_t cnt = ho[s].count;
+        c->hfirst[s] = k;
+        c->hcount[s] = cnt;
+        c->hcarry[s] = ho[s].st;
+        if (cnt) {
+            if (on_host) {
+                memcpy(&c->hcache[k], hr + ho[s].first, cnt * sizeof(drec));
+            } else {
+                HIP_OR(hipMemcpyAsync(&c->hcache[k], slots_base + hb[s], cnt * sizeof(drec), hipMemcpyDeviceToHost,
+                                      c->stream),
+                       HVWS_EHIP);
+            }
+        }
+        k += cnt;
+    }
+    if (!on_host) HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    c->nseg = nseg;
+    c->nfr = total;
+    c->nfr_known = true;
+    c->rx = nullptr;   // the device frame table is not populated: hvws_unmask refuses
+    c->rx_len = 0;
+    c->have_scan = true;
+    c->ev_unmask = false;
+    c->hcache_valid = true;
+    if (carry) {
+        for (uint32_t s = 0; s < nseg; ++s) {
+            void* keep = carry[s].data;
+            from_dcarry(c->hcarry[s], carry[s]);
+            carry[s].data = keep;
+        }
+    }
     return HVWS_OK;
 }
 
@@ -318,8 +579,12 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         b->release();
     for (dbuf* b : {&c->segs, &c->carry_in, &c->carry_out, &c->counts, &c->bases, &c->total, &c->f_hdr, &c->f_off,
                     &c->f_len, &c->f_length, &c->f_key, &c->f_keyrot, &c->f_info, &c->tile_first, &c->tile_key, &c->tile_kind, &c->stage,
-                    &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad})
+                    &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad, &c->tx_size, &c->tx_off,
+                    &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->d_small_in, &c->d_small_slots})
         b->release();
+    c->h_tx.release();
+    c->h_small_in.release();
+    c->h_small_out.release();
     c->h_segs.release();
     c->h_carry.release();
     c->h_total.release();
@@ -415,7 +680,7 @@ int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
         return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
     HIP_OR(hipEventRecord(c->ev[2], c->stream), HVWS_EHIP);
     HIP_OR(launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(),
-                         c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->nfr, c->stream),
+                         c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->total.as<uint64_t>(), c->stream),
            HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[3], c->stream), HVWS_EHIP);
     c->ev_unmask = true;
@@ -431,6 +696,7 @@ int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* s
 
 int64_t hvws_frame_count(hvws_ctx* c) {
     if (!c || !c->have_scan) return -1;
+    if (check_ctx(c) != HVWS_OK || ensure_count(c) != HVWS_OK) return -1;
     return (int64_t)c->nfr;
 }
 
@@ -438,8 +704,13 @@ int hvws_get_frames(hvws_ctx* c, hvws_frame* out, uint64_t first, uint64_t n) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    if ((rc = ensure_count(c)) != HVWS_OK) return rc;
     if (first > c->nfr || n > c->nfr - first) return set_err(HVWS_EINVAL, "frame range out of bounds");
     if (n == 0) return HVWS_OK;
+    if (c->hcache_valid) {
+        memcpy(out, c->hcache.data() + first, n * sizeof(hvws_frame));
+        return HVWS_OK;
+    }
     std::vector<int64_t> hdr(n);
     std::vector<uint64_t> off(n), len(n), length(n);
     std::vector<uint32_t> key(n), info(n);
@@ -472,6 +743,11 @@ int hvws_get_segment_frames(hvws_ctx* c, uint64_t* first, uint64_t* count) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    if (c->hcache_valid) {
+        if (first) memcpy(first, c->hfirst.data(), (uint64_t)c->nseg * 8);
+        if (count) memcpy(count, c->hcount.data(), (uint64_t)c->nseg * 8);
+        return HVWS_OK;
+    }
     if (first)
         HIP_OR(hipMemcpyAsync(first, c->bases.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
                HVWS_EHIP);
@@ -486,15 +762,22 @@ int hvws_get_carry(hvws_ctx* c, websocket_parser* out, int* started) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
-    std::vector<dcarry> h(c->nseg);
-    if (c->nseg)
-        HIP_OR(hipMemcpyAsync(h.data(), c->carry_out.p, (uint64_t)c->nseg * sizeof(dcarry),
-                              hipMemcpyDeviceToHost, c->stream),
-               HVWS_EHIP);
-    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    std::vector<dcarry> h;
+    const dcarry* src;
+    if (c->hcache_valid) {
+        src = c->hcarry.data();
+    } else {
+        h.resize(c->nseg);
+        if (c->nseg)
+            HIP_OR(hipMemcpyAsync(h.data(), c->carry_out.p, (uint64_t)c->nseg * sizeof(dcarry),
+                                  hipMemcpyDeviceToHost, c->stream),
+                   HVWS_EHIP);
+        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+        src = h.data();
+    }
     for (uint32_t s = 0; s < c->nseg; ++s) {
-        if (out) from_dcarry(h[s], out[s]);
-        if (started) started[s] = (int)h[s].started;
+        if (out) from_dcarry(src[s], out[s]);
+        if (started) started[s] = (int)src[s].started;
     }
     return HVWS_OK;
 }
@@ -525,6 +808,8 @@ int hvws_rx_batch(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* 
                   uint32_t nseg, int unmask) {
     int rc = check_ctx(c);
     if (rc) return rc;
+    if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
+    if (small_eligible(c, len, segs, nseg)) return rx_batch_small(c, h_rx, len, segs, carry, nseg, unmask);
     HIP_OR(c->stage.ensure(len + 64), HVWS_ENOMEM);
     uint8_t* d = c->stage.as<uint8_t>();
     if ((rc = upload_segments(c, segs, carry, nseg, len)) != HVWS_OK) return rc;
@@ -534,13 +819,14 @@ int hvws_rx_batch(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* 
         if ((rc = hvws_unmask(c, d, len)) != HVWS_OK) return rc;
         if (len) HIP_OR(hipMemcpyAsync(h_rx, d, len, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     }
-    std::vector<void*> keep(nseg);
-    for (uint32_t s = 0; s < nseg; ++s) keep[s] = carry ? carry[s].data : nullptr;
+    // one round trip for the results (the D2H of the bytes above is ordered before it)
+    if ((rc = readback_all(c)) != HVWS_OK) return rc;
     if (carry) {
-        if ((rc = hvws_get_carry(c, carry, nullptr)) != HVWS_OK) return rc;
-        for (uint32_t s = 0; s < nseg; ++s) carry[s].data = keep[s];
-    } else {
-        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+        for (uint32_t s = 0; s < nseg; ++s) {
+            void* keep = carry[s].data;
+            from_dcarry(c->hcarry[s], carry[s]);
+            carry[s].data = keep;
+        }
     }
     return HVWS_OK;
 }
@@ -645,7 +931,7 @@ int hvws_synth(hvws_ctx* c, uint8_t* d_buf, uint64_t buf_len, uint64_t seed, uin
     HIP_OR(c->synth_tiles.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
     HIP_OR(c->synth_bad.ensure(8), HVWS_ENOMEM);
     HIP_OR(launch_frame_sizes(d_flags, d_length, nframes, c->synth_sizes.as<uint64_t>(), c->stream), HVWS_EHIP);
-    HIP_OR(launch_tile_index(d_frame_off, c->synth_sizes.as<uint64_t>(), nframes, c->synth_tiles.as<uint32_t>(),
+    HIP_OR(launch_tile_index(d_frame_off, c->synth_sizes.as<uint64_t>(), nframes, nullptr, c->synth_tiles.as<uint32_t>(),
                              ntiles, tile, c->stream),
            HVWS_EHIP);
     HIP_OR(hipMemsetAsync(c->synth_bad.p, 0, 8, c->stream), HVWS_EHIP);
@@ -673,6 +959,75 @@ int hvws_digest(hvws_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* out) 
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (out) *out = v;
     return HVWS_OK;
+}
+
+// --------------------------------------------------------------- transmit
+int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8_t* d_payload, uint64_t payload_len,
+                      const uint64_t* d_pay_off, const uint64_t* d_len, const uint8_t* d_flags, const uint32_t* d_mask,
+                      uint64_t n, uint64_t* d_out_off, uint64_t* out_len) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (out_len) *out_len = 0;
+    if (n == 0) return HVWS_OK;
+    if (!d_out || !d_pay_off || !d_len || !d_flags) return set_err(HVWS_EINVAL, "build_frames: null table");
+    if (n >= 0xFFFFFFFFull) return set_err(HVWS_EINVAL, "build_frames: %llu frames (max 2^32-2)", (unsigned long long)n);
+    const uint64_t nb = (n + 1023) / 1024;
+    HIP_OR(c->tx_size.ensure(n * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->tx_scan.ensure((4 * nb + 64) * 8), HVWS_ENOMEM);
+    HIP_OR(c->tx_stat.ensure(16), HVWS_ENOMEM);
+    HIP_OR(c->h_tx.ensure(16), HVWS_ENOMEM);
+    uint64_t* off = d_out_off;
+    if (!off) {
+        HIP_OR(c->tx_off.ensure(n * 8 + 8), HVWS_ENOMEM);
+        off = c->tx_off.as<uint64_t>();
+    }
+    uint64_t* stat = c->tx_stat.as<uint64_t>();   // [0] total bytes, [1] payload ranges out of bounds
+    HIP_OR(hipMemsetAsync(stat, 0, 16, c->stream), HVWS_EHIP);
+    HIP_OR(launch_frame_sizes(d_flags, d_len, n, c->tx_size.as<uint64_t>(), c->stream), HVWS_EHIP);
+    HIP_OR(launch_exclusive_scan(c->tx_size.as<uint64_t>(), off, n, c->tx_scan.as<uint64_t>(), stat, c->stream),
+           HVWS_EHIP);
+    HIP_OR(launch_tx_check(d_pay_off, d_len, d_flags, d_mask, n, payload_len, stat + 1, c->stream), HVWS_EHIP);
+    uint64_t* h = c->h_tx.as<uint64_t>();
+    HIP_OR(hipMemcpyAsync(h, stat, 16, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    if (h[1]) return set_err(HVWS_EINVAL, "build_frames: %llu frames read outside the payload buffer or lack a mask",
+                             (unsigned long long)h[1]);
+    const uint64_t total = h[0];
+    if (out_len) *out_len = total;
+    if (total > out_cap)
+        return set_err(HVWS_EINVAL, "build_frames: output needs %llu bytes, capacity %llu", (unsigned long long)total,
+                       (unsigned long long)out_cap);
+    const uint64_t tile = tx_tile();
+    const uint64_t ntiles = (total + tile - 1) / tile;
+    HIP_OR(c->tx_tiles.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(launch_tile_index(off, c->tx_size.as<uint64_t>(), n, nullptr, c->tx_tiles.as<uint32_t>(), ntiles, tile,
+                             c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
+    HIP_OR(launch_build(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
+                        c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), n, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
+    c->ev_build = true;
+    return HVWS_OK;
+}
+
+int hvws_last_build_ms(hvws_ctx* c, float* ms) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->ev_build) return set_err(HVWS_EINVAL, "no build_frames call yet");
+    HIP_OR(hipEventSynchronize(c->ev[5]), HVWS_EHIP);
+    HIP_OR(hipEventElapsedTime(ms, c->ev[4], c->ev[5]), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+const char* hvws_build_kernel_name(void) { return build_kernel_name(); }
+
+uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
+    if (!c) c = hvws::thread_ctx();   // the calling thread's reference-API context
+    const uint64_t old = c->small_limit ? c->small_limit : kSmallBatch;
+    c->small_limit = bytes;
+    return old;
 }
 
 const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant()); }

@@ -51,6 +51,23 @@ struct dframes {
     uint32_t* info;
 };
 
+// One frame record as handed to the host (layout of hvws_frame, 40 bytes).
+struct drec {
+    int64_t  hdr_off;
+    uint64_t pay_off;
+    uint64_t pay_len;
+    uint64_t length;
+    uint32_t key;
+    uint32_t info;
+};
+
+// Per-segment result of the small-batch kernel, written to pinned host memory.
+struct dsmall_out {
+    uint64_t first;   // index of the segment's first record in the host record area
+    uint64_t count;
+    dcarry   st;      // carry out
+};
+
 constexpr int SCAN_THREADS = 256;           // 4 waves, one segment per wave
 constexpr int SCAN_U = 4;                   // predicted frames per lane per round
 constexpr int UNMASK_MAXF = 512;            // frames staged in LDS per tile
@@ -64,6 +81,14 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint64_t* total_pred;
 };
 
+// Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
+// b+16, ... to one XCD; map them to adjacent tiles so each XCD's L2 and
+// memory channels see one contiguous range.
+__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
+    const uint64_t q = ntiles >> 3, r = ntiles & 7u, x = b & 7u, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // Kernel launchers (hvws_kernels.hip).
 // COUNT pass (emit=false): counts[], bases[] (exclusive scan) and *total.
 // EMIT pass: frame table at bases[], carry_out[].
@@ -72,8 +97,15 @@ hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg
                        uint64_t* total, scan_scratch sc, dframes fr, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
-hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
-                             uint64_t ntiles, uint64_t tile, hipStream_t st);
+hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
+                             uint32_t* tile_first, uint64_t ntiles, uint64_t tile, hipStream_t st);
+// Small batches, whole path in one launch (one wave per segment): records
+// into slots[slot_base[s]..], then compacted into h_rec (pinned host) when
+// they fit h_rec_cap; results into h_out[s]; unmasked chunks into h_rx
+// (pinned host, same layout as rx).  *rec_total must be 0 on entry.
+hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
+                        const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
+                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, hipStream_t st);
 // k_unmask geometry variants (threads x chunks/thread, XCD-ordered tiles)
 int unmask_variant();                      // process default ($HVWS_UNMASK or 0)
 int set_unmask_variant(int v);             // -1 if out of range
@@ -81,8 +113,8 @@ int unmask_variant_count();
 uint64_t unmask_tile(int variant);         // bytes per workgroup tile
 const char* unmask_name(int variant);
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
-                         const uint32_t* tile_key, const uint8_t* tile_kind, uint64_t nfr, hipStream_t st);
-hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, uint64_t nfr,
+                         const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st);
+hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
                              const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
                              uint64_t tile, uint64_t rx_len, hipStream_t st);
 hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
@@ -98,5 +130,18 @@ hipError_t launch_digest(const uint8_t* buf, uint64_t len, unsigned long long* o
 hipError_t launch_frame_sizes(const uint8_t* flags, const uint64_t* length, uint64_t nframes,
                               uint64_t* out, hipStream_t st);
 uint64_t synth_tile();
+
+// Transmit side (hvws_tx.hip).
+// out[i] = sum(in[0..i)), *total = sum(in); tmp >= 4 * ceil(n / 1024) + 64 words.
+hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp, uint64_t* total,
+                                 hipStream_t st);
+// *bad += frames whose payload range leaves [0, plen) or that are masked without a key table.
+hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
+                           uint64_t n, uint64_t plen, uint64_t* bad, hipStream_t st);
+uint64_t tx_tile();   // output bytes per k_build workgroup
+const char* build_kernel_name();   // k_build geometry in use ($HVWS_BUILD)
+hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
+                        const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
+                        const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st);
 
 }  // namespace hvws

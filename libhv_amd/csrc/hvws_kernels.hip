@@ -431,6 +431,108 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
     }
 }
 
+// Whole frames from segment offset `pos` on (wave-wide speculative walk,
+// 64 x SCAN_U predictions per round), then the exact state machine for the
+// frame cut by the segment end.  Advances st/pos/n; emit(idx, rec) is called
+// (EMIT only) by the lane owning record idx of the segment.
+template <bool EMIT, typename Emit>
+__device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint64_t rx_len, uint64_t sb, uint64_t L,
+                                            dcarry& st, uint64_t& pos, uint64_t& n, Emit&& emit) {
+    const uint32_t lane = threadIdx.x & 63u;
+    constexpr uint32_t NPRED = 64u * SCAN_U;
+    uint64_t stride = 0;
+    while (st.state == S_START && pos < L) {
+        const uint64_t rem = L - pos;
+        if (stride == 0) {
+            hdr h0;
+            if (!parse_at(rx, rx_len, sb, L, pos, h0)) break;   // incomplete: tail
+            stride = (uint64_t)h0.hlen + h0.length;
+        }
+        uint64_t lo[SCAN_U], hi[SCAN_U];
+        bool inr[SCAN_U];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; ++u) {
+            const uint32_t j = (uint32_t)u * 64u + lane;
+            inr[u] = rem >= 2 && (j == 0 || stride <= (rem - 2) / j);
+            lo[u] = hi[u] = 0;
+            if (inr[u]) ld16(rx, rx_len, sb + pos + (uint64_t)j * stride, lo[u], hi[u]);
+        }
+        hdr h[SCAN_U];
+        bool whole[SCAN_U];
+        uint32_t f = NPRED;
+#pragma unroll
+        for (int u = 0; u < SCAN_U; ++u) {
+            const uint32_t j = (uint32_t)u * 64u + lane;
+            const uint64_t q = pos + (uint64_t)j * stride;
+            h[u] = parse_hdr(lo[u], hi[u]);
+            const uint64_t rq = inr[u] ? L - q : 0;
+            whole[u] = inr[u] && h[u].hlen <= rq && h[u].length <= rq - h[u].hlen;
+            const bool ok = whole[u] && (uint64_t)h[u].hlen + h[u].length == stride;
+            const unsigned long long bad = __ballot(!ok);
+            if (f == NPRED && bad) f = (uint32_t)u * 64u + (uint32_t)(__ffsll((long long)bad) - 1);
+        }
+        uint32_t last_flags = 0, last_key = 0;
+        uint64_t last_len = 0;
+        bool any_masked = false;
+#pragma unroll
+        for (int u = 0; u < SCAN_U; ++u) {
+            const uint32_t j = (uint32_t)u * 64u + lane;
+            const bool mine = j < f;
+            if (EMIT && mine) {
+                frec v;
+                whole_frame_rec(v, pos + (uint64_t)j * stride, h[u]);
+                emit(n + j, v);
+            }
+            const unsigned long long mm = __ballot(mine && (h[u].flags & F_MASK));
+            if (mm) {
+                const int src = 63 - __clzll((long long)mm);
+                last_key = __shfl(h[u].key, src);
+                any_masked = true;
+            }
+            if (f > (uint32_t)u * 64u && f <= (uint32_t)u * 64u + 64u) {
+                const int src = (int)(f - 1 - (uint32_t)u * 64u);
+                last_flags = __shfl(h[u].flags, src);
+                last_len = __shfl(h[u].length, src);
+            }
+        }
+        if (f > 0) {
+            st.flags = last_flags;   // Q14: the last frame's fields persist
+            st.length = last_len;
+            st.require = 0;
+            st.offset = 0;
+            st.mask_offset = (last_flags & F_MASK) ? (uint32_t)(last_len & 3u) : 0u;
+            st.started = 0;
+            if (any_masked) st.mask = last_key;
+        }
+        n += f;
+        pos += (uint64_t)f * stride;
+        if (f == NPRED) continue;
+        if (pos >= L) break;
+        bool wf = false;
+        uint64_t sf = 0;
+        const uint32_t uf = f >> 6, lf = f & 63u;
+#pragma unroll
+        for (int u = 0; u < SCAN_U; ++u) {
+            const bool w = __shfl((int)whole[u], (int)lf) != 0;
+            const uint64_t sz = __shfl((uint64_t)h[u].hlen + h[u].length, (int)lf);
+            if ((uint32_t)u == uf) {
+                wf = w;
+                sf = sz;
+            }
+        }
+        if (!wf) break;
+        stride = sf;
+    }
+
+    if (st.state == S_START && pos < L) {   // frame cut by the segment end
+        frec r;
+        if (scalar_frame(rx + sb, L, st, pos, r)) {
+            if (EMIT && lane == 0) emit(n, r);
+            ++n;
+        }
+    }
+}
+
 // ----------------------------------------------------------------- k_walk
 template <bool EMIT>
 __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict__ rx, uint64_t rx_len,
@@ -443,18 +545,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ bases, dframes fr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
-    constexpr uint32_t NPRED = 64u * SCAN_U;
 
     for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
         const uint64_t sb = segs[s].off;
         const uint64_t L = segs[s].len;
-        const uint8_t* seg = rx + sb;
         const dmid m = mid[s];
         dcarry st = m.st;
         uint64_t pos = m.pos;
         uint64_t n = m.n_a;
         const uint64_t obase = EMIT ? bases[s] : 0;
-        frec r;
 
         // Skip the prefix k_verify proved; restore the fields the reference
         // leaves behind after its last frame (Q14).
@@ -477,101 +576,127 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
             }
         }
 
-        uint64_t stride = 0;
-        while (st.state == S_START && pos < L) {
-            const uint64_t rem = L - pos;
-            if (stride == 0) {
-                hdr h0;
-                if (!parse_at(rx, rx_len, sb, L, pos, h0)) break;   // incomplete: tail
-                stride = (uint64_t)h0.hlen + h0.length;
-            }
-            uint64_t lo[SCAN_U], hi[SCAN_U];
-            bool inr[SCAN_U];
-#pragma unroll
-            for (int u = 0; u < SCAN_U; ++u) {
-                const uint32_t j = (uint32_t)u * 64u + lane;
-                inr[u] = rem >= 2 && (j == 0 || stride <= (rem - 2) / j);
-                lo[u] = hi[u] = 0;
-                if (inr[u]) ld16(rx, rx_len, sb + pos + (uint64_t)j * stride, lo[u], hi[u]);
-            }
-            hdr h[SCAN_U];
-            bool whole[SCAN_U];
-            uint32_t f = NPRED;
-#pragma unroll
-            for (int u = 0; u < SCAN_U; ++u) {
-                const uint32_t j = (uint32_t)u * 64u + lane;
-                const uint64_t q = pos + (uint64_t)j * stride;
-                h[u] = parse_hdr(lo[u], hi[u]);
-                const uint64_t rq = inr[u] ? L - q : 0;
-                whole[u] = inr[u] && h[u].hlen <= rq && h[u].length <= rq - h[u].hlen;
-                const bool ok = whole[u] && (uint64_t)h[u].hlen + h[u].length == stride;
-                const unsigned long long bad = __ballot(!ok);
-                if (f == NPRED && bad) f = (uint32_t)u * 64u + (uint32_t)(__ffsll((long long)bad) - 1);
-            }
-            uint32_t last_flags = 0, last_key = 0;
-            uint64_t last_len = 0;
-            bool any_masked = false;
-#pragma unroll
-            for (int u = 0; u < SCAN_U; ++u) {
-                const uint32_t j = (uint32_t)u * 64u + lane;
-                const bool mine = j < f;
-                if (EMIT && mine) {
-                    frec v;
-                    whole_frame_rec(v, pos + (uint64_t)j * stride, h[u]);
-                    store_frame(fr, obase + n + j, sb, v);
-                }
-                const unsigned long long mm = __ballot(mine && (h[u].flags & F_MASK));
-                if (mm) {
-                    const int src = 63 - __clzll((long long)mm);
-                    last_key = __shfl(h[u].key, src);
-                    any_masked = true;
-                }
-                if (f > (uint32_t)u * 64u && f <= (uint32_t)u * 64u + 64u) {
-                    const int src = (int)(f - 1 - (uint32_t)u * 64u);
-                    last_flags = __shfl(h[u].flags, src);
-                    last_len = __shfl(h[u].length, src);
-                }
-            }
-            if (f > 0) {
-                st.flags = last_flags;   // Q14: the last frame's fields persist
-                st.length = last_len;
-                st.require = 0;
-                st.offset = 0;
-                st.mask_offset = (last_flags & F_MASK) ? (uint32_t)(last_len & 3u) : 0u;
-                st.started = 0;
-                if (any_masked) st.mask = last_key;
-            }
-            n += f;
-            pos += (uint64_t)f * stride;
-            if (f == NPRED) continue;
-            if (pos >= L) break;
-            bool wf = false;
-            uint64_t sf = 0;
-            const uint32_t uf = f >> 6, lf = f & 63u;
-#pragma unroll
-            for (int u = 0; u < SCAN_U; ++u) {
-                const bool w = __shfl((int)whole[u], (int)lf) != 0;
-                const uint64_t sz = __shfl((uint64_t)h[u].hlen + h[u].length, (int)lf);
-                if ((uint32_t)u == uf) {
-                    wf = w;
-                    sf = sz;
-                }
-            }
-            if (!wf) break;
-            stride = sf;
-        }
-
-        if (st.state == S_START && pos < L) {   // frame cut by the segment end
-            if (scalar_frame(seg, L, st, pos, r)) {
-                if (EMIT && lane == 0) store_frame(fr, obase + n, sb, r);
-                ++n;
-            }
-        }
+        walk_frames<EMIT>(rx, rx_len, sb, L, st, pos, n,
+                          [&](uint64_t idx, const frec& v) { store_frame(fr, obase + idx, sb, v); });
         if (lane == 0) {
             if (!EMIT) counts[s] = n;
             else carry_out[s] = st;
         }
     }
+}
+
+// ----------------------------------------------------------------- k_small
+//
+// Small batches (an event loop's reads, FeedRecvData): one wavefront per
+// segment runs the whole hot path in a single launch -- the carried-in frame
+// (exact state machine), the speculative walk and the tail (the same device
+// code as the COUNT/EMIT kernels), records into a slot the host sized from the
+// segment length, then the XOR of the segment's masked payload bytes -- and
+// writes its results straight into pinned host memory: the changed 16-byte
+// chunks, the records (compacted by one atomic per segment), the count and the
+// carry.  One H2D copy, one launch and one sync replace the ~15 operations of
+// the general path, whose fixed cost dominates reads of a few KiB.
+__global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                              const dseg* __restrict__ segs, const dcarry* __restrict__ carry_in,
+                                              const uint64_t* __restrict__ slot_base, drec* __restrict__ slots,
+                                              unsigned long long* __restrict__ rec_total, drec* __restrict__ h_rec,
+                                              uint64_t h_rec_cap, dsmall_out* __restrict__ h_out,
+                                              uint8_t* __restrict__ h_rx, int unmask) {
+    const uint32_t s = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t sb = segs[s].off, L = segs[s].len;
+    drec* slot = slots + slot_base[s];
+    dcarry st = carry_in[s];
+    st.started = 0;
+    uint64_t pos = 0, n = 0;
+    auto emit = [&](uint64_t idx, const frec& v) {
+        drec o;
+        o.hdr_off = v.hdr_off < 0 ? -1 : (int64_t)(sb + (uint64_t)v.hdr_off);
+        o.pay_off = sb + v.pay_off;
+        o.pay_len = v.pay_len;
+        o.length = v.length;
+        o.key = v.key;
+        o.info = v.info;
+        slot[idx] = o;
+    };
+    if (st.state != S_START) {
+        frec r;
+        if (scalar_frame(rx + sb, L, st, pos, r)) {
+            if (lane == 0) emit(0, r);
+            n = 1;
+        }
+    }
+    walk_frames<true>(rx, rx_len, sb, L, st, pos, n, emit);
+    __threadfence_block();
+    __syncthreads();
+
+    if (unmask && n) {
+        const uint64_t se = sb + L;
+        for (uint64_t c = (sb & ~15ull) + (uint64_t)lane * 16u; c < se; c += 64u * 16u) {
+            uint64_t k = 0, k_end = n;   // first record whose payload ends after c
+            while (k < k_end) {
+                const uint64_t mid = (k + k_end) >> 1;
+                if (slot[mid].pay_off + slot[mid].pay_len > c) k_end = mid;
+                else k = mid + 1;
+            }
+            uint64_t mlo = 0, mhi = 0;
+            for (; k < n; ++k) {
+                const drec f = slot[k];
+                if (f.pay_off >= c + 16) break;
+                if (!(f.info & F_MASK) || f.pay_len == 0) continue;
+                const uint32_t phase = (f.info >> 8) & 3u;
+                const uint64_t pe = f.pay_off + f.pay_len;
+                if (f.pay_off <= c && c + 16 <= pe) {   // whole chunk inside this payload
+                    const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + (c - f.pay_off)) & 3u));
+                    mlo = mhi = (uint64_t)kw | ((uint64_t)kw << 32);
+                    break;
+                }
+                const uint64_t a = f.pay_off > c ? f.pay_off : c;
+                const uint64_t e = pe < c + 16 ? pe : c + 16;
+                for (uint64_t x = a; x < e; ++x) {
+                    const uint64_t kb = (f.key >> (8u * (uint32_t)((phase + (x - f.pay_off)) & 3u))) & 0xFFu;
+                    const uint32_t b = (uint32_t)(x - c);
+                    if (b < 8) mlo |= kb << (8 * b);
+                    else mhi |= kb << (8 * (b - 8));
+                }
+            }
+            if (!(mlo | mhi)) continue;   // no masked byte (or a zero key): bytes unchanged
+            if (c >= sb && c + 16 <= se) {
+                u32x4 v = *reinterpret_cast<const u32x4*>(rx + c);
+                v ^= u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+                *reinterpret_cast<u32x4*>(h_rx + c) = v;
+            } else {   // chunk shared with a neighbouring segment: own bytes only
+                for (uint32_t b = 0; b < 16; ++b) {
+                    const uint64_t x = c + b;
+                    if (x < sb || x >= se) continue;
+                    const uint32_t kb = (uint32_t)((b < 8 ? mlo >> (8 * b) : mhi >> (8 * (b - 8))) & 0xFFu);
+                    if (kb) h_rx[x] = rx[x] ^ (uint8_t)kb;
+                }
+            }
+        }
+    }
+
+    uint64_t base = 0;
+    if (lane == 0 && n) base = atomicAdd(rec_total, (unsigned long long)n);
+    base = __shfl(base, 0);
+    if (base + n <= h_rec_cap)
+        for (uint64_t i = lane; i < n; i += 64) h_rec[base + i] = slot[i];
+    if (lane == 0) {
+        dsmall_out o;
+        o.first = base;
+        o.count = n;
+        o.st = st;
+        h_out[s] = o;
+    }
+}
+
+hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
+                        const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
+                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_small, dim3(nseg), dim3(64), 0, st, rx, rx_len, segs, carry_in, slot_base, slots, rec_total,
+                       h_rec, h_rec_cap, h_out, h_rx, unmask);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------- k_offsets
@@ -605,11 +730,14 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ c
 
 // ---------------------------------------------------------- k_tile_index
 // tile_first[t] = first frame k with off[k] + len[k] > t*tile (t <= ntiles).
+// nfr_p (device) overrides nfr_v when given: the frame count of a batch can
+// stay on the device, so a small batch needs no host round trip before EMIT.
 __global__ void k_tile_index(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
-                             uint64_t nfr, uint32_t* __restrict__ tile_first, uint64_t ntiles,
-                             uint64_t tile) {
+                             uint64_t nfr_v, const uint64_t* __restrict__ nfr_p, uint32_t* __restrict__ tile_first,
+                             uint64_t ntiles, uint64_t tile) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
+    const uint64_t nfr = nfr_p ? *nfr_p : nfr_v;
     const uint64_t x = t * tile;
     uint64_t lo = 0, hi = nfr;
     while (lo < hi) {
@@ -626,11 +754,12 @@ __global__ void k_tile_index(const uint64_t* __restrict__ off, const uint64_t* _
 enum : uint32_t { TILE_GENERAL = 0, TILE_SINGLE = 1, TILE_NONE = 2 };
 
 __global__ void k_tile_class(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
-                             const uint32_t* __restrict__ keyrot, uint64_t nfr,
+                             const uint32_t* __restrict__ keyrot, const uint64_t* __restrict__ nfr_p,
                              const uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
                              uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile, uint64_t rx_len) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
+    const uint64_t nfr = *nfr_p;
     const uint64_t x = t * tile;
     const uint64_t xe = x + tile < rx_len ? x + tile : rx_len;
     const uint32_t k = tile_first[t];
@@ -713,12 +842,8 @@ __device__ __forceinline__ bool xor_chunk(u32x4& v, uint64_t c, uint32_t nf, OFF
     return true;
 }
 
-// Bijective XCD-contiguous tile order (cdna_hip_programming.md sec. 5, "XCD
-// swizzle must be bijective").  Placement only changes speed, never results.
-__device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
-    const uint64_t q = ntiles >> 3, r = ntiles & 7u, x = b & 7u, i = b >> 3;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
+// Tiles are visited in xcd_tile order (hvws_internal.h; cdna_hip_programming.md
+// sec. 5, "XCD swizzle must be bijective").  Placement only changes speed.
 
 template <int T, int U, bool SWZ>
 __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t rx_len,
@@ -727,8 +852,8 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
                                               const uint32_t* __restrict__ keyrot,
                                               const uint32_t* __restrict__ tile_first,
                                               const uint32_t* __restrict__ tile_key,
-                                              const uint8_t* __restrict__ tile_kind, uint64_t nfr,
-                                              uint64_t tile0, uint64_t ntiles) {
+                                              const uint8_t* __restrict__ tile_kind,
+                                              const uint64_t* __restrict__ nfr_p, uint64_t tile0, uint64_t ntiles) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     __shared__ uint64_t s_off[UNMASK_MAXF];
     __shared__ uint64_t s_end[UNMASK_MAXF];
@@ -770,6 +895,7 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
         }
     }
 
+    const uint64_t nfr = *nfr_p;
     const uint32_t k0 = tile_first[t];
     const uint32_t k1r = tile_first[t + 1];
     const uint32_t k1 = (uint64_t)k1r + 1 < nfr ? k1r + 1 : (uint32_t)nfr;
@@ -910,20 +1036,20 @@ hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg
     return hipGetLastError();
 }
 
-hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
-                             uint64_t ntiles, uint64_t tile, hipStream_t st) {
+hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
+                             uint32_t* tile_first, uint64_t ntiles, uint64_t tile, hipStream_t st) {
     const uint64_t n = ntiles + 1;
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_tile_index, dim3(blocks), dim3(256), 0, st, off, len, nfr, tile_first, ntiles, tile);
+    hipLaunchKernelGGL(k_tile_index, dim3(blocks), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, uint64_t nfr,
+hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
                              const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
                              uint64_t tile, uint64_t rx_len, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)((ntiles + 255) / 256);
-    hipLaunchKernelGGL(k_tile_class, dim3(blocks), dim3(256), 0, st, off, len, keyrot, nfr, tile_first, tile_key,
+    hipLaunchKernelGGL(k_tile_class, dim3(blocks), dim3(256), 0, st, off, len, keyrot, nfr_dev, tile_first, tile_key,
                        tile_kind, ntiles, tile, rx_len);
     return hipGetLastError();
 }
@@ -990,8 +1116,8 @@ static uint64_t max_tiles_per_launch(int threads) {
 }
 
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
-                         const uint32_t* tile_key, const uint8_t* tile_kind, uint64_t nfr, hipStream_t st) {
-    if (rx_len == 0 || nfr == 0) return hipSuccess;
+                         const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st) {
+    if (rx_len == 0) return hipSuccess;
     if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
     const uint64_t tile = unmask_tile(variant);
     const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
@@ -1001,7 +1127,7 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
 #define HVWS_K k_unmask
 #define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, fr.keyrot, \
-                  tile_first, tile_key, tile_kind, nfr, tile0, ntiles
+                  tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
         switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
 #undef HVWS_K
 #undef HVWS_ARGS

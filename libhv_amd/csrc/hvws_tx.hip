@@ -1,0 +1,337 @@
+// hvws_tx.hip -- transmit side: build many frames
+// back to back on the device, byte-identical to the reference's
+// websocket_build_frame (http/websocket_parser.c:207-256): header, optional
+// key, payload XOR-masked from phase 0 (websocket_encode = websocket_decode,
+// http/websocket_parser.h:84).  The same rotating-key XOR as k_unmask, run
+// out of place from a payload buffer into the frame buffer.
+#include <stdlib.h>
+
+#include "hvws_internal.h"
+
+namespace hvws {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t tx_hdr_len(uint32_t flags, uint64_t n) {
+    const uint32_t ext = n < 126 ? 0u : (n <= 0xFFFFu ? 2u : 8u);
+    return 2u + ext + ((flags & F_MASK) ? 4u : 0u);
+}
+
+// Byte h of a frame header (flags: websocket_flags, n payload bytes, key);
+// layout of http/websocket_parser.c:215-246.
+__device__ __forceinline__ uint32_t tx_hdr_byte(uint32_t flags, uint64_t n, uint32_t key, uint32_t h) {
+    const uint32_t ext = n < 126 ? 0u : (n <= 0xFFFFu ? 2u : 8u);
+    if (h == 0) return ((flags & F_FIN) ? 0x80u : 0u) | (flags & F_OPMASK);
+    if (h == 1) return ((flags & F_MASK) ? 0x80u : 0u) | (n < 126 ? (uint32_t)n : (ext == 2 ? 126u : 127u));
+    if (h < 2 + ext) return (uint32_t)(n >> (8 * (ext - 1 - (h - 2)))) & 0xFFu;
+    return (key >> (8 * (h - 2 - ext))) & 0xFFu;
+}
+
+// ---- device-wide exclusive scan of u64 (block sums, scan of sums, add) ----
+constexpr int SCAN_B = 1024;
+
+__global__ __launch_bounds__(SCAN_B) void k_scan_blocks(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                        uint64_t n, uint64_t* __restrict__ block_sums) {
+    __shared__ uint64_t s[SCAN_B];
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
+    const uint64_t v = i < n ? in[i] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < SCAN_B; d <<= 1) {
+        const uint64_t a = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+        __syncthreads();
+        s[threadIdx.x] += a;
+        __syncthreads();
+    }
+    if (i < n) out[i] = s[threadIdx.x] - v;   // exclusive within the block
+    if (threadIdx.x == SCAN_B - 1) block_sums[blockIdx.x] = s[SCAN_B - 1];
+}
+
+__global__ __launch_bounds__(SCAN_B) void k_add_block_base(uint64_t* __restrict__ out, uint64_t n,
+                                                           const uint64_t* __restrict__ block_base) {
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
+    if (i < n) out[i] += block_base[blockIdx.x];
+}
+
+// ------------------------------------------------------------- k_build
+//
+// One workgroup of 256 threads per output tile of 256*U*16 bytes, tiles in
+// XCD-contiguous order.  A tile lying inside one frame's payload (all but
+// the boundary tile of a 64 KiB frame) takes the streaming path: the frame
+// is found once per tile, the U source vectors are loaded back to back and
+// realigned to the output's 16-B phase (two aligned loads per chunk when the
+// payload and output phases differ), XORed with the rotated key word and
+// stored.  Other tiles build chunk by chunk: binary search of the frame
+// table within the tile's frame range, then 16 payload bytes or, at headers
+// and frame boundaries, byte by byte.
+
+// 16 payload bytes starting at arbitrary offset p of a buffer of plen bytes.
+__device__ __forceinline__ void ld16_any(const uint8_t* pay, uint64_t plen, uint64_t p, uint64_t& lo, uint64_t& hi) {
+    const uint64_t a = p & ~15ull;
+    const uint32_t s = (uint32_t)(p & 15u);
+    if (a + 32 <= plen) {
+        const u32x4 va = *reinterpret_cast<const u32x4*>(pay + a);
+        const u32x4 vb = *reinterpret_cast<const u32x4*>(pay + a + 16);
+        const uint64_t w0 = va.x | ((uint64_t)va.y << 32), w1 = va.z | ((uint64_t)va.w << 32);
+        const uint64_t w2 = vb.x | ((uint64_t)vb.y << 32), w3 = vb.z | ((uint64_t)vb.w << 32);
+        const uint64_t x0 = s < 8 ? w0 : w1, x1 = s < 8 ? w1 : w2, x2 = s < 8 ? w2 : w3;
+        const uint32_t sh = (s & 7u) * 8u;
+        lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+        hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+    } else {
+        lo = hi = 0;
+        for (int b = 0; b < 16; ++b) {
+            const uint64_t q = p + b;
+            const uint64_t v = q < plen ? pay[q] : 0;
+            if (b < 8) lo |= v << (8 * b);
+            else hi |= v << (8 * (b - 8));
+        }
+    }
+}
+
+// bytes s..s+15 of the 32-byte little-endian pair (a, b), s in [0, 16)
+__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t s) {
+    const uint64_t w0 = a.x | ((uint64_t)a.y << 32), w1 = a.z | ((uint64_t)a.w << 32);
+    const uint64_t w2 = b.x | ((uint64_t)b.y << 32), w3 = b.z | ((uint64_t)b.w << 32);
+    const uint64_t x0 = s < 8 ? w0 : w1, x1 = s < 8 ? w1 : w2, x2 = s < 8 ? w2 : w3;
+    const uint32_t sh = (s & 7u) * 8u;
+    const uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+    const uint64_t hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+    return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+__device__ __forceinline__ void build_chunk(uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay,
+                                            uint64_t plen, const uint64_t* __restrict__ pay_off,
+                                            const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
+                                            const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off,
+                                            const uint64_t* __restrict__ size, uint64_t n, uint64_t k_lo,
+                                            uint64_t k_hi, uint64_t c) {
+    uint64_t k = k_lo, k_end = k_hi;   // first frame ending after c
+    while (k < k_end) {
+        const uint64_t mid = (k + k_end) >> 1;
+        if (out_off[mid] + size[mid] > c) k_end = mid;
+        else k = mid + 1;
+    }
+    if (k < n && c + 16 <= out_len) {
+        const uint32_t fl = flags[k];
+        const uint64_t ln = len[k];
+        const uint64_t ps = out_off[k] + tx_hdr_len(fl, ln);
+        if (ps <= c && c + 16 <= ps + ln) {   // 16 payload bytes of one frame
+            const uint64_t j0 = c - ps;
+            uint64_t lo, hi;
+            ld16_any(pay, plen, pay_off[k] + j0, lo, hi);
+            if (fl & F_MASK) {
+                const uint32_t key = mask[k];
+                const uint32_t r = (uint32_t)(j0 & 3u) * 8u;
+                const uint32_t kw = r ? (key >> r) | (key << (32u - r)) : key;
+                const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                lo ^= kk;
+                hi ^= kk;
+            }
+            __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                        reinterpret_cast<u32x4*>(out + c));
+            return;
+        }
+    }
+    // header bytes / frame boundaries / tail: byte by byte
+    for (uint32_t b = 0; b < 16 && c + b < out_len; ++b) {
+        const uint64_t a = c + b;
+        while (k < n && out_off[k] + size[k] <= a) ++k;
+        if (k >= n || out_off[k] > a) continue;
+        const uint32_t fl = flags[k];
+        const uint64_t ln = len[k];
+        const uint32_t key = (fl & F_MASK) ? mask[k] : 0u;
+        const uint32_t hl = tx_hdr_len(fl, ln);
+        const uint64_t rel = a - out_off[k];
+        uint32_t v;
+        if (rel < hl) {
+            v = tx_hdr_byte(fl, ln, key, (uint32_t)rel);
+        } else {
+            const uint64_t j = rel - hl;
+            v = pay[pay_off[k] + j];
+            if (fl & F_MASK) v ^= (key >> (8 * (j & 3u))) & 0xFFu;
+        }
+        out[a] = (uint8_t)v;
+    }
+}
+
+template <int U, bool SWZ, bool NT>
+__global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64_t out_len,
+                                               const uint8_t* __restrict__ pay, uint64_t plen,
+                                               const uint64_t* __restrict__ pay_off,
+                                               const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
+                                               const uint32_t* __restrict__ mask,
+                                               const uint64_t* __restrict__ out_off,
+                                               const uint64_t* __restrict__ size,
+                                               const uint32_t* __restrict__ tile_first, uint64_t n, uint64_t tile0,
+                                               uint64_t ntiles) {
+    constexpr uint64_t TILE = 256ull * U * 16u;
+    const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
+    const uint64_t base = t * TILE;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t k_lo = tile_first[t];
+    if (k_lo < n && base + TILE <= out_len) {
+        const uint32_t fl = flags[k_lo];
+        const uint64_t ln = len[k_lo];
+        const uint64_t ps = out_off[k_lo] + tx_hdr_len(fl, ln);
+        const uint64_t src = pay_off[k_lo] + (base - ps);   // payload byte of the tile's first output byte
+        const uint64_t src_a = src & ~15ull;
+        if (ps <= base && base + TILE <= ps + ln && src_a + TILE + 16 <= plen) {
+            uint32_t kw = 0;
+            if (fl & F_MASK) {
+                const uint32_t key = mask[k_lo];
+                const uint32_t r = (uint32_t)((base - ps) & 3u) * 8u;
+                kw = r ? (key >> r) | (key << (32u - r)) : key;
+            }
+            const u32x4 kv = u32x4{kw, kw, kw, kw};
+            const uint32_t sft = (uint32_t)(src & 15u);
+            const uint8_t* sp = pay + src_a;
+            u32x4 v[U];
+            if (sft == 0) {
+#pragma unroll
+                for (int i = 0; i < U; ++i)
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * 256 + tid) * 16u));
+            } else {
+                u32x4 w[U], x[U];
+#pragma unroll
+                for (int i = 0; i < U; ++i) {
+                    const u32x4* q = reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * 256 + tid) * 16u);
+                    if (NT) {
+                        w[i] = __builtin_nontemporal_load(q);
+                        x[i] = __builtin_nontemporal_load(q + 1);
+                    } else {
+                        w[i] = q[0];
+                        x[i] = q[1];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < U; ++i) v[i] = funnel16(w[i], x[i], sft);
+            }
+#pragma unroll
+            for (int i = 0; i < U; ++i)
+                __builtin_nontemporal_store(v[i] ^ kv, reinterpret_cast<u32x4*>(out + base + ((uint64_t)i * 256 + tid) * 16u));
+            return;
+        }
+    }
+    const uint64_t k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
+#pragma unroll 1
+    for (int i = 0; i < U; ++i) {
+        const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+        if (c >= out_len) break;
+        build_chunk(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, n, k_lo, k_hi, c);
+    }
+}
+
+hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp, uint64_t* total,
+                                 hipStream_t st) {
+    if (n == 0) return hipMemsetAsync(total, 0, 8, st);
+    const uint64_t nb = (n + SCAN_B - 1) / SCAN_B;
+    uint64_t* sums = tmp;
+    uint64_t* base = tmp + nb;
+    hipLaunchKernelGGL(k_scan_blocks, dim3((uint32_t)nb), dim3(SCAN_B), 0, st, in, out, n, sums);
+    if (nb == 1) {
+        hipError_t e = hipMemsetAsync(base, 0, 8, st);
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(total, sums, 8, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    } else {
+        hipError_t e = launch_exclusive_scan(sums, base, nb, tmp + 2 * nb, total, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_add_block_base, dim3((uint32_t)nb), dim3(SCAN_B), 0, st, out, n, base);
+    }
+    return hipGetLastError();
+}
+
+__global__ void k_tx_check(const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len,
+                           const uint8_t* __restrict__ flags, const uint32_t* __restrict__ mask, uint64_t n,
+                           uint64_t plen, unsigned long long* __restrict__ bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool b = false;
+    if (i < n) {
+        const uint64_t o = pay_off[i], l = len[i];
+        b = o > plen || l > plen - o || ((flags[i] & F_MASK) && !mask);
+    }
+    const uint64_t m = __ballot(b);
+    if (m && (threadIdx.x & 63) == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
+}
+
+hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
+                           uint64_t n, uint64_t plen, uint64_t* bad, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tx_check, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, pay_off, len, flags, mask, n,
+                       plen, reinterpret_cast<unsigned long long*>(bad));
+    return hipGetLastError();
+}
+
+// Build geometries: X(index, chunks per thread, XCD order, nontemporal
+// realigning loads); 0 is the default.
+#define HVWS_BUILD_GEOMS(X) \
+    X(0, 4, false, false)   \
+    X(1, 8, false, false)   \
+    X(2, 2, false, false)   \
+    X(3, 4, true, false)    \
+    X(4, 4, false, true)    \
+    X(5, 16, false, false)  \
+    X(6, 1, false, false)   \
+    X(7, 8, false, true)
+
+namespace {
+int build_variant() {
+    static const int v = [] {
+        const char* e = getenv("HVWS_BUILD");
+        const int x = e ? atoi(e) : 0;
+        return (x >= 0 && x < 8) ? x : 0;
+    }();
+    return v;
+}
+uint64_t build_tile(int v) {
+    switch (v) {
+#define X(I, U, S, N) \
+    case I:           \
+        return 256ull * U * 16u;
+        HVWS_BUILD_GEOMS(X)
+#undef X
+    }
+    return 0;
+}
+}  // namespace
+
+const char* build_kernel_name() {
+    switch (build_variant()) {
+#define X(I, U, S, N) \
+    case I:           \
+        return "k_build<" #U "," #S "," #N ">";
+        HVWS_BUILD_GEOMS(X)
+#undef X
+    }
+    return "?";
+}
+
+uint64_t tx_tile() { return build_tile(build_variant()); }
+
+hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
+                        const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
+                        const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st) {
+    const int v = build_variant();
+    const uint64_t tile = build_tile(v);
+    const uint64_t ntiles = (out_len + tile - 1) / tile;
+    // a grid beyond 2^32-1 work-items is silently truncated: split the launch
+    const uint64_t per_launch = 0xFFFFFFFFull / 256;
+    for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
+        const uint64_t nt = min(per_launch, ntiles - t0);
+        switch (v) {
+#define X(I, U, S, N)                                                                                          \
+    case I:                                                                                                    \
+        hipLaunchKernelGGL((k_build<U, S, N>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off, \
+                           len, flags, mask, out_off, size, tile_first, n, t0, nt);                            \
+        break;
+            HVWS_BUILD_GEOMS(X)
+#undef X
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace hvws

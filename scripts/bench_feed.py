@@ -8,6 +8,8 @@ connection's next read to the parser:
   * gpu_each : WebSocketParser::FeedRecvData per connection (a round trip each);
   * cpu_ref  : the reference frame parser + restated WebSocketParser callbacks
                (oracle/_ref), per connection, one core.
+  * *_general: the same through the general COUNT/EMIT/unmask sequence
+               (small-batch single-launch path disabled).
 Reports per-iteration latency and payload throughput.  Prints JSON lines.
 """
 from __future__ import annotations
@@ -43,9 +45,11 @@ def main():
         streams = [host[o:o + ln] for o, ln in plan.segments]
         payload_per_read = READ * 1024 / 1032
         res = {"connections": n, "read_bytes": READ, "iterations": iters}
-        for mode in ("gpu_many", "gpu_each", "cpu_ref"):
-            if mode == "gpu_each" and n > 256:
+        for mode in ("gpu_many", "gpu_each", "gpu_many_general", "gpu_each_general", "cpu_ref"):
+            if mode.startswith("gpu_each") and n > 256:
                 continue
+            # *_general: the COUNT/EMIT/unmask sequence instead of the single-launch small-batch kernel
+            L.hvws_set_small_batch_limit(None, (1 << 64) - 1 if mode.endswith("_general") else 0)
             bufs = [np.array(s[:per_conn], copy=True) for s in streams]
             if mode == "cpu_ref":
                 hs = [R.msgp_new() for _ in range(n)]
@@ -74,7 +78,7 @@ def main():
                 for it in range(iters):
                     for i in range(n):
                         ds[i] = bufs[i].ctypes.data + it * READ
-                    if mode == "gpu_many":
+                    if mode.startswith("gpu_many"):
                         L.hvws_wsp_feed_many(hv, ds, lens, n, rets)
                     else:
                         for i in range(n):

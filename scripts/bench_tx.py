@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Transmit-side measurement: hvws_build_frames
+over the config-3 shape (1M masked binary frames x 64 KiB), device resident.
+
+Two payload layouts:
+  * "rx_layout": the payloads sit where the receive path left them (the
+    unmasked rx batch) -- payload and output 16-B phases agree;
+  * "packed": payloads back to back in a send arena -- every 64 KiB frame's
+    14-byte header shifts the output phase, so loads are realigned.
+Algorithmic bytes per launch = payload read + frames written.  Device time
+from HIP events around the kernel on the ctx stream.  Prints JSON lines.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT]
+
+import libhv_amd  # noqa: E402
+from libhv_amd import synth  # noqa: E402
+
+PEAK = 8000.0
+
+
+def main():
+    reps = int(os.environ.get("REPS", "5"))
+    name = os.environ.get("CONFIG", "c3")
+    eng = libhv_amd.Engine(int(os.environ.get("HVWS_BENCH_DEVICE", "0")))
+    p = synth.config_plan(name, 1).split(4096)
+    dp = libhv_amd.DevicePlan(eng, p)
+    hdr = synth.frame_size(p.flags, p.length) - p.length
+    rx = eng.alloc(p.total + 64)
+    out = eng.alloc(p.total + 64)
+    eng.synth(rx, p.total, p.seed, dp, 0)
+    eng.step(rx, p.total, p.segments)
+    eng.sync()
+    alg = p.payload_bytes + p.total
+    pack_off = np.concatenate([[0], np.cumsum(p.length)[:-1]]).astype(np.uint64)
+    for layout, offs in (("rx_layout", p.frame_off + hdr), ("packed", pack_off)):
+        tx = libhv_amd.TxPlan(eng, offs, p.length, p.flags, p.mask)
+        ms = []
+        t0 = time.perf_counter()
+        for _ in range(reps + 1):
+            n = eng.build_frames(out, p.total + 64, rx, p.total, tx)
+            ms.append(eng.last_build_ms())
+        wall = (time.perf_counter() - t0) / (reps + 1)
+        assert n == p.total
+        ok = None
+        if layout == "rx_layout":
+            ok = eng.synth(out, p.total, p.seed, dp, 1) == 0
+        k = float(np.mean(ms[1:]))
+        print(json.dumps({
+            "bench": "build_frames", "kernel": libhv_amd.lib().hvws_build_kernel_name().decode(), "config": name,
+            "layout": layout, "frames": p.n,
+            "payload_bytes": p.payload_bytes, "out_bytes": p.total, "alg_bytes_per_launch": alg,
+            "kernel_ms": round(k, 3), "kernel_GBps": round(alg / k / 1e6, 1),
+            "frac_of_8TBps": round(alg / k / 1e6 / PEAK, 4),
+            "call_ms": round(wall * 1e3, 3), "payload_GiBps_call": round(p.payload_bytes / wall / 2**30, 1),
+            "verified": ok,
+        }), flush=True)
+        tx.free()
+    rx.free()
+    out.free()
+    dp.free()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,22 @@ import wsharness as H
 
 pytestmark = pytest.mark.gpu
 
+@pytest.fixture(params=["small", "general"], autouse=True)
+def rx_path(request):
+    """Run every case through both host-batch paths: the single-launch
+    small-batch kernel (default for reads this size) and the general
+    COUNT/EMIT/unmask sequence.  Results must be identical."""
+    L = libhv_amd.lib()
+    limit = 0 if request.param == "small" else (1 << 64) - 1
+    L.hvws_set_small_batch_limit(None, limit)
+    eng = request.getfixturevalue("eng") if "eng" in request.fixturenames else None
+    if eng:
+        L.hvws_set_small_batch_limit(eng.ctx, limit)
+    yield request.param
+    L.hvws_set_small_batch_limit(None, 0)
+    if eng:
+        L.hvws_set_small_batch_limit(eng.ctx, 0)
+
 
 def _clamp(chunks, n):
     """chunk sizes that exactly cover n bytes (rand_chunks may overshoot)"""

@@ -1,0 +1,149 @@
+"""GPU, transmit side: hvws_build_frames against
+the reference's websocket_build_frame (http/websocket_parser.c:207-256, via
+oracle/_ref when built, else the oracle restatement), frame by frame, plus the
+size-independent round trip at batch scale: synthesise a masked batch,
+unmask it in place with the receive path, rebuild every frame from the
+plaintext payloads with the same flags and keys -- the result must be the
+original masked batch byte for byte."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import libhv_amd
+import wsharness as H
+from libhv_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+EDGE_LENS = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 125, 126, 127, 128, 4095, 65535, 65536, 65537, 70001]
+
+
+def _frames(rng, n, lens=None, p_mask=0.6):
+    out = []
+    for i in range(n):
+        ln = int(lens[i]) if lens is not None else int(rng.choice([rng.integers(0, 126), rng.integers(126, 3000),
+                                                                   rng.integers(0, 40)]))
+        op = int(rng.choice([0, 1, 2, 8, 9, 10, 3, 15]))
+        flags = op | (0x10 if rng.random() < 0.8 else 0) | (0x20 if rng.random() < p_mask else 0)
+        key = bytes(rng.integers(0, 256, 4, dtype=np.uint8)) if flags & 0x20 else None
+        out.append((flags, bytes(rng.integers(0, 256, ln, dtype=np.uint8)), key))
+    return out
+
+
+def _gpu_build(eng, frames, gap_rng=None, with_off=False):
+    """Lay payloads out with random gaps (misaligned offsets) and build on the GPU."""
+    pay = bytearray()
+    offs = []
+    for _, p, _k in frames:
+        if gap_rng is not None:
+            pay += bytes(int(gap_rng.integers(0, 19)))
+        offs.append(len(pay))
+        pay += p
+    flags = [f for f, _, _ in frames]
+    mask = [int.from_bytes(k, "little") if k else 0 for _, _, k in frames]
+    lens = [len(p) for _, p, _ in frames]
+    total = int(synth.frame_size(np.array(flags, dtype=np.uint8), np.array(lens, dtype=np.uint64)).sum()) if frames else 0
+    payload = eng.to_device(np.frombuffer(bytes(pay), dtype=np.uint8)) if pay else eng.alloc(16)
+    tx = libhv_amd.TxPlan(eng, offs, lens, flags, mask)
+    out = eng.alloc(total + 64)
+    ooff = eng.alloc(8 * max(len(frames), 1)) if with_off else None
+    try:
+        n = eng.build_frames(out, total + 64, payload, len(pay), tx, ooff)
+        assert n == total
+        got = bytes(out.download(n))
+        offv = ooff.download(8 * len(frames), np.uint64) if with_off else None
+    finally:
+        for b in (payload, out, ooff):
+            if b is not None:
+                b.free()
+        tx.free()
+    return got, offv
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_build_random_vs_reference(eng, seed):
+    rng = np.random.default_rng(seed)
+    frames = _frames(rng, 400)
+    got, off = _gpu_build(eng, frames, gap_rng=rng, with_off=True)
+    assert got == H.build_frames_ref(frames)
+    sizes = [len(H.build_frames_ref([f])) for f in frames]
+    assert off.tolist() == list(np.cumsum([0] + sizes[:-1]))
+
+
+def test_build_length_edges(eng):
+    rng = np.random.default_rng(7)
+    for p_mask in (0.0, 1.0, 0.5):
+        frames = _frames(rng, len(EDGE_LENS), lens=EDGE_LENS, p_mask=p_mask)
+        got, _ = _gpu_build(eng, frames, gap_rng=rng)
+        assert got == H.build_frames_ref(frames)
+
+
+def test_build_dense_tiny_frames(eng):
+    # thousands of frames per 16 KiB output tile: header-only and 1-byte frames
+    rng = np.random.default_rng(11)
+    frames = _frames(rng, 20000, lens=rng.integers(0, 3, 20000))
+    got, _ = _gpu_build(eng, frames)
+    assert got == H.build_frames_ref(frames)
+
+
+def test_build_aligned_large(eng):
+    rng = np.random.default_rng(5)
+    frames = _frames(rng, 12, lens=[1 << 20] * 4 + [(1 << 20) + 3] * 4 + [200003] * 4, p_mask=0.7)
+    got, _ = _gpu_build(eng, frames)
+    assert got == H.build_frames_ref(frames)
+
+
+def test_build_empty_batch(eng):
+    tx = libhv_amd.TxPlan(eng, [], [], [], [])
+    out = eng.alloc(64)
+    try:
+        assert eng.build_frames(out, 64, None, 0, tx) == 0
+    finally:
+        out.free()
+        tx.free()
+
+
+def test_build_rejects_bad_tables(eng):
+    pay = eng.alloc(1024)
+    out = eng.alloc(4096)
+    try:
+        tx = libhv_amd.TxPlan(eng, [1000], [100], [0x12], [0])        # payload range past the end
+        with pytest.raises(libhv_amd.HvwsError, match="outside"):
+            eng.build_frames(out, 4096, pay, 1024, tx)
+        tx.free()
+        tx = libhv_amd.TxPlan(eng, [0], [10], [0x32])                # masked but no key table
+        with pytest.raises(libhv_amd.HvwsError, match="mask"):
+            eng.build_frames(out, 4096, pay, 1024, tx)
+        tx.free()
+        tx = libhv_amd.TxPlan(eng, [0], [1000], [0x12], [0])          # output too small
+        with pytest.raises(libhv_amd.HvwsError, match="capacity"):
+            eng.build_frames(out, 100, pay, 1024, tx)
+        tx.free()
+    finally:
+        pay.free()
+        out.free()
+
+
+@pytest.mark.parametrize("name,plan", [("mixed", lambda: synth.mixed_plan(1 << 30, 3)),
+                                       ("c2", lambda: synth.config_plan("c2", 1))])
+def test_build_roundtrip_batch(eng, name, plan):
+    """rx unmask then tx build with the same flags/keys == the masked batch."""
+    p = plan().split(64)
+    dp = libhv_amd.DevicePlan(eng, p)
+    rx = eng.alloc(p.total + 64)
+    out = eng.alloc(p.total + 64)
+    hdr = synth.frame_size(p.flags, p.length) - p.length
+    tx = libhv_amd.TxPlan(eng, p.frame_off + hdr, p.length, p.flags, p.mask)
+    try:
+        eng.synth(rx, p.total, p.seed, dp, 0)
+        eng.step(rx, p.total, p.segments)
+        assert eng.synth(rx, p.total, p.seed, dp, 2) == 0           # rx holds plaintext payloads
+        n = eng.build_frames(out, p.total + 64, rx, p.total, tx)
+        assert n == p.total
+        assert eng.synth(out, p.total, p.seed, dp, 1) == 0          # rebuilt == masked batch
+    finally:
+        for b in (rx, out):
+            b.free()
+        dp.free()
+        tx.free()
