@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--host-gib", type=float, default=4.0, help="host-inclusive sample size (0: skip)")
     ap.add_argument("--sweep-unmask", action="store_true",
                     help="rank 0: time every k_unmask geometry on the same batch (design record)")
+    ap.add_argument("--no-tx", action="store_true", help="skip the transmit-side (hvws_build_frames) measurement")
     return ap.parse_args()
 
 
@@ -234,6 +235,38 @@ def main():
                      for n, t in times.items()}
             extra["unmask_sweep_GBps"] = sweep
         extra["unmask_ms_mean"] = round(mean_unmask, 3)
+
+        if not args.no_tx:
+            # transmit side: rebuild every frame of the
+            # batch from its plaintext payload with hvws_build_frames; the output
+            # must be the masked batch byte for byte
+            if passes % 2 == 0:
+                eng.step(rx, plan.total, segs)   # leave rx holding plaintext payloads
+            hdr = synth.frame_size(plan.flags, plan.length) - plan.length
+            tx = libhv_amd.TxPlan(eng, plan.frame_off + hdr, plan.length, plan.flags, plan.mask)
+            out_buf = eng.alloc(plan.total + 64)
+            tms = []
+            for _ in range(4):
+                eng.build_frames(out_buf, plan.total + 64, rx, plan.total, tx)
+                tms.append(eng.last_build_ms())
+            ok = eng.synth(out_buf, plan.total, plan.seed, dp, 1) == 0
+            tx_alg = plan.payload_bytes + plan.total
+            tx_ach = tx_alg / (float(np.mean(tms[1:])) * 1e-3) / 1e9
+            bname = libhv_amd.lib().hvws_build_kernel_name().decode()
+            tx_traffic = None
+            if os.path.exists(tpath):
+                ent = json.load(open(tpath)).get(bname, {}).get(str(plan.total))
+                tx_traffic = ent["hbm_bytes"] if ent else None
+            extra["tx"] = {
+                "kernel": bname, "traffic": tx_traffic,
+                "achieved": round(tx_ach, 1), "unit": "GB/s", "frac": round(tx_ach / HBM_PEAK_GBS, 4),
+                "alg_bytes_per_launch": tx_alg, "kernel_ms_mean": round(float(np.mean(tms[1:])), 3),
+                "verified": ok,
+            }
+            out_buf.free()
+            tx.free()
+            if not ok:
+                raise SystemExit("transmit build differs from the masked batch")
 
         # host-inclusive: pinned host rx -> device -> scan+unmask -> host
         if args.host_gib > 0:

@@ -65,6 +65,27 @@ def main():
             "verified": ok,
         }), flush=True)
         tx.free()
+    # ceilings: runtime D2D copy of the same bytes, and one huge unmasked frame
+    # (k_build's streaming path as a plain realigning copy)
+    import ctypes
+    L = libhv_amd.lib()
+    ev = []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        L.hvws_d2d(eng.ctx, out.ptr, rx.ptr, p.payload_bytes)
+        eng.sync()
+        ev.append(time.perf_counter() - t0)
+    d2d = float(np.mean(ev[1:]))
+    one = libhv_amd.TxPlan(eng, [0], [p.payload_bytes], [0x12], [0])
+    ms = []
+    for _ in range(reps + 1):
+        eng.build_frames(out, p.total + 64, rx, p.total, one)
+        ms.append(eng.last_build_ms())
+    k1 = float(np.mean(ms[1:]))
+    one.free()
+    print(json.dumps({"bench": "copy_ceiling", "bytes_moved": 2 * p.payload_bytes,
+                      "d2d_GBps_wall": round(2 * p.payload_bytes / d2d / 1e9, 1),
+                      "one_frame_build_GBps": round((2 * p.payload_bytes + 10) / k1 / 1e6, 1)}), flush=True)
     rx.free()
     out.free()
     dp.free()

@@ -40,11 +40,13 @@ def main():
     fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
     for k in sorted(set(fetch) & set(write)):
-        if not (k.startswith("k_unmask") or k.startswith("k_stream_xor")):
+        if not (k.startswith("k_unmask") or k.startswith("k_stream_xor") or k.startswith("k_build")):
             continue
         rd = 2 * statistics.median(fetch[k]) * 1024
         wr = statistics.median(write[k]) * 1024
-        name = k.replace(" ", "").replace("true", "xcd").replace("false", "linear")
+        name = k.replace(" ", "")
+        if not name.startswith("k_build"):   # hvws_unmask_kernel_name spelling
+            name = name.replace("true", "xcd").replace("false", "linear")
         db.setdefault(name, {})[str(a.rx_bytes)] = {
             "config": a.config, "read_bytes": int(rd), "write_bytes": int(wr), "hbm_bytes": int(rd + wr),
             "dispatches": min(len(fetch[k]), len(write[k])),
