@@ -248,7 +248,7 @@ def main():
             tms = []
             for _ in range(4):
                 eng.build_frames(out_buf, plan.total + 64, rx, plan.total, tx)
-                tms.append(eng.last_build_ms())
+                tms.append(eng.last_kernel_ms())
             ok = eng.synth(out_buf, plan.total, plan.seed, dp, 1) == 0
             tx_alg = plan.payload_bytes + plan.total
             tx_ach = tx_alg / (float(np.mean(tms[1:])) * 1e-3) / 1e9

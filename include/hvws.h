@@ -18,6 +18,8 @@
  *                WebSocketChannel::sendFrame via ws_build_frame,
  *                http/WebSocketChannel.cpp:66-79, http/wsdef.c:36-46)
  *                for a whole batch of outgoing frames at once.
+ *   hvws_encode_keys  the handshake digest ws_encode_key (http/wsdef.c:11-20)
+ *                for a batch of upgrade requests.
  *   hvws_wsp_*   C handle over the WebSocketParser class
  *                (http/WebSocketParser.h:19-31) for FFI callers.
  *
@@ -55,6 +57,19 @@ enum {
 #define HVWS_I_BODY        (1u << 11) /* >= 1 payload byte here (on_frame_body fires)   */
 #define HVWS_I_END         (1u << 12) /* frame completed here (on_frame_end fires)      */
 #define HVWS_I_START       (1u << 13) /* first header byte is inside this segment       */
+#define HVWS_I_INVALID     (1u << 14) /* header violates an enabled validation class    */
+#define HVWS_I_VSHIFT      16         /* HVWS_V_* classes violated, bits 16-21           */
+
+/* Optional protocol validation (hvws_set_validation), RFC 6455 sec. 5.1-5.5.
+ * The reference checks none of these, so all are off by
+ * default and results are then identical to the reference's. */
+#define HVWS_V_RSV       (1u << 0)  /* RSV1-3 set (no extension is negotiated)        */
+#define HVWS_V_OPCODE    (1u << 1)  /* reserved opcode 3-7 or 0xB-0xF                 */
+#define HVWS_V_CONTROL   (1u << 2)  /* control frame with FIN = 0 or > 125 bytes      */
+#define HVWS_V_LEN64     (1u << 3)  /* 64-bit length with its most significant bit set */
+#define HVWS_V_NONMIN    (1u << 4)  /* length not in its minimal encoding             */
+#define HVWS_V_UNMASKED  (1u << 5)  /* client-to-server frame without a mask          */
+#define HVWS_V_ALL       0x3Fu
 
 typedef struct hvws_ctx hvws_ctx;
 
@@ -89,6 +104,7 @@ void  hvws_host_free(hvws_ctx* ctx, void* p);
 int   hvws_h2d(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async, ctx stream */
 int   hvws_d2h(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async, ctx stream */
 int   hvws_memset(hvws_ctx* ctx, void* dst, int v, uint64_t n);
+int   hvws_d2d(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async, ctx stream */
 int   hvws_sync(hvws_ctx* ctx);
 
 /* ---- the hot path, device resident ---------------------------------- */
@@ -142,9 +158,19 @@ int hvws_build_frames(hvws_ctx* ctx, uint8_t* d_out, uint64_t out_cap, const uin
                       uint64_t payload_len, const uint64_t* d_pay_off, const uint64_t* d_len,
                       const uint8_t* d_flags, const uint32_t* d_mask, uint64_t n, uint64_t* d_out_off,
                       uint64_t* out_len);
-/* Device time (ms) of the last build kernel, and its name. */
-int hvws_last_build_ms(hvws_ctx* ctx, float* ms);
+/* Device time (ms, HIP events on the ctx stream) of the last
+ * hvws_build_frames or hvws_encode_keys kernel; the build kernel's name. */
+int hvws_last_kernel_ms(hvws_ctx* ctx, float* ms);
 const char* hvws_build_kernel_name(void);
+
+/* ---- handshake, device resident --------------------------------------- */
+/* Sec-WebSocket-Accept for n upgrade requests: accept + 32*i receives the 28
+ * characters ws_encode_key (http/wsdef.c:11-20) writes for key i (the bytes
+ * d_keys[key_off[i] .. + key_len[i]), no NUL inside), followed by 4 zero bytes
+ * -- the callers' zeroed char[32] (http/server/HttpHandler.cpp:986).
+ * d_accept must be 16-byte aligned.  Asynchronous on the ctx stream. */
+int hvws_encode_keys(hvws_ctx* ctx, const char* d_keys, const uint64_t* d_key_off, const uint32_t* d_key_len,
+                     uint64_t n, char* d_accept);
 
 /* ---- host memory in, host memory out -------------------------------- */
 /* Copies h_rx to the device, runs scan (+ unmask if `unmask`), copies the
@@ -152,6 +178,19 @@ const char* hvws_build_kernel_name(void);
  * available through hvws_get_frames(). */
 int hvws_rx_batch(hvws_ctx* ctx, uint8_t* h_rx, uint64_t len, const hvws_segment* segs,
                   websocket_parser* carry, uint32_t nseg, int unmask);
+
+/* Enable protocol validation classes (HVWS_V_*; 0 = off, the default) for
+ * later batches on ctx (NULL = the calling thread's reference-API context).
+ * Device API: a frame whose header violates an enabled class carries
+ * HVWS_I_INVALID and the classes in its info.  Reference API: the library
+ * rejects such a frame the way a failing on_frame_header callback would --
+ * websocket_parser_execute / FeedRecvData return the index of the header's
+ * last byte (< len), so HttpHandler::FeedRecvData reports ERR_PARSE and the
+ * connection closes (http/server/HttpHandler.cpp:757-763); on_frame_header
+ * is not called for it.  A header split across reads keeps its partial
+ * validation state in the padding byte after websocket_parser.mask_offset.
+ * Returns the previous classes. */
+uint32_t hvws_set_validation(hvws_ctx* ctx, uint32_t classes);
 
 /* Batches of at most `bytes` (default 64 MiB; each segment <= 1 MiB) take
  * the single-launch small-batch path inside hvws_rx_batch (and so inside

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -90,6 +90,7 @@ _SIGS = {
     "hvws_host_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "hvws_h2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_d2h": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "hvws_d2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_memset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]),
     "hvws_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "hvws_scan": (
@@ -128,7 +129,11 @@ _SIGS = {
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
          ctypes.POINTER(ctypes.c_uint64)],
     ),
-    "hvws_last_build_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "hvws_encode_keys": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p],
+    ),
+    "hvws_last_kernel_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "hvws_wsp_new": (ctypes.c_void_p, []),
     "hvws_wsp_free": (None, [ctypes.c_void_p]),
     "hvws_wsp_set_sink": (None, [ctypes.c_void_p, MSG_CB, ctypes.c_void_p]),
@@ -143,6 +148,7 @@ _SIGS = {
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
+    "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),
     "hvws_set_unmask_variant": (ctypes.c_int, [ctypes.c_int]),
     # reference ABI (include/websocket_parser.h, include/wsdef.h)
     "websocket_parser_init": (None, [ctypes.c_void_p]),
@@ -359,9 +365,28 @@ class Engine:
         )
         return int(n.value)
 
-    def last_build_ms(self) -> float:
+    def encode_keys(self, keys: Sequence[bytes]) -> List[bytes]:
+        """Sec-WebSocket-Accept for every key (ws_encode_key, batched on the GPU)."""
+        n = len(keys)
+        if n == 0:
+            return []
+        lens = np.array([len(k) for k in keys], dtype=np.uint32)
+        offs = np.zeros(n, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+        dk, do, dl = self.to_device(blob), self.to_device(offs), self.to_device(lens)
+        acc = self.alloc(32 * n)
+        try:
+            _check(lib().hvws_encode_keys(self.ctx, dk.ptr, do.ptr, dl.ptr, n, acc.ptr), "hvws_encode_keys")
+            raw = acc.download(32 * n).tobytes()
+        finally:
+            for b in (dk, do, dl, acc):
+                b.free()
+        return [raw[32 * i:32 * i + 32] for i in range(n)]
+
+    def last_kernel_ms(self) -> float:
         out = ctypes.c_float(0)
-        _check(lib().hvws_last_build_ms(self.ctx, ctypes.byref(out)), "hvws_last_build_ms")
+        _check(lib().hvws_last_kernel_ms(self.ctx, ctypes.byref(out)), "hvws_last_kernel_ms")
         return float(out.value)
 
     def digest(self, buf: DeviceBuffer, n: int) -> int:

@@ -53,14 +53,24 @@ namespace {
 // The reference's per-frame message logic (http/WebSocketParser.cpp:8-50)
 // over the frame records of one connection; `base` is where offset `base_off`
 // of the batch buffer sits in the caller's (already unmasked) bytes.
-void replay_messages(WebSocketParser* wp, const char* base, uint64_t base_off, const hvws_frame* frames, size_t n,
-                     const websocket_parser& out) {
+// Returns the bytes consumed: len, or -- when hvws_set_validation rejects a
+// header -- the index of that header's last byte, as execute reports a
+// failing on_frame_header (the parser is left as that callback would see it).
+size_t replay_messages(WebSocketParser* wp, const char* base, uint64_t base_off, const hvws_frame* frames, size_t n,
+                       const websocket_parser& out, size_t len) {
     websocket_parser* parser = wp->parser;
     for (size_t i = 0; i < n; ++i) {
         const hvws_frame& f = frames[i];
         const uint32_t fl = f.info & HVWS_I_FLAGS;
         parser->flags = (websocket_flags)fl;
         parser->length = f.length;
+        if ((f.info & HVWS_I_HDR) && (f.info & HVWS_I_INVALID)) {
+            if (fl & WS_HAS_MASK) memcpy(parser->mask, &f.key, 4);
+            parser->offset = 0;
+            parser->state = f.length ? 4u : 0u;   // s_body / s_start
+            parser->require = f.length;
+            return (size_t)(f.pay_off - base_off) - 1;
+        }
         if (f.info & HVWS_I_HDR) {
             const int op = (int)(fl & WS_OP_MASK);
             if (op != WS_OP_CONTINUE) wp->opcode = op;
@@ -87,6 +97,7 @@ void replay_messages(WebSocketParser* wp, const char* base, uint64_t base_off, c
     void* keep = parser->data;
     *parser = out;
     parser->data = keep;
+    return len;
 }
 
 }  // namespace
@@ -98,8 +109,7 @@ int WebSocketParser::FeedRecvData(const char* data, size_t len) {
     int started = 0;
     char* buf = const_cast<char*>(data);   // unmasked in place, like the reference
     hvws::gpu_feed(buf, len, *parser, true, frames, out, started);
-    replay_messages(this, buf, 0, frames.data(), frames.size(), out);
-    return (int)len;
+    return (int)replay_messages(this, buf, 0, frames.data(), frames.size(), out, len);
 }
 
 // One GPU round trip for many connections' reads:
@@ -150,8 +160,9 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
         char* dst = const_cast<char*>(data[i]);
         if (len[i]) memcpy(dst, stage + segs[i].off, len[i]);   // in place, like the reference
         carry[i].data = parsers[i]->parser->data;
-        replay_messages(parsers[i], dst, segs[i].off, frames.data() + first[i], (size_t)count[i], carry[i]);
-        if (rets) rets[i] = (int)len[i];
+        const size_t used =
+            replay_messages(parsers[i], dst, segs[i].off, frames.data() + first[i], (size_t)count[i], carry[i], len[i]);
+        if (rets) rets[i] = (int)used;
     }
     return n;
 }

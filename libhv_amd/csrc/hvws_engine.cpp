@@ -110,6 +110,7 @@ struct hvws_ctx {
     hbuf h_small_in, h_small_out;
     dbuf d_small_in, d_small_slots;
     uint64_t small_limit = 0;   // bytes; 0 = default
+    uint32_t vmask = 0;         // protocol validation classes (V_*); 0 = reference behaviour
     // transmit side (hvws_build_frames)
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat;
     hbuf h_tx;
@@ -180,7 +181,9 @@ void to_dcarry(const websocket_parser& p, dcarry& d) {
     d.require = p.require;
     d.offset = p.offset;
     d.started = 0;
-    d.pad = 0;
+    // Validation state of a partial header lives in the struct's padding
+    // byte after mask_offset (offset 13), invisible to the reference API.
+    d.viol = reinterpret_cast<const uint8_t*>(&p)[offsetof(websocket_parser, mask_offset) + 1];
 }
 
 void from_dcarry(const dcarry& d, websocket_parser& p) {
@@ -191,6 +194,7 @@ void from_dcarry(const dcarry& d, websocket_parser& p) {
     p.length = d.length;
     p.require = d.require;
     p.offset = d.offset;
+    reinterpret_cast<uint8_t*>(&p)[offsetof(websocket_parser, mask_offset) + 1] = (uint8_t)d.viol;
 }
 
 int check_ctx(hvws_ctx* c) {
@@ -224,7 +228,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const dcarry* cin = c->carry_in.as<dcarry>();
     HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
     HIP_OR(launch_scan(false, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->stream),
+                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream),
            HVWS_EHIP);
     // Frame records are bounded: after a segment's first record every frame
     // spends >= 2 of its bytes.  When the bound fits the table, EMIT follows
@@ -245,7 +249,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         c->nfr_known = true;
     }
     HIP_OR(launch_scan(true, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->stream),
+                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream),
            HVWS_EHIP);
     c->variant = unmask_variant();
     const uint64_t tile = unmask_tile(c->variant);
@@ -471,7 +475,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     HIP_OR(launch_small(d + o_data, len, (const dseg*)(d + o_segs), (const dcarry*)(d + o_carry), nseg,
                         (const uint64_t*)(d + o_slot), c->d_small_slots.as<drec>(), (unsigned long long*)d,
                         (drec*)(ho_d + nseg), hcap, ho_d, user_mapped ? user_mapped : hp_d + o_data, unmask,
-                        c->stream),
+                        c->vmask, c->stream),
            HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
@@ -652,6 +656,13 @@ int hvws_memset(hvws_ctx* c, void* dst, int v, uint64_t n) {
     int rc = check_ctx(c);
     if (rc) return rc;
     HIP_OR(hipMemsetAsync(dst, v, n, c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_d2d(hvws_ctx* c, void* dst, const void* src, uint64_t n) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream), HVWS_EHIP);
     return HVWS_OK;
 }
 
@@ -1012,16 +1023,38 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     return HVWS_OK;
 }
 
-int hvws_last_build_ms(hvws_ctx* c, float* ms) {
+int hvws_encode_keys(hvws_ctx* c, const char* d_keys, const uint64_t* d_key_off, const uint32_t* d_key_len,
+                     uint64_t n, char* d_accept) {
     int rc = check_ctx(c);
     if (rc) return rc;
-    if (!c->ev_build) return set_err(HVWS_EINVAL, "no build_frames call yet");
+    if (n == 0) return HVWS_OK;
+    if (!d_keys || !d_key_off || !d_key_len || !d_accept) return set_err(HVWS_EINVAL, "encode_keys: null table");
+    if (((uintptr_t)d_accept & 15u) != 0) return set_err(HVWS_EINVAL, "encode_keys: accept buffer must be 16-byte aligned");
+    HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
+    HIP_OR(launch_encode_keys((const uint8_t*)d_keys, d_key_off, d_key_len, n, (uint8_t*)d_accept, c->stream),
+           HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
+    c->ev_build = true;
+    return HVWS_OK;
+}
+
+int hvws_last_kernel_ms(hvws_ctx* c, float* ms) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->ev_build) return set_err(HVWS_EINVAL, "no build_frames / encode_keys call yet");
     HIP_OR(hipEventSynchronize(c->ev[5]), HVWS_EHIP);
     HIP_OR(hipEventElapsedTime(ms, c->ev[4], c->ev[5]), HVWS_EHIP);
     return HVWS_OK;
 }
 
 const char* hvws_build_kernel_name(void) { return build_kernel_name(); }
+
+uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {
+    if (!c) c = hvws::thread_ctx();
+    const uint32_t old = c->vmask;
+    c->vmask = classes & V_ALL;
+    return old;
+}
 
 uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
     if (!c) c = hvws::thread_ctx();   // the calling thread's reference-API context

@@ -10,7 +10,22 @@ namespace hvws {
 enum : uint32_t { S_START = 0, S_HEAD = 1, S_LENGTH = 2, S_MASK = 3, S_BODY = 4 };
 enum : uint32_t { F_OPMASK = 0x0Fu, F_FIN = 0x10u, F_MASK = 0x20u };
 enum : uint32_t {
-    I_HDR = 1u << 10, I_BODY = 1u << 11, I_END = 1u << 12, I_START = 1u << 13
+    I_HDR = 1u << 10, I_BODY = 1u << 11, I_END = 1u << 12, I_START = 1u << 13, I_INVALID = 1u << 14
+};
+// Optional protocol validation (RFC 6455 sec. 5.1-5.5; the reference checks
+// none of these).  Violation classes, reported in info bits
+// I_VSHIFT.. of a frame whose header completes, only for classes enabled in
+// the context's validation mask (0 = off = reference behaviour).
+enum : uint32_t {
+    V_RSV = 1u,        // RSV1-3 set with no extension negotiated
+    V_OPCODE = 2u,     // reserved opcode 3-7 / 0xB-0xF
+    V_CONTROL = 4u,    // control frame fragmented (FIN = 0) or longer than 125 bytes
+    V_LEN64 = 8u,      // 64-bit length with the most significant bit set
+    V_NONMIN = 16u,    // length not in its minimal encoding
+    V_UNMASKED = 32u,  // client-to-server frame without a mask
+    V_ALL = 63u,
+    V_ENC_SHIFT = 6u,  // (carry only) 2-bit length encoding of a partial header: 1 = 16-bit, 2 = 64-bit
+    I_VSHIFT = 16u
 };
 
 // Device-side carry (the websocket_parser fields the walk needs), 48 bytes.
@@ -23,7 +38,7 @@ struct dcarry {
     uint64_t require;
     uint64_t offset;
     uint32_t started;      // first header byte of the pending frame was in this segment
-    uint32_t pad;
+    uint32_t viol;         // V_* bits (+ encoding) of the partial header, for validation
 };
 
 // Per-segment state between the discovery kernels (k_head -> k_verify -> k_walk).
@@ -94,7 +109,7 @@ __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
 // EMIT pass: frame table at bases[], carry_out[].
 hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
-                       uint64_t* total, scan_scratch sc, dframes fr, hipStream_t st);
+                       uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
@@ -105,7 +120,11 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
 // (pinned host, same layout as rx).  *rec_total must be 0 on entry.
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
-                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, hipStream_t st);
+                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
+                        hipStream_t st);
+// Batched handshake digest (hvws_keys.hip): accept[32*i..] = base64(SHA-1(key_i + GUID)), 28 chars + 4 zero bytes.
+hipError_t launch_encode_keys(const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len, uint64_t n,
+                              uint8_t* accept, hipStream_t st);
 // k_unmask geometry variants (threads x chunks/thread, XCD-ordered tiles)
 int unmask_variant();                      // process default ($HVWS_UNMASK or 0)
 int set_unmask_variant(int v);             // -1 if out of range

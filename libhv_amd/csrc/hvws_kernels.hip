@@ -71,7 +71,10 @@ struct hdr {
     uint32_t hlen;
     uint32_t flags;
     uint32_t key;
+    uint32_t viol;   // V_* classes this header violates (reported only if enabled)
 };
+
+__device__ __forceinline__ bool reserved_opcode(uint32_t op) { return (op >= 3 && op <= 7) || op >= 0xB; }
 
 // Fixed-format header decode from its first 16 bytes (lo = bytes 0..7 LE).
 // Layout per websocket_build_frame (http/websocket_parser.c:207-256):
@@ -91,6 +94,12 @@ __device__ __forceinline__ hdr parse_hdr(uint64_t lo, uint64_t hi) {
     h.length = len7 < 126 ? (uint64_t)len7 : (len7 == 126 ? len16 : len64);
     uint32_t k0 = (uint32_t)(lo >> 16), k2 = (uint32_t)(lo >> 32), k8 = (uint32_t)(hi >> 16);
     h.key = m ? (ext == 0 ? k0 : (ext == 2 ? k2 : k8)) : 0u;
+    const uint32_t op = b0 & F_OPMASK;
+    h.viol = ((b0 & 0x70u) ? V_RSV : 0u) | (reserved_opcode(op) ? V_OPCODE : 0u) |
+             ((op & 8u) && (!(b0 & 0x80u) || h.length > 125) ? V_CONTROL : 0u) |
+             (ext == 8 && (h.length >> 63) ? V_LEN64 : 0u) |
+             ((ext == 2 && h.length < 126) || (ext == 8 && h.length <= 0xFFFFu) ? V_NONMIN : 0u) |
+             (m ? 0u : V_UNMASKED);
     return h;
 }
 
@@ -116,8 +125,13 @@ __device__ __forceinline__ void store_frame(const dframes& fr, uint64_t idx, uin
     fr.info[idx] = r.info;
 }
 
-__device__ __forceinline__ void hdr_complete(frec& r, const dcarry& st, uint64_t pay_off) {
-    r.info = (r.info & ~0xFFu & ~(3u << 8)) | (st.flags & 0xFFu) | I_HDR;
+__device__ __forceinline__ uint32_t invalid_bits(uint32_t viol, uint32_t vmask) {
+    const uint32_t v = viol & vmask & V_ALL;
+    return v ? I_INVALID | (v << I_VSHIFT) : 0u;
+}
+
+__device__ __forceinline__ void hdr_complete(frec& r, const dcarry& st, uint64_t pay_off, uint32_t vmask) {
+    r.info = (r.info & ~0xFFu & ~(3u << 8)) | (st.flags & 0xFFu) | I_HDR | invalid_bits(st.viol, vmask);
     r.pay_off = pay_off;
     r.pay_len = 0;
     r.length = st.length;
@@ -132,7 +146,7 @@ __device__ __forceinline__ void hdr_complete(frec& r, const dcarry& st, uint64_t
 // Returns true when any callback of the reference would fire for this frame
 // inside the segment (then `r` holds its record).  All lanes run it
 // redundantly on the same bytes, so control flow stays wave-uniform.
-__device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_t& pos, frec& r) {
+__device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_t& pos, frec& r, uint32_t vmask) {
     r.hdr_off = -1;
     r.pay_off = 0;
     r.pay_len = 0;
@@ -147,6 +161,7 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
         st.length = 0;
         st.mask_offset = 0;
         st.flags = (b0 & F_OPMASK) | ((b0 & 0x80u) ? F_FIN : 0u);
+        st.viol = ((b0 & 0x70u) ? V_RSV : 0u) | (reserved_opcode(b0 & F_OPMASK) ? V_OPCODE : 0u);
         st.state = S_HEAD;
         st.started = 1;
         r.hdr_off = (int64_t)pos;
@@ -159,6 +174,9 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
         ++pos;
         st.length = b1 & 0x7Fu;
         if (b1 & 0x80u) st.flags |= F_MASK;
+        if ((st.flags & 8u) && !(st.flags & F_FIN)) st.viol |= V_CONTROL;   // length checked once decoded
+        if (!(b1 & 0x80u)) st.viol |= V_UNMASKED;
+        if (st.length >= 126) st.viol |= (st.length == 127 ? 2u : 1u) << V_ENC_SHIFT;
         if (st.length >= 126) {
             st.require = st.length == 127 ? 8 : 2;
             st.length = 0;
@@ -169,11 +187,11 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
         } else if (st.length) {
             st.state = S_BODY;
             st.require = st.length;
-            hdr_complete(r, st, pos);
+            hdr_complete(r, st, pos, vmask);
             have = true;
         } else {
             st.state = S_START;
-            hdr_complete(r, st, pos);
+            hdr_complete(r, st, pos, vmask);
             r.info |= I_END;
             return true;
         }
@@ -185,17 +203,23 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
             ++pos;
         }
         if (st.require) return false;
+        {
+            const uint32_t enc = (st.viol >> V_ENC_SHIFT) & 3u;
+            if (enc == 2 && (st.length >> 63)) st.viol |= V_LEN64;
+            if ((enc == 1 && st.length < 126) || (enc == 2 && st.length <= 0xFFFFu)) st.viol |= V_NONMIN;
+            if ((st.flags & 8u) && st.length > 125) st.viol |= V_CONTROL;
+        }
         if (st.flags & F_MASK) {
             st.state = S_MASK;
             st.require = 4;
         } else if (st.length) {
             st.state = S_BODY;
             st.require = st.length;
-            hdr_complete(r, st, pos);
+            hdr_complete(r, st, pos, vmask);
             have = true;
         } else {
             st.state = S_START;
-            hdr_complete(r, st, pos);
+            hdr_complete(r, st, pos, vmask);
             r.info |= I_END;
             return true;
         }
@@ -211,11 +235,11 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
         if (st.length) {
             st.state = S_BODY;
             st.require = st.length;
-            hdr_complete(r, st, pos);
+            hdr_complete(r, st, pos, vmask);
             have = true;
         } else {
             st.state = S_START;
-            hdr_complete(r, st, pos);
+            hdr_complete(r, st, pos, vmask);
             r.info |= I_END;
             return true;
         }
@@ -293,13 +317,13 @@ __device__ __forceinline__ bool parse_at(const uint8_t* rx, uint64_t rx_len, uin
     return h.hlen <= rq && h.length <= rq - h.hlen;
 }
 
-__device__ __forceinline__ void whole_frame_rec(frec& v, uint64_t q, const hdr& h) {
+__device__ __forceinline__ void whole_frame_rec(frec& v, uint64_t q, const hdr& h, uint32_t vmask) {
     v.hdr_off = (int64_t)q;
     v.pay_off = q + h.hlen;
     v.pay_len = h.length;
     v.length = h.length;
     v.key = h.key;
-    v.info = h.flags | I_HDR | I_START | I_END | (h.length ? I_BODY : 0u);
+    v.info = h.flags | I_HDR | I_START | I_END | (h.length ? I_BODY : 0u) | invalid_bits(h.viol, vmask);
 }
 
 template <bool EMIT>
@@ -308,7 +332,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        const dcarry* __restrict__ carry_in, dmid* __restrict__ mid,
                                                        uint64_t* __restrict__ npred, uint64_t* __restrict__ first_fail,
                                                        uint64_t* __restrict__ last_masked,
-                                                       const uint64_t* __restrict__ bases, dframes fr) {
+                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
     for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
@@ -317,7 +341,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
         st.started = 0;
         uint64_t pos = 0, n = 0;
         frec r;
-        if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, r)) {
+        if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, r, vmask)) {
             if (EMIT && lane == 0) store_frame(fr, bases[s], sb, r);
             ++n;
         }
@@ -369,7 +393,7 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
                                                 const uint64_t* __restrict__ total_pred,
                                                 uint64_t* __restrict__ first_fail,
                                                 uint64_t* __restrict__ last_masked,
-                                                const uint64_t* __restrict__ bases, dframes fr) {
+                                                const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
     const uint64_t total = *total_pred;
     if (total == 0) return;
     const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
@@ -403,7 +427,7 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
                 atomicMin((unsigned long long*)&first_fail[s], (unsigned long long)j);
         } else if (j < first_fail[s]) {
             frec v;
-            whole_frame_rec(v, q, h);
+            whole_frame_rec(v, q, h, vmask);
             store_frame(fr, bases[s] + m.n_a + j, segs[s].off, v);
             if (h.flags & F_MASK) {
                 if (ms != s && mmax) {
@@ -437,7 +461,7 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
 // (EMIT only) by the lane owning record idx of the segment.
 template <bool EMIT, typename Emit>
 __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint64_t rx_len, uint64_t sb, uint64_t L,
-                                            dcarry& st, uint64_t& pos, uint64_t& n, Emit&& emit) {
+                                            dcarry& st, uint64_t& pos, uint64_t& n, uint32_t vmask, Emit&& emit) {
     const uint32_t lane = threadIdx.x & 63u;
     constexpr uint32_t NPRED = 64u * SCAN_U;
     uint64_t stride = 0;
@@ -480,7 +504,7 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
             const bool mine = j < f;
             if (EMIT && mine) {
                 frec v;
-                whole_frame_rec(v, pos + (uint64_t)j * stride, h[u]);
+                whole_frame_rec(v, pos + (uint64_t)j * stride, h[u], vmask);
                 emit(n + j, v);
             }
             const unsigned long long mm = __ballot(mine && (h[u].flags & F_MASK));
@@ -526,7 +550,7 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
 
     if (st.state == S_START && pos < L) {   // frame cut by the segment end
         frec r;
-        if (scalar_frame(rx + sb, L, st, pos, r)) {
+        if (scalar_frame(rx + sb, L, st, pos, r, vmask)) {
             if (EMIT && lane == 0) emit(n, r);
             ++n;
         }
@@ -542,7 +566,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ first_fail,
                                                        const uint64_t* __restrict__ last_masked,
                                                        dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
-                                                       const uint64_t* __restrict__ bases, dframes fr) {
+                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
 
@@ -576,7 +600,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
             }
         }
 
-        walk_frames<EMIT>(rx, rx_len, sb, L, st, pos, n,
+        walk_frames<EMIT>(rx, rx_len, sb, L, st, pos, n, vmask,
                           [&](uint64_t idx, const frec& v) { store_frame(fr, obase + idx, sb, v); });
         if (lane == 0) {
             if (!EMIT) counts[s] = n;
@@ -601,7 +625,7 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
                                               const uint64_t* __restrict__ slot_base, drec* __restrict__ slots,
                                               unsigned long long* __restrict__ rec_total, drec* __restrict__ h_rec,
                                               uint64_t h_rec_cap, dsmall_out* __restrict__ h_out,
-                                              uint8_t* __restrict__ h_rx, int unmask) {
+                                              uint8_t* __restrict__ h_rx, int unmask, uint32_t vmask) {
     const uint32_t s = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const uint64_t sb = segs[s].off, L = segs[s].len;
@@ -621,12 +645,12 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
     };
     if (st.state != S_START) {
         frec r;
-        if (scalar_frame(rx + sb, L, st, pos, r)) {
+        if (scalar_frame(rx + sb, L, st, pos, r, vmask)) {
             if (lane == 0) emit(0, r);
             n = 1;
         }
     }
-    walk_frames<true>(rx, rx_len, sb, L, st, pos, n, emit);
+    walk_frames<true>(rx, rx_len, sb, L, st, pos, n, vmask, emit);
     __threadfence_block();
     __syncthreads();
 
@@ -692,10 +716,11 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
 
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
-                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, hipStream_t st) {
+                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
+                        hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     hipLaunchKernelGGL(k_small, dim3(nseg), dim3(64), 0, st, rx, rx_len, segs, carry_in, slot_base, slots, rec_total,
-                       h_rec, h_rec_cap, h_out, h_rx, unmask);
+                       h_rec, h_rec_cap, h_out, h_rx, unmask, vmask);
     return hipGetLastError();
 }
 
@@ -1006,26 +1031,26 @@ static uint32_t wave_blocks(uint32_t nseg) {
 
 hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
-                       uint64_t* total, scan_scratch sc, dframes fr, hipStream_t st) {
+                       uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     const uint32_t wb = wave_blocks(nseg);
     const uint32_t vb = 2048;
     if (!emit) {
         hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr);
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
-                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr);
+                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
     } else {
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr);
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
-                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr);
+                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask);
     }
     return hipGetLastError();
 }

@@ -1,0 +1,155 @@
+// hvws_keys.hip -- batched WebSocket handshake digest (SURVEY.md sec. 8(f)
+// row 3): Sec-WebSocket-Accept = base64(SHA-1(key + GUID)) for many upgrade
+// requests at once, byte-identical to the reference's ws_encode_key
+// (http/wsdef.c:11-20; SHA-1 per util/sha1.c / FIPS 180-4, base64 per
+// util/base64.c:53-85 -- 28 characters, no terminator).
+//
+// One lane per key.  A conforming client key is 24 base64 characters
+// (RFC 6455 sec. 4.1: a 16-byte nonce), so key + GUID is 60 bytes and the
+// message is exactly two SHA-1 blocks: the first holds 6 key words and the 9
+// GUID words plus the 0x80 pad byte, the second only the bit length -- a
+// constant block whose message schedule the compiler folds.  Keys of any
+// other length take a generic byte-assembling loop.  Integer VALU-bound.
+#include "hvws_internal.h"
+
+namespace hvws {
+
+namespace {
+
+// "258EAFA5-E914-47DA-95CA-C5AB0DC85B11" as big-endian words (RFC 6455 sec. 1.3)
+__constant__ uint32_t kGuidW[9] = {0x32353845u, 0x41464135u, 0x2D453931u, 0x342D3437u, 0x44412D39u,
+                                   0x3543412Du, 0x43354142u, 0x30444338u, 0x35423131u};
+
+__device__ __forceinline__ uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+__device__ __forceinline__ void sha1_block(uint32_t h[5], uint32_t w[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rol(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        uint32_t f, k;
+        if (t < 20) {
+            f = (b & c) | (~b & d);
+            k = 0x5A827999u;
+        } else if (t < 40) {
+            f = b ^ c ^ d;
+            k = 0x6ED9EBA1u;
+        } else if (t < 60) {
+            f = (b & c) | (b & d) | (c & d);
+            k = 0x8F1BBCDCu;
+        } else {
+            f = b ^ c ^ d;
+            k = 0xCA62C1D6u;
+        }
+        const uint32_t tmp = rol(a, 5) + f + e + k + wt;
+        e = d;
+        d = c;
+        c = rol(b, 30);
+        b = a;
+        a = tmp;
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+}
+
+__device__ __forceinline__ uint32_t b64c(uint32_t v) {   // util/base64.c alphabet
+    return v < 26 ? 'A' + v : v < 52 ? 'a' + (v - 26) : v < 62 ? '0' + (v - 52) : v == 62 ? '+' : '/';
+}
+
+__device__ __forceinline__ uint8_t msg_byte(const uint8_t* key, uint64_t kl, uint64_t i, uint64_t total) {
+    if (i < kl) return key[i];
+    if (i < kl + 36) {
+        const uint64_t g = i - kl;
+        return (uint8_t)(kGuidW[g >> 2] >> (24 - 8 * (g & 3)));
+    }
+    if (i == kl + 36) return 0x80;
+    const uint64_t bits = (kl + 36) * 8;
+    if (i >= total - 8) return (uint8_t)(bits >> (8 * (total - 1 - i)));
+    return 0;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_encode_keys(const uint8_t* __restrict__ keys,
+                                                     const uint64_t* __restrict__ key_off,
+                                                     const uint32_t* __restrict__ key_len, uint64_t n,
+                                                     uint8_t* __restrict__ accept) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* key = keys + key_off[i];
+    const uint32_t kl = key_len[i];
+    uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    uint32_t w[16];
+    if (kl == 24) {
+        if (((uintptr_t)key & 3u) == 0) {   // 6 dword loads, byte-swapped to SHA-1's big-endian words
+            const uint32_t* kw = reinterpret_cast<const uint32_t*>(key);
+#pragma unroll
+            for (int t = 0; t < 6; ++t) w[t] = __builtin_bswap32(kw[t]);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+                w[t] = (uint32_t)key[4 * t] << 24 | (uint32_t)key[4 * t + 1] << 16 | (uint32_t)key[4 * t + 2] << 8 |
+                       key[4 * t + 3];
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[6 + t] = kGuidW[t];
+        w[15] = 0x80000000u;
+        sha1_block(h, w);
+#pragma unroll
+        for (int t = 0; t < 15; ++t) w[t] = 0;
+        w[15] = 60u * 8u;
+        sha1_block(h, w);
+    } else {
+        const uint64_t total = ((uint64_t)kl + 36 + 8) / 64 * 64 + 64;
+        for (uint64_t blk = 0; blk < total; blk += 64) {
+            for (int t = 0; t < 16; ++t) {
+                uint32_t v = 0;
+                for (int b = 0; b < 4; ++b) v = v << 8 | msg_byte(key, kl, blk + 4 * t + b, total);
+                w[t] = v;
+            }
+            sha1_block(h, w);
+        }
+    }
+    // base64 of the 20-byte digest: 6 groups of 3 bytes, then 2 bytes + '='
+    uint8_t d[21];
+#pragma unroll
+    for (int j = 0; j < 20; ++j) d[j] = (uint8_t)(h[j >> 2] >> (24 - 8 * (j & 3)));
+    d[20] = 0;
+    uint32_t o[8];
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+        const uint32_t v = (uint32_t)d[3 * g] << 16 | (uint32_t)d[3 * g + 1] << 8 | (g < 6 ? d[3 * g + 2] : 0u);
+        const uint32_t c3 = g < 6 ? b64c(v & 63) : '=';
+        o[g] = b64c(v >> 18) | b64c((v >> 12) & 63) << 8 | b64c((v >> 6) & 63) << 16 | c3 << 24;
+    }
+    o[7] = 0;   // the 4 bytes after the 28 characters read as zero, like the callers' zeroed buffers
+    uint32_t* out = reinterpret_cast<uint32_t*>(accept + i * 32);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<u32x4*>(out)[0] = u32x4{o[0], o[1], o[2], o[3]};
+    reinterpret_cast<u32x4*>(out)[1] = u32x4{o[4], o[5], o[6], o[7]};
+}
+
+hipError_t launch_encode_keys(const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len, uint64_t n,
+                              uint8_t* accept, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t per = 0xFFFFFFFFull / 256 * 256;   // keep each grid below 2^32 work-items
+    for (uint64_t a = 0; a < n; a += per) {
+        const uint64_t m = n - a < per ? n - a : per;
+        hipLaunchKernelGGL(k_encode_keys, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, st, keys, key_off + a,
+                           key_len + a, m, accept + a * 32);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace hvws

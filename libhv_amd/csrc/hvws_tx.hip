@@ -100,6 +100,10 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t s) {
     return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 
+constexpr uint32_t BUILD_MAXF = 128;   // frames per boundary tile staged in LDS
+
+__device__ __forceinline__ uint32_t tx_rotr(uint32_t x, uint32_t r) { return r ? (x >> r) | (x << (32u - r)) : x; }
+
 __device__ __forceinline__ void build_chunk(uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay,
                                             uint64_t plen, const uint64_t* __restrict__ pay_off,
                                             const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
@@ -214,6 +218,87 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
         }
     }
     const uint64_t k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
+    const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
+    if (nf && nf <= BUILD_MAXF && base + TILE <= out_len) {
+        // Boundary tile: the tile's frames staged in LDS; chunks inside one
+        // payload still stream (loads issued for all U chunks first), chunks
+        // holding header bytes or a frame boundary are assembled byte by byte.
+        __shared__ uint64_t s_off[BUILD_MAXF], s_ps[BUILD_MAXF], s_end[BUILD_MAXF], s_src[BUILD_MAXF];
+        __shared__ uint32_t s_key[BUILD_MAXF], s_fl[BUILD_MAXF];
+        if (tid < nf) {
+            const uint64_t k = k_lo + tid;
+            const uint32_t fl = flags[k];
+            const uint64_t ln = len[k], o = out_off[k];
+            const uint64_t ps = o + tx_hdr_len(fl, ln);
+            s_off[tid] = o;
+            s_ps[tid] = ps;
+            s_end[tid] = ps + ln;
+            s_src[tid] = pay_off[k];
+            s_key[tid] = (fl & F_MASK) ? mask[k] : 0u;
+            s_fl[tid] = fl;
+        }
+        __syncthreads();
+        u32x4 w[U], x[U];
+        uint32_t kw[U], sft[U], fi[U];
+        bool fast[U];
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            fi[i] = j;
+            fast[i] = false;
+            w[i] = x[i] = u32x4{0, 0, 0, 0};
+            kw[i] = 0;
+            sft[i] = 0;
+            if (j < nf) {
+                const uint64_t ps = s_ps[j];
+                const uint64_t src = s_src[j] + (c - ps);
+                if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
+                    fast[i] = true;
+                    sft[i] = (uint32_t)(src & 15u);
+                    const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
+                    w[i] = q[0];
+                    if (sft[i]) x[i] = q[1];
+                    kw[i] = tx_rotr(s_key[j], (uint32_t)((c - ps) & 3u) * 8u);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            u32x4 v;
+            if (fast[i]) {
+                v = (sft[i] ? funnel16(w[i], x[i], sft[i]) : w[i]) ^ u32x4{kw[i], kw[i], kw[i], kw[i]};
+            } else {
+                uint64_t lo = 0, hi = 0;
+                uint32_t j = fi[i];
+                for (uint32_t b = 0; b < 16; ++b) {
+                    const uint64_t a = c + b;
+                    while (j < nf && s_end[j] <= a) ++j;
+                    if (j >= nf || s_off[j] > a) continue;
+                    const uint32_t fl = s_fl[j];
+                    const uint64_t ps = s_ps[j];
+                    uint64_t byte;
+                    if (a < ps) {
+                        byte = tx_hdr_byte(fl, s_end[j] - ps, s_key[j], (uint32_t)(a - s_off[j]));
+                    } else {
+                        const uint64_t jj = a - ps;
+                        byte = pay[s_src[j] + jj] ^ ((s_key[j] >> (8 * (jj & 3u))) & 0xFFu);
+                    }
+                    if (b < 8) lo |= byte << (8 * b);
+                    else hi |= byte << (8 * (b - 8));
+                }
+                v = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+            }
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
+        }
+        return;
+    }
 #pragma unroll 1
     for (int i = 0; i < U; ++i) {
         const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
@@ -264,23 +349,24 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 }
 
 // Build geometries: X(index, chunks per thread, XCD order, nontemporal
-// realigning loads); 0 is the default.
+// realigning loads); 0 is the default.  On-device sweep (profiles/,
+// DESIGN.md): 256 x 2 linear reaches the copy ceiling; larger tiles lose
+// occupancy to the boundary-tile registers, and the XCD-contiguous order that
+// helps the in-place unmask halves this out-of-place stream.
 #define HVWS_BUILD_GEOMS(X) \
-    X(0, 4, false, false)   \
-    X(1, 8, false, false)   \
-    X(2, 2, false, false)   \
-    X(3, 4, true, false)    \
-    X(4, 4, false, true)    \
-    X(5, 16, false, false)  \
-    X(6, 1, false, false)   \
-    X(7, 8, false, true)
+    X(0, 2, false, false)   \
+    X(1, 4, false, false)   \
+    X(2, 1, false, false)   \
+    X(3, 2, true, false)    \
+    X(4, 2, false, true)    \
+    X(5, 8, false, false)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 8) ? x : 0;
+        return (x >= 0 && x < 6) ? x : 0;
     }();
     return v;
 }

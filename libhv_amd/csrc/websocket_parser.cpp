@@ -9,6 +9,7 @@
 // execute returns the index of the byte under the reference's cursor,
 // http/websocket_parser.c:14-32).  The decode/encode helpers run the XOR on
 // the GPU.  There is no CPU fallback: without a device these abort().
+#include <stddef.h>
 #include <string.h>
 
 #include <vector>
@@ -74,6 +75,8 @@ size_t websocket_parser_execute(websocket_parser* parser, const websocket_parser
                 p->require = 0;
             }
             const size_t at = (size_t)rel_pay - 1;   // last header byte
+            // hvws_set_validation: reject as a failing on_frame_header would
+            if (f.info & HVWS_I_INVALID) return at;
             if (settings->on_frame_header && settings->on_frame_header(p) != 0) return at;
             if (!f.length && (f.info & HVWS_I_END)) {
                 if (settings->on_frame_end && settings->on_frame_end(p) != 0) return at;
@@ -120,6 +123,9 @@ size_t websocket_parser_execute(websocket_parser* parser, const websocket_parser
     p->require = out.require;
     p->offset = out.offset;
     p->data = keep;
+    // partial-header validation state (padding byte after mask_offset; see hvws_set_validation)
+    reinterpret_cast<uint8_t*>(p)[offsetof(websocket_parser, mask_offset) + 1] =
+        reinterpret_cast<const uint8_t*>(&out)[offsetof(websocket_parser, mask_offset) + 1];
     if (out.state != S_START && started && !pending_has_record) p->mask_offset = 0;
     else p->mask_offset = mo;
     return len;

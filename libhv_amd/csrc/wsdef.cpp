@@ -63,7 +63,8 @@ int base64(const uint8_t* in, size_t n, char* out) {
         out[o++] = i + 1 < n ? tbl[(v >> 6) & 63] : '=';
         out[o++] = i + 2 < n ? tbl[v & 63] : '=';
     }
-    out[o] = 0;
+    // No terminator, like hv_base64_encode: ws_encode_key writes exactly 28
+    // bytes and its callers pass zeroed 32-byte buffers (HttpHandler.cpp:986).
     return (int)o;
 }
 

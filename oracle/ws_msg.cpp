@@ -197,4 +197,23 @@ uint64_t msgp_bench_decode_spans(char* rx, const uint64_t* off, const uint64_t* 
     return total;
 }
 
+#ifdef OWS_USE_REF
+/* Handshake digest baseline: the reference ws_encode_key (http/wsdef.c:11-20)
+ * over n keys of klen bytes laid out `stride` apart; out: 32 bytes per key. */
+void ws_encode_key(const char* key, char accept[]);
+uint64_t msgp_bench_keys(const char* keys, uint64_t n, uint32_t stride, uint32_t klen, char* out) {
+    char k[256];
+    uint64_t x = 0;
+    if (klen >= sizeof(k)) return 0;
+    for (uint64_t i = 0; i < n; i++) {
+        memcpy(k, keys + i * stride, klen);
+        k[klen] = 0;
+        memset(out + i * 32, 0, 32);
+        ws_encode_key(k, out + i * 32);
+        x += (uint8_t)out[i * 32];
+    }
+    return x;
+}
+#endif
+
 }  // extern "C"

@@ -117,6 +117,26 @@ def make_kat():
     print("kat written")
 
 
+def make_keys():
+    """Sec-WebSocket-Accept for 1500 conforming keys (base64 of a 16-byte
+    nonce) and 500 keys of other lengths (0-200 printable bytes), from the
+    reference ws_encode_key."""
+    import base64
+    L = H.ref()
+    rng = random.Random(4455)
+    keys = [base64.b64encode(rng.randbytes(16)) for _ in range(1500)]
+    keys += [bytes(rng.randrange(33, 127) for _ in range(rng.randrange(0, 201))) for _ in range(500)]
+    out = []
+    for k in keys:
+        acc = ctypes.create_string_buffer(32)
+        L.ws_encode_key(k, acc)
+        out.append([k.decode(), acc.raw.decode("latin-1")])
+    with open(os.path.join(HERE, "ws_keys.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py make_keys", "source": "oracle/_ref/libwsref.so "
+                   "ws_encode_key into zeroed char[32]", "cases": out}, f, indent=0)
+    print(f"ws_keys: {len(out)} cases")
+
+
 def ref_build(plan) -> np.ndarray:
     """Batch built frame by frame by the reference websocket_build_frame."""
     L = H.ref()
@@ -169,9 +189,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c1,c2")
     ap.add_argument("--skip-streams", action="store_true")
+    ap.add_argument("--only-keys", action="store_true")
     a = ap.parse_args()
+    if a.only_keys:
+        make_keys()
+        return
     if not a.skip_streams:
         make_kat()
+        make_keys()
         make_streams()
     if a.configs:
         make_configs([c for c in a.configs.split(",") if c])

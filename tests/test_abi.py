@@ -53,6 +53,14 @@ def test_every_declared_symbol_is_exported():
     assert not missing, missing
 
 
+def test_every_batch_entry_point_has_a_binding_signature():
+    """The Python binding declares argtypes for every hvws_* entry point, so
+    no pointer argument is ever passed through ctypes' default int conversion."""
+    names = [n for n in _declared_functions() if n.startswith("hvws_")]
+    missing = [n for n in sorted(names) if n not in libhv_amd._SIGS]
+    assert not missing, missing
+
+
 def test_cxx_drop_in_symbols_exported():
     out = subprocess.run(["nm", "-D", "--defined-only", libhv_amd.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
