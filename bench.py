@@ -223,17 +223,27 @@ def main():
             while L.hvws_set_unmask_variant(v) == 0:
                 names.append((v, L.hvws_unmask_kernel_name().decode()))
                 v += 1
+            stimes = {}
             for _ in range(3):
                 for v, name in names:
                     L.hvws_set_unmask_variant(v)
                     for _ in range(2):
                         eng.step(rx, plan.total, segs)
                         times.setdefault(name, []).append(eng.last_times()[1])
+                    # the in-place STREAM ceiling with the same geometry (two passes: no net change)
+                    eng.sync()
+                    t = time.perf_counter()
+                    for _ in range(2):
+                        eng.stream_xor(rx, plan.total & ~15, 0x5A5A5A5A)
+                    eng.sync()
+                    stimes.setdefault(name, []).append((time.perf_counter() - t) / 2)
             L.hvws_set_unmask_variant(0)
             ok = eng.synth(rx, plan.total, plan.seed, dp, 2 if passes % 2 else 1) == 0
             sweep = {n: (round(alg_bytes / (float(np.median(t)) * 1e-3) / 1e9, 1) if ok else None)
                      for n, t in times.items()}
             extra["unmask_sweep_GBps"] = sweep
+            extra["stream_sweep_GBps"] = {n: round(2 * (plan.total & ~15) / float(np.median(t)) / 1e9, 1)
+                                          for n, t in stimes.items()}
         extra["unmask_ms_mean"] = round(mean_unmask, 3)
 
         if not args.no_tx:

@@ -138,6 +138,12 @@ const char* hvws_unmask_kernel_name(void);
 /* Select another k_unmask geometry for later scans (tuning; process-wide). */
 int hvws_set_unmask_variant(int variant);
 
+/* Uniform runs of at least `frames` predicted frames in one segment are
+ * verified grid-wide (k_verify); shorter ones by the per-segment wave walk.
+ * Tuning only (process-wide, default 4096, 0 = default); results never
+ * depend on it.  Returns the previous value. */
+uint64_t hvws_set_spec_min(uint64_t frames);
+
 /* STREAM-style in-place ceiling: d[i] ^= pattern over n bytes (16-B aligned). */
 int hvws_stream_xor(hvws_ctx* ctx, uint8_t* d, uint64_t n, uint32_t pattern);
 
@@ -219,6 +225,10 @@ int   hvws_wsp_feed_many(void* const* handles, const char* const* data, const si
 /* Device used by the reference-API entry points on the calling thread
  * (default: $HVWS_DEVICE or 0). */
 int hvws_set_thread_device(int device);
+/* Free the calling thread's reference-API context (streams, device tables,
+ * pinned staging); call at event-loop thread exit.  The next call on the
+ * thread creates a fresh one. */
+void hvws_thread_release(void);
 
 #ifdef __cplusplus
 }

@@ -145,7 +145,9 @@ _SIGS = {
          ctypes.POINTER(ctypes.c_int)],
     ),
     "hvws_set_thread_device": (ctypes.c_int, [ctypes.c_int]),
+    "hvws_thread_release": (None, []),
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
+    "hvws_set_spec_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),

@@ -108,6 +108,7 @@ struct hvws_ctx {
     dbuf synth_sizes, synth_tiles, synth_bad;
     // small-batch path (k_small): upload packet, record slots, pinned results
     hbuf h_small_in, h_small_out;
+    hbuf h_feed;   // hvws_feed_many's gather buffer (reference-API thread contexts)
     dbuf d_small_in, d_small_slots;
     uint64_t small_limit = 0;   // bytes; 0 = default
     uint32_t vmask = 0;         // protocol validation classes (V_*); 0 = reference behaviour
@@ -136,6 +137,7 @@ struct hvws_ctx {
 namespace {
 constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
 constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
+constexpr uint64_t kSingleEstimate = 1ull << 26;   // records: one-stream table size before the count is known
 // Small-batch path (k_small): batches up to kSmallBatch bytes whose segments
 // are each at most kSmallSegment bytes run as one launch.
 constexpr uint64_t kSmallBatch = 64ull << 20;
@@ -154,6 +156,7 @@ dframes frames_of(hvws_ctx* c) {
     f.key = c->f_key.as<uint32_t>();
     f.keyrot = c->f_keyrot.as<uint32_t>();
     f.info = c->f_info.as<uint32_t>();
+    f.cap = c->frame_cap;
     return f;
 }
 
@@ -227,9 +230,18 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const dseg* segs = c->segs.as<dseg>();
     const dcarry* cin = c->carry_in.as<dcarry>();
     HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
-    HIP_OR(launch_scan(false, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream),
-           HVWS_EHIP);
+    auto pass = [&](int which) {
+        return launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
+                           c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream);
+    };
+    auto read_count = [&](uint64_t& n) -> int {
+        HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+        n = *c->h_total.as<uint64_t>();
+        if (n >= 0xFFFFFFF0ull)
+            return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
+        return HVWS_OK;
+    };
     // Frame records are bounded: after a segment's first record every frame
     // spends >= 2 of its bytes.  When the bound fits the table, EMIT follows
     // COUNT with no host round trip and the count stays on the device (the
@@ -237,20 +249,35 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const uint64_t bound = rx_len / 2 + 2 * (uint64_t)nseg + 1;
     uint64_t nfr = bound;
     c->nfr_known = false;
-    if (bound <= kFastFrameBound) {
-        HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
+    if (nseg == 1) {
+        // One stream: its base is 0, so EMIT needs no COUNT walk (a mixed-size
+        // stream's serial walk runs once).  The table is sized by the bound,
+        // or by an estimate that is checked after the pass and re-emitted
+        // into an exact-size table in the rare case it overflowed.
+        const uint64_t cap = std::min<uint64_t>(bound, std::max<uint64_t>(kFastFrameBound, kSingleEstimate));
+        HIP_OR(ensure_frames(c, cap), HVWS_ENOMEM);
+        HIP_OR(pass(SCAN_SINGLE), HVWS_EHIP);
+        if (bound > c->frame_cap) {
+            int rc = read_count(nfr);
+            if (rc) return rc;
+            if (nfr > c->frame_cap) {
+                HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
+                HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
+            }
+            c->nfr_known = true;
+        }
     } else {
-        HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
-        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
-        nfr = *c->h_total.as<uint64_t>();
-        if (nfr >= 0xFFFFFFF0ull)
-            return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)nfr);
-        HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
-        c->nfr_known = true;
+        HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
+        if (bound <= kFastFrameBound) {
+            HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
+        } else {
+            int rc = read_count(nfr);
+            if (rc) return rc;
+            HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
+            c->nfr_known = true;
+        }
+        HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
     }
-    HIP_OR(launch_scan(true, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                       c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream),
-           HVWS_EHIP);
     c->variant = unmask_variant();
     const uint64_t tile = unmask_tile(c->variant);
     const uint64_t ntiles = (rx_len + tile - 1) / tile;
@@ -589,6 +616,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     c->h_tx.release();
     c->h_small_in.release();
     c->h_small_out.release();
+    c->h_feed.release();
     c->h_segs.release();
     c->h_carry.release();
     c->h_total.release();
@@ -1065,10 +1093,17 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
 
 const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant()); }
 
+uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
+
 int hvws_set_unmask_variant(int v) {
     if (set_unmask_variant(v) < 0) return set_err(HVWS_EINVAL, "unmask variant %d out of range [0,%d)", v,
                                                   unmask_variant_count());
     return HVWS_OK;
+}
+
+void hvws_thread_release(void) {
+    if (t_ctx) hvws_ctx_destroy(t_ctx);
+    t_ctx = nullptr;
 }
 
 int hvws_set_thread_device(int device) {
@@ -1105,11 +1140,10 @@ hvws_ctx* thread_ctx() {
 
 // Per-thread pinned staging for batched host entry points.
 char* pinned_stage(uint64_t bytes) {
-    thread_local hbuf stage;
     hvws_ctx* c = thread_ctx();
-    if (hipSetDevice(c->device) != hipSuccess || stage.ensure(bytes + 64) != hipSuccess)
+    if (hipSetDevice(c->device) != hipSuccess || c->h_feed.ensure(bytes + 64) != hipSuccess)
         fatal("pinned staging allocation");
-    return stage.as<char>();
+    return c->h_feed.as<char>();
 }
 
 // XOR `n` host bytes at src into dst with key/phase on the GPU.

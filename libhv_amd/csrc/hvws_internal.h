@@ -64,6 +64,7 @@ struct dframes {
     uint32_t* key;       // raw key
     uint32_t* keyrot;    // key rotated for 4-byte aligned words (0 if not masked)
     uint32_t* info;
+    uint64_t  cap;       // records the arrays hold; EMIT drops records beyond it (counts stay exact)
 };
 
 // One frame record as handed to the host (layout of hvws_frame, 40 bytes).
@@ -107,7 +108,11 @@ __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
 // Kernel launchers (hvws_kernels.hip).
 // COUNT pass (emit=false): counts[], bases[] (exclusive scan) and *total.
 // EMIT pass: frame table at bases[], carry_out[].
-hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
+// SINGLE (one segment, base 0 known): COUNT's speculation only, then EMIT,
+// which also writes counts[] -- the serial walk of a mixed-size stream runs
+// once instead of twice.
+enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2 };
+hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
@@ -125,6 +130,9 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // Batched handshake digest (hvws_keys.hip): accept[32*i..] = base64(SHA-1(key_i + GUID)), 28 chars + 4 zero bytes.
 hipError_t launch_encode_keys(const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len, uint64_t n,
                               uint8_t* accept, hipStream_t st);
+// Predicted frames above which a uniform segment is verified grid-wide (k_verify).
+uint64_t spec_min();
+uint64_t set_spec_min(uint64_t v);   // 0 = default; returns the previous value
 // k_unmask geometry variants (threads x chunks/thread, XCD-ordered tiles)
 int unmask_variant();                      // process default ($HVWS_UNMASK or 0)
 int set_unmask_variant(int v);             // -1 if out of range

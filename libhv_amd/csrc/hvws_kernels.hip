@@ -6,7 +6,7 @@
 //                 Replaces the per-byte switch of websocket_parser_execute
 //                 (reference http/websocket_parser.c:53-171).
 //   k_offsets     exclusive scan of per-segment frame counts.
-//   k_tile_index  first frame touching each 32 KiB tile of the rx buffer.
+//   k_tile_scatter / k_tile_fixup  first frame touching each unmask tile.
 //   k_unmask      rotating 32-bit XOR of every masked payload byte, in place,
 //                 16-B coalesced loads/stores, tile frame table staged in LDS.
 //                 Replaces websocket_parser_decode's byte loop
@@ -113,6 +113,7 @@ struct frec {
 };
 
 __device__ __forceinline__ void store_frame(const dframes& fr, uint64_t idx, uint64_t seg_off, const frec& r) {
+    if (idx >= fr.cap) return;   // table sized by an estimate (SCAN_SINGLE): the host re-emits if it overflowed
     uint32_t phase = (r.info >> 8) & 3u;
     bool masked = (r.info & F_MASK) != 0;
     uint64_t abs_pay = seg_off + r.pay_off;
@@ -291,7 +292,7 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
 //   k_head    one wavefront per segment: finish the frame carried in from the
 //             previous batch (exact byte state machine), then parse the first
 //             whole frame; its size is the speculation stride.  Long segments
-//             (>= SPEC_MIN predicted frames) are handed to k_verify.
+//             (>= spec_min() predicted frames) are handed to k_verify.
 //   k_verify  the whole grid checks the predicted headers of every long
 //             segment at pos + j*stride in parallel (first break per segment
 //             by atomicMin); every prediction before the first break is a
@@ -304,7 +305,26 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
 //             then the exact state machine for the frame cut by the segment
 //             end.  Mixed-size streams advance >= 1 frame per round trip.
 
-constexpr uint64_t SPEC_MIN = 256;   // predicted frames that make a segment "long"
+// Predicted frames that make a segment "long" (grid-wide k_verify); shorter
+// uniform runs are verified by k_walk's wave-wide speculation, 256 frames
+// per round, all segments in parallel.  $HVWS_SPEC_MIN overrides (tuning).
+constexpr uint64_t SPEC_MIN_DEFAULT = 4096;
+static uint64_t g_spec_min = 0;   // 0: not yet read from the environment
+
+uint64_t spec_min() {
+    if (!g_spec_min) {
+        const char* e = getenv("HVWS_SPEC_MIN");
+        const long long x = e ? atoll(e) : 0;
+        g_spec_min = x > 0 ? (uint64_t)x : SPEC_MIN_DEFAULT;
+    }
+    return g_spec_min;
+}
+
+uint64_t set_spec_min(uint64_t v) {
+    const uint64_t old = spec_min();
+    g_spec_min = v ? v : SPEC_MIN_DEFAULT;
+    return old;
+}
 
 __device__ __forceinline__ bool parse_at(const uint8_t* rx, uint64_t rx_len, uint64_t seg_off, uint64_t L,
                                          uint64_t q, hdr& h) {
@@ -332,7 +352,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        const dcarry* __restrict__ carry_in, dmid* __restrict__ mid,
                                                        uint64_t* __restrict__ npred, uint64_t* __restrict__ first_fail,
                                                        uint64_t* __restrict__ last_masked,
-                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
+                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
+                                                       uint64_t spec_min) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
     for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
@@ -350,7 +371,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
         if (st.state == S_START && parse_at(rx, rx_len, sb, L, pos, h)) {
             stride = (uint64_t)h.hlen + h.length;
             const uint64_t cnt = (L - pos) / stride;
-            if (cnt >= SPEC_MIN) {
+            if (cnt >= spec_min) {
                 // Probe before committing the grid: lanes 0-31 check
                 // predictions 2^(l/2) (near the start), lanes 32-63 spread over
                 // the whole range.  Speculation stops at the first probe that
@@ -367,7 +388,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                     const uint64_t other = __shfl_xor(jb, o);
                     jb = other < jb ? other : jb;
                 }
-                np = jb >= SPEC_MIN ? jb : 0;
+                np = jb >= spec_min ? jb : 0;
             }
         }
         if (lane == 0) {
@@ -440,15 +461,35 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
         }
     }
     if (EMIT) {
-        // wave-uniform segment: reduce in registers, one lane publishes
+        // Segment-uniform block (the common case): reduce in registers and
+        // LDS, one atomic per block -- one per wave still serialised 16K
+        // same-address atomics for a 1M-frame stream (~80 us).
+        __shared__ uint32_t s_seg[256 / 64];
+        __shared__ uint64_t s_max[256 / 64];
         const uint32_t ms0 = __shfl(ms, 0);
-        if (__all(ms == ms0)) {
-            for (int o = 32; o > 0; o >>= 1) {
-                const uint64_t other = __shfl_xor(mmax, o);
-                mmax = other > mmax ? other : mmax;
+        const bool wave_uniform = __all(ms == ms0);
+        uint64_t wmax = mmax;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t other = __shfl_xor(wmax, o);
+            wmax = other > wmax ? other : wmax;
+        }
+        const uint32_t w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63u) == 0) {
+            s_seg[w] = wave_uniform ? ms0 : 0xFFFFFFFFu;
+            s_max[w] = wmax;
+        }
+        __syncthreads();
+        bool block_uniform = true;
+        for (uint32_t i = 0; i < blockDim.x / 64; ++i) block_uniform &= s_seg[i] == s_seg[0] && s_seg[i] != 0xFFFFFFFFu;
+        if (block_uniform) {
+            if (threadIdx.x == 0) {
+                uint64_t bmax = 0;
+                for (uint32_t i = 0; i < blockDim.x / 64; ++i) bmax = s_max[i] > bmax ? s_max[i] : bmax;
+                if (bmax) atomicMax((unsigned long long*)&last_masked[s_seg[0]], (unsigned long long)bmax);
             }
-            if ((threadIdx.x & 63u) == 0 && mmax)
-                atomicMax((unsigned long long*)&last_masked[ms0], (unsigned long long)mmax);
+        } else if (wave_uniform) {
+            if ((threadIdx.x & 63u) == 0 && wmax)
+                atomicMax((unsigned long long*)&last_masked[ms0], (unsigned long long)wmax);
         } else if (mmax) {
             atomicMax((unsigned long long*)&last_masked[ms], (unsigned long long)mmax);
         }
@@ -566,7 +607,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ first_fail,
                                                        const uint64_t* __restrict__ last_masked,
                                                        dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
-                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
+                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
+                                                       int emit_counts) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
 
@@ -603,8 +645,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
         walk_frames<EMIT>(rx, rx_len, sb, L, st, pos, n, vmask,
                           [&](uint64_t idx, const frec& v) { store_frame(fr, obase + idx, sb, v); });
         if (lane == 0) {
-            if (!EMIT) counts[s] = n;
-            else carry_out[s] = st;
+            if (!EMIT || emit_counts) counts[s] = n;
+            if (EMIT) carry_out[s] = st;
         }
     }
 }
@@ -755,13 +797,38 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ c
 
 // ---------------------------------------------------------- k_tile_index
 // tile_first[t] = first frame k with off[k] + len[k] > t*tile (t <= ntiles).
+// Two kernels: k_tile_scatter has each frame k write the tiles whose start
+// lies in [end(k-1), end(k)) (ends are non-decreasing) -- no search, one
+// write per tile; frames spanning more than TILE_SPAN_MAX tiles and the
+// tiles after the last frame are left marked, and k_tile_fixup binary
+// searches those.  A per-tile binary search for every tile cost ~100 us at
+// config 3 (4M tiles x 20 dependent loads).
 // nfr_p (device) overrides nfr_v when given: the frame count of a batch can
 // stay on the device, so a small batch needs no host round trip before EMIT.
-__global__ void k_tile_index(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
-                             uint64_t nfr_v, const uint64_t* __restrict__ nfr_p, uint32_t* __restrict__ tile_first,
-                             uint64_t ntiles, uint64_t tile) {
+constexpr uint32_t TILE_MARK = 0xFFFFFFFFu;
+constexpr uint64_t TILE_SPAN_MAX = 64;
+
+__global__ void k_tile_scatter(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t nfr_v,
+                               const uint64_t* __restrict__ nfr_p, uint32_t* __restrict__ tile_first, uint64_t ntiles,
+                               uint64_t tile) {
+    const uint64_t nfr = nfr_p ? *nfr_p : nfr_v;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nfr; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t lo = k ? off[k - 1] + len[k - 1] : 0;
+        const uint64_t hi = off[k] + len[k];
+        if (hi <= lo) continue;
+        const uint64_t t0 = (lo + tile - 1) / tile;
+        uint64_t t1 = (hi + tile - 1) / tile;
+        if (t1 > ntiles + 1) t1 = ntiles + 1;
+        if (t1 <= t0 || t1 - t0 > TILE_SPAN_MAX) continue;
+        for (uint64_t t = t0; t < t1; ++t) tile_first[t] = (uint32_t)k;
+    }
+}
+
+__global__ void k_tile_fixup(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t nfr_v,
+                             const uint64_t* __restrict__ nfr_p, uint32_t* __restrict__ tile_first, uint64_t ntiles,
+                             uint64_t tile) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
+    if (t > ntiles || tile_first[t] != TILE_MARK) return;
     const uint64_t nfr = nfr_p ? *nfr_p : nfr_v;
     const uint64_t x = t * tile;
     uint64_t lo = 0, hi = nfr;
@@ -1029,28 +1096,45 @@ static uint32_t wave_blocks(uint32_t nseg) {
     return blocks > 65536u ? 65536u : (blocks ? blocks : 1u);
 }
 
-hipError_t launch_scan(bool emit, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
+hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     const uint32_t wb = wave_blocks(nseg);
     const uint32_t vb = 2048;
-    if (!emit) {
+    if (pass == SCAN_SINGLE) {
         hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask);
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
+        hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
+                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
+        hipError_t e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
+        hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
+                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
+        hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 1);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+        return hipGetLastError();
+    }
+    if (pass == SCAN_COUNT) {
+        hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
     } else {
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask);
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0);
     }
     return hipGetLastError();
 }
@@ -1064,8 +1148,11 @@ hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
                              uint32_t* tile_first, uint64_t ntiles, uint64_t tile, hipStream_t st) {
     const uint64_t n = ntiles + 1;
+    hipError_t e = hipMemsetAsync(tile_first, 0xFF, n * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tile_scatter, dim3(2048), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_tile_index, dim3(blocks), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
+    hipLaunchKernelGGL(k_tile_fixup, dim3(blocks), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
     return hipGetLastError();
 }
 
@@ -1095,7 +1182,10 @@ struct unmask_geom {
     X(5, 256, 2, true)                                                                    \
     X(6, 256, 8, true)                                                                    \
     X(7, 256, 8, false)                                                                   \
-    X(8, 64, 8, true)
+    X(8, 64, 8, true)                                                                     \
+    X(9, 256, 4, false)                                                                   \
+    X(10, 256, 2, false)                                                                  \
+    X(11, 512, 2, false)
 #define HVWS_GEOM_ENTRY(i, t, u, s) {t, u, s},
 static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
 static int g_geom = -1;

@@ -33,6 +33,17 @@ def rx_path(request):
         L.hvws_set_small_batch_limit(eng.ctx, 0)
 
 
+@pytest.fixture(params=[256, 0], ids=["verify256", "verify_default"])
+def spec_min(request):
+    """Grid-wide uniform-run verification (k_verify) from 256 predicted frames
+    (so these small cases exercise it) and at the default threshold (where
+    k_walk's wave speculation verifies them)."""
+    L = libhv_amd.lib()
+    old = L.hvws_set_spec_min(request.param)
+    yield request.param
+    L.hvws_set_spec_min(old)
+
+
 # ------------------------------------------------ reference frame-layer ABI
 @pytest.mark.parametrize("name,data", S.quirk_streams(), ids=[n for n, _ in S.quirk_streams()])
 @pytest.mark.parametrize("mode", ["one", "bytes", "small"])
@@ -224,7 +235,7 @@ def test_synth_matches_oracle(eng):
 
 @pytest.mark.parametrize("nseg", [1, 7, 256])
 @pytest.mark.parametrize("kind", ["u1k", "u64k", "mixed"])
-def test_batch_configs_small(eng, kind, nseg):
+def test_batch_configs_small(eng, spec_min, kind, nseg):
     plan = {"u1k": lambda: synth.uniform_plan(4000, 1024, 11),
             "u64k": lambda: synth.uniform_plan(300, 65536, 12),
             "mixed": lambda: synth.mixed_plan(24 << 20, 13)}[kind]().split(nseg)
@@ -272,7 +283,7 @@ def test_stream_xor_roundtrip(eng):
     b.free()
 
 
-def test_batch_dense_tiny_frames(eng):
+def test_batch_dense_tiny_frames(eng, spec_min):
     """Many frames inside one 16-byte chunk (2-byte unmasked empties between
     masked ones) at every alignment: the unmask kernel's boundary merge must
     visit each payload piece."""
@@ -293,7 +304,7 @@ def test_batch_dense_tiny_frames(eng):
         _compare_batch(eng, buf, [(pad, len(data) - pad)])
 
 
-def test_long_segment_speculation_breaks(eng):
+def test_long_segment_speculation_breaks(eng, spec_min):
     """Uniform runs verified in parallel, broken by a different size at many
     positions (the prefix verifier must stop exactly at the first break)."""
     rng = random.Random(31)
@@ -311,7 +322,7 @@ def test_long_segment_speculation_breaks(eng):
         _compare_batch(eng, rest, [(0, len(rest))], [st])
 
 
-def test_long_segment_last_frame_unmasked(eng):
+def test_long_segment_last_frame_unmasked(eng, spec_min):
     """Verified prefix ending in an unmasked frame of the same stride: the
     carried mask must be the last *masked* key (Q14, stale mask)."""
     rng = random.Random(41)
