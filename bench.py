@@ -101,6 +101,38 @@ def cpu_baseline(sample: np.ndarray, seconds: float, threads: int):
     return payload * sum(counts) / dt / 2**30, kind, passes, payload * sum(counts)
 
 
+def cpu_decode_only(sample: np.ndarray, plan, seconds: float):
+    """Reference websocket_decode alone (http/websocket_parser.c:182-189) over
+    the masked payload spans of the sample's frames, one core: the XOR the
+    GPU kernel replaces, without parsing or message assembly."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wsharness as H
+    from libhv_amd import synth
+
+    L = H.ref() if H.have_ref() else H.oracle()
+    hdr = synth.frame_size(plan.flags, plan.length) - plan.length
+    end = plan.frame_off + synth.frame_size(plan.flags, plan.length)
+    m = int(np.searchsorted(end, sample.nbytes, side="right"))
+    sel = (plan.flags[:m] & synth.MASK) != 0
+    off = np.ascontiguousarray((plan.frame_off[:m] + hdr[:m])[sel], dtype=np.uint64)
+    ln = np.ascontiguousarray(plan.length[:m][sel], dtype=np.uint64)
+    key = np.ascontiguousarray(plan.mask[:m][sel], dtype=np.uint32)
+    buf = sample.copy()
+    L.msgp_bench_decode_spans.restype = ctypes.c_uint64
+    L.msgp_bench_decode_spans.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_size_t]
+    args = (buf.ctypes.data, off.ctypes.data, ln.ctypes.data, key.ctypes.data, len(ln))
+    t0 = time.perf_counter()
+    per = L.msgp_bench_decode_spans(*args)
+    one = max(time.perf_counter() - t0, 1e-6)
+    passes = max(1, int(seconds / one))
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        L.msgp_bench_decode_spans(*args)
+    dt = time.perf_counter() - t0
+    return per * passes / dt / 2**30
+
+
 def init_dist():
     """(rank, world, local_rank, dist-or-None).  One process per GPU; gloo
     carries only the barrier and the timing reduction (no data collectives)."""
@@ -323,6 +355,8 @@ def main():
                 "sample": f"{sample.nbytes} B of the same batch ({args.config} frames) x {passes1} passes, "
                           "WebSocketParser semantics (header parse + in-place unmask + message append), 8 KiB chunks",
                 "multi_thread": {"value": round(vn, 3), "threads": nthr},
+                "decode_only": {"value": round(cpu_decode_only(sample, plan, args.cpu_seconds / 4), 3), "cores": 1,
+                                "note": "websocket_decode over the sample's masked payload spans"},
             }
         out = {
             "metric": "device-resident WS unmask GiB/s, 64 KiB masked frames, 1/2/4/8 MI355X",

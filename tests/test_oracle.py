@@ -97,6 +97,9 @@ def test_oracle_matches_reference_live():
         assert H.run_messages("oracle", data, chunks) == H.run_messages("ref", data, chunks)
 
 
+I_HDR, I_END = 1 << 10, 1 << 12   # HVWS_I_HDR / HVWS_I_END (include/hvws.h)
+
+
 def test_scan_records_consistent_with_callbacks():
     """ows_scan_segment (frame records, the GPU table's CPU twin) agrees with the
     callback stream: one record per frame with any callback in the segment."""
@@ -108,9 +111,8 @@ def test_scan_records_consistent_with_callbacks():
         recs2, st2, _, out2 = H.scan_segment(data[cut:], st1)
         msgs, _, _, buf = H.run_messages("oracle", data, [cut, len(data) - cut] if cut else [len(data)])
         assert out1 + out2 == buf
-        hdrs = int(((recs1["info"] & H.__dict__.get("I_HDR", 1 << 10)) != 0).sum() +
-                   ((recs2["info"] & (1 << 10)) != 0).sum())
-        ends = int(((recs1["info"] & (1 << 12)) != 0).sum() + ((recs2["info"] & (1 << 12)) != 0).sum())
+        hdrs = int(((recs1["info"] & I_HDR) != 0).sum() + ((recs2["info"] & I_HDR) != 0).sum())
+        ends = int(((recs1["info"] & I_END) != 0).sum() + ((recs2["info"] & I_END) != 0).sum())
         log = H.parse_log(H.run_evlog("oracle", data, [cut, len(data) - cut] if cut else [len(data)])[0])
         assert hdrs == sum(1 for e in log if e[0] == "H")
         assert ends == sum(1 for e in log if e[0] == "E")
