@@ -506,6 +506,12 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
     const uint32_t lane = threadIdx.x & 63u;
     constexpr uint32_t NPRED = 64u * SCAN_U;
     uint64_t stride = 0;
+    // Speculation width (wave-uniform): predictions loaded per round.  A run
+    // of equal sizes doubles it up to NPRED; a break shrinks it to about
+    // twice the frames the round proved, so a mixed-size stream costs ~2
+    // header loads per frame (one HBM round trip) instead of NPRED scattered
+    // loads, most of them TLB misses.
+    uint32_t width = NPRED;
     while (st.state == S_START && pos < L) {
         const uint64_t rem = L - pos;
         if (stride == 0) {
@@ -518,7 +524,7 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
 #pragma unroll
         for (int u = 0; u < SCAN_U; ++u) {
             const uint32_t j = (uint32_t)u * 64u + lane;
-            inr[u] = rem >= 2 && (j == 0 || stride <= (rem - 2) / j);
+            inr[u] = j < width && rem >= 2 && (j == 0 || stride <= (rem - 2) / j);
             lo[u] = hi[u] = 0;
             if (inr[u]) ld16(rx, rx_len, sb + pos + (uint64_t)j * stride, lo[u], hi[u]);
         }
@@ -571,7 +577,11 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
         }
         n += f;
         pos += (uint64_t)f * stride;
-        if (f == NPRED) continue;
+        if (f == width) {   // every prediction held: widen, same stride
+            width = width * 2 < NPRED ? width * 2 : NPRED;
+            continue;
+        }
+        width = f * 2 < 2 ? 2 : (f * 2 < NPRED ? f * 2 : NPRED);
         if (pos >= L) break;
         bool wf = false;
         uint64_t sf = 0;
