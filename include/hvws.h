@@ -132,6 +132,11 @@ int     hvws_get_carry(hvws_ctx* ctx, websocket_parser* out, int* started);
  * unmask: out[0] = scan kernels (count + offsets + emit + tile index),
  * out[1] = unmask kernel. */
 int hvws_last_times(hvws_ctx* ctx, float out[2]);
+/* The same for each of the last min(max_steps, 32) scans, oldest first:
+ * out[2*i] = scan ms, out[2*i+1] = unmask ms (-1 if the step had none).
+ * Waits for those steps only; returns the number of steps written (< 0 on
+ * error).  Lets a caller time a run of asynchronous steps afterwards. */
+int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
 
 /* Name of the k_unmask geometry in use (e.g. "k_unmask<256,8,xcd>"). */
 const char* hvws_unmask_kernel_name(void);

@@ -107,6 +107,7 @@ _SIGS = {
     "hvws_get_segment_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "hvws_get_carry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "hvws_last_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "hvws_step_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "hvws_stream_xor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]),
     "hvws_rx_batch": (
         ctypes.c_int,
@@ -333,6 +334,14 @@ class Engine:
         out = (ctypes.c_float * 2)()
         _check(lib().hvws_last_times(self.ctx, out), "hvws_last_times")
         return float(out[0]), float(out[1])
+
+    def step_times(self, max_steps: int = 32) -> List[Tuple[float, float]]:
+        """(scan ms, unmask ms) of the last max_steps steps (at most 32), oldest first."""
+        out = (ctypes.c_float * (2 * max_steps))()
+        n = lib().hvws_step_times(self.ctx, out, max_steps)
+        if n < 0:
+            _check(n, "hvws_step_times")
+        return [(float(out[2 * i]), float(out[2 * i + 1])) for i in range(n)]
 
     def stream_xor(self, buf: DeviceBuffer, n: int, pattern: int) -> None:
         _check(lib().hvws_stream_xor(self.ctx, buf.ptr, n, pattern), "hvws_stream_xor")

@@ -101,7 +101,14 @@ struct hvws_ctx {
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first, tile_key, tile_kind;
     uint64_t frame_cap = 0;
-    hbuf h_segs, h_carry, h_total;
+    hbuf h_segs, h_total;
+    // Segment/carry upload staging: two pinned slots used in turn, each
+    // reusable once the H2D copy that read it has run (event), so a step
+    // never waits for the previous step's kernels.
+    hbuf h_up[2];
+    hipEvent_t up_ev[2] = {nullptr, nullptr};
+    bool up_pending[2] = {false, false};
+    int up_next = 0;
     // staging for host-memory entry points
     dbuf stage;
     dbuf xor_stage;
@@ -122,8 +129,15 @@ struct hvws_ctx {
     uint64_t rx_len = 0;
     const uint8_t* rx = nullptr;
     bool have_scan = false;
-    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // scan, unmask, build
-    bool ev_unmask = false;
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // [4], [5]: build / keys
+    // Per-step timing: scan begin/end and unmask begin/end events for the
+    // last kTimeRing steps, read after the fact (hvws_step_times) so a caller
+    // timing many steps need not synchronise after each.
+    static constexpr int kTimeRing = 32;
+    hipEvent_t tev[kTimeRing][4] = {};
+    bool t_unmask[kTimeRing] = {};
+    uint64_t t_seq = 0;   // scans recorded so far
+    int t_cur = 0;        // ring slot of the last scan
     int variant = 0;   // k_unmask geometry the tile index was built for
     bool nfr_known = false;   // else c->nfr is an upper bound, the count is on the device
     // host copy of the last scan's results (readback_all)
@@ -206,6 +220,27 @@ int check_ctx(hvws_ctx* c) {
     return HVWS_OK;
 }
 
+// Next slot of the timing ring: record the scan-begin event there.
+hipError_t begin_timed_scan(hvws_ctx* c) {
+    c->t_cur = (int)(c->t_seq % hvws_ctx::kTimeRing);
+    c->t_unmask[c->t_cur] = false;
+    ++c->t_seq;
+    return hipEventRecord(c->tev[c->t_cur][0], c->stream);
+}
+
+// out[0] = scan ms, out[1] = unmask ms (-1: no unmask) of the step in ring `slot`.
+int step_times_at(hvws_ctx* c, int slot, float* out) {
+    hipEvent_t* e = c->tev[slot];
+    out[0] = out[1] = -1.0f;
+    HIP_OR(hipEventSynchronize(e[1]), HVWS_EHIP);
+    HIP_OR(hipEventElapsedTime(&out[0], e[0], e[1]), HVWS_EHIP);
+    if (c->t_unmask[slot]) {
+        HIP_OR(hipEventSynchronize(e[3]), HVWS_EHIP);
+        HIP_OR(hipEventElapsedTime(&out[1], e[2], e[3]), HVWS_EHIP);
+    }
+    return HVWS_OK;
+}
+
 // Scan with the carry-in already resident in c->carry_in (device).
 int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_t nseg) {
     HIP_OR(c->counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
@@ -229,7 +264,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.total_pred = c->sc_total.as<uint64_t>();
     const dseg* segs = c->segs.as<dseg>();
     const dcarry* cin = c->carry_in.as<dcarry>();
-    HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
+    HIP_OR(begin_timed_scan(c), HVWS_EHIP);
     auto pass = [&](int which) {
         return launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
                            c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream);
@@ -292,13 +327,12 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                              c->tile_first.as<uint32_t>(), c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(),
                              ntiles, tile, rx_len, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
     c->nseg = nseg;
     c->nfr = nfr;
     c->rx = d_rx;
     c->rx_len = rx_len;
     c->have_scan = true;
-    c->ev_unmask = false;
     c->hcache_valid = false;
     return HVWS_OK;
 }
@@ -402,12 +436,18 @@ int upload_segments(hvws_ctx* c, const hvws_segment* segs, const websocket_parse
     }
     HIP_OR(c->segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
     HIP_OR(c->carry_in.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
-    HIP_OR(c->h_segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
-    HIP_OR(c->h_carry.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
-    // The pinned staging may still be the source of an in-flight copy.
-    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
-    dseg* hs = c->h_segs.as<dseg>();
-    dcarry* hc = c->h_carry.as<dcarry>();
+    // Pinned staging slot: it may still be the source of the copy issued two
+    // uploads ago -- wait for that copy only (not for the kernels after it).
+    const int u = c->up_next;
+    c->up_next ^= 1;
+    if (c->up_pending[u]) {
+        HIP_OR(hipEventSynchronize(c->up_ev[u]), HVWS_EHIP);
+        c->up_pending[u] = false;
+    }
+    const uint64_t o_carry = ((uint64_t)nseg * sizeof(dseg) + 63) & ~63ull;
+    HIP_OR(c->h_up[u].ensure(o_carry + (uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    dseg* hs = c->h_up[u].as<dseg>();
+    dcarry* hc = reinterpret_cast<dcarry*>(c->h_up[u].as<uint8_t>() + o_carry);
     for (uint32_t s = 0; s < nseg; ++s) {
         hs[s].off = segs[s].off;
         hs[s].len = segs[s].len;
@@ -421,6 +461,8 @@ int upload_segments(hvws_ctx* c, const hvws_segment* segs, const websocket_parse
            HVWS_EHIP);
     HIP_OR(hipMemcpyAsync(c->carry_in.p, hc, (uint64_t)nseg * sizeof(dcarry), hipMemcpyHostToDevice, c->stream),
            HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->up_ev[u], c->stream), HVWS_EHIP);
+    c->up_pending[u] = true;
     return HVWS_OK;
 }
 
@@ -498,13 +540,13 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     uint8_t* d = c->d_small_in.as<uint8_t>();
     HIP_OR(hipMemcpyAsync(d, hp, pkt, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
     if (user_mapped && len) HIP_OR(hipMemcpyAsync(d + o_data, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->ev[0], c->stream), HVWS_EHIP);
+    HIP_OR(begin_timed_scan(c), HVWS_EHIP);
     HIP_OR(launch_small(d + o_data, len, (const dseg*)(d + o_segs), (const dcarry*)(d + o_carry), nseg,
                         (const uint64_t*)(d + o_slot), c->d_small_slots.as<drec>(), (unsigned long long*)d,
                         (drec*)(ho_d + nseg), hcap, ho_d, user_mapped ? user_mapped : hp_d + o_data, unmask,
                         c->vmask, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->ev[1], c->stream), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (!user_mapped && unmask && len) memcpy(h_rx, hp + o_data, len);
     // host cache in segment order
@@ -540,7 +582,6 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     c->rx = nullptr;   // the device frame table is not populated: hvws_unmask refuses
     c->rx_len = 0;
     c->have_scan = true;
-    c->ev_unmask = false;
     c->hcache_valid = true;
     if (carry) {
         for (uint32_t s = 0; s < nseg; ++s) {
@@ -592,12 +633,15 @@ hvws_ctx* hvws_ctx_create(int device) {
         hvws_ctx_destroy(c);
         return nullptr;
     }
-    for (auto& ev : c->ev) {
-        if (hipEventCreate(&ev) != hipSuccess) {
-            set_err(HVWS_EHIP, "event creation failed");
-            hvws_ctx_destroy(c);
-            return nullptr;
-        }
+    bool ev_ok = true;
+    for (auto& ev : c->ev) ev_ok = ev_ok && hipEventCreate(&ev) == hipSuccess;
+    for (auto& row : c->tev)
+        for (auto& ev : row) ev_ok = ev_ok && hipEventCreate(&ev) == hipSuccess;
+    for (auto& ev : c->up_ev) ev_ok = ev_ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok) {
+        set_err(HVWS_EHIP, "event creation failed");
+        hvws_ctx_destroy(c);
+        return nullptr;
     }
     return c;
 }
@@ -618,9 +662,14 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     c->h_small_out.release();
     c->h_feed.release();
     c->h_segs.release();
-    c->h_carry.release();
+    for (hbuf& b : c->h_up) b.release();
     c->h_total.release();
     for (auto& ev : c->ev)
+        if (ev) hipEventDestroy(ev);
+    for (auto& row : c->tev)
+        for (auto& ev : row)
+            if (ev) hipEventDestroy(ev);
+    for (auto& ev : c->up_ev)
         if (ev) hipEventDestroy(ev);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy_in) hipStreamDestroy(c->copy_in);
@@ -717,12 +766,13 @@ int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     if (!c->have_scan) return set_err(HVWS_EINVAL, "hvws_unmask without a preceding hvws_scan");
     if (d_rx != c->rx || rx_len != c->rx_len)
         return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
-    HIP_OR(hipEventRecord(c->ev[2], c->stream), HVWS_EHIP);
+    hipEvent_t* tev = c->tev[c->t_cur];
+    HIP_OR(hipEventRecord(tev[2], c->stream), HVWS_EHIP);
     HIP_OR(launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(),
                          c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->total.as<uint64_t>(), c->stream),
            HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->ev[3], c->stream), HVWS_EHIP);
-    c->ev_unmask = true;
+    HIP_OR(hipEventRecord(tev[3], c->stream), HVWS_EHIP);
+    c->t_unmask[c->t_cur] = true;
     return HVWS_OK;
 }
 
@@ -825,14 +875,21 @@ int hvws_last_times(hvws_ctx* c, float out[2]) {
     int rc = check_ctx(c);
     if (rc) return rc;
     out[0] = out[1] = -1.0f;
-    if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
-    HIP_OR(hipEventSynchronize(c->ev[1]), HVWS_EHIP);
-    HIP_OR(hipEventElapsedTime(&out[0], c->ev[0], c->ev[1]), HVWS_EHIP);
-    if (c->ev_unmask) {
-        HIP_OR(hipEventSynchronize(c->ev[3]), HVWS_EHIP);
-        HIP_OR(hipEventElapsedTime(&out[1], c->ev[2], c->ev[3]), HVWS_EHIP);
+    if (!c->have_scan || c->t_seq == 0) return set_err(HVWS_EINVAL, "no scan");
+    return step_times_at(c, c->t_cur, out);
+}
+
+int hvws_step_times(hvws_ctx* c, float* out, int max_steps) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!out || max_steps < 0) return set_err(HVWS_EINVAL, "bad output");
+    uint64_t n = std::min<uint64_t>(c->t_seq, hvws_ctx::kTimeRing);
+    n = std::min<uint64_t>(n, (uint64_t)max_steps);
+    for (uint64_t i = 0; i < n; ++i) {
+        const int slot = (int)((c->t_seq - n + i) % hvws_ctx::kTimeRing);
+        if ((rc = step_times_at(c, slot, out + 2 * i)) != HVWS_OK) return rc;
     }
-    return HVWS_OK;
+    return (int)n;
 }
 
 int hvws_stream_xor(hvws_ctx* c, uint8_t* d, uint64_t n, uint32_t pattern) {
@@ -918,6 +975,7 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
             // k's carry-in (a frame may straddle the chunk boundary).
             const dseg ds = {0, n};
             e = hipStreamSynchronize(c->stream);
+            if (e == hipSuccess) e = c->h_segs.ensure(sizeof(ds));
             if (e != hipSuccess) break;
             memcpy(c->h_segs.p, &ds, sizeof(ds));
             e = hipMemcpyAsync(c->segs.p, c->h_segs.p, sizeof(ds), hipMemcpyHostToDevice, c->stream);
