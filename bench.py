@@ -210,6 +210,7 @@ def main():
         eng.step(rx, plan.total, segs)
     barrier()
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    scan_path = libhv_amd.lib().hvws_last_scan_path(eng.ctx)
     times = eng.step_times(min(args.steps, 32))
     scan_ms = [t[0] for t in times]
     unmask_ms = [t[1] for t in times]
@@ -247,6 +248,8 @@ def main():
         ceiling = 2 * (plan.total & ~15) * reps / (time.perf_counter() - t) / 1e9
         extra["stream_ceiling_GBps"] = round(ceiling, 1)
         extra["scan_ms_mean"] = round(float(np.mean(scan_ms)), 3)
+        extra["scan_path"] = {0: "count_emit", 1: "count_read_emit", 2: "single", 3: "speculative",
+                              4: "speculative_rejected"}.get(scan_path, scan_path)
         if args.sweep_unmask:
             # every geometry, interleaved round by round in this process; an
             # even number of passes per geometry leaves the batch masked, which

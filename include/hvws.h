@@ -108,8 +108,10 @@ int   hvws_d2d(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async
 int   hvws_sync(hvws_ctx* ctx);
 
 /* ---- the hot path, device resident ---------------------------------- */
-/* Frame discovery + header parse for every segment.  Synchronises once (to
- * size the frame table).  Results stay on the device in `ctx`. */
+/* Frame discovery + header parse for every segment.  Waits for the device
+ * once (to size the frame table, or for its speculative table's check; see
+ * hvws_set_speculation) -- not for earlier work on the stream to finish.
+ * Results stay on the device in `ctx`. */
 int hvws_scan(hvws_ctx* ctx, const uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
               const websocket_parser* carry_in, uint32_t nseg);
 /* Unmask, in place, every masked payload span found by the last scan.
@@ -148,6 +150,33 @@ int hvws_set_unmask_variant(int variant);
  * Tuning only (process-wide, default 4096, 0 = default); results never
  * depend on it.  Returns the previous value. */
 uint64_t hvws_set_spec_min(uint64_t frames);
+
+/* Speculative frame table for large multi-segment batches: when the last
+ * batch's per-segment record counts matched the uniform-stride estimates,
+ * the next scan emits straight into the table at the estimated offsets and
+ * the device checks it (one walk, no host round trip before EMIT); a failed
+ * check re-scans exactly.  mode -1 = that automatic choice (default, or
+ * $HVWS_SPEC unset), 0 = never speculate, 1 = always try first (tests).
+ * Results never depend on it.  ctx NULL = the calling thread's context.
+ * Returns the previous mode. */
+int hvws_set_speculation(hvws_ctx* ctx, int mode);
+
+/* How the last hvws_scan on ctx found its frames (tests, benchmarks). */
+enum {
+    HVWS_PATH_COUNT_EMIT = 0,       /* COUNT then EMIT, table sized by the record bound, no wait */
+    HVWS_PATH_COUNT_READ_EMIT = 1,  /* COUNT, wait for the count, EMIT */
+    HVWS_PATH_SINGLE = 2,           /* one segment: one walk into an estimated table */
+    HVWS_PATH_SPEC = 3,             /* speculative table checked exact on the device */
+    HVWS_PATH_SPEC_FAILED = 4       /* speculation rejected by the check, then COUNT/EMIT */
+};
+int hvws_last_scan_path(hvws_ctx* ctx);
+/* Batches whose record bound (rx_len / 2 + 2 * nseg + 1) is at most
+ * `records` are scanned COUNT -> EMIT with the table sized by that bound
+ * (default 2^24); larger ones wait for a count (or speculate).  1 makes
+ * every multi-segment batch take the large-batch path, 0 restores the
+ * default.  Tuning/testing only; results never depend on it.  Returns the
+ * previous bound. */
+uint64_t hvws_set_fast_bound(hvws_ctx* ctx, uint64_t records);
 
 /* STREAM-style in-place ceiling: d[i] ^= pattern over n bytes (16-B aligned). */
 int hvws_stream_xor(hvws_ctx* ctx, uint8_t* d, uint64_t n, uint32_t pattern);

@@ -62,13 +62,14 @@ struct dbuf {
 struct hbuf {   // grow-only pinned host allocation
     void* p = nullptr;
     uint64_t cap = 0;
+    unsigned flags = hipHostMallocDefault;   // hipHostMallocCoherent: device reads/writes bypass its caches
     hipError_t ensure(uint64_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
         if (p) hipHostFree(p);
         p = nullptr;
         cap = 0;
         uint64_t want = std::max<uint64_t>(bytes + bytes / 2, 4096);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, flags);
         if (e == hipSuccess) cap = want;
         return e;
     }
@@ -105,10 +106,25 @@ struct hvws_ctx {
     // Segment/carry upload staging: two pinned slots used in turn, each
     // reusable once the H2D copy that read it has run (event), so a step
     // never waits for the previous step's kernels.
+    // The scan's first kernel reads the slot through its device mapping (no
+    // copy); up_src_* point at the slot the next scan is to read.
     hbuf h_up[2];
     hipEvent_t up_ev[2] = {nullptr, nullptr};
     bool up_pending[2] = {false, false};
     int up_next = 0;
+    int up_slot = -1;
+    const dseg* up_src_segs = nullptr;
+    const dcarry* up_src_carry = nullptr;
+    // Speculative EMIT (SCAN_SPEC): per-segment estimates, the device's
+    // verdict in pinned memory, and whether the last exact scan says the
+    // estimates hold (then the next batch speculates).
+    dbuf sc_est;
+    hbuf h_status;
+    uint64_t scan_seq = 0;
+    bool spec_ok = false;
+    int spec_mode = -1;   // -1 auto, 0 never, 1 always try first ($HVWS_SPEC / hvws_set_speculation)
+    uint64_t fast_bound = 0;   // record bound below which COUNT -> EMIT needs no host wait; 0 = default
+    int scan_path = -1;        // HVWS_PATH_* of the last scan
     // staging for host-memory entry points
     dbuf stage;
     dbuf xor_stage;
@@ -136,6 +152,7 @@ struct hvws_ctx {
     static constexpr int kTimeRing = 32;
     hipEvent_t tev[kTimeRing][4] = {};
     bool t_unmask[kTimeRing] = {};
+    bool t_adjacent[kTimeRing] = {};   // unmask started at the scan's end event
     uint64_t t_seq = 0;   // scans recorded so far
     int t_cur = 0;        // ring slot of the last scan
     int variant = 0;   // k_unmask geometry the tile index was built for
@@ -220,6 +237,14 @@ int check_ctx(hvws_ctx* c) {
     return HVWS_OK;
 }
 
+// Device address of a pinned host buffer.
+template <typename T>
+T* mapped(hbuf& b) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, b.p, 0) != hipSuccess) return nullptr;
+    return reinterpret_cast<T*>(d);
+}
+
 // Next slot of the timing ring: record the scan-begin event there.
 hipError_t begin_timed_scan(hvws_ctx* c) {
     c->t_cur = (int)(c->t_seq % hvws_ctx::kTimeRing);
@@ -236,13 +261,57 @@ int step_times_at(hvws_ctx* c, int slot, float* out) {
     HIP_OR(hipEventElapsedTime(&out[0], e[0], e[1]), HVWS_EHIP);
     if (c->t_unmask[slot]) {
         HIP_OR(hipEventSynchronize(e[3]), HVWS_EHIP);
-        HIP_OR(hipEventElapsedTime(&out[1], e[2], e[3]), HVWS_EHIP);
+        HIP_OR(hipEventElapsedTime(&out[1], c->t_adjacent[slot] ? e[1] : e[2], e[3]), HVWS_EHIP);
     }
     return HVWS_OK;
 }
 
+// Wait until k_spec_check has published scan `seq` in the (fine-grained)
+// pinned status: the device stores it with system-scope release as its last
+// write, so the host polls it instead of a stream event (an event marker
+// costs ~10 us of device idle between the check and the tile kernels).  A
+// stream that drains without publishing is an error, never a hang.
+int wait_status(hvws_ctx* c, uint64_t seq) {
+    const dspec_status* st = c->h_status.as<dspec_status>();
+    for (uint64_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+                return set_err(HVWS_EHIP, "scan check did not publish (seq %llu)", (unsigned long long)seq);
+            }
+            if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "stream error: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // Scan with the carry-in already resident in c->carry_in (device).
-int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_t nseg) {
+// Unmask kernel launch with its timing events (no argument checks).
+// after_scan: queued right behind the scan's end event, which then doubles
+// as the unmask's start (one timing marker fewer).
+hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
+    hipEvent_t* tev = c->tev[c->t_cur];
+    c->t_adjacent[c->t_cur] = after_scan;
+    hipError_t e;
+    if (!after_scan && (e = hipEventRecord(tev[2], c->stream)) != hipSuccess) return e;
+    if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(),
+                           c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->total.as<uint64_t>(),
+                           c->stream)) != hipSuccess)
+        return e;
+    if ((e = hipEventRecord(tev[3], c->stream)) != hipSuccess) return e;
+    c->t_unmask[c->t_cur] = true;
+    return hipSuccess;
+}
+
+// unmask_into: the caller will unmask d_rx right after the scan (hvws_step).
+// On the speculative path the unmask is then queued before the host waits
+// for the device's check -- a rejected table has a zero count, so that
+// unmask does nothing -- and *unmasked reports whether it stands.
+int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint8_t* unmask_into = nullptr,
+                      bool* unmasked = nullptr) {
+    if (unmasked) *unmasked = false;
     HIP_OR(c->counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->total.ensure(8), HVWS_ENOMEM);
@@ -255,6 +324,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     HIP_OR(c->sc_fail.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->sc_masked.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->sc_total.ensure(8), HVWS_ENOMEM);
+    HIP_OR(c->sc_est.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->h_status.ensure(sizeof(dspec_status)), HVWS_ENOMEM);
     scan_scratch sc;
     sc.mid = c->sc_mid.as<dmid>();
     sc.npred = c->sc_npred.as<uint64_t>();
@@ -262,12 +333,39 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.first_fail = c->sc_fail.as<uint64_t>();
     sc.last_masked = c->sc_masked.as<uint64_t>();
     sc.total_pred = c->sc_total.as<uint64_t>();
+    sc.est = c->sc_est.as<uint64_t>();
+    sc.src_segs = c->up_src_segs;
+    sc.src_carry = c->up_src_carry;
+    sc.segs_w = c->segs.as<dseg>();
+    sc.carry_w = c->carry_in.as<dcarry>();
+    sc.status = nullptr;
+    sc.seq = 0;
+    dspec_status* status_d = mapped<dspec_status>(c->h_status);
+    const dspec_status* status_h = c->h_status.as<dspec_status>();
+    if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
     const dseg* segs = c->segs.as<dseg>();
     const dcarry* cin = c->carry_in.as<dcarry>();
     HIP_OR(begin_timed_scan(c), HVWS_EHIP);
+    // After the first pass the device tables hold the uploaded segments; the
+    // pinned slot is free once that pass's first kernel has run.
+    const int up_slot = c->up_slot;
+    c->up_slot = -1;
+    c->up_src_segs = nullptr;
+    c->up_src_carry = nullptr;
+    bool slot_released = up_slot < 0;
     auto pass = [&](int which) {
-        return launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(), c->counts.as<uint64_t>(),
-                           c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc, frames_of(c), c->vmask, c->stream);
+        const hipError_t e = launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(),
+                                         c->counts.as<uint64_t>(), c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc,
+                                         frames_of(c), c->vmask, c->stream);
+        sc.src_segs = nullptr;
+        sc.src_carry = nullptr;
+        if (e == hipSuccess && !slot_released) {
+            slot_released = true;
+            const hipError_t e2 = hipEventRecord(c->up_ev[up_slot], c->stream);
+            c->up_pending[up_slot] = e2 == hipSuccess;
+            return e2;
+        }
+        return e;
     };
     auto read_count = [&](uint64_t& n) -> int {
         HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
@@ -277,6 +375,30 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
         return HVWS_OK;
     };
+    // k_spec_check's verdict for the pass just issued (after a wait on the
+    // stream or for the published status): the record count and the SPEC_* flags.
+    auto read_status = [&](uint64_t& n, uint32_t& flags) -> int {
+        if (status_h->seq != sc.seq) return set_err(HVWS_EHIP, "scan status not published (seq %llu, want %llu)",
+                                                    (unsigned long long)status_h->seq, (unsigned long long)sc.seq);
+        n = status_h->total;
+        flags = status_h->flags;
+        if (n >= 0xFFFFFFF0ull)
+            return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
+        return HVWS_OK;
+    };
+    c->variant = unmask_variant();
+    const uint64_t tile = unmask_tile(c->variant);
+    const uint64_t ntiles = (rx_len + tile - 1) / tile;
+    HIP_OR(c->tile_first.ensure((ntiles + 8) * 4), HVWS_ENOMEM);
+    HIP_OR(c->tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(c->tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
+    auto tiles = [&]() -> int {
+        HIP_OR(launch_unmask_tiles(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), c->f_keyrot.as<uint32_t>(),
+                                   c->total.as<uint64_t>(), c->tile_first.as<uint32_t>(), c->tile_key.as<uint32_t>(),
+                                   c->tile_kind.as<uint8_t>(), ntiles, tile, rx_len, c->stream),
+               HVWS_EHIP);
+        return HVWS_OK;
+    };
     // Frame records are bounded: after a segment's first record every frame
     // spends >= 2 of its bytes.  When the bound fits the table, EMIT follows
     // COUNT with no host round trip and the count stays on the device (the
@@ -284,7 +406,9 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const uint64_t bound = rx_len / 2 + 2 * (uint64_t)nseg + 1;
     uint64_t nfr = bound;
     c->nfr_known = false;
+    bool tiles_done = false;
     if (nseg == 1) {
+        c->scan_path = HVWS_PATH_SINGLE;
         // One stream: its base is 0, so EMIT needs no COUNT walk (a mixed-size
         // stream's serial walk runs once).  The table is sized by the bound,
         // or by an estimate that is checked after the pass and re-emitted
@@ -301,33 +425,55 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             }
             c->nfr_known = true;
         }
-    } else {
+    } else if (bound <= (c->fast_bound ? c->fast_bound : kFastFrameBound)) {
+        c->scan_path = HVWS_PATH_COUNT_EMIT;
         HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
-        if (bound <= kFastFrameBound) {
-            HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
-        } else {
-            int rc = read_count(nfr);
-            if (rc) return rc;
-            HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
-            c->nfr_known = true;
-        }
+        HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
         HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
+    } else {
+        // Large batch: the table is sized from a count.  With the estimates
+        // holding on the last batch, EMIT speculatively into the table as
+        // it is (SCAN_SPEC) and let the device check it -- one walk, no
+        // host round trip before EMIT, and the tile kernels queued behind
+        // the check; the host then waits for the check only.  Otherwise (or
+        // when the check fails) COUNT, read the count, EMIT.
+        int rc;
+        uint32_t flags = 0;
+        sc.status = status_d;
+        bool done = false;
+        c->scan_path = HVWS_PATH_COUNT_READ_EMIT;
+        if ((c->spec_ok && c->spec_mode != 0) || c->spec_mode == 1) {
+            sc.seq = ++c->scan_seq;
+            HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
+            if ((rc = tiles()) != HVWS_OK) return rc;
+            if (unmask_into) {
+                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
+            }
+            if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
+            if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            done = (flags & SPEC_OK) != 0;
+            c->spec_ok = done;
+            c->scan_path = done ? HVWS_PATH_SPEC : HVWS_PATH_SPEC_FAILED;
+            if (done && unmask_into && unmasked) *unmasked = true;
+            tiles_done = done;
+        }
+        if (!done) {
+            sc.seq = ++c->scan_seq;
+            HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
+            HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+            if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            c->spec_ok = (flags & SPEC_MATCH) != 0;
+            HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
+            HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
+        }
+        c->nfr_known = true;
     }
-    c->variant = unmask_variant();
-    const uint64_t tile = unmask_tile(c->variant);
-    const uint64_t ntiles = (rx_len + tile - 1) / tile;
-    HIP_OR(c->tile_first.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
-    HIP_OR(c->tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
-    HIP_OR(c->tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
-    const uint64_t* nfr_dev = c->total.as<uint64_t>();
-    HIP_OR(launch_tile_index(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), 0, nfr_dev,
-                             c->tile_first.as<uint32_t>(), ntiles, tile, c->stream),
-           HVWS_EHIP);
-    HIP_OR(launch_tile_class(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), c->f_keyrot.as<uint32_t>(), nfr_dev,
-                             c->tile_first.as<uint32_t>(), c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(),
-                             ntiles, tile, rx_len, c->stream),
-           HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
+    if (!tiles_done) {
+        int rc = tiles();
+        if (rc) return rc;
+    }
+    if (!(unmasked && *unmasked)) HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
     c->nseg = nseg;
     c->nfr = nfr;
     c->rx = d_rx;
@@ -436,8 +582,8 @@ int upload_segments(hvws_ctx* c, const hvws_segment* segs, const websocket_parse
     }
     HIP_OR(c->segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
     HIP_OR(c->carry_in.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
-    // Pinned staging slot: it may still be the source of the copy issued two
-    // uploads ago -- wait for that copy only (not for the kernels after it).
+    // Pinned staging slot: the scan two uploads ago may still be about to
+    // read it -- wait for that scan's first kernel only.
     const int u = c->up_next;
     c->up_next ^= 1;
     if (c->up_pending[u]) {
@@ -457,12 +603,14 @@ int upload_segments(hvws_ctx* c, const hvws_segment* segs, const websocket_parse
             memset(&hc[s], 0, sizeof(dcarry));
         }
     }
-    HIP_OR(hipMemcpyAsync(c->segs.p, hs, (uint64_t)nseg * sizeof(dseg), hipMemcpyHostToDevice, c->stream),
-           HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(c->carry_in.p, hc, (uint64_t)nseg * sizeof(dcarry), hipMemcpyHostToDevice, c->stream),
-           HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->up_ev[u], c->stream), HVWS_EHIP);
-    c->up_pending[u] = true;
+    // No copy: the scan's first kernel reads the slot through its device
+    // mapping and writes c->segs / c->carry_in (a DMA copy of these tables
+    // cost ~40 us of idle device per step).
+    uint8_t* dev = mapped<uint8_t>(c->h_up[u]);
+    if (!dev) return set_err(HVWS_EHIP, "pinned upload slot not device-mapped");
+    c->up_slot = u;
+    c->up_src_segs = reinterpret_cast<const dseg*>(dev);
+    c->up_src_carry = reinterpret_cast<const dcarry*>(dev + o_carry);
     return HVWS_OK;
 }
 
@@ -476,13 +624,6 @@ uint8_t* host_mapped(void* p) {
     }
     if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
     return (uint8_t*)a.devicePointer + ((uint8_t*)p - (uint8_t*)a.hostPointer);
-}
-
-template <typename T>
-T* mapped(hbuf& b) {
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, b.p, 0) != hipSuccess) return nullptr;
-    return reinterpret_cast<T*>(d);
 }
 
 bool small_eligible(hvws_ctx* c, uint64_t len, const hvws_segment* segs, uint32_t nseg) {
@@ -593,6 +734,18 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     return HVWS_OK;
 }
 
+// Unmask launch.  after_scan: queued right behind the scan's end event,
+// which then doubles as the unmask's start (one timing marker fewer).
+int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!c->have_scan) return set_err(HVWS_EINVAL, "hvws_unmask without a preceding hvws_scan");
+    if (d_rx != c->rx || rx_len != c->rx_len)
+        return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
+    HIP_OR(issue_unmask(c, d_rx, rx_len, after_scan), HVWS_EHIP);
+    return HVWS_OK;
+}
+
 thread_local int t_device = -1;
 thread_local hvws_ctx* t_ctx = nullptr;
 
@@ -626,6 +779,12 @@ hvws_ctx* hvws_ctx_create(int device) {
     }
     hvws_ctx* c = new hvws_ctx();
     c->device = device;
+    // Tables the device reads (upload slots) or writes (check verdict) in
+    // host memory while the host uses them between launches: fine-grained,
+    // so no stale copy can sit in a device cache across reuses.
+    for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
+    c->h_status.flags = hipHostMallocCoherent;
+    if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : -1);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess) {
@@ -671,6 +830,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
             if (ev) hipEventDestroy(ev);
     for (auto& ev : c->up_ev)
         if (ev) hipEventDestroy(ev);
+    c->sc_est.release();
+    c->h_status.release();
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy_in) hipStreamDestroy(c->copy_in);
     if (c->copy_out) hipStreamDestroy(c->copy_out);
@@ -760,27 +921,18 @@ int hvws_scan(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, const hvws_segm
     return scan_device_carry(c, d_rx, rx_len, nseg);
 }
 
-int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
-    int rc = check_ctx(c);
-    if (rc) return rc;
-    if (!c->have_scan) return set_err(HVWS_EINVAL, "hvws_unmask without a preceding hvws_scan");
-    if (d_rx != c->rx || rx_len != c->rx_len)
-        return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
-    hipEvent_t* tev = c->tev[c->t_cur];
-    HIP_OR(hipEventRecord(tev[2], c->stream), HVWS_EHIP);
-    HIP_OR(launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(),
-                         c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->total.as<uint64_t>(), c->stream),
-           HVWS_EHIP);
-    HIP_OR(hipEventRecord(tev[3], c->stream), HVWS_EHIP);
-    c->t_unmask[c->t_cur] = true;
-    return HVWS_OK;
-}
+int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) { return unmask_impl(c, d_rx, rx_len, false); }
 
 int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
               const websocket_parser* carry_in, uint32_t nseg) {
-    int rc = hvws_scan(c, d_rx, rx_len, segs, carry_in, nseg);
+    int rc = check_ctx(c);
     if (rc) return rc;
-    return hvws_unmask(c, d_rx, rx_len);
+    if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
+    if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
+    if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
+    bool unmasked = false;
+    if ((rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked)) != HVWS_OK) return rc;
+    return unmasked ? HVWS_OK : unmask_impl(c, d_rx, rx_len, true);
 }
 
 int64_t hvws_frame_count(hvws_ctx* c) {
@@ -910,9 +1062,10 @@ int hvws_rx_batch(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* 
     uint8_t* d = c->stage.as<uint8_t>();
     if ((rc = upload_segments(c, segs, carry, nseg, len)) != HVWS_OK) return rc;
     if (len) HIP_OR(hipMemcpyAsync(d, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
-    if ((rc = scan_device_carry(c, d, len, nseg)) != HVWS_OK) return rc;
+    bool unmasked = false;
+    if ((rc = scan_device_carry(c, d, len, nseg, unmask ? d : nullptr, &unmasked)) != HVWS_OK) return rc;
     if (unmask) {
-        if ((rc = hvws_unmask(c, d, len)) != HVWS_OK) return rc;
+        if (!unmasked && (rc = unmask_impl(c, d, len, true)) != HVWS_OK) return rc;
         if (len) HIP_OR(hipMemcpyAsync(h_rx, d, len, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     }
     // one round trip for the results (the D2H of the bytes above is ordered before it)
@@ -1152,6 +1305,23 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
 const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant()); }
 
 uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
+
+int hvws_last_scan_path(hvws_ctx* c) { return c ? c->scan_path : -1; }
+
+uint64_t hvws_set_fast_bound(hvws_ctx* c, uint64_t records) {
+    if (!c) return 0;
+    const uint64_t old = c->fast_bound ? c->fast_bound : kFastFrameBound;
+    c->fast_bound = records;
+    return old;
+}
+
+int hvws_set_speculation(hvws_ctx* c, int mode) {
+    if (!c) c = thread_ctx();
+    if (!c) return HVWS_ENODEV;
+    const int old = c->spec_mode;
+    c->spec_mode = mode < 0 ? -1 : (mode > 1 ? 1 : mode);
+    return old;
+}
 
 int hvws_set_unmask_variant(int v) {
     if (set_unmask_variant(v) < 0) return set_err(HVWS_EINVAL, "unmask variant %d out of range [0,%d)", v,

@@ -88,6 +88,19 @@ constexpr int SCAN_THREADS = 256;           // 4 waves, one segment per wave
 constexpr int SCAN_U = 4;                   // predicted frames per lane per round
 constexpr int UNMASK_MAXF = 512;            // frames staged in LDS per tile
 
+// Result of k_spec_check, written by the device into pinned host memory.
+struct dspec_status {
+    uint64_t seq;     // scan sequence number it belongs to
+    uint64_t total;   // records of the batch (sum of the true counts)
+    uint32_t flags;   // SPEC_*
+    uint32_t pad;
+    uint64_t pad2[5];
+};
+enum : uint32_t {
+    SPEC_MATCH = 1u,   // every segment's record count equals k_head's estimate
+    SPEC_OK = 2u       // SCAN_SPEC: the speculative table is the exact table (match and within capacity)
+};
+
 struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     dmid*     mid;
     uint64_t* npred;
@@ -95,6 +108,16 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint64_t* first_fail;
     uint64_t* last_masked;   // 1 + index of the last masked verified frame, 0 none
     uint64_t* total_pred;
+    uint64_t* est;           // records k_head predicts per segment (uniform-stride hypothesis)
+    // Zero-copy upload: when src_segs is set, the first k_head of the scan
+    // reads the segment and carry tables from these (device-mapped pinned
+    // host) arrays and writes the device tables the later kernels read.
+    const dseg*   src_segs;
+    const dcarry* src_carry;
+    dseg*         segs_w;
+    dcarry*       carry_w;
+    dspec_status* status;    // device-mapped pinned host
+    uint64_t      seq;
 };
 
 // Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
@@ -111,7 +134,14 @@ __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
 // SINGLE (one segment, base 0 known): COUNT's speculation only, then EMIT,
 // which also writes counts[] -- the serial walk of a mixed-size stream runs
 // once instead of twice.
-enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2 };
+// SPEC (several segments, frame table of known capacity): EMIT at bases
+// taken from k_head's per-segment estimates, then k_spec_check compares the
+// true counts with them -- equal everywhere means the table is exact, so a
+// uniform batch is discovered with one walk and no host round trip before
+// EMIT; otherwise *total is zeroed (the tile kernels and k_unmask then do
+// nothing) and the host re-runs COUNT + EMIT.  COUNT also runs the check,
+// to tell the host whether the next batch is worth speculating on.
+enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2, SCAN_SPEC = 3 };
 hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
@@ -144,6 +174,11 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
 hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
                              const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
                              uint64_t tile, uint64_t rx_len, hipStream_t st);
+// Tile index + tile classes for k_unmask in one sequence (fill, scatter,
+// fused fixup/classify); tile_first must hold ntiles + 8 entries.
+hipError_t launch_unmask_tiles(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
+                               uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
+                               uint64_t tile, uint64_t rx_len, hipStream_t st);
 hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
 hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st);
 

@@ -353,12 +353,40 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        uint64_t* __restrict__ npred, uint64_t* __restrict__ first_fail,
                                                        uint64_t* __restrict__ last_masked,
                                                        const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
-                                                       uint64_t spec_min) {
+                                                       uint64_t spec_min, uint64_t* __restrict__ est,
+                                                       const dseg* __restrict__ src_segs,
+                                                       const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
+                                                       dcarry* __restrict__ carry_w) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
     for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
-        const uint64_t sb = segs[s].off, L = segs[s].len;
-        dcarry st = carry_in[s];
+        dseg sg;
+        dcarry st;
+        if (src_segs) {
+            // Zero-copy upload: lanes 0-3 each fetch one 16-B piece of the
+            // segment's 64 bytes (segment + carry) from host memory, store it
+            // into the device tables and broadcast it -- one PCIe read per
+            // piece instead of one per lane.
+            u32x4 piece = {0u, 0u, 0u, 0u};
+            if (lane == 0) piece = *reinterpret_cast<const u32x4*>(&src_segs[s]);
+            else if (lane < 4) piece = reinterpret_cast<const u32x4*>(&src_carry[s])[lane - 1];
+            if (lane == 0) *reinterpret_cast<u32x4*>(&segs_w[s]) = piece;
+            else if (lane < 4) reinterpret_cast<u32x4*>(&carry_w[s])[lane - 1] = piece;
+            uint32_t w[16];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                w[4 * p + 0] = __shfl(piece.x, p);
+                w[4 * p + 1] = __shfl(piece.y, p);
+                w[4 * p + 2] = __shfl(piece.z, p);
+                w[4 * p + 3] = __shfl(piece.w, p);
+            }
+            __builtin_memcpy(&sg, &w[0], sizeof(sg));
+            __builtin_memcpy(&st, &w[4], sizeof(st));
+        } else {
+            sg = segs[s];
+            st = carry_in[s];
+        }
+        const uint64_t sb = sg.off, L = sg.len;
         st.started = 0;
         uint64_t pos = 0, n = 0;
         frec r;
@@ -391,7 +419,26 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                 np = jb >= spec_min ? jb : 0;
             }
         }
+        uint64_t e = n;   // records if every frame after pos had size `stride`
+        if (est && st.state == S_START && pos < L) {
+            uint64_t q = pos;
+            if (stride) {
+                const uint64_t cnt = (L - pos) / stride;
+                e += cnt;
+                q += cnt * stride;
+            }
+            // the frame cut by the segment end fires a record iff its
+            // header completes inside the segment
+            const uint64_t rem = L - q;
+            if (rem >= 2) {
+                const uint32_t b1 = rx[sb + q + 1];
+                const uint32_t len7 = b1 & 0x7Fu;
+                const uint64_t hl = 2u + (len7 == 126 ? 2u : (len7 == 127 ? 8u : 0u)) + ((b1 & 0x80u) ? 4u : 0u);
+                if (hl <= rem) ++e;
+            }
+        }
         if (lane == 0) {
+            if (est) est[s] = e;
             dmid m;
             m.st = st;
             m.pos = pos;
@@ -805,6 +852,58 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ c
     if (t == 1023u) *total = part[1023];
 }
 
+// ----------------------------------------------------------- k_spec_check
+// Compare the true per-segment record counts with k_head's estimates (one
+// block).  SPEC: the table was emitted at the estimates' offsets, so it is
+// exact iff every count matches and the records fit the table; then *total
+// = the record count, else 0 (everything downstream becomes a no-op and the
+// host re-scans exactly).  COUNT (observe only): report whether the
+// estimates would have held, leave *total alone.  Results go to pinned host
+// memory (status), tagged with the scan's sequence number.
+template <bool SPEC>
+__global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict__ counts,
+                                                     const uint64_t* __restrict__ est, uint32_t nseg,
+                                                     uint64_t* __restrict__ total, uint64_t cap,
+                                                     dspec_status* __restrict__ status, uint64_t seq) {
+    __shared__ uint64_t s_sum[1024 / 64];
+    __shared__ uint32_t s_bad[1024 / 64];
+    const uint32_t t = threadIdx.x;
+    uint64_t sum = 0;
+    uint32_t bad = 0;
+    for (uint32_t i = t; i < nseg; i += 1024) {
+        const uint64_t c = counts[i];
+        sum += c;
+        bad |= c != est[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        bad |= __shfl_xor(bad, o);
+    }
+    if ((t & 63u) == 0) {
+        s_sum[t >> 6] = sum;
+        s_bad[t >> 6] = bad;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t all = 0;
+        uint32_t any_bad = 0;
+        for (int w = 0; w < 1024 / 64; ++w) {
+            all += s_sum[w];
+            any_bad |= s_bad[w];
+        }
+        uint32_t flags = any_bad ? 0u : SPEC_MATCH;
+        if (SPEC) {
+            const bool ok = !any_bad && all <= cap;
+            if (ok) flags |= SPEC_OK;
+            *total = ok ? all : 0;
+        }
+        status->total = all;
+        status->flags = flags;
+        // last: the host polls seq (fine-grained pinned memory)
+        __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ---------------------------------------------------------- k_tile_index
 // tile_first[t] = first frame k with off[k] + len[k] > t*tile (t <= ntiles).
 // Two kernels: k_tile_scatter has each frame k write the tiles whose start
@@ -871,6 +970,40 @@ __global__ void k_tile_class(const uint64_t* __restrict__ off, const uint64_t* _
     } else if (off[k] <= x && xe <= off[k] + len[k] && xe == x + tile) {
         key = keyrot[k];
         kind = key ? TILE_SINGLE : TILE_NONE;   // one payload; zero key word = no-op
+    }
+    tile_key[t] = key;
+    tile_kind[t] = (uint8_t)kind;
+}
+
+// k_tile_fixup + k_tile_class in one pass over the tiles (the scan's unmask
+// tiles): resolve a tile k_tile_scatter left marked, then classify it.
+__global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                                 const uint32_t* __restrict__ keyrot, const uint64_t* __restrict__ nfr_p,
+                                 uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
+                                 uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile, uint64_t rx_len) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t nfr = *nfr_p;
+    const uint64_t x = t * tile;
+    uint32_t k = tile_first[t];
+    if (k == TILE_MARK) {
+        uint64_t lo = 0, hi = nfr;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (off[mid] + len[mid] > x) hi = mid;
+            else lo = mid + 1;
+        }
+        k = (uint32_t)lo;
+        tile_first[t] = k;
+    }
+    if (t == ntiles) return;   // sentinel entry: index only
+    const uint64_t xe = x + tile < rx_len ? x + tile : rx_len;
+    uint32_t kind = TILE_GENERAL, key = 0;
+    if (k >= nfr || off[k] >= xe) {
+        kind = TILE_NONE;
+    } else if (off[k] <= x && xe <= off[k] + len[k] && xe == x + tile) {
+        key = keyrot[k];
+        kind = key ? TILE_SINGLE : TILE_NONE;
     }
     tile_key[t] = key;
     tile_kind[t] = (uint8_t)kind;
@@ -1112,39 +1245,47 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
     if (nseg == 0) return hipSuccess;
     const uint32_t wb = wave_blocks(nseg);
     const uint32_t vb = 2048;
-    if (pass == SCAN_SINGLE) {
+    // k_head<false> opens every pass but EMIT; it takes the zero-copy tables.
+    auto head_count = [&](uint64_t* est) {
         hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
+                           sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
-        hipError_t e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st);
-        if (e != hipSuccess) return e;
+    };
+    auto emit = [&](int emit_counts) {
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
+                           (uint64_t*)nullptr, (const dseg*)nullptr, (const dcarry*)nullptr, (dseg*)nullptr,
+                           (dcarry*)nullptr);
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 1);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, emit_counts);
+    };
+    if (pass == SCAN_SINGLE) {
+        head_count(nullptr);
+        hipError_t e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st);
+        if (e != hipSuccess) return e;
+        emit(1);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
-        return hipGetLastError();
-    }
-    if (pass == SCAN_COUNT) {
-        hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
-        hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
-                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
+    } else if (pass == SCAN_SPEC) {
+        head_count(sc.est);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
+        emit(1);
+        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
+                           sc.status, sc.seq);
+    } else if (pass == SCAN_COUNT) {
+        head_count(sc.status ? sc.est : nullptr);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+        if (sc.status)
+            hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
+                               sc.status, sc.seq);
     } else {
-        hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
-                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min());
-        hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
-                           sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
-        hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0);
+        emit(0);
     }
     return hipGetLastError();
 }
@@ -1163,6 +1304,21 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
     hipLaunchKernelGGL(k_tile_scatter, dim3(2048), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_tile_fixup, dim3(blocks), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
+    return hipGetLastError();
+}
+
+hipError_t launch_unmask_tiles(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
+                               uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
+                               uint64_t tile, uint64_t rx_len, hipStream_t st) {
+    const uint64_t n = ntiles + 1;
+    // fill whole 16-B words (one fill kernel instead of an aligned body + tail)
+    hipError_t e = hipMemsetD32Async(tile_first, TILE_MARK, (n + 3) & ~3ull, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tile_scatter, dim3(2048), dim3(256), 0, st, off, len, (uint64_t)0, nfr_dev, tile_first,
+                       ntiles, tile);
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_tile_fix_class, dim3(blocks), dim3(256), 0, st, off, len, keyrot, nfr_dev, tile_first,
+                       tile_key, tile_kind, ntiles, tile, rx_len);
     return hipGetLastError();
 }
 

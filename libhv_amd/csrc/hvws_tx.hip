@@ -104,6 +104,84 @@ constexpr uint32_t BUILD_MAXF = 128;   // frames per boundary tile staged in LDS
 
 __device__ __forceinline__ uint32_t tx_rotr(uint32_t x, uint32_t r) { return r ? (x >> r) | (x << (32u - r)) : x; }
 
+// OR bytes [0, b1 - b0) of the 16-byte little-endian value (vlo, vhi) into
+// bytes [b0, b1) of the chunk (olo, ohi); 0 <= b0 < b1 <= 16.
+__device__ __forceinline__ void put_bytes(uint64_t& olo, uint64_t& ohi, uint64_t vlo, uint64_t vhi, uint32_t b0,
+                                          uint32_t b1) {
+    const uint32_t n = b1 - b0;
+    if (n < 8) {
+        vlo &= ~0ull >> (64u - 8u * n);
+        vhi = 0;
+    } else if (n < 16) {
+        vhi = n == 8 ? 0 : vhi & (~0ull >> (64u - 8u * (n - 8u)));
+    }
+    if (b0 >= 8) {
+        vhi = vlo << (8u * (b0 - 8u));
+        vlo = 0;
+    } else if (b0) {
+        vhi = (vhi << (8u * b0)) | (vlo >> (64u - 8u * b0));
+        vlo <<= 8u * b0;
+    }
+    olo |= vlo;
+    ohi |= vhi;
+}
+
+// Frame header as a 16-byte little-endian value (bytes beyond its length 0);
+// layout of http/websocket_parser.c:215-246 (same bytes as tx_hdr_byte).
+__device__ __forceinline__ void tx_hdr128(uint32_t fl, uint64_t n, uint32_t key, uint64_t& lo, uint64_t& hi) {
+    const uint64_t b0 = ((fl & F_FIN) ? 0x80u : 0u) | (fl & F_OPMASK);
+    const uint64_t m = (fl & F_MASK) ? 0x80u : 0u;
+    const uint64_t k = (fl & F_MASK) ? key : 0u;
+    if (n < 126) {
+        lo = b0 | ((m | n) << 8) | (k << 16);
+        hi = 0;
+    } else if (n <= 0xFFFFu) {
+        lo = b0 | ((m | 126u) << 8) | (((n >> 8) & 0xFFu) << 16) | ((n & 0xFFu) << 24) | (k << 32);
+        hi = 0;
+    } else {
+        const uint64_t be = __builtin_bswap64(n);
+        lo = b0 | ((m | 127u) << 8) | (be << 16);
+        hi = (be >> 48) | (k << 16);
+    }
+}
+
+// (lo, hi) >> 8*r bytes, r < 16
+__device__ __forceinline__ void shr_bytes(uint64_t& lo, uint64_t& hi, uint32_t r) {
+    if (r >= 8) {
+        lo = hi >> (8u * (r - 8u));
+        hi = 0;
+    } else if (r) {
+        lo = (lo >> (8u * r)) | (hi << (64u - 8u * r));
+        hi >>= 8u * r;
+    }
+}
+
+// The bytes of output chunk [c, c+16) that belong to one frame (header at o,
+// payload [ps, e) taken from pay + src0, key 0 when unmasked): the header
+// piece cut out of tx_hdr128, the payload piece as one realigned 16-byte
+// load XORed with the key rotated to its phase -- no per-byte work.
+__device__ __forceinline__ void frame_piece(uint64_t& olo, uint64_t& ohi, uint64_t c, uint64_t o, uint64_t ps,
+                                            uint64_t e, uint64_t src0, uint32_t key, uint32_t fl,
+                                            const uint8_t* __restrict__ pay, uint64_t plen) {
+    const uint64_t ce = c + 16;
+    const uint64_t hb = o > c ? o : c, he = ps < ce ? ps : ce;
+    if (hb < he) {
+        uint64_t vlo, vhi;
+        tx_hdr128(fl, e - ps, key, vlo, vhi);
+        shr_bytes(vlo, vhi, (uint32_t)(hb - o));
+        put_bytes(olo, ohi, vlo, vhi, (uint32_t)(hb - c), (uint32_t)(he - c));
+    }
+    const uint64_t pb = ps > c ? ps : c, pe = e < ce ? e : ce;
+    if (pb < pe) {
+        uint64_t vlo, vhi;
+        ld16_any(pay, plen, src0 + (pb - ps), vlo, vhi);
+        const uint32_t r = (uint32_t)((pb - ps) & 3u) * 8u;
+        const uint32_t kw = r ? (key >> r) | (key << (32u - r)) : key;
+        const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+        put_bytes(olo, ohi, vlo ^ kk, vhi ^ kk, (uint32_t)(pb - c), (uint32_t)(pe - c));
+    }
+}
+
 __device__ __forceinline__ void build_chunk(uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay,
                                             uint64_t plen, const uint64_t* __restrict__ pay_off,
                                             const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
@@ -137,25 +215,20 @@ __device__ __forceinline__ void build_chunk(uint8_t* __restrict__ out, uint64_t 
             return;
         }
     }
-    // header bytes / frame boundaries / tail: byte by byte
-    for (uint32_t b = 0; b < 16 && c + b < out_len; ++b) {
-        const uint64_t a = c + b;
-        while (k < n && out_off[k] + size[k] <= a) ++k;
-        if (k >= n || out_off[k] > a) continue;
+    // header bytes / frame boundaries / tail: frame by frame
+    uint64_t lo = 0, hi = 0;
+    for (; k < n && out_off[k] < c + 16; ++k) {
         const uint32_t fl = flags[k];
-        const uint64_t ln = len[k];
-        const uint32_t key = (fl & F_MASK) ? mask[k] : 0u;
-        const uint32_t hl = tx_hdr_len(fl, ln);
-        const uint64_t rel = a - out_off[k];
-        uint32_t v;
-        if (rel < hl) {
-            v = tx_hdr_byte(fl, ln, key, (uint32_t)rel);
-        } else {
-            const uint64_t j = rel - hl;
-            v = pay[pay_off[k] + j];
-            if (fl & F_MASK) v ^= (key >> (8 * (j & 3u))) & 0xFFu;
-        }
-        out[a] = (uint8_t)v;
+        const uint64_t ln = len[k], o = out_off[k];
+        const uint64_t ps = o + tx_hdr_len(fl, ln);
+        frame_piece(lo, hi, c, o, ps, ps + ln, pay_off[k], (fl & F_MASK) ? mask[k] : 0u, fl, pay, plen);
+    }
+    if (c + 16 <= out_len) {
+        __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                    reinterpret_cast<u32x4*>(out + c));
+    } else {
+        for (uint32_t b = 0; b < 16 && c + b < out_len; ++b)
+            out[c + b] = (uint8_t)((b < 8 ? lo >> (8u * b) : hi >> (8u * (b - 8u))) & 0xFFu);
     }
 }
 
@@ -239,8 +312,8 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
         }
         __syncthreads();
         u32x4 w[U], x[U];
-        uint32_t kw[U], sft[U], fi[U];
-        bool fast[U];
+        uint32_t kw[U], sft[U];
+        uint32_t fastmask = 0;
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
@@ -250,8 +323,6 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
                 if (s_end[mid] > c) je = mid;
                 else j = mid + 1;
             }
-            fi[i] = j;
-            fast[i] = false;
             w[i] = x[i] = u32x4{0, 0, 0, 0};
             kw[i] = 0;
             sft[i] = 0;
@@ -259,7 +330,7 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
                 const uint64_t ps = s_ps[j];
                 const uint64_t src = s_src[j] + (c - ps);
                 if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
-                    fast[i] = true;
+                    fastmask |= 1u << i;
                     sft[i] = (uint32_t)(src & 15u);
                     const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
                     w[i] = q[0];
@@ -270,32 +341,27 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
         }
 #pragma unroll
         for (int i = 0; i < U; ++i) {
+            if (!((fastmask >> i) & 1u)) continue;
             const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
-            u32x4 v;
-            if (fast[i]) {
-                v = (sft[i] ? funnel16(w[i], x[i], sft[i]) : w[i]) ^ u32x4{kw[i], kw[i], kw[i], kw[i]};
-            } else {
-                uint64_t lo = 0, hi = 0;
-                uint32_t j = fi[i];
-                for (uint32_t b = 0; b < 16; ++b) {
-                    const uint64_t a = c + b;
-                    while (j < nf && s_end[j] <= a) ++j;
-                    if (j >= nf || s_off[j] > a) continue;
-                    const uint32_t fl = s_fl[j];
-                    const uint64_t ps = s_ps[j];
-                    uint64_t byte;
-                    if (a < ps) {
-                        byte = tx_hdr_byte(fl, s_end[j] - ps, s_key[j], (uint32_t)(a - s_off[j]));
-                    } else {
-                        const uint64_t jj = a - ps;
-                        byte = pay[s_src[j] + jj] ^ ((s_key[j] >> (8 * (jj & 3u))) & 0xFFu);
-                    }
-                    if (b < 8) lo |= byte << (8 * b);
-                    else hi |= byte << (8 * (b - 8));
-                }
-                v = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-            }
+            const u32x4 v = (sft[i] ? funnel16(w[i], x[i], sft[i]) : w[i]) ^ u32x4{kw[i], kw[i], kw[i], kw[i]};
             __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
+        }
+        // chunks holding header bytes or a frame boundary, one at a time
+#pragma unroll 1
+        for (int i = 0; i < U; ++i) {
+            if ((fastmask >> i) & 1u) continue;
+            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            uint64_t lo = 0, hi = 0;
+            for (; j < nf && s_off[j] < c + 16; ++j)
+                frame_piece(lo, hi, c, s_off[j], s_ps[j], s_end[j], s_src[j], s_key[j], s_fl[j], pay, plen);
+            __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                        reinterpret_cast<u32x4*>(out + c));
         }
         return;
     }

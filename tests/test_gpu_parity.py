@@ -155,21 +155,46 @@ def _oracle_batch(buf: np.ndarray, segs, carries):
     return np.concatenate(recs) if recs else np.zeros(0, libhv_amd.FRAME_DTYPE), outs, starts, exp
 
 
-def _compare_batch(eng, buf: np.ndarray, segs, carries=None):
-    rx = eng.to_device(buf)
-    eng.step(rx, len(buf), segs, carries)
-    got = rx.download(len(buf))
-    frames = eng.frames()
-    cout, started = eng.carry(len(segs))
-    rx.free()
-    exp_recs, exp_carry, exp_started, exp = _oracle_batch(buf, segs, carries)
-    assert len(frames) == len(exp_recs)
+# Scan paths a multi-segment batch can take (include/hvws.h HVWS_PATH_*):
+# (fast-bound threshold, speculation mode).  The default sends these small
+# batches COUNT -> EMIT with no wait; threshold 1 forces the large-batch
+# path, without speculation (COUNT, read, EMIT) and with it (speculative
+# EMIT checked on the device, exact re-scan when the check fails).
+SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1)]
+
+
+def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, mode):
+    L = libhv_amd.lib()
+    _, bound, spec = mode
+    old_b = L.hvws_set_fast_bound(eng.ctx, bound)
+    old_s = L.hvws_set_speculation(eng.ctx, spec)
+    try:
+        rx = eng.to_device(buf)
+        eng.step(rx, len(buf), segs, carries)
+        got = rx.download(len(buf))
+        frames = eng.frames()
+        cout, started = eng.carry(len(segs))
+        rx.free()
+        path = L.hvws_last_scan_path(eng.ctx)
+    finally:
+        L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
+        L.hvws_set_speculation(eng.ctx, old_s)
+    assert len(frames) == len(exp_recs), mode
     for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
-        assert np.array_equal(frames[f], exp_recs[f]), f
-    assert np.array_equal(got, exp)
+        assert np.array_equal(frames[f], exp_recs[f]), (mode, f)
+    assert np.array_equal(got, exp), mode
     for s in range(len(segs)):
-        assert cout[s].fields() == exp_carry[s].fields(), s
-        assert started[s] == exp_started[s], s
+        assert cout[s].fields() == exp_carry[s].fields(), (mode, s)
+        assert started[s] == exp_started[s], (mode, s)
+    return path
+
+
+def _compare_batch(eng, buf: np.ndarray, segs, carries=None):
+    """The batch through every scan path, each bit-exact against the oracle.
+    Returns {mode name: HVWS_PATH_* taken}."""
+    exp_recs, exp_carry, exp_started, exp = _oracle_batch(buf, segs, carries)
+    return {m[0]: _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, m)
+            for m in SCAN_MODES}
 
 
 def test_batch_segments_with_carry(eng):
@@ -335,3 +360,60 @@ def test_long_segment_last_frame_unmasked(eng, spec_min):
         # and with a partial header of a next frame after it
         data2 = data + H.build_frames_ref([(0x1 | 0x20, b"abc", b"wxyz")])[:4]
         _compare_batch(eng, np.frombuffer(data2, np.uint8).copy(), [(0, len(data2))])
+
+
+def _cut_uniform(rng, nframes, size, nseg, masked=True):
+    """One uniform stream cut into nseg segments at random bytes (headers
+    split across segments included); returns (buf, segs, carries)."""
+    frames = [((0x2 | 0x10 | 0x20) if masked else (0x2 | 0x10), rng.randbytes(size), rng.randbytes(4) if masked else None)
+              for _ in range(nframes)]
+    data = H.build_frames_ref(frames)
+    cuts = sorted(rng.sample(range(1, len(data)), nseg - 1))
+    bounds = [0] + cuts + [len(data)]
+    segs, carries = [], []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        _, st, _, _ = H.scan_segment(data[:a])
+        segs.append((a, b - a))
+        carries.append(st)
+    return np.frombuffer(data, np.uint8).copy(), segs, carries
+
+
+def test_speculative_table_uniform(eng):
+    """Uniform streams cut anywhere: every segment's record count is what
+    k_head estimates, so the speculative table passes the device check."""
+    rng = random.Random(77)
+    for size, nframes, nseg in ((1024, 900, 13), (100, 3000, 64), (70000, 40, 9), (0, 500, 5), (125, 700, 700)):
+        buf, segs, carries = _cut_uniform(rng, nframes, size, nseg)
+        paths = _compare_batch(eng, buf, segs, carries)
+        assert paths["speculate"] == 3, paths   # HVWS_PATH_SPEC
+        assert paths["count_read"] == 1, paths
+
+
+def test_speculative_table_rejected(eng):
+    """Mixed sizes: the estimates fail, the device zeroes the count (no tile
+    or unmask work) and the host re-scans exactly -- same bytes and records."""
+    plan = synth.mixed_plan(6 << 20, 17, hi=1 << 17).split(37)
+    host = H.synth_cpu(plan)
+    paths = _compare_batch(eng, host, plan.segments)
+    assert paths["speculate"] == 4, paths       # HVWS_PATH_SPEC_FAILED
+
+
+def test_speculation_adapts(eng):
+    """Automatic mode: a uniform batch scanned exactly teaches the context to
+    speculate on the next one; a mixed batch then fails the check once and
+    turns it off again.  Results stay exact throughout."""
+    L = libhv_amd.lib()
+    rng = random.Random(5)
+    ubuf, usegs, ucarry = _cut_uniform(rng, 600, 1024, 11)
+    mplan = synth.mixed_plan(4 << 20, 19, hi=1 << 16).split(11)
+    mbuf = H.synth_cpu(mplan)
+    uexp = _oracle_batch(ubuf, usegs, ucarry)
+    mexp = _oracle_batch(mbuf, mplan.segments, None)
+    auto = ("auto", 1, -1)
+    seq = [(ubuf, usegs, ucarry, uexp, 1), (ubuf, usegs, ucarry, uexp, 3), (mbuf, mplan.segments, None, mexp, 4),
+           (mbuf, mplan.segments, None, mexp, 1), (ubuf, usegs, ucarry, uexp, 1), (ubuf, usegs, ucarry, uexp, 3)]
+    L.hvws_set_speculation(eng.ctx, 0)   # forget what earlier tests taught the context
+    _step_checked(eng, mbuf, mplan.segments, None, *mexp, ("reset", 1, 0))
+    for buf, segs, carries, exp, want in seq:
+        path = _step_checked(eng, buf, segs, carries, *exp, auto)
+        assert path == want, (path, want)
