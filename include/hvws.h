@@ -120,6 +120,15 @@ int hvws_unmask(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len);
 /* scan + unmask */
 int hvws_step(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
               const websocket_parser* carry_in, uint32_t nseg);
+/* hvws_step for a batch whose bytes are already complete in device memory
+ * (nothing queued on the context stream still writes them).  Its discovery
+ * then runs on the context's second stream, overlapping the unmask of the
+ * previous step, whose tables are kept in the other of two table sets; the
+ * unmask is queued on the context stream after it, as with hvws_step.  Frames
+ * and carry of the call are readable (hvws_get_*) until the next scan; work
+ * queued on the context stream afterwards sees the unmasked bytes. */
+int hvws_step_resident(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+                       const websocket_parser* carry_in, uint32_t nseg);
 
 int64_t hvws_frame_count(hvws_ctx* ctx);
 int     hvws_get_frames(hvws_ctx* ctx, hvws_frame* out, uint64_t first, uint64_t n);

@@ -102,6 +102,10 @@ _SIGS = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32],
     ),
+    "hvws_step_resident": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32],
+    ),
     "hvws_frame_count": (ctypes.c_int64, [ctypes.c_void_p]),
     "hvws_get_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "hvws_get_segment_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -313,6 +317,14 @@ class Engine:
         else:
             s, c, n = self._segs(segs), self._carry(len(segs), carry), len(segs)
         _check(lib().hvws_step(self.ctx, rx.ptr, rx_len, s, c, n), "hvws_step")
+
+    def step_resident(self, rx: DeviceBuffer, rx_len: int, segs, carry=None) -> None:
+        """hvws_step_resident: discovery overlaps the previous step's unmask."""
+        if isinstance(segs, Prepared):
+            s, c, n = segs.segs, segs.carry, segs.n
+        else:
+            s, c, n = self._segs(segs), self._carry(len(segs), carry), len(segs)
+        _check(lib().hvws_step_resident(self.ctx, rx.ptr, rx_len, s, c, n), "hvws_step_resident")
 
     def frames(self) -> np.ndarray:
         n = lib().hvws_frame_count(self.ctx)

@@ -91,17 +91,44 @@ hvws_ctx* thread_ctx();
 static_assert(sizeof(drec) == sizeof(hvws_frame), "drec mirrors hvws_frame");
 static_assert(sizeof(dsmall_out) == 64, "dsmall_out layout");
 
+// What one scan produces (frame table, tile index, per-segment results and
+// scratch); the context holds two.
+struct tset {
+    dbuf carry_out, counts, bases, total;
+    dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total, sc_est;
+    dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
+    dbuf tile_first, tile_key, tile_kind;
+    uint64_t frame_cap = 0;
+    hipEvent_t free_ev = nullptr;   // recorded after the last kernel reading the set (pipelined steps)
+    bool free_pending = false;
+    void release() {
+        for (dbuf* b : {&carry_out, &counts, &bases, &total, &sc_mid, &sc_npred, &sc_pbase, &sc_fail, &sc_masked,
+                        &sc_total, &sc_est, &f_hdr, &f_off, &f_len, &f_length, &f_key, &f_keyrot, &f_info,
+                        &tile_first, &tile_key, &tile_kind})
+            b->release();
+        frame_cap = 0;
+    }
+};
+
 struct hvws_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // compute
     hipStream_t copy_in = nullptr;   // pipeline H2D
     hipStream_t copy_out = nullptr;  // pipeline D2H
-    // per-batch tables
-    dbuf segs, carry_in, carry_out, counts, bases, total;
-    dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total;
-    dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
-    dbuf tile_first, tile_key, tile_kind;
-    uint64_t frame_cap = 0;
+    // Pipelined steps (hvws_step_resident): discovery on sstream, overlapping
+    // the previous batch's unmask on `stream`.  cs = the stream the current
+    // scan enqueues on.
+    hipStream_t sstream = nullptr;
+    hipStream_t cs = nullptr;
+    hipEvent_t scan_done = nullptr;
+    bool piped = false;   // the last step was pipelined (set free events are being kept)
+    // per-batch tables: the segment/carry tables the scan reads, and two
+    // sets of everything a scan produces, used in turn, so a batch's scan
+    // can run while the previous batch's unmask still reads its tables
+    dbuf segs, carry_in;
+    tset ts[2];
+    int cur = 0;
+    tset& T() { return ts[cur]; }
     hbuf h_segs, h_total;
     // Segment/carry upload staging: two pinned slots used in turn, each
     // reusable once the H2D copy that read it has run (event), so a step
@@ -118,7 +145,6 @@ struct hvws_ctx {
     // Speculative EMIT (SCAN_SPEC): per-segment estimates, the device's
     // verdict in pinned memory, and whether the last exact scan says the
     // estimates hold (then the next batch speculates).
-    dbuf sc_est;
     hbuf h_status;
     uint64_t scan_seq = 0;
     bool spec_ok = false;
@@ -180,29 +206,29 @@ namespace {
 
 dframes frames_of(hvws_ctx* c) {
     dframes f;
-    f.hdr_off = c->f_hdr.as<int64_t>();
-    f.pay_off = c->f_off.as<uint64_t>();
-    f.pay_len = c->f_len.as<uint64_t>();
-    f.length = c->f_length.as<uint64_t>();
-    f.key = c->f_key.as<uint32_t>();
-    f.keyrot = c->f_keyrot.as<uint32_t>();
-    f.info = c->f_info.as<uint32_t>();
-    f.cap = c->frame_cap;
+    f.hdr_off = c->T().f_hdr.as<int64_t>();
+    f.pay_off = c->T().f_off.as<uint64_t>();
+    f.pay_len = c->T().f_len.as<uint64_t>();
+    f.length = c->T().f_length.as<uint64_t>();
+    f.key = c->T().f_key.as<uint32_t>();
+    f.keyrot = c->T().f_keyrot.as<uint32_t>();
+    f.info = c->T().f_info.as<uint32_t>();
+    f.cap = c->T().frame_cap;
     return f;
 }
 
 hipError_t ensure_frames(hvws_ctx* c, uint64_t n) {
-    if (n <= c->frame_cap && c->f_off.p) return hipSuccess;
+    if (n <= c->T().frame_cap && c->T().f_off.p) return hipSuccess;
     uint64_t want = std::max<uint64_t>(n + n / 4, 1024);
     hipError_t e;
-    if ((e = c->f_hdr.ensure(want * 8)) != hipSuccess) return e;
-    if ((e = c->f_off.ensure(want * 8)) != hipSuccess) return e;
-    if ((e = c->f_len.ensure(want * 8)) != hipSuccess) return e;
-    if ((e = c->f_length.ensure(want * 8)) != hipSuccess) return e;
-    if ((e = c->f_key.ensure(want * 4)) != hipSuccess) return e;
-    if ((e = c->f_keyrot.ensure(want * 4)) != hipSuccess) return e;
-    if ((e = c->f_info.ensure(want * 4)) != hipSuccess) return e;
-    c->frame_cap = want;
+    if ((e = c->T().f_hdr.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->T().f_off.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->T().f_len.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->T().f_length.ensure(want * 8)) != hipSuccess) return e;
+    if ((e = c->T().f_key.ensure(want * 4)) != hipSuccess) return e;
+    if ((e = c->T().f_keyrot.ensure(want * 4)) != hipSuccess) return e;
+    if ((e = c->T().f_info.ensure(want * 4)) != hipSuccess) return e;
+    c->T().frame_cap = want;
     return hipSuccess;
 }
 
@@ -250,7 +276,7 @@ hipError_t begin_timed_scan(hvws_ctx* c) {
     c->t_cur = (int)(c->t_seq % hvws_ctx::kTimeRing);
     c->t_unmask[c->t_cur] = false;
     ++c->t_seq;
-    return hipEventRecord(c->tev[c->t_cur][0], c->stream);
+    return hipEventRecord(c->tev[c->t_cur][0], c->cs);
 }
 
 // out[0] = scan ms, out[1] = unmask ms (-1: no unmask) of the step in ring `slot`.
@@ -276,7 +302,7 @@ int wait_status(hvws_ctx* c, uint64_t seq) {
     for (uint64_t spin = 0;; ++spin) {
         if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
         if ((spin & 1023) == 1023) {
-            const hipError_t q = hipStreamQuery(c->stream);
+            const hipError_t q = hipStreamQuery(c->cs);
             if (q == hipSuccess) {
                 if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
                 return set_err(HVWS_EHIP, "scan check did not publish (seq %llu)", (unsigned long long)seq);
@@ -293,15 +319,25 @@ int wait_status(hvws_ctx* c, uint64_t seq) {
 // as the unmask's start (one timing marker fewer).
 hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
     hipEvent_t* tev = c->tev[c->t_cur];
-    c->t_adjacent[c->t_cur] = after_scan;
     hipError_t e;
+    const bool piped = c->cs != c->stream;
+    if (piped) {   // the scan ran on the side stream: join it
+        after_scan = false;
+        if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
+    }
+    c->t_adjacent[c->t_cur] = after_scan;
     if (!after_scan && (e = hipEventRecord(tev[2], c->stream)) != hipSuccess) return e;
-    if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->tile_first.as<uint32_t>(),
-                           c->tile_key.as<uint32_t>(), c->tile_kind.as<uint8_t>(), c->total.as<uint64_t>(),
+    if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
+                           c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(), c->T().total.as<uint64_t>(),
                            c->stream)) != hipSuccess)
         return e;
     if ((e = hipEventRecord(tev[3], c->stream)) != hipSuccess) return e;
     c->t_unmask[c->t_cur] = true;
+    if (piped) {   // the next pipelined scan into this set waits for this unmask
+        if ((e = hipEventRecord(c->T().free_ev, c->stream)) != hipSuccess) return e;
+        c->T().free_pending = true;
+    }
     return hipSuccess;
 }
 
@@ -312,28 +348,36 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_
 int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint8_t* unmask_into = nullptr,
                       bool* unmasked = nullptr) {
     if (unmasked) *unmasked = false;
-    HIP_OR(c->counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(c->bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(c->total.ensure(8), HVWS_ENOMEM);
-    HIP_OR(c->carry_out.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    // The other table set: the previous batch's tables stay intact while its
+    // unmask may still be running (pipelined steps).
+    c->cur ^= 1;
+    if (c->cs == c->stream) c->piped = false;   // a later pipelined step re-arms the set events
+    if (c->cs != c->stream && c->T().free_pending) {
+        HIP_OR(hipStreamWaitEvent(c->cs, c->T().free_ev, 0), HVWS_EHIP);
+        c->T().free_pending = false;
+    }
+    HIP_OR(c->T().counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().total.ensure(8), HVWS_ENOMEM);
+    HIP_OR(c->T().carry_out.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
     HIP_OR(c->h_total.ensure(8), HVWS_ENOMEM);
     HIP_OR(ensure_frames(c, 1), HVWS_ENOMEM);
-    HIP_OR(c->sc_mid.ensure((uint64_t)nseg * sizeof(dmid) + 64), HVWS_ENOMEM);
-    HIP_OR(c->sc_npred.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(c->sc_pbase.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(c->sc_fail.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(c->sc_masked.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(c->sc_total.ensure(8), HVWS_ENOMEM);
-    HIP_OR(c->sc_est.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_mid.ensure((uint64_t)nseg * sizeof(dmid) + 64), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_npred.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_pbase.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_fail.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_masked.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_total.ensure(8), HVWS_ENOMEM);
+    HIP_OR(c->T().sc_est.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->h_status.ensure(sizeof(dspec_status)), HVWS_ENOMEM);
     scan_scratch sc;
-    sc.mid = c->sc_mid.as<dmid>();
-    sc.npred = c->sc_npred.as<uint64_t>();
-    sc.pbase = c->sc_pbase.as<uint64_t>();
-    sc.first_fail = c->sc_fail.as<uint64_t>();
-    sc.last_masked = c->sc_masked.as<uint64_t>();
-    sc.total_pred = c->sc_total.as<uint64_t>();
-    sc.est = c->sc_est.as<uint64_t>();
+    sc.mid = c->T().sc_mid.as<dmid>();
+    sc.npred = c->T().sc_npred.as<uint64_t>();
+    sc.pbase = c->T().sc_pbase.as<uint64_t>();
+    sc.first_fail = c->T().sc_fail.as<uint64_t>();
+    sc.last_masked = c->T().sc_masked.as<uint64_t>();
+    sc.total_pred = c->T().sc_total.as<uint64_t>();
+    sc.est = c->T().sc_est.as<uint64_t>();
     sc.src_segs = c->up_src_segs;
     sc.src_carry = c->up_src_carry;
     sc.segs_w = c->segs.as<dseg>();
@@ -354,22 +398,22 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     c->up_src_carry = nullptr;
     bool slot_released = up_slot < 0;
     auto pass = [&](int which) {
-        const hipError_t e = launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->carry_out.as<dcarry>(),
-                                         c->counts.as<uint64_t>(), c->bases.as<uint64_t>(), c->total.as<uint64_t>(), sc,
-                                         frames_of(c), c->vmask, c->stream);
+        const hipError_t e = launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->T().carry_out.as<dcarry>(),
+                                         c->T().counts.as<uint64_t>(), c->T().bases.as<uint64_t>(), c->T().total.as<uint64_t>(), sc,
+                                         frames_of(c), c->vmask, c->cs);
         sc.src_segs = nullptr;
         sc.src_carry = nullptr;
         if (e == hipSuccess && !slot_released) {
             slot_released = true;
-            const hipError_t e2 = hipEventRecord(c->up_ev[up_slot], c->stream);
+            const hipError_t e2 = hipEventRecord(c->up_ev[up_slot], c->cs);
             c->up_pending[up_slot] = e2 == hipSuccess;
             return e2;
         }
         return e;
     };
     auto read_count = [&](uint64_t& n) -> int {
-        HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
-        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+        HIP_OR(hipMemcpyAsync(c->h_total.p, c->T().total.p, 8, hipMemcpyDeviceToHost, c->cs), HVWS_EHIP);
+        HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
         n = *c->h_total.as<uint64_t>();
         if (n >= 0xFFFFFFF0ull)
             return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
@@ -389,13 +433,13 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     c->variant = unmask_variant();
     const uint64_t tile = unmask_tile(c->variant);
     const uint64_t ntiles = (rx_len + tile - 1) / tile;
-    HIP_OR(c->tile_first.ensure((ntiles + 8) * 4), HVWS_ENOMEM);
-    HIP_OR(c->tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
-    HIP_OR(c->tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
+    HIP_OR(c->T().tile_first.ensure((ntiles + 8) * 4), HVWS_ENOMEM);
+    HIP_OR(c->T().tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    HIP_OR(c->T().tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
     auto tiles = [&]() -> int {
-        HIP_OR(launch_unmask_tiles(c->f_off.as<uint64_t>(), c->f_len.as<uint64_t>(), c->f_keyrot.as<uint32_t>(),
-                                   c->total.as<uint64_t>(), c->tile_first.as<uint32_t>(), c->tile_key.as<uint32_t>(),
-                                   c->tile_kind.as<uint8_t>(), ntiles, tile, rx_len, c->stream),
+        HIP_OR(launch_unmask_tiles(c->T().f_off.as<uint64_t>(), c->T().f_len.as<uint64_t>(), c->T().f_keyrot.as<uint32_t>(),
+                                   c->T().total.as<uint64_t>(), c->T().tile_first.as<uint32_t>(), c->T().tile_key.as<uint32_t>(),
+                                   c->T().tile_kind.as<uint8_t>(), ntiles, tile, rx_len, c->cs),
                HVWS_EHIP);
         return HVWS_OK;
     };
@@ -416,10 +460,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         const uint64_t cap = std::min<uint64_t>(bound, std::max<uint64_t>(kFastFrameBound, kSingleEstimate));
         HIP_OR(ensure_frames(c, cap), HVWS_ENOMEM);
         HIP_OR(pass(SCAN_SINGLE), HVWS_EHIP);
-        if (bound > c->frame_cap) {
+        if (bound > c->T().frame_cap) {
             int rc = read_count(nfr);
             if (rc) return rc;
-            if (nfr > c->frame_cap) {
+            if (nfr > c->T().frame_cap) {
                 HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
                 HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
             }
@@ -447,7 +491,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
             if ((rc = tiles()) != HVWS_OK) return rc;
             if (unmask_into) {
-                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
+                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
@@ -461,7 +505,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         if (!done) {
             sc.seq = ++c->scan_seq;
             HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
-            HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+            HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
             c->spec_ok = (flags & SPEC_MATCH) != 0;
             HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
@@ -473,7 +517,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         int rc = tiles();
         if (rc) return rc;
     }
-    if (!(unmasked && *unmasked)) HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
+    if (!(unmasked && *unmasked)) HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
     c->nseg = nseg;
     c->nfr = nfr;
     c->rx = d_rx;
@@ -487,7 +531,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
 // scan left it on the device).
 int ensure_count(hvws_ctx* c) {
     if (c->nfr_known) return HVWS_OK;
-    HIP_OR(hipMemcpyAsync(c->h_total.p, c->total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(c->h_total.p, c->T().total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     c->nfr = *c->h_total.as<uint64_t>();
     c->nfr_known = true;
@@ -512,11 +556,11 @@ int readback_all(hvws_ctx* c) {
     uint64_t* count = first + nseg;
     dcarry* carry = (dcarry*)(count + nseg);
     hipStream_t s = c->stream;
-    HIP_OR(hipMemcpyAsync(total, c->total.p, 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(total, c->T().total.p, 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
     if (nseg) {
-        HIP_OR(hipMemcpyAsync(first, c->bases.p, (uint64_t)nseg * 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
-        HIP_OR(hipMemcpyAsync(count, c->counts.p, (uint64_t)nseg * 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
-        HIP_OR(hipMemcpyAsync(carry, c->carry_out.p, (uint64_t)nseg * sizeof(dcarry), hipMemcpyDeviceToHost, s),
+        HIP_OR(hipMemcpyAsync(first, c->T().bases.p, (uint64_t)nseg * 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
+        HIP_OR(hipMemcpyAsync(count, c->T().counts.p, (uint64_t)nseg * 8, hipMemcpyDeviceToHost, s), HVWS_EHIP);
+        HIP_OR(hipMemcpyAsync(carry, c->T().carry_out.p, (uint64_t)nseg * sizeof(dcarry), hipMemcpyDeviceToHost, s),
                HVWS_EHIP);
     }
     // SoA staging sized for `cap` records (exact count known) or the prefix
@@ -532,13 +576,13 @@ int readback_all(hvws_ctx* c) {
         if (b <= a) return hipSuccess;
         const uint64_t n = b - a;
         hipError_t e2;
-        if ((e2 = hipMemcpyAsync(f_hdr + a, c->f_hdr.as<int64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
-        if ((e2 = hipMemcpyAsync(f_off + a, c->f_off.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
-        if ((e2 = hipMemcpyAsync(f_len + a, c->f_len.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
-        if ((e2 = hipMemcpyAsync(f_length + a, c->f_length.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s)))
+        if ((e2 = hipMemcpyAsync(f_hdr + a, c->T().f_hdr.as<int64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
+        if ((e2 = hipMemcpyAsync(f_off + a, c->T().f_off.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
+        if ((e2 = hipMemcpyAsync(f_len + a, c->T().f_len.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s))) return e2;
+        if ((e2 = hipMemcpyAsync(f_length + a, c->T().f_length.as<uint64_t>() + a, n * 8, hipMemcpyDeviceToHost, s)))
             return e2;
-        if ((e2 = hipMemcpyAsync(f_key + a, c->f_key.as<uint32_t>() + a, n * 4, hipMemcpyDeviceToHost, s))) return e2;
-        return hipMemcpyAsync(f_info + a, c->f_info.as<uint32_t>() + a, n * 4, hipMemcpyDeviceToHost, s);
+        if ((e2 = hipMemcpyAsync(f_key + a, c->T().f_key.as<uint32_t>() + a, n * 4, hipMemcpyDeviceToHost, s))) return e2;
+        return hipMemcpyAsync(f_info + a, c->T().f_info.as<uint32_t>() + a, n * 4, hipMemcpyDeviceToHost, s);
     };
     HIP_OR(copy_range(0, c->nfr_known ? c->nfr : nrec), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(s), HVWS_EHIP);
@@ -787,7 +831,8 @@ hvws_ctx* hvws_ctx_create(int device) {
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : -1);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess) {
         set_err(HVWS_EHIP, "stream creation failed");
         hvws_ctx_destroy(c);
         return nullptr;
@@ -797,6 +842,9 @@ hvws_ctx* hvws_ctx_create(int device) {
     for (auto& row : c->tev)
         for (auto& ev : row) ev_ok = ev_ok && hipEventCreate(&ev) == hipSuccess;
     for (auto& ev : c->up_ev) ev_ok = ev_ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    for (tset& t : c->ts) ev_ok = ev_ok && hipEventCreateWithFlags(&t.free_ev, hipEventDisableTiming) == hipSuccess;
+    ev_ok = ev_ok && hipEventCreateWithFlags(&c->scan_done, hipEventDisableTiming) == hipSuccess;
+    c->cs = c->stream;
     if (!ev_ok) {
         set_err(HVWS_EHIP, "event creation failed");
         hvws_ctx_destroy(c);
@@ -809,12 +857,13 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (dbuf* b : {&c->sc_mid, &c->sc_npred, &c->sc_pbase, &c->sc_fail, &c->sc_masked, &c->sc_total})
-        b->release();
-    for (dbuf* b : {&c->segs, &c->carry_in, &c->carry_out, &c->counts, &c->bases, &c->total, &c->f_hdr, &c->f_off,
-                    &c->f_len, &c->f_length, &c->f_key, &c->f_keyrot, &c->f_info, &c->tile_first, &c->tile_key, &c->tile_kind, &c->stage,
-                    &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad, &c->tx_size, &c->tx_off,
-                    &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->d_small_in, &c->d_small_slots})
+    if (c->sstream) hipStreamSynchronize(c->sstream);
+    for (tset& t : c->ts) {
+        t.release();
+        if (t.free_ev) hipEventDestroy(t.free_ev);
+    }
+    for (dbuf* b : {&c->segs, &c->carry_in, &c->stage, &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad,
+                    &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->d_small_in, &c->d_small_slots})
         b->release();
     c->h_tx.release();
     c->h_small_in.release();
@@ -830,11 +879,12 @@ void hvws_ctx_destroy(hvws_ctx* c) {
             if (ev) hipEventDestroy(ev);
     for (auto& ev : c->up_ev)
         if (ev) hipEventDestroy(ev);
-    c->sc_est.release();
     c->h_status.release();
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy_in) hipStreamDestroy(c->copy_in);
     if (c->copy_out) hipStreamDestroy(c->copy_out);
+    if (c->sstream) hipStreamDestroy(c->sstream);
+    if (c->scan_done) hipEventDestroy(c->scan_done);
     delete c;
 }
 
@@ -908,6 +958,7 @@ int hvws_sync(hvws_ctx* c) {
     int rc = check_ctx(c);
     if (rc) return rc;
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->sstream), HVWS_EHIP);
     return HVWS_OK;
 }
 
@@ -922,6 +973,30 @@ int hvws_scan(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, const hvws_segm
 }
 
 int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) { return unmask_impl(c, d_rx, rx_len, false); }
+
+int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+                       const websocket_parser* carry_in, uint32_t nseg) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
+    if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
+    if (!c->piped) {
+        // Entering pipelined mode: both table sets may still be read by work
+        // queued on the context stream.
+        for (tset& t : c->ts) {
+            HIP_OR(hipEventRecord(t.free_ev, c->stream), HVWS_EHIP);
+            t.free_pending = true;
+        }
+        c->piped = true;
+    }
+    if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
+    c->cs = c->sstream;
+    bool unmasked = false;
+    rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked);
+    if (rc == HVWS_OK && !unmasked) rc = unmask_impl(c, d_rx, rx_len, false);
+    c->cs = c->stream;
+    return rc;
+}
 
 int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
               const websocket_parser* carry_in, uint32_t nseg) {
@@ -955,18 +1030,18 @@ int hvws_get_frames(hvws_ctx* c, hvws_frame* out, uint64_t first, uint64_t n) {
     std::vector<int64_t> hdr(n);
     std::vector<uint64_t> off(n), len(n), length(n);
     std::vector<uint32_t> key(n), info(n);
-    HIP_OR(hipMemcpyAsync(hdr.data(), c->f_hdr.as<int64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
+    HIP_OR(hipMemcpyAsync(hdr.data(), c->T().f_hdr.as<int64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(off.data(), c->f_off.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
+    HIP_OR(hipMemcpyAsync(off.data(), c->T().f_off.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(len.data(), c->f_len.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
+    HIP_OR(hipMemcpyAsync(len.data(), c->T().f_len.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(length.data(), c->f_length.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost,
+    HIP_OR(hipMemcpyAsync(length.data(), c->T().f_length.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost,
                           c->stream),
            HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(key.data(), c->f_key.as<uint32_t>() + first, n * 4, hipMemcpyDeviceToHost, c->stream),
+    HIP_OR(hipMemcpyAsync(key.data(), c->T().f_key.as<uint32_t>() + first, n * 4, hipMemcpyDeviceToHost, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipMemcpyAsync(info.data(), c->f_info.as<uint32_t>() + first, n * 4, hipMemcpyDeviceToHost, c->stream),
+    HIP_OR(hipMemcpyAsync(info.data(), c->T().f_info.as<uint32_t>() + first, n * 4, hipMemcpyDeviceToHost, c->stream),
            HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     for (uint64_t i = 0; i < n; ++i) {
@@ -990,10 +1065,10 @@ int hvws_get_segment_frames(hvws_ctx* c, uint64_t* first, uint64_t* count) {
         return HVWS_OK;
     }
     if (first)
-        HIP_OR(hipMemcpyAsync(first, c->bases.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
+        HIP_OR(hipMemcpyAsync(first, c->T().bases.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
                HVWS_EHIP);
     if (count)
-        HIP_OR(hipMemcpyAsync(count, c->counts.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
+        HIP_OR(hipMemcpyAsync(count, c->T().counts.p, (uint64_t)c->nseg * 8, hipMemcpyDeviceToHost, c->stream),
                HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     return HVWS_OK;
@@ -1010,7 +1085,7 @@ int hvws_get_carry(hvws_ctx* c, websocket_parser* out, int* started) {
     } else {
         h.resize(c->nseg);
         if (c->nseg)
-            HIP_OR(hipMemcpyAsync(h.data(), c->carry_out.p, (uint64_t)c->nseg * sizeof(dcarry),
+            HIP_OR(hipMemcpyAsync(h.data(), c->T().carry_out.p, (uint64_t)c->nseg * sizeof(dcarry),
                                   hipMemcpyDeviceToHost, c->stream),
                    HVWS_EHIP);
         HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
@@ -1133,7 +1208,7 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
             memcpy(c->h_segs.p, &ds, sizeof(ds));
             e = hipMemcpyAsync(c->segs.p, c->h_segs.p, sizeof(ds), hipMemcpyHostToDevice, c->stream);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(c->carry_in.p, c->carry_out.p, sizeof(dcarry), hipMemcpyDeviceToDevice,
+                e = hipMemcpyAsync(c->carry_in.p, c->T().carry_out.p, sizeof(dcarry), hipMemcpyDeviceToDevice,
                                    c->stream);
             if (e != hipSuccess) break;
         }

@@ -160,7 +160,8 @@ def _oracle_batch(buf: np.ndarray, segs, carries):
 # batches COUNT -> EMIT with no wait; threshold 1 forces the large-batch
 # path, without speculation (COUNT, read, EMIT) and with it (speculative
 # EMIT checked on the device, exact re-scan when the check fails).
-SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1)]
+SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1),
+              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1)]
 
 
 def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, mode):
@@ -170,7 +171,10 @@ def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp
     old_s = L.hvws_set_speculation(eng.ctx, spec)
     try:
         rx = eng.to_device(buf)
-        eng.step(rx, len(buf), segs, carries)
+        if mode[0].startswith("pipelined"):
+            eng.step_resident(rx, len(buf), segs, carries)
+        else:
+            eng.step(rx, len(buf), segs, carries)
         got = rx.download(len(buf))
         frames = eng.frames()
         cout, started = eng.carry(len(segs))
@@ -417,3 +421,53 @@ def test_speculation_adapts(eng):
     for buf, segs, carries, exp, want in seq:
         path = _step_checked(eng, buf, segs, carries, *exp, auto)
         assert path == want, (path, want)
+
+
+def test_pipelined_steps_back_to_back(eng):
+    """hvws_step_resident on several resident batches with no wait between
+    calls: each batch's discovery runs on the second stream while the
+    previous batch is unmasked; every buffer must come out exact, and the
+    last step's frames and carry must be its own."""
+    L = libhv_amd.lib()
+    rng = random.Random(123)
+    batches = []
+    for i in range(8):
+        if i % 3 == 2:
+            plan = synth.mixed_plan(3 << 20, 40 + i, hi=1 << 16).split(9)
+            buf, segs, carries = H.synth_cpu(plan), plan.segments, None
+        else:
+            buf, segs, carries = _cut_uniform(rng, 400 + 50 * i, rng.choice([100, 1024, 3000]), 7 + i)
+        batches.append((buf, segs, carries))
+    for bound, spec in ((0, -1), (1, 1), (1, -1)):
+        old_b = L.hvws_set_fast_bound(eng.ctx, bound)
+        old_s = L.hvws_set_speculation(eng.ctx, spec)
+        try:
+            devs = [eng.to_device(b) for b, _, _ in batches]
+            for d, (b, segs, carries) in zip(devs, batches):
+                eng.step_resident(d, len(b), segs, carries)
+            # a second pass over the first buffer restores its masked bytes
+            # (its bytes must be complete first: the API's precondition)
+            eng.sync()
+            eng.step_resident(devs[0], len(batches[0][0]), batches[0][1], batches[0][2])
+            frames = eng.frames()
+            cout, started = eng.carry(len(batches[0][1]))
+            got = [d.download(len(b)) for d, (b, _, _) in zip(devs, batches)]
+            for d in devs:
+                d.free()
+        finally:
+            L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
+            L.hvws_set_speculation(eng.ctx, old_s)
+        assert np.array_equal(got[0], batches[0][0]), (bound, spec)
+        for i in range(1, len(batches)):
+            b, segs, carries = batches[i]
+            assert np.array_equal(got[i], _oracle_batch(b, segs, carries)[3]), (bound, spec, i)
+        # the last call scanned batch 0 in its unmasked state: its frames are
+        # those of the unmasked bytes
+        b0, segs0, carries0 = batches[0]
+        unm = _oracle_batch(b0, segs0, carries0)[3]
+        exp_recs, exp_carry, _, _ = _oracle_batch(unm, segs0, carries0)
+        assert len(frames) == len(exp_recs)
+        for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
+            assert np.array_equal(frames[f], exp_recs[f]), f
+        for k in range(len(segs0)):
+            assert cout[k].fields() == exp_carry[k].fields(), k
