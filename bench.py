@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--host-gib", type=float, default=4.0, help="host-inclusive sample size (0: skip)")
+    ap.add_argument("--host-chunk-mib", type=int, default=64, help="hvws_pipeline chunk size")
     ap.add_argument("--sweep-unmask", action="store_true",
                     help="rank 0: time every k_unmask geometry on the same batch (design record)")
     ap.add_argument("--no-tx", action="store_true", help="skip the transmit-side (hvws_build_frames) measurement")
@@ -133,6 +134,51 @@ def cpu_decode_only(sample: np.ndarray, plan, seconds: float):
         L.msgp_bench_decode_spans(*args)
     dt = time.perf_counter() - t0
     return per * passes / dt / 2**30
+
+
+def pcie_ceiling(device: int, nbytes: int = 1 << 30, piece: int = 64 << 20, reps: int = 3) -> dict:
+    """This box's host link, measured in the same run with the HIP runtime
+    directly and the same call pattern as hvws_pipeline (pinned buffers,
+    `piece`-sized hipMemcpyAsync on non-blocking streams): H2D alone, D2H
+    alone, and both at once on two streams.  GB/s per direction."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    hip.hipSetDevice(device)
+    h_in, h_out, d_in, d_out, s1, s2 = vp(), vp(), vp(), vp(), vp(), vp()
+    assert hip.hipHostMalloc(ctypes.byref(h_in), ctypes.c_size_t(nbytes), 0) == 0
+    assert hip.hipHostMalloc(ctypes.byref(h_out), ctypes.c_size_t(nbytes), 0) == 0
+    assert hip.hipMalloc(ctypes.byref(d_in), ctypes.c_size_t(nbytes)) == 0
+    assert hip.hipMalloc(ctypes.byref(d_out), ctypes.c_size_t(nbytes)) == 0
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(s1), 1) == 0   # hipStreamNonBlocking
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(s2), 1) == 0
+    H2D, D2H = 1, 2   # hipMemcpyHostToDevice, hipMemcpyDeviceToHost
+
+    def run(h2d: bool, d2h: bool) -> float:
+        best = None
+        for _ in range(reps):
+            hip.hipDeviceSynchronize()
+            t = time.perf_counter()
+            for o in range(0, nbytes, piece):
+                n = ctypes.c_size_t(min(piece, nbytes - o))
+                if h2d:
+                    hip.hipMemcpyAsync(vp(d_in.value + o), vp(h_in.value + o), n, H2D, s1)
+                if d2h:
+                    hip.hipMemcpyAsync(vp(h_out.value + o), vp(d_out.value + o), n, D2H, s2)
+            hip.hipStreamSynchronize(s1)
+            hip.hipStreamSynchronize(s2)
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        return best
+
+    t_in, t_out, t_both = run(True, False), run(False, True), run(True, True)
+    for p in (d_in, d_out):
+        hip.hipFree(p)
+    for p in (h_in, h_out):
+        hip.hipHostFree(p)
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
+    return {"h2d_GBps": round(nbytes / t_in / 1e9, 2), "d2h_GBps": round(nbytes / t_out / 1e9, 2),
+            "concurrent_GBps_per_direction": round(nbytes / t_both / 1e9, 2), "bytes": nbytes, "piece": piece}
 
 
 def init_dist():
@@ -304,11 +350,48 @@ def main():
                                           for n, t in stimes.items()}
         extra["unmask_ms_mean"] = round(mean_unmask, 3)
 
+        rx_plain = passes % 2 == 1   # payloads currently unmasked
+        # (measured before the transmit leg: the pipeline's own allocations
+        # ran measurably slower after that leg's 68.7 GB buffer came and went)
+        # host-inclusive: pinned host rx -> device -> scan+unmask -> host
+        if args.host_gib > 0:
+            sizes = synth.frame_size(plan.flags, plan.length)
+            ends = np.cumsum(sizes)
+            m = int(np.searchsorted(ends, int(args.host_gib * 2**30), side="right"))
+            m = max(1, min(m, plan.n))
+            hbytes = int(ends[m - 1])
+            eng.synth(rx, plan.total, plan.seed, dp, 0)
+            rx_plain = False
+            L = libhv_amd.lib()
+            pinned = L.hvws_host_alloc(eng.ctx, hbytes)
+            host = np.ctypeslib.as_array((ctypes.c_uint8 * hbytes).from_address(pinned))
+            libhv_amd._check(L.hvws_d2h(eng.ctx, pinned, rx.ptr, hbytes), "d2h")
+            eng.sync()
+            # CPU baseline sample = the first whole frames of the same (masked) batch
+            sample = None
+            if args.cpu_seconds > 0:
+                ms = max(1, int(np.searchsorted(ends, args.cpu_sample_mib << 20, side="right")))
+                sample = np.array(host[: int(ends[ms - 1])], copy=True)
+            carry = libhv_amd.WsParser()
+            L.websocket_parser_init(ctypes.byref(carry))
+            t = time.perf_counter()
+            chunk = args.host_chunk_mib << 20
+            libhv_amd._check(L.hvws_pipeline(eng.ctx, pinned, hbytes, chunk, ctypes.byref(carry)), "pipeline")
+            dt = time.perf_counter() - t
+            extra["host_inclusive"] = {
+                "GiBps_payload": round(float(plan.length[:m].sum()) / dt / 2**30, 2),
+                "GBps_wire": round(hbytes / dt / 1e9, 2),
+                "bytes": hbytes, "chunk": chunk,
+                "note": "pinned H2D + scan + unmask + D2H, 3-slot ring, PCIe-bound",
+                "link": pcie_ceiling(device, piece=chunk),
+            }
+            L.hvws_host_free(eng.ctx, pinned)
+
         if not args.no_tx:
             # transmit side: rebuild every frame of the
             # batch from its plaintext payload with hvws_build_frames; the output
             # must be the masked batch byte for byte
-            if passes % 2 == 0:
+            if not rx_plain:
                 eng.step(rx, plan.total, segs)   # leave rx holding plaintext payloads
             hdr = synth.frame_size(plan.flags, plan.length) - plan.length
             tx = libhv_amd.TxPlan(eng, plan.frame_off + hdr, plan.length, plan.flags, plan.mask)
@@ -335,37 +418,6 @@ def main():
             tx.free()
             if not ok:
                 raise SystemExit("transmit build differs from the masked batch")
-
-        # host-inclusive: pinned host rx -> device -> scan+unmask -> host
-        if args.host_gib > 0:
-            sizes = synth.frame_size(plan.flags, plan.length)
-            ends = np.cumsum(sizes)
-            m = int(np.searchsorted(ends, int(args.host_gib * 2**30), side="right"))
-            m = max(1, min(m, plan.n))
-            hbytes = int(ends[m - 1])
-            eng.synth(rx, plan.total, plan.seed, dp, 0)
-            L = libhv_amd.lib()
-            pinned = L.hvws_host_alloc(eng.ctx, hbytes)
-            host = np.ctypeslib.as_array((ctypes.c_uint8 * hbytes).from_address(pinned))
-            libhv_amd._check(L.hvws_d2h(eng.ctx, pinned, rx.ptr, hbytes), "d2h")
-            eng.sync()
-            # CPU baseline sample = the first whole frames of the same (masked) batch
-            sample = None
-            if args.cpu_seconds > 0:
-                ms = max(1, int(np.searchsorted(ends, args.cpu_sample_mib << 20, side="right")))
-                sample = np.array(host[: int(ends[ms - 1])], copy=True)
-            carry = libhv_amd.WsParser()
-            L.websocket_parser_init(ctypes.byref(carry))
-            t = time.perf_counter()
-            libhv_amd._check(L.hvws_pipeline(eng.ctx, pinned, hbytes, 64 << 20, ctypes.byref(carry)), "pipeline")
-            dt = time.perf_counter() - t
-            extra["host_inclusive"] = {
-                "GiBps_payload": round(float(plan.length[:m].sum()) / dt / 2**30, 2),
-                "GBps_wire": round(hbytes / dt / 1e9, 2),
-                "bytes": hbytes, "chunk": 64 << 20,
-                "note": "pinned H2D + scan + unmask + D2H, 3-slot ring, PCIe-bound",
-            }
-            L.hvws_host_free(eng.ctx, pinned)
 
     dp.free()
     rx.free()

@@ -151,6 +151,7 @@ struct hvws_ctx {
     int spec_mode = -1;   // -1 auto, 0 never, 1 always try first ($HVWS_SPEC / hvws_set_speculation)
     uint64_t fast_bound = 0;   // record bound below which COUNT -> EMIT needs no host wait; 0 = default
     int scan_path = -1;        // HVWS_PATH_* of the last scan
+    uint64_t single_hint = 0;  // records of the last one-segment scan whose count was read
     // staging for host-memory entry points
     dbuf stage;
     dbuf xor_stage;
@@ -194,7 +195,7 @@ struct hvws_ctx {
 namespace {
 constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
 constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
-constexpr uint64_t kSingleEstimate = 1ull << 26;   // records: one-stream table size before the count is known
+constexpr uint64_t kSingleMin = 1ull << 20;   // records: smallest one-stream table before its count is known
 // Small-batch path (k_small): batches up to kSmallBatch bytes whose segments
 // are each at most kSmallSegment bytes run as one launch.
 constexpr uint64_t kSmallBatch = 64ull << 20;
@@ -217,9 +218,9 @@ dframes frames_of(hvws_ctx* c) {
     return f;
 }
 
-hipError_t ensure_frames(hvws_ctx* c, uint64_t n) {
+hipError_t ensure_frames(hvws_ctx* c, uint64_t n, bool exact = false) {
     if (n <= c->T().frame_cap && c->T().f_off.p) return hipSuccess;
-    uint64_t want = std::max<uint64_t>(n + n / 4, 1024);
+    uint64_t want = std::max<uint64_t>(exact ? n : n + n / 4, 1024);
     hipError_t e;
     if ((e = c->T().f_hdr.ensure(want * 8)) != hipSuccess) return e;
     if ((e = c->T().f_off.ensure(want * 8)) != hipSuccess) return e;
@@ -454,10 +455,14 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     if (nseg == 1) {
         c->scan_path = HVWS_PATH_SINGLE;
         // One stream: its base is 0, so EMIT needs no COUNT walk (a mixed-size
-        // stream's serial walk runs once).  The table is sized by the bound,
-        // or by an estimate that is checked after the pass and re-emitted
-        // into an exact-size table in the rare case it overflowed.
-        const uint64_t cap = std::min<uint64_t>(bound, std::max<uint64_t>(kFastFrameBound, kSingleEstimate));
+        // stream's serial walk runs once).  The table is sized by the bound
+        // when that is small, else by an estimate (1.25 x the last one-stream
+        // count, at least 2^20 records) that is checked after the pass and
+        // re-emitted into an exact-size table if it overflowed.  (Sizing by
+        // the bound would give a 256 MiB chunk of 64 KiB frames a 3.2 GB
+        // table for its ~4000 records.)
+        const uint64_t guess = std::max<uint64_t>(kSingleMin, c->single_hint + c->single_hint / 4);
+        const uint64_t cap = std::min<uint64_t>(bound, guess);
         HIP_OR(ensure_frames(c, cap), HVWS_ENOMEM);
         HIP_OR(pass(SCAN_SINGLE), HVWS_EHIP);
         if (bound > c->T().frame_cap) {
@@ -468,6 +473,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
             }
             c->nfr_known = true;
+            c->single_hint = nfr;
         }
     } else if (bound <= (c->fast_bound ? c->fast_bound : kFastFrameBound)) {
         c->scan_path = HVWS_PATH_COUNT_EMIT;
@@ -487,6 +493,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         bool done = false;
         c->scan_path = HVWS_PATH_COUNT_READ_EMIT;
         if ((c->spec_ok && c->spec_mode != 0) || c->spec_mode == 1) {
+            // a set not used yet gets the other set's capacity (the table
+            // must hold the estimated records for the check to pass)
+            if (c->T().frame_cap < c->ts[c->cur ^ 1].frame_cap)
+                HIP_OR(ensure_frames(c, c->ts[c->cur ^ 1].frame_cap, /*exact=*/true), HVWS_ENOMEM);
             sc.seq = ++c->scan_seq;
             HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
             if ((rc = tiles()) != HVWS_OK) return rc;
@@ -1172,6 +1182,14 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
         hipEventCreateWithFlags(&comp_done[i], hipEventDisableTiming);
         hipEventCreateWithFlags(&out_done[i], hipEventDisableTiming);
     }
+    // every chunk's segment {0, n}, resident before the loop
+    dbuf pipe_segs;
+    HIP_OR(pipe_segs.ensure(nchunks * sizeof(dseg)), HVWS_ENOMEM);
+    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);   // h_segs may still feed an earlier copy
+    HIP_OR(c->h_segs.ensure(nchunks * sizeof(dseg)), HVWS_ENOMEM);
+    for (uint64_t k = 0; k < nchunks; ++k) c->h_segs.as<dseg>()[k] = dseg{0, std::min(chunk, len - k * chunk)};
+    HIP_OR(hipMemcpyAsync(pipe_segs.p, c->h_segs.p, nchunks * sizeof(dseg), hipMemcpyHostToDevice, c->stream),
+           HVWS_EHIP);
     hvws_segment seg0 = {0, 0};
     void* keep = carry->data;
     int out_rc = HVWS_OK;
@@ -1201,12 +1219,9 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
         } else {
             // The carry chains on the device: chunk k-1's carry-out is chunk
             // k's carry-in (a frame may straddle the chunk boundary).
-            const dseg ds = {0, n};
-            e = hipStreamSynchronize(c->stream);
-            if (e == hipSuccess) e = c->h_segs.ensure(sizeof(ds));
-            if (e != hipSuccess) break;
-            memcpy(c->h_segs.p, &ds, sizeof(ds));
-            e = hipMemcpyAsync(c->segs.p, c->h_segs.p, sizeof(ds), hipMemcpyHostToDevice, c->stream);
+            // Both tables are copied device to device, so the host never
+            // waits inside the loop (each chunk's segment is preloaded).
+            e = hipMemcpyAsync(c->segs.p, pipe_segs.as<dseg>() + k, sizeof(dseg), hipMemcpyDeviceToDevice, c->stream);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(c->carry_in.p, c->T().carry_out.p, sizeof(dcarry), hipMemcpyDeviceToDevice,
                                    c->stream);
@@ -1236,6 +1251,7 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
         hipEventDestroy(out_done[i]);
         slot[i].release();
     }
+    pipe_segs.release();
     carry->data = keep;
     // The slots are gone: forget the scan that referenced them.
     c->have_scan = false;

@@ -471,3 +471,23 @@ def test_pipelined_steps_back_to_back(eng):
             assert np.array_equal(frames[f], exp_recs[f]), f
         for k in range(len(segs0)):
             assert cout[k].fields() == exp_carry[k].fields(), k
+
+
+def test_single_segment_table_overflow():
+    """One segment with more records than the first one-stream table guess
+    (2^20): the pass overflows, the count is read, the segment is re-emitted
+    into an exact table; the next batch on the context is sized from it."""
+    rng = random.Random(8)
+    k = b"\x11\x22\x33\x44"
+    frames = []
+    for _ in range(1_200_000):
+        if rng.random() < 0.8:
+            frames.append((0x2 | 0x10, b"", None))                         # 2-byte unmasked empty
+        else:
+            frames.append((0x1 | 0x10 | 0x20, rng.randbytes(rng.randint(0, 9)), k))
+    data = H.build_frames_ref(frames)
+    buf = np.frombuffer(data, np.uint8).copy()
+    with libhv_amd.Engine(0) as fresh:
+        paths = _compare_batch(fresh, buf, [(0, len(buf))])
+        assert set(paths.values()) == {2}, paths   # HVWS_PATH_SINGLE
+        _compare_batch(fresh, buf[:len(buf) // 2].copy(), [(0, len(buf) // 2)])
