@@ -160,6 +160,23 @@ int hvws_set_unmask_variant(int variant);
  * depend on it.  Returns the previous value. */
 uint64_t hvws_set_spec_min(uint64_t frames);
 
+/* Frame sieve: one segment of at least `bytes` after its first whole frame,
+ * whose frame sizes vary, is discovered by data-parallel passes (every byte
+ * position tested for a plausible client frame header chained 3 headers
+ * deep, then pointer doubling from the first frame along exact successors)
+ * instead of the serial header-to-header walk; frames the chain cannot reach
+ * (unmasked, RSV bits, reserved opcodes) are walked exactly from there.
+ * Tuning only (process-wide, default 8 MiB, 0 = default; $HVWS_SIEVE_MIN);
+ * results never depend on it.  Returns the previous value. */
+uint64_t hvws_set_sieve_min(uint64_t bytes);
+
+/* What the frame sieve did in the last one-segment scan on ctx (NULL = the
+ * calling thread's context; waits for that scan): out[0] = 0 not run or not
+ * wanted (uniform sizes, short segment), 1 sieved, 2 more survivors than its
+ * table held (walked instead); out[1] = survivors; out[2] = frames on the
+ * chain; out[3] = segment offset where the exact walk resumed. */
+int hvws_last_sieve(hvws_ctx* ctx, uint64_t out[4]);
+
 /* Speculative frame table for large multi-segment batches: when the last
  * batch's per-segment record counts matched the uniform-stride estimates,
  * the next scan emits straight into the table at the estimated offsets and

@@ -156,6 +156,8 @@ _SIGS = {
     "hvws_thread_release": (None, []),
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_spec_min": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "hvws_set_sieve_min": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "hvws_last_sieve": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),

@@ -152,6 +152,16 @@ struct hvws_ctx {
     uint64_t fast_bound = 0;   // record bound below which COUNT -> EMIT needs no host wait; 0 = default
     int scan_path = -1;        // HVWS_PATH_* of the last scan
     uint64_t single_hint = 0;  // records of the last one-segment scan whose count was read
+    // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
+    // parallel.  h_sv receives the device state + survivor and chain counts
+    // after each sieved scan (read as hints by the next one).
+    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_S, sv_J0, sv_J1, sv_mark, sv_rank, sv_cnt, sv_tmp;
+    uint64_t sv_cap = 0;
+    hbuf h_sv;
+    uint32_t sv_skip = 0;      // one-stream scans left before the sieve is tried again on uniform traffic
+    bool sv_ran = false;       // the last scan launched the sieve
+    hipEvent_t sv_ev = nullptr;   // h_sv holds the last sieved scan's state once this has completed
+    uint64_t sv_gen = 0;       // sieve_generation() the history below belongs to
     // staging for host-memory entry points
     dbuf stage;
     dbuf xor_stage;
@@ -314,6 +324,52 @@ int wait_status(hvws_ctx* c, uint64_t seq) {
     }
 }
 
+// The last sieved scan's state has landed in h_sv.
+bool sieve_state_ready(hvws_ctx* c) { return c->sv_ran && c->sv_ev && hipEventQuery(c->sv_ev) == hipSuccess; }
+
+// Frame-sieve buffers for a one-segment scan of rx_len bytes.  The survivor
+// capacity is sized from the batch (one survivor per KiB) and from the last
+// sieved scan's survivor count; a batch with more survivors than that leaves
+// the sieve off (the exact walk runs) and the next one gets room.
+int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
+    const uint64_t* h = c->h_sv.as<uint64_t>();
+    const uint64_t seen = sieve_state_ready(c) ? h[sizeof(dsieve) / 8] : 0;   // survivors of the last sieved scan
+    uint64_t cap = std::max<uint64_t>({1ull << 20, rx_len / 1024, seen + seen / 4 + 1});
+    cap = std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+    if (cap > c->sv_cap) c->sv_cap = cap;
+    cap = c->sv_cap;
+    const uint64_t ntm = sieve_tiles_max(rx_len);
+    const uint64_t nmax = std::max(cap, ntm);
+    HIP_OR(c->sv_state.ensure(sizeof(dsieve)), HVWS_ENOMEM);
+    HIP_OR(c->sv_tcount.ensure(ntm * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_tbase.ensure(ntm * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_slot.ensure(sieve_slot_words(rx_len) * 4), HVWS_ENOMEM);
+    HIP_OR(c->sv_S.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_pool.ensure(cap * 4), HVWS_ENOMEM);
+    HIP_OR(c->sv_J0.ensure(cap * 4), HVWS_ENOMEM);
+    HIP_OR(c->sv_J1.ensure(cap * 4), HVWS_ENOMEM);
+    HIP_OR(c->sv_mark.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_rank.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_cnt.ensure(24), HVWS_ENOMEM);
+    HIP_OR(c->sv_tmp.ensure((4 * ((nmax + 1023) / 1024) + 64) * 8), HVWS_ENOMEM);
+    b.state = c->sv_state.as<dsieve>();
+    b.tcount = c->sv_tcount.as<uint64_t>();
+    b.tbase = c->sv_tbase.as<uint64_t>();
+    b.slot = c->sv_slot.as<uint32_t>();
+    b.pool = c->sv_pool.as<uint32_t>();
+    b.pool_n = c->sv_cnt.as<uint64_t>() + 2;
+    b.S = c->sv_S.as<uint64_t>();
+    b.J0 = c->sv_J0.as<uint32_t>();
+    b.J1 = c->sv_J1.as<uint32_t>();
+    b.mark = c->sv_mark.as<uint64_t>();
+    b.rank = c->sv_rank.as<uint64_t>();
+    b.m_total = c->sv_cnt.as<uint64_t>();
+    b.npath = c->sv_cnt.as<uint64_t>() + 1;
+    b.tmp = c->sv_tmp.as<uint64_t>();
+    b.capS = cap;
+    return HVWS_OK;
+}
+
 // Scan with the carry-in already resident in c->carry_in (device).
 // Unmask kernel launch with its timing events (no argument checks).
 // after_scan: queued right behind the scan's end event, which then doubles
@@ -385,6 +441,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.carry_w = c->carry_in.as<dcarry>();
     sc.status = nullptr;
     sc.seq = 0;
+    sc.sieve = nullptr;
     dspec_status* status_d = mapped<dspec_status>(c->h_status);
     const dspec_status* status_h = c->h_status.as<dspec_status>();
     if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
@@ -464,6 +521,29 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         const uint64_t guess = std::max<uint64_t>(kSingleMin, c->single_hint + c->single_hint / 4);
         const uint64_t cap = std::min<uint64_t>(bound, guess);
         HIP_OR(ensure_frames(c, cap), HVWS_ENOMEM);
+        // A long segment is sieved (parallel discovery) unless the last
+        // sieved scan found uniform sizes: then 15 scans walk before the next
+        // try.  Results never depend on it.
+        sieve_bufs svb;
+        if (c->sv_gen != sieve_generation()) {
+            c->sv_gen = sieve_generation();
+            c->sv_skip = 0;
+            c->sv_ran = false;
+        }
+        if (rx_len >= sieve_min()) {
+            if (sieve_state_ready(c) && c->h_sv.as<dsieve>()->active == 0 && c->sv_skip == 0) c->sv_skip = 15;
+            if (c->sv_skip) {
+                --c->sv_skip;
+                c->sv_ran = false;
+            } else {
+                HIP_OR(c->h_sv.ensure(sizeof(dsieve) + 16), HVWS_ENOMEM);
+                if (!c->sv_ev) HIP_OR(hipEventCreateWithFlags(&c->sv_ev, hipEventDisableTiming), HVWS_EHIP);
+                const int rc = ensure_sieve(c, rx_len, svb);
+                if (rc) return rc;
+                sc.sieve = &svb;
+                c->sv_ran = true;
+            }
+        }
         HIP_OR(pass(SCAN_SINGLE), HVWS_EHIP);
         if (bound > c->T().frame_cap) {
             int rc = read_count(nfr);
@@ -475,6 +555,13 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             c->nfr_known = true;
             c->single_hint = nfr;
         }
+        if (c->sv_ran) {   // state and counts for the next scan's choices and hvws_last_sieve
+            HIP_OR(hipMemcpyAsync(c->h_sv.p, c->sv_state.p, sizeof(dsieve), hipMemcpyDeviceToHost, c->cs), HVWS_EHIP);
+            HIP_OR(hipMemcpyAsync(c->h_sv.as<uint8_t>() + sizeof(dsieve), c->sv_cnt.p, 16, hipMemcpyDeviceToHost, c->cs),
+                   HVWS_EHIP);
+            HIP_OR(hipEventRecord(c->sv_ev, c->cs), HVWS_EHIP);
+        }
+        sc.sieve = nullptr;
     } else if (bound <= (c->fast_bound ? c->fast_bound : kFastFrameBound)) {
         c->scan_path = HVWS_PATH_COUNT_EMIT;
         HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
@@ -872,6 +959,11 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         t.release();
         if (t.free_ev) hipEventDestroy(t.free_ev);
     }
+    for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_S, &c->sv_J0, &c->sv_J1,
+                    &c->sv_mark, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
+        b->release();
+    c->h_sv.release();
+    if (c->sv_ev) hipEventDestroy(c->sv_ev);
     for (dbuf* b : {&c->segs, &c->carry_in, &c->stage, &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad,
                     &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->d_small_in, &c->d_small_slots})
         b->release();
@@ -1396,6 +1488,24 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
 const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant()); }
 
 uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
+
+uint64_t hvws_set_sieve_min(uint64_t bytes) { return set_sieve_min(bytes); }
+
+int hvws_last_sieve(hvws_ctx* c, uint64_t out[4]) {
+    if (!c) c = thread_ctx();
+    if (!c || !out) return set_err(HVWS_EINVAL, "hvws_last_sieve: NULL argument");
+    out[0] = out[1] = out[2] = out[3] = 0;
+    if (!c->sv_ran) return HVWS_OK;
+    HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
+    const dsieve* d = c->h_sv.as<dsieve>();
+    const uint64_t* n = reinterpret_cast<const uint64_t*>(c->h_sv.as<uint8_t>() + sizeof(dsieve));
+    out[0] = d->active ? (n[0] <= c->sv_cap ? 1 : 2) : 0;
+    out[1] = d->active ? n[0] : 0;
+    out[2] = d->use ? d->npath : 0;
+    out[3] = d->use ? d->pend : 0;
+    return HVWS_OK;
+}
 
 int hvws_last_scan_path(hvws_ctx* c) { return c ? c->scan_path : -1; }
 

@@ -101,6 +101,8 @@ enum : uint32_t {
     SPEC_OK = 2u       // SCAN_SPEC: the speculative table is the exact table (match and within capacity)
 };
 
+struct sieve_bufs;
+
 struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     dmid*     mid;
     uint64_t* npred;
@@ -118,6 +120,7 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     dcarry*       carry_w;
     dspec_status* status;    // device-mapped pinned host
     uint64_t      seq;
+    const sieve_bufs* sieve; // SINGLE / its re-EMIT: frame sieve buffers, nullptr = no sieve
 };
 
 // Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
@@ -127,6 +130,46 @@ __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
     const uint64_t q = ntiles >> 3, r = ntiles & 7u, x = b & 7u, i = b >> 3;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
+
+// Frame sieve (hvws_sieve.hip): parallel discovery of one long mixed-size
+// stream.  State of the current scan, device side.
+struct dsieve {
+    uint64_t active;        // this scan's one segment is sieved
+    uint64_t use;           // k_walk resumes at pend with npath chain frames recorded
+    uint64_t pend;          // segment offset where the exact walk resumes
+    uint64_t last;          // 1 + S index of the chain's last frame
+    uint64_t last_masked;   // 1 + S index of the chain's last masked frame
+    uint64_t npath;         // frames on the chain
+    uint64_t pad[2];
+};
+
+// Device buffers of the sieve (per context; scans run in order on one stream).
+struct sieve_bufs {
+    dsieve*   state;
+    uint64_t* tcount;    // per 8 KiB tile: survivors        (sieve_tiles_max entries)
+    uint64_t* tbase;     // exclusive scan of tcount          (sieve_tiles_max)
+    uint32_t* slot;      // first survivors of each tile      (sieve_slot_words)
+    uint32_t* pool;      // survivors of tiles with more      (capS)
+    uint64_t* pool_n;    // pool entries used
+    uint64_t* S;         // survivor segment offsets, sorted  (capS)
+    uint32_t* J0;        // successor / doubling tables       (capS each)
+    uint32_t* J1;
+    uint64_t* mark;      // 1 = on the chain                  (capS)
+    uint64_t* rank;      // exclusive scan of mark            (capS)
+    uint64_t* m_total;   // survivors
+    uint64_t* npath;     // chain frames
+    uint64_t* tmp;       // scan scratch (>= 4 * ceil(max(capS, tiles) / 1024) + 64 words)
+    uint64_t  capS;      // < 2^32
+};
+uint64_t sieve_tiles_max(uint64_t rx_len);
+uint64_t sieve_slot_words(uint64_t rx_len);
+uint64_t sieve_min();                  // bytes after the first whole frame from which a mixed stream is sieved
+uint64_t set_sieve_min(uint64_t v);    // 0 = default; returns the previous value
+uint64_t sieve_generation();           // bumped by set_sieve_min (contexts forget their sieve history)
+hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid, const uint64_t* npred,
+                        const sieve_bufs& b, hipStream_t st);
+hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid,
+                             const sieve_bufs& b, dframes fr, uint32_t vmask, hipStream_t st);
 
 // Kernel launchers (hvws_kernels.hip).
 // COUNT pass (emit=false): counts[], bases[] (exclusive scan) and *total.

@@ -19,125 +19,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
-#include "hvws_internal.h"
+#include "hvws_dev.h"
 
 namespace hvws {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// ---------------------------------------------------------------- helpers
-
-__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
-    r &= 31u;
-    return r ? (x >> r) | (x << (32u - r)) : x;
-}
-
-// Key word for 4-byte aligned words of a payload whose first byte sits at
-// absolute offset `pay_off` with mask phase `phase`: byte at address a uses
-// mask[(a - pay_off + phase) & 3] (http/websocket_parser.c:175).
-__device__ __forceinline__ uint32_t key_for_aligned(uint32_t key, uint64_t pay_off, uint32_t phase) {
-    uint32_t rot = (phase - (uint32_t)pay_off) & 3u;
-    return rotr32(key, 8u * rot);
-}
-
-__device__ __forceinline__ uint64_t ld64_guard(const uint8_t* rx, uint64_t rx_len, uint64_t a) {
-    if (a + 8 <= rx_len) return *reinterpret_cast<const uint64_t*>(rx + a);
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (a + k < rx_len) v |= (uint64_t)rx[a + k] << (8 * k);
-    return v;
-}
-
-// 16 bytes starting at arbitrary absolute offset q (bytes past rx_len read 0).
-__device__ __forceinline__ void ld16(const uint8_t* rx, uint64_t rx_len, uint64_t q, uint64_t& lo,
-                                     uint64_t& hi) {
-    uint64_t a = q & ~7ull;
-    uint32_t sh = (uint32_t)(q & 7u) * 8u;
-    uint64_t w0 = ld64_guard(rx, rx_len, a);
-    uint64_t w1 = ld64_guard(rx, rx_len, a + 8);
-    if (sh == 0) {
-        lo = w0;
-        hi = w1;
-        return;
-    }
-    uint64_t w2 = ld64_guard(rx, rx_len, a + 16);
-    lo = (w0 >> sh) | (w1 << (64u - sh));
-    hi = (w1 >> sh) | (w2 << (64u - sh));
-}
-
-struct hdr {
-    uint64_t length;
-    uint32_t hlen;
-    uint32_t flags;
-    uint32_t key;
-    uint32_t viol;   // V_* classes this header violates (reported only if enabled)
-};
-
-__device__ __forceinline__ bool reserved_opcode(uint32_t op) { return (op >= 3 && op <= 7) || op >= 0xB; }
-
-// Fixed-format header decode from its first 16 bytes (lo = bytes 0..7 LE).
-// Layout per websocket_build_frame (http/websocket_parser.c:207-256):
-// b0 = FIN<<7 | opcode, b1 = MASK<<7 | len7, then 0/2/8 big-endian length
-// bytes, then the 4 key bytes if MASK.  RSV bits are dropped (Q1).
-__device__ __forceinline__ hdr parse_hdr(uint64_t lo, uint64_t hi) {
-    hdr h;
-    uint32_t b0 = (uint32_t)lo & 0xFFu;
-    uint32_t b1 = (uint32_t)(lo >> 8) & 0xFFu;
-    uint32_t len7 = b1 & 0x7Fu;
-    bool m = (b1 & 0x80u) != 0;
-    h.flags = (b0 & F_OPMASK) | ((b0 & 0x80u) ? F_FIN : 0u) | (m ? F_MASK : 0u);
-    uint32_t ext = len7 == 126 ? 2u : (len7 == 127 ? 8u : 0u);
-    h.hlen = 2u + ext + (m ? 4u : 0u);
-    uint64_t len16 = (((lo >> 16) & 0xFFu) << 8) | ((lo >> 24) & 0xFFu);
-    uint64_t len64 = __builtin_bswap64((lo >> 16) | (hi << 48));
-    h.length = len7 < 126 ? (uint64_t)len7 : (len7 == 126 ? len16 : len64);
-    uint32_t k0 = (uint32_t)(lo >> 16), k2 = (uint32_t)(lo >> 32), k8 = (uint32_t)(hi >> 16);
-    h.key = m ? (ext == 0 ? k0 : (ext == 2 ? k2 : k8)) : 0u;
-    const uint32_t op = b0 & F_OPMASK;
-    h.viol = ((b0 & 0x70u) ? V_RSV : 0u) | (reserved_opcode(op) ? V_OPCODE : 0u) |
-             ((op & 8u) && (!(b0 & 0x80u) || h.length > 125) ? V_CONTROL : 0u) |
-             (ext == 8 && (h.length >> 63) ? V_LEN64 : 0u) |
-             ((ext == 2 && h.length < 126) || (ext == 8 && h.length <= 0xFFFFu) ? V_NONMIN : 0u) |
-             (m ? 0u : V_UNMASKED);
-    return h;
-}
-
-struct frec {
-    int64_t  hdr_off;   // segment-relative here; made absolute on store
-    uint64_t pay_off;   // segment-relative
-    uint64_t pay_len;
-    uint64_t length;
-    uint32_t key;
-    uint32_t info;
-};
-
-__device__ __forceinline__ void store_frame(const dframes& fr, uint64_t idx, uint64_t seg_off, const frec& r) {
-    if (idx >= fr.cap) return;   // table sized by an estimate (SCAN_SINGLE): the host re-emits if it overflowed
-    uint32_t phase = (r.info >> 8) & 3u;
-    bool masked = (r.info & F_MASK) != 0;
-    uint64_t abs_pay = seg_off + r.pay_off;
-    fr.hdr_off[idx] = r.hdr_off < 0 ? -1 : (int64_t)(seg_off + (uint64_t)r.hdr_off);
-    fr.pay_off[idx] = abs_pay;
-    fr.pay_len[idx] = r.pay_len;
-    fr.length[idx] = r.length;
-    fr.key[idx] = r.key;
-    fr.keyrot[idx] = masked ? key_for_aligned(r.key, abs_pay, phase) : 0u;
-    fr.info[idx] = r.info;
-}
-
-__device__ __forceinline__ uint32_t invalid_bits(uint32_t viol, uint32_t vmask) {
-    const uint32_t v = viol & vmask & V_ALL;
-    return v ? I_INVALID | (v << I_VSHIFT) : 0u;
-}
-
-__device__ __forceinline__ void hdr_complete(frec& r, const dcarry& st, uint64_t pay_off, uint32_t vmask) {
-    r.info = (r.info & ~0xFFu & ~(3u << 8)) | (st.flags & 0xFFu) | I_HDR | invalid_bits(st.viol, vmask);
-    r.pay_off = pay_off;
-    r.pay_len = 0;
-    r.length = st.length;
-    r.key = (st.flags & F_MASK) ? st.mask : 0u;
-}
 
 // Exact byte-level state machine for one frame episode starting from `st` at
 // segment-relative `pos`: used for the carry-in frame and for the incomplete
@@ -326,26 +210,6 @@ uint64_t set_spec_min(uint64_t v) {
     return old;
 }
 
-__device__ __forceinline__ bool parse_at(const uint8_t* rx, uint64_t rx_len, uint64_t seg_off, uint64_t L,
-                                         uint64_t q, hdr& h) {
-    // true when the frame at segment offset q is whole inside [0, L)
-    if (q >= L || L - q < 2) return false;
-    uint64_t lo, hi;
-    ld16(rx, rx_len, seg_off + q, lo, hi);
-    h = parse_hdr(lo, hi);
-    const uint64_t rq = L - q;
-    return h.hlen <= rq && h.length <= rq - h.hlen;
-}
-
-__device__ __forceinline__ void whole_frame_rec(frec& v, uint64_t q, const hdr& h, uint32_t vmask) {
-    v.hdr_off = (int64_t)q;
-    v.pay_off = q + h.hlen;
-    v.pay_len = h.length;
-    v.length = h.length;
-    v.key = h.key;
-    v.info = h.flags | I_HDR | I_START | I_END | (h.length ? I_BODY : 0u) | invalid_bits(h.viol, vmask);
-}
-
 template <bool EMIT>
 __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                        const dseg* __restrict__ segs, uint32_t nseg,
@@ -356,7 +220,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        uint64_t spec_min, uint64_t* __restrict__ est,
                                                        const dseg* __restrict__ src_segs,
                                                        const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
-                                                       dcarry* __restrict__ carry_w) {
+                                                       dcarry* __restrict__ carry_w, int probe_mixed) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
     for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
@@ -394,12 +258,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
             if (EMIT && lane == 0) store_frame(fr, bases[s], sb, r);
             ++n;
         }
-        uint64_t stride = 0, np = 0;
+        uint64_t stride = 0, np = 0, mixed = 0;
         hdr h;
         if (st.state == S_START && parse_at(rx, rx_len, sb, L, pos, h)) {
             stride = (uint64_t)h.hlen + h.length;
             const uint64_t cnt = (L - pos) / stride;
-            if (cnt >= spec_min) {
+            // probe_mixed (one-stream passes): run the probe at any length and
+            // record whether the sizes vary -- the frame sieve's trigger.
+            if (cnt >= spec_min || (probe_mixed && cnt >= 2)) {
                 // Probe before committing the grid: lanes 0-31 check
                 // predictions 2^(l/2) (near the start), lanes 32-63 spread over
                 // the whole range.  Speculation stops at the first probe that
@@ -416,7 +282,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                     const uint64_t other = __shfl_xor(jb, o);
                     jb = other < jb ? other : jb;
                 }
-                np = jb >= spec_min ? jb : 0;
+                np = cnt >= spec_min && jb >= spec_min ? jb : 0;
+                mixed = jb < cnt;
+            } else if (probe_mixed) {
+                mixed = 1;   // the first frame covers over half the segment: sizes unknown
             }
         }
         uint64_t e = n;   // records if every frame after pos had size `stride`
@@ -444,7 +313,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
             m.pos = pos;
             m.stride = stride;
             m.n_a = n;
-            m.pad = 0;
+            m.pad = mixed;   // read by the frame sieve (hvws_sieve.hip)
             mid[s] = m;
             npred[s] = np;
             if (!EMIT) first_fail[s] = np;
@@ -665,7 +534,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ last_masked,
                                                        dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
                                                        const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
-                                                       int emit_counts) {
+                                                       int emit_counts, const dsieve* __restrict__ sv,
+                                                       const uint64_t* __restrict__ sv_S) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
 
@@ -695,6 +565,27 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
             if (EMIT && last_masked[s]) {
                 hdr hm;
                 parse_at(rx, rx_len, sb, L, m.pos + (last_masked[s] - 1) * m.stride, hm);
+                st.mask = hm.key;
+            }
+        }
+
+        // One stream sieved (hvws_sieve.hip): its chain of whole frames is
+        // recorded; resume after it with the fields its last frame leaves.
+        if (sv && s == 0 && sv->use) {
+            const uint64_t np = sv->pend;
+            hdr h;
+            parse_at(rx, rx_len, sb, L, sv_S[sv->last - 1], h);
+            n += sv->npath;
+            pos = np;
+            st.flags = h.flags;
+            st.length = h.length;
+            st.require = 0;
+            st.offset = 0;
+            st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
+            st.started = 0;
+            if (sv->last_masked) {
+                hdr hm;
+                parse_at(rx, rx_len, sb, L, sv_S[sv->last_masked - 1], hm);
                 st.mask = hm.key;
             }
         }
@@ -1245,47 +1136,60 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
     if (nseg == 0) return hipSuccess;
     const uint32_t wb = wave_blocks(nseg);
     const uint32_t vb = 2048;
+    // The frame sieve (one segment): its chain of whole frames is found in
+    // parallel between the COUNT-side head and EMIT; k_walk resumes after it.
+    const bool sieve = sc.sieve && nseg == 1 && (pass == SCAN_SINGLE || pass == SCAN_EMIT);
+    const dsieve* sv = sieve ? sc.sieve->state : nullptr;
+    const uint64_t* sv_S = sieve ? sc.sieve->S : nullptr;
     // k_head<false> opens every pass but EMIT; it takes the zero-copy tables.
     auto head_count = [&](uint64_t* est) {
         hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
-                           sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w);
+                           sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, (int)(pass == SCAN_SINGLE && sieve));
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
     };
-    auto emit = [&](int emit_counts) {
+    auto emit = [&](int emit_counts) -> hipError_t {
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
                            (uint64_t*)nullptr, (const dseg*)nullptr, (const dcarry*)nullptr, (dseg*)nullptr,
-                           (dcarry*)nullptr);
+                           (dcarry*)nullptr, 0);
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
+        if (sieve) {
+            const hipError_t e = launch_sieve_emit(rx, rx_len, segs, sc.mid, *sc.sieve, fr, vmask, st);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, emit_counts);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, emit_counts,
+                           sv, sv_S);
+        return hipSuccess;
     };
     if (pass == SCAN_SINGLE) {
         head_count(nullptr);
-        hipError_t e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st);
-        if (e != hipSuccess) return e;
-        emit(1);
+        hipError_t e;
+        if (sieve && (e = launch_sieve(rx, rx_len, segs, sc.mid, sc.npred, *sc.sieve, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st)) != hipSuccess) return e;
+        if ((e = emit(1)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
     } else if (pass == SCAN_SPEC) {
         head_count(sc.est);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
-        emit(1);
+        if (hipError_t e = emit(1); e != hipSuccess) return e;
         hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
                            sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
         head_count(sc.status ? sc.est : nullptr);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
-                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0);
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0,
+                           (const dsieve*)nullptr, (const uint64_t*)nullptr);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
         if (sc.status)
             hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
                                sc.status, sc.seq);
     } else {
-        emit(0);
+        if (hipError_t e = emit(0); e != hipSuccess) return e;
     }
     return hipGetLastError();
 }

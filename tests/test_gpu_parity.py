@@ -491,3 +491,135 @@ def test_single_segment_table_overflow():
         paths = _compare_batch(fresh, buf, [(0, len(buf))])
         assert set(paths.values()) == {2}, paths   # HVWS_PATH_SINGLE
         _compare_batch(fresh, buf[:len(buf) // 2].copy(), [(0, len(buf) // 2)])
+
+
+# ------------------------------------------------------------ frame sieve
+@pytest.fixture
+def sieve_low():
+    """Sieve one-segment batches from 4 KiB after their first whole frame
+    (default 8 MiB) so these cases exercise it."""
+    L = libhv_amd.lib()
+    old = L.hvws_set_sieve_min(4096)
+    yield
+    L.hvws_set_sieve_min(old)
+
+
+def _last_sieve(eng):
+    out = (ctypes.c_uint64 * 4)()
+    assert libhv_amd.lib().hvws_last_sieve(eng.ctx, out) == 0
+    return list(out)
+
+
+@pytest.mark.parametrize("target,lo,hi,seed", [(24 << 20, 128, 1 << 20, 51), (3 << 20, 1, 4096, 52),
+                                               (1 << 20, 1, 200, 53), (12 << 20, 100, 70000, 54)])
+def test_sieve_mixed_stream(eng, sieve_low, target, lo, hi, seed):
+    """Config-4-shaped streams (fragments, pings, every length encoding) as
+    one segment: the sieve's chain covers every frame, records and bytes
+    bit-exact through every scan path."""
+    plan = synth.mixed_plan(target, seed, lo=lo, hi=hi)
+    host = H.synth_cpu(plan)
+    paths = _compare_batch(eng, host, [(0, plan.total)])
+    assert set(paths.values()) == {2}, paths   # HVWS_PATH_SINGLE
+    active, surv, npath, pend = _last_sieve(eng)
+    assert active == 1 and npath == plan.n and pend == plan.total, (active, surv, npath, pend, plan.n)
+    assert surv >= plan.n
+
+
+def test_sieve_cut_and_carried(eng, sieve_low):
+    """A sieved stream cut at arbitrary bytes (inside headers, payloads, key
+    bytes): the first batch ends with a partial frame, the second resumes
+    from its carry -- both exact."""
+    rng = random.Random(61)
+    plan = synth.mixed_plan(2 << 20, 62, lo=1, hi=3000)
+    data = H.synth_cpu(plan).tobytes()
+    offs = [int(x) for x in plan.frame_off]
+    for cut in [len(data) - 1, len(data) - 3, offs[-1] + 1, offs[-1] + 5, offs[-2] + 3, rng.randrange(len(data)),
+                rng.randrange(len(data))]:
+        _compare_batch(eng, np.frombuffer(data[:cut], np.uint8).copy(), [(0, cut)])
+        _, st, _, _ = H.scan_segment(data[:cut])
+        rest = np.frombuffer(data[cut:], np.uint8).copy()
+        if len(rest):
+            _compare_batch(eng, rest, [(0, len(rest))], [st])
+
+
+def test_sieve_chain_breaks_on_quirks(eng, sieve_low):
+    """Frames the plausibility filter rejects (unmasked, RSV bits, reserved
+    opcodes, non-minimal lengths -- all accepted by the reference) inside a
+    long mixed stream: the chain stops there and the exact walk takes over;
+    results identical to the oracle."""
+    rng = random.Random(71)
+    base = H.synth_cpu(synth.mixed_plan(1 << 20, 72, lo=1, hi=5000)).tobytes()
+    hdrs = [int(r) for r in H.scan_segment(base)[0]["hdr_off"]]
+    k = b"\x0a\x0b\x0c\x0d"
+    odd = [H.build_frames_ref([(0x2 | 0x10, rng.randbytes(300), None)]),                 # unmasked
+           S.with_rsv(H.build_frames_ref([(0x1 | 0x10 | 0x20, rng.randbytes(40), k)])),   # RSV1
+           H.build_frames_ref([(0x3 | 0x10 | 0x20, rng.randbytes(70), k)]),               # reserved opcode
+           bytes([0x82, 0xFE, 0x00, 0x05]) + k + rng.randbytes(5)]                        # 16-bit length 5
+    for pos_frac in (0.0, 0.3, 0.97):
+        for o in odd:
+            data = H.build_frames_ref([(0x1 | 0x10 | 0x20, b"first", k)])
+            cut = int(len(base) * pos_frac)
+            bnd = int(min((r for r in hdrs if r >= cut), default=len(base)))   # a frame boundary
+            stream = data + base[:bnd] + o + base[bnd:]
+            buf = np.frombuffer(stream, np.uint8).copy()
+            _compare_batch(eng, buf, [(0, len(buf))])
+            active, _, npath, pend = _last_sieve(eng)
+            # the chain ends at or before the odd frame (a true frame survives
+            # only if the 3 headers after it are plausible too)
+            assert active == 1 and pend <= len(data) + bnd and (bnd < 20000 or npath > 0), (npath, pend, bnd)
+
+
+def test_sieve_uniform_then_mixed(eng, sieve_low):
+    """Uniform traffic leaves the sieve unwanted (the walk's stride
+    speculation is exact and cheap); mixed traffic after it is sieved again
+    once the context retries.  Results exact throughout."""
+    rng = random.Random(81)
+    ubuf, _, _ = _cut_uniform(rng, 3000, 1000, 1)
+    mplan = synth.mixed_plan(2 << 20, 82, lo=1, hi=4000)
+    mbuf = H.synth_cpu(mplan)
+    _compare_batch(eng, ubuf, [(0, len(ubuf))])
+    assert _last_sieve(eng)[0] == 0
+    for _ in range(20):
+        _compare_batch(eng, mbuf, [(0, len(mbuf))])
+    assert _last_sieve(eng)[0] == 1
+
+
+def test_sieve_survivor_overflow():
+    """More survivors than the first table holds (2^20): the sieve stands
+    down, the exact walk runs, and the next batch gets a table that fits."""
+    rng = random.Random(91)
+    k = b"\x21\x43\x65\x87"
+    frames = [(0x2 | 0x10 | 0x20, rng.randbytes(rng.randint(0, 9)), k) for _ in range(1_100_000)]
+    data = H.build_frames_ref(frames)
+    buf = np.frombuffer(data, np.uint8).copy()
+    L = libhv_amd.lib()
+    old = L.hvws_set_sieve_min(4096)
+    try:
+        with libhv_amd.Engine(0) as fresh:
+            _compare_batch(fresh, buf, [(0, len(buf))])
+            st = _last_sieve(fresh)
+            assert st[0] == 1 and st[2] == len(frames), st   # sized from the first pass's count
+    finally:
+        L.hvws_set_sieve_min(old)
+
+
+def test_sieve_pipelined_same_buffer(eng, sieve_low):
+    """bench.py's pattern: one resident one-segment batch stepped back to back
+    with hvws_step_resident, so each step's discovery runs while the previous
+    step still unmasks the same bytes.  Headers never change, so every step's
+    records are the batch's; an even number of steps restores the bytes."""
+    plan = synth.mixed_plan(16 << 20, 95, lo=1, hi=1 << 18)
+    host = H.synth_cpu(plan)
+    exp_recs, _, _, _ = _oracle_batch(host, [(0, plan.total)], None)
+    rx = eng.to_device(host)
+    for _ in range(6):
+        eng.step_resident(rx, plan.total, [(0, plan.total)], None)
+    eng.sync()
+    frames = eng.frames()
+    got = rx.download(plan.total)
+    rx.free()
+    assert np.array_equal(got, host)
+    assert len(frames) == len(exp_recs)
+    for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
+        assert np.array_equal(frames[f], exp_recs[f]), f
+    assert _last_sieve(eng)[0] == 1
