@@ -155,7 +155,7 @@ struct hvws_ctx {
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
     // after each sieved scan (read as hints by the next one).
-    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_S, sv_J0, sv_J1, sv_mark, sv_rank, sv_cnt, sv_tmp;
+    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_rank, sv_cnt, sv_tmp;
     uint64_t sv_cap = 0;
     hbuf h_sv;
     uint32_t sv_skip = 0;      // one-stream scans left before the sieve is tried again on uniform traffic
@@ -333,11 +333,15 @@ bool sieve_state_ready(hvws_ctx* c) { return c->sv_ran && c->sv_ev && hipEventQu
 // the sieve off (the exact walk runs) and the next one gets room.
 int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     const uint64_t* h = c->h_sv.as<uint64_t>();
-    const uint64_t seen = sieve_state_ready(c) ? h[sizeof(dsieve) / 8] : 0;   // survivors of the last sieved scan
-    uint64_t cap = std::max<uint64_t>({1ull << 20, rx_len / 1024, seen + seen / 4 + 1});
+    // entries (before HBM verification) of the last sieved scan
+    const uint64_t seen = sieve_state_ready(c) ? h[sizeof(dsieve) / 8 + 3] : 0;
+    // Capacity from the last sieved scan's entry count when there is one (the
+    // chain steps and their scans run over the whole capacity), else one
+    // entry per KiB of the batch.
+    uint64_t cap = seen ? std::max<uint64_t>({1ull << 18, rx_len / 8192, seen + seen / 4 + 1024})
+                        : std::max<uint64_t>(1ull << 20, rx_len / 1024);
     cap = std::min<uint64_t>(cap, 0xFFFFFFF0ull);
-    if (cap > c->sv_cap) c->sv_cap = cap;
-    cap = c->sv_cap;
+    c->sv_cap = cap;
     const uint64_t ntm = sieve_tiles_max(rx_len);
     const uint64_t nmax = std::max(cap, ntm);
     HIP_OR(c->sv_state.ensure(sizeof(dsieve)), HVWS_ENOMEM);
@@ -345,12 +349,13 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     HIP_OR(c->sv_tbase.ensure(ntm * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_slot.ensure(sieve_slot_words(rx_len) * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_S.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_Spre.ensure(cap * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_pool.ensure(cap * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_J0.ensure(cap * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_J1.ensure(cap * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_mark.ensure(cap * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_rank.ensure(cap * 8), HVWS_ENOMEM);
-    HIP_OR(c->sv_cnt.ensure(24), HVWS_ENOMEM);
+    HIP_OR(c->sv_cnt.ensure(32), HVWS_ENOMEM);
     HIP_OR(c->sv_tmp.ensure((4 * ((nmax + 1023) / 1024) + 64) * 8), HVWS_ENOMEM);
     b.state = c->sv_state.as<dsieve>();
     b.tcount = c->sv_tcount.as<uint64_t>();
@@ -359,6 +364,8 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     b.pool = c->sv_pool.as<uint32_t>();
     b.pool_n = c->sv_cnt.as<uint64_t>() + 2;
     b.S = c->sv_S.as<uint64_t>();
+    b.Spre = c->sv_Spre.as<uint64_t>();
+    b.m_pre = c->sv_cnt.as<uint64_t>() + 3;
     b.J0 = c->sv_J0.as<uint32_t>();
     b.J1 = c->sv_J1.as<uint32_t>();
     b.mark = c->sv_mark.as<uint64_t>();
@@ -536,7 +543,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 --c->sv_skip;
                 c->sv_ran = false;
             } else {
-                HIP_OR(c->h_sv.ensure(sizeof(dsieve) + 16), HVWS_ENOMEM);
+                HIP_OR(c->h_sv.ensure(sizeof(dsieve) + 32), HVWS_ENOMEM);
                 if (!c->sv_ev) HIP_OR(hipEventCreateWithFlags(&c->sv_ev, hipEventDisableTiming), HVWS_EHIP);
                 const int rc = ensure_sieve(c, rx_len, svb);
                 if (rc) return rc;
@@ -557,7 +564,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         }
         if (c->sv_ran) {   // state and counts for the next scan's choices and hvws_last_sieve
             HIP_OR(hipMemcpyAsync(c->h_sv.p, c->sv_state.p, sizeof(dsieve), hipMemcpyDeviceToHost, c->cs), HVWS_EHIP);
-            HIP_OR(hipMemcpyAsync(c->h_sv.as<uint8_t>() + sizeof(dsieve), c->sv_cnt.p, 16, hipMemcpyDeviceToHost, c->cs),
+            HIP_OR(hipMemcpyAsync(c->h_sv.as<uint8_t>() + sizeof(dsieve), c->sv_cnt.p, 32, hipMemcpyDeviceToHost, c->cs),
                    HVWS_EHIP);
             HIP_OR(hipEventRecord(c->sv_ev, c->cs), HVWS_EHIP);
         }
@@ -959,7 +966,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         t.release();
         if (t.free_ev) hipEventDestroy(t.free_ev);
     }
-    for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_S, &c->sv_J0, &c->sv_J1,
+    for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
                     &c->sv_mark, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
         b->release();
     c->h_sv.release();
@@ -1500,7 +1507,7 @@ int hvws_last_sieve(hvws_ctx* c, uint64_t out[4]) {
     HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
     const dsieve* d = c->h_sv.as<dsieve>();
     const uint64_t* n = reinterpret_cast<const uint64_t*>(c->h_sv.as<uint8_t>() + sizeof(dsieve));
-    out[0] = d->active ? (n[0] <= c->sv_cap ? 1 : 2) : 0;
+    out[0] = d->active ? (n[3] <= c->sv_cap ? 1 : 2) : 0;
     out[1] = d->active ? n[0] : 0;
     out[2] = d->use ? d->npath : 0;
     out[3] = d->use ? d->pend : 0;

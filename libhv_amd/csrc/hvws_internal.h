@@ -151,6 +151,8 @@ struct sieve_bufs {
     uint32_t* slot;      // first survivors of each tile      (sieve_slot_words)
     uint32_t* pool;      // survivors of tiles with more      (capS)
     uint64_t* pool_n;    // pool entries used
+    uint64_t* Spre;      // survivors before HBM verification (capS)
+    uint64_t* m_pre;     // entries of Spre
     uint64_t* S;         // survivor segment offsets, sorted  (capS)
     uint32_t* J0;        // successor / doubling tables       (capS each)
     uint32_t* J1;

@@ -17,8 +17,12 @@
 //                    candidate survives with probability ~57^-3).  Survivors
 //                    of each 8 KiB tile are counted and kept in a small
 //                    per-tile slot, or a run of a shared pool when more.
-//   scan             tile counts -> tile bases (sorted survivor array S).
-//   k_sieve_fill     S from the slots (and the pool runs of busy tiles).
+//   scan             tile counts -> tile bases.
+//   k_sieve_fill     sorted array of survivors from the slots (and the pool
+//                    runs of busy tiles); a candidate whose chain left its
+//                    tile is flagged, and
+//   k_sieve_verify   finishes those from HBM, one thread each;
+//   scan, compact    -> sorted survivor array S.
 //   k_sieve_link     succ(j) = index of S[j] + size(S[j]) in S (binary
 //                    search), or none.
 //   k_sieve_jump     pointer doubling from the stream's first whole frame
@@ -41,7 +45,7 @@ namespace hvws {
 constexpr uint32_t SV_THREADS = 256;
 constexpr uint32_t SV_PER = 32;                        // byte positions per thread
 constexpr uint32_t SV_TILE = SV_THREADS * SV_PER;      // 8 KiB
-constexpr uint32_t SV_HALO = 256;                      // bytes staged past the tile (headers, short hops)
+constexpr uint32_t SV_HALO = 512;                      // bytes staged past the tile (headers, 7-bit-length hops)
 constexpr uint32_t SV_SLOT = 16;                       // survivors kept per tile by the count pass
 constexpr int SV_DEPTH = 3;                            // hops a survivor's chain must stay plausible
 constexpr uint32_t SV_TERM = 0xFFFFFFFFu;
@@ -70,59 +74,40 @@ __device__ __forceinline__ void lds_ld16(const uint32_t* l, uint32_t p, uint64_t
     hi = (uint64_t)b2 | ((uint64_t)b3 << 32);
 }
 
-// Header at segment offset x: from the LDS tile when it is staged there
-// (tile base T0 absolute), else from HBM.
-__device__ __forceinline__ hdr hdr_at(const uint8_t* rx, uint64_t rx_len, const uint32_t* l, uint64_t T0,
-                                      uint64_t a) {
-    uint64_t lo, hi;
-    if (a >= T0 && a - T0 + 16 <= SV_TILE + SV_HALO) lds_ld16(l, (uint32_t)(a - T0), lo, hi);
-    else ld16(rx, rx_len, a, lo, hi);
-    return parse_hdr(lo, hi);
-}
+// Survivor test of the candidate at absolute a (segment [sb, sb + L)): a
+// whole frame with a plausible header whose next SV_DEPTH headers are
+// plausible, or end the stream (exactly, or with a header or frame cut by
+// the segment end).  LOCAL: headers are read from the staged tile only, and
+// the answer is SV_PENDING when the chain leaves it (k_sieve_verify finishes
+// those from HBM, off the tile loop's critical path).
+enum : uint32_t { SV_NO = 0, SV_YES = 1, SV_PENDING = 2 };
 
-// Candidate at absolute a (segment [sb, sb + L)): a whole frame with a
-// plausible header whose next SV_DEPTH headers are plausible, or end the
-// stream (exactly, or with a header or frame cut by the segment end).
-__device__ bool survivor(const uint8_t* rx, uint64_t rx_len, const uint32_t* l, uint64_t T0, uint64_t sb,
-                         uint64_t L, uint64_t a) {
+template <bool LOCAL>
+__device__ uint32_t survivor(const uint8_t* rx, uint64_t rx_len, const uint32_t* l, uint64_t T0, uint64_t sb,
+                             uint64_t L, uint64_t a) {
     const uint64_t end = sb + L;
-    hdr h = hdr_at(rx, rx_len, l, T0, a);
+    auto staged = [&](uint64_t x) { return x >= T0 && x - T0 + 16 <= SV_TILE + SV_HALO; };
+    auto load = [&](uint64_t x) {
+        uint64_t lo, hi;
+        if (LOCAL) lds_ld16(l, (uint32_t)(x - T0), lo, hi);
+        else ld16(rx, rx_len, x, lo, hi);
+        return parse_hdr(lo, hi);
+    };
+    hdr h = load(a);
     const uint64_t r0 = end - a;
-    if (!plausible(h) || h.hlen > r0 || h.length > r0 - h.hlen) return false;
+    if (!plausible(h) || h.hlen > r0 || h.length > r0 - h.hlen) return SV_NO;
     uint64_t x = a + h.hlen + h.length;
 #pragma unroll 1
     for (int d = 0; d < SV_DEPTH; ++d) {
         const uint64_t r = end - x;
-        if (r < 14) return true;   // end of stream, or a header that may be cut by it
-        h = hdr_at(rx, rx_len, l, T0, x);
-        if (!plausible(h)) return false;
-        if (h.length > r - h.hlen) return true;   // frame cut by the segment end
+        if (r < 14) return SV_YES;   // end of stream, or a header that may be cut by it
+        if (LOCAL && !staged(x)) return SV_PENDING;
+        h = load(x);
+        if (!plausible(h)) return SV_NO;
+        if (h.length > r - h.hlen) return SV_YES;   // frame cut by the segment end
         x += h.hlen + h.length;
     }
-    return true;
-}
-
-// Candidate mask of the thread's 32 positions (bit i = position 32*t + i):
-// byte b0 with (b0 & 0x74) == 0 and (b0 & 3) != 3 (RSV clear, opcode 0-2 or
-// 8-A) followed by a byte with MASK set.  SWAR over 4 positions per dword.
-__device__ __forceinline__ uint32_t candidates(const uint32_t* l, uint32_t t) {
-    uint32_t w[SV_PER / 4 + 1];
-#pragma unroll
-    for (int k = 0; k <= (int)(SV_PER / 4); ++k) w[k] = l[t * (SV_PER / 4) + k];
-    uint32_t mask = 0;
-#pragma unroll
-    for (int k = 0; k < (int)(SV_PER / 4); ++k) {
-        const uint32_t v = w[k];
-        const uint32_t v1 = __builtin_amdgcn_alignbyte(w[k + 1], v, 1);   // next byte of each
-        const uint32_t z = v & 0x74747474u;
-        const uint32_t bad = (z + 0x7F7F7F7Fu) | z;                      // bit 7: byte of z non-zero
-        const uint32_t x = (v & 0x03030303u) ^ 0x03030303u;
-        const uint32_t ok = (x + 0x7F7F7F7Fu) | x;                       // bit 7: (b0 & 3) != 3
-        const uint32_t c = ~bad & ok & v1 & 0x80808080u;
-        const uint32_t c4 = ((c >> 7) & 1u) | ((c >> 14) & 2u) | ((c >> 21) & 4u) | ((c >> 28) & 8u);
-        mask |= c4 << (4 * k);
-    }
-    return mask;
+    return SV_YES;
 }
 
 // Tile staging in two halves so the next tile's loads can be in flight while
@@ -130,12 +115,19 @@ __device__ __forceinline__ uint32_t candidates(const uint32_t* l, uint32_t t) {
 // (and t + 512 for the halo) of [T0, T0 + SV_TILE + SV_HALO) into registers,
 // then stores them to LDS.  Bytes past rx_len read 0.
 typedef uint32_t sv_u32x4 __attribute__((ext_vector_type(4)));
-constexpr uint32_t SV_CHUNKS = (SV_TILE + SV_HALO) / 16;   // 528
+// Thread t holds chunks t and t + 256 of the tile, and threads 8h hold halo
+// chunk 512 + h (h < 32), each with the dword that follows it.
 struct tile_regs {
     sv_u32x4 v[3];
+    uint32_t nx[3];
 };
+constexpr uint32_t SV_HCH = SV_HALO / 16;   // halo chunks
 
-__device__ __forceinline__ sv_u32x4 load_chunk(const uint8_t* rx, uint64_t rx_len, uint64_t a) {
+__device__ __forceinline__ bool halo_lane(uint32_t t) { return (t & 7u) == 0 && (t >> 3) < SV_HCH; }
+
+// 16 bytes at a, bytes past rx_len read 0 (the last tile only: kept out of
+// line so its byte loop does not raise the kernel's register allocation).
+__device__ __attribute__((noinline)) sv_u32x4 load_chunk(const uint8_t* rx, uint64_t rx_len, uint64_t a) {
     if (a + 16 <= rx_len) return *reinterpret_cast<const sv_u32x4*>(rx + a);
     uint32_t b[4] = {0u, 0u, 0u, 0u};
     for (uint32_t k = 0; a + k < rx_len && k < 16; ++k) b[k >> 2] |= (uint32_t)rx[a + k] << (8 * (k & 3));
@@ -144,115 +136,231 @@ __device__ __forceinline__ sv_u32x4 load_chunk(const uint8_t* rx, uint64_t rx_le
 
 __device__ __forceinline__ void load_tile(const uint8_t* rx, uint64_t rx_len, uint64_t T0, tile_regs& r) {
     const uint32_t t = threadIdx.x;
+    const uint32_t hc = 2 * SV_THREADS + (t >> 3);   // halo chunk of a halo lane
+    const bool hl = halo_lane(t);
+    const uint8_t* p = rx + T0;
+    if (T0 + SV_TILE + SV_HALO + 16 <= rx_len) {   // every tile but the last
+        r.v[0] = *reinterpret_cast<const sv_u32x4*>(p + 16 * t);
+        r.v[1] = *reinterpret_cast<const sv_u32x4*>(p + 16 * (t + SV_THREADS));
+        r.nx[0] = *reinterpret_cast<const uint32_t*>(p + 16 * (t + 1));
+        r.nx[1] = *reinterpret_cast<const uint32_t*>(p + 16 * (t + SV_THREADS + 1));
+        if (hl) {
+            r.v[2] = *reinterpret_cast<const sv_u32x4*>(p + 16 * hc);
+            r.nx[2] = *reinterpret_cast<const uint32_t*>(p + 16 * (hc + 1));
+        }
+        return;
+    }
     r.v[0] = load_chunk(rx, rx_len, T0 + (uint64_t)t * 16);
     r.v[1] = load_chunk(rx, rx_len, T0 + (uint64_t)(t + SV_THREADS) * 16);
-    r.v[2] = t + 2 * SV_THREADS < SV_CHUNKS ? load_chunk(rx, rx_len, T0 + (uint64_t)(t + 2 * SV_THREADS) * 16)
-                                            : sv_u32x4{0u, 0u, 0u, 0u};
+    r.nx[0] = load_chunk(rx, rx_len, T0 + (uint64_t)(t + 1) * 16).x;
+    r.nx[1] = load_chunk(rx, rx_len, T0 + (uint64_t)(t + SV_THREADS + 1) * 16).x;
+    if (hl) {
+        r.v[2] = load_chunk(rx, rx_len, T0 + (uint64_t)hc * 16);
+        r.nx[2] = load_chunk(rx, rx_len, T0 + (uint64_t)(hc + 1) * 16).x;
+    }
 }
 
 __device__ __forceinline__ void store_tile(uint32_t* l, const tile_regs& r) {
     const uint32_t t = threadIdx.x;
     *reinterpret_cast<sv_u32x4*>(l + 4 * t) = r.v[0];
     *reinterpret_cast<sv_u32x4*>(l + 4 * (t + SV_THREADS)) = r.v[1];
-    if (t + 2 * SV_THREADS < SV_CHUNKS) *reinterpret_cast<sv_u32x4*>(l + 4 * (t + 2 * SV_THREADS)) = r.v[2];
+    if (halo_lane(t)) *reinterpret_cast<sv_u32x4*>(l + 4 * (2 * SV_THREADS + (t >> 3))) = r.v[2];
 }
 
-// Candidate bitmap of the staged tile + halo into cb (bit p = byte p of the
-// tile); bits of positions whose second byte is not staged are never read.
-__device__ __forceinline__ void candidate_bits(const uint32_t* l, uint32_t* cb) {
-    const uint32_t t = threadIdx.x;
-    cb[t] = candidates(l, t);
-    if (t < SV_HALO / SV_PER) cb[SV_TILE / SV_PER + t] = candidates(l, SV_TILE / SV_PER + t);
+// Candidate word of one 16-byte chunk (positions q = 16c + 4d + j, d = dword,
+// j = byte): a byte b0 with (b0 & 0x77) <= 2 -- RSV clear, opcode 0-2 or 8-A
+// -- followed by a byte with MASK set.  SWAR, 4 positions per dword:
+// (b0 & 0x77) + 0x7D sets bit 7 iff (b0 & 0x77) >= 3, with no carry between
+// bytes.  The result is kept transposed: bit 8j + d of the word is position
+// 4d + j of the chunk (cand_bit() reads it).
+__device__ __forceinline__ uint32_t chunk_candidates(sv_u32x4 v, uint32_t next) {
+    const uint32_t w[5] = {v.x, v.y, v.z, v.w, next};
+    uint32_t out = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t bad = (w[d] & 0x77777777u) + 0x7D7D7D7Du;
+        const uint32_t b1 = __builtin_amdgcn_alignbyte(w[d + 1], w[d], 1);   // the byte after each
+        const uint32_t c = b1 & ~bad & 0x80808080u;
+        out |= c >> (7 - d);
+    }
+    return out;
+}
+
+__device__ __forceinline__ uint32_t cand_bit(const uint32_t* cb, uint32_t q) {
+    return (cb[q >> 4] >> (8u * (q & 3u) + ((q >> 2) & 3u))) & 1u;
 }
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* l, uint32_t p) { return (l[p >> 2] >> (8 * (p & 3u))) & 0xFFu; }
 
-// Survivor mask of the thread's positions in tile T0 (segment [sb+pos, sb+L)).
-// A short candidate (7-bit length) whose next header position is staged and
-// is not itself a candidate is rejected by one bitmap test -- the full check
-// would reject it too (a plausible header is a candidate) -- so only ~1 in
-// 57 candidates pays the full parse and hops.
-__device__ __forceinline__ uint32_t survivors(const uint8_t* rx, uint64_t rx_len, const uint32_t* l,
-                                              const uint32_t* cb, uint64_t T0, uint64_t sb, uint64_t L, uint64_t pos) {
-    const uint32_t t = threadIdx.x;
-    uint32_t cm = cb[t];
-    const uint64_t a0 = T0 + (uint64_t)t * SV_PER;
-    const uint64_t lo = sb + pos, hi = sb + L;
-    if (a0 < lo) cm &= lo - a0 >= SV_PER ? 0u : ~0u << (uint32_t)(lo - a0);
-    if (a0 + SV_PER > hi) cm &= a0 >= hi ? 0u : (1u << (uint32_t)(hi - a0)) - 1u;
-    // Phase 1: the bitmap filter (LDS only).  Phase 2: full checks of what
-    // is left -- about one per thread at most -- so a wave waits for one
-    // chain of dependent header loads, not one per candidate.
-    uint32_t pm = 0;
-    while (cm) {
-        const uint32_t i = __builtin_ctz(cm);
-        cm &= cm - 1;
-        const uint32_t p = t * SV_PER + i;
-        const uint32_t len7 = lds_byte(l, p + 1) & 0x7Fu;
-        if (len7 < 126) {
-            const uint32_t x = p + 6u + len7;   // next header (the candidate is masked)
-            if (x + 16 <= SV_TILE + SV_HALO && T0 + x + 14 <= hi && !((cb[x >> 5] >> (x & 31u)) & 1u)) continue;
-        }
-        pm |= 1u << i;
+// Verdict from the staged bytes and the candidate bitmap where that is
+// enough: SV_NO and SV_PENDING as survivor<true> would answer, SV_FULL when
+// survivor<true> must decide.  Every rejection is implied by survivor<true>
+// rejecting: control frames must be FIN and <= 125 bytes, lengths minimal
+// and < 2^48, and a header the chain reaches must be a candidate -- followed
+// through the bitmap for 7-bit lengths while the next header is staged.
+// A plausible 16-bit-length candidate whose next header lies beyond the
+// staged bytes is SV_PENDING without a parse (k_sieve_verify finishes it).
+constexpr uint32_t SV_FULL = 3;
+
+__device__ __forceinline__ uint32_t quick_verdict(const uint32_t* l, const uint32_t* cb, uint32_t q, uint32_t hrel) {
+    // hrel: segment end relative to the tile start (clamped; 32-bit math only)
+    const uint32_t b0 = lds_byte(l, q), len7 = lds_byte(l, q + 1) & 0x7Fu;
+    if ((b0 & 8u) && (!(b0 & 0x80u) || len7 >= 126)) return SV_NO;   // control frame
+    if (len7 == 127) return (lds_byte(l, q + 2) | lds_byte(l, q + 3)) ? SV_NO : SV_FULL;
+    if (len7 == 126) {
+        const uint32_t n = (lds_byte(l, q + 2) << 8) | lds_byte(l, q + 3);
+        if (n < 126) return SV_NO;
+        const uint32_t x = q + 8u + n;
+        if (x > hrel) return SV_NO;                                   // not whole
+        return x + 14 <= hrel && x + 16 > SV_TILE + SV_HALO ? SV_PENDING : SV_FULL;
     }
-    uint32_t sm = 0;
-    while (pm) {
-        const uint32_t i = __builtin_ctz(pm);
-        pm &= pm - 1;
-        if (survivor(rx, rx_len, l, T0, sb, L, a0 + i)) sm |= 1u << i;
+    uint32_t x = q + 6u + len7;
+#pragma unroll 1
+    for (int d = 0; d < SV_DEPTH; ++d) {
+        if (x + 16 > SV_TILE + SV_HALO || x + 14 > hrel) return SV_FULL;
+        if (!cand_bit(cb, x)) return SV_NO;
+        const uint32_t n7 = lds_byte(l, x + 1) & 0x7Fu;
+        if (n7 >= 126) return SV_FULL;
+        x += 6u + n7;
     }
-    return sm;
+    return SV_FULL;
 }
 
-// Block-wide exclusive prefix of v (thread order); *tot = block sum.
-__device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t* ws, uint32_t& tot) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+// Wave-wide exclusive prefix of v; *tot = wave sum.
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& tot) {
+    const uint32_t lane = threadIdx.x & 63u;
     uint32_t x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o);
         if (lane >= (uint32_t)o) x += y;
     }
-    if (lane == 63) ws[w] = x;
-    __syncthreads();
-    uint32_t base = 0;
-    tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < SV_THREADS / 64; ++k) {
-        if (k < w) base += ws[k];
-        tot += ws[k];
-    }
-    __syncthreads();
-    return base + x - v;
+    tot = __shfl(x, 63);
+    return x - v;
 }
+
+constexpr uint32_t SV_WLIST = 512;   // candidates a wave handles per round
 
 struct sieve_lds {
-    uint32_t l[(SV_TILE + SV_HALO) / 4 + 8];
-    uint32_t cb[(SV_TILE + SV_HALO) / SV_PER];
-    uint32_t ws[SV_THREADS / 64];
-    uint32_t nover;
-    uint32_t over[SV_THREADS];
+    uint32_t l[(SV_TILE + SV_HALO) / 4 + 8];   // the tile's bytes (+ halo)
+    uint32_t cb[(SV_TILE + SV_HALO) / 16];     // candidate words, one per 16-byte chunk
+    uint32_t sbits[2][SV_TILE / 32];           // survivors (and pending ones), bit p of word p / 32; by tile parity
+    uint32_t pbits[2][SV_TILE / 32];           // survivors still to be verified from HBM
+    uint16_t list[SV_THREADS / 64][SV_WLIST];  // each wave's candidate positions
 };
 
-// Sieve one tile whose bytes are in r (stored to LDS here); `next` (if any)
-// is loaded into r meanwhile.  Returns this thread's survivor mask and its
-// exclusive prefix / the tile total.
-__device__ __forceinline__ uint32_t sieve_tile(const uint8_t* rx, uint64_t rx_len, sieve_lds& sh, tile_regs& r,
-                                               uint64_t T0, bool have_next, uint64_t next_T0, uint64_t sb,
-                                               uint64_t L, uint64_t pos, uint32_t& before, uint32_t& tot) {
+// Candidates of the staged tile, then the survivor test: each wave compacts
+// its own candidates into a list so every lane checks about one (a loop over
+// each thread's 32 positions waited for the busiest lane); survivors land in
+// the tile's bitmaps.  Two block barriers per tile: tile + candidate words
+// staged, and survivors complete.
+template <int MODE>
+__device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, sieve_lds& sh, tile_regs& r, int par,
+                                           uint64_t T0, bool have_next, uint64_t next_T0, uint64_t sb, uint64_t L,
+                                           uint64_t pos) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     store_tile(sh.l, r);
+    const uint32_t w0 = chunk_candidates(r.v[0], r.nx[0]);
+    const uint32_t w1 = chunk_candidates(r.v[1], r.nx[1]);
+    sh.cb[t] = w0;
+    sh.cb[t + SV_THREADS] = w1;
+    if (halo_lane(t)) sh.cb[2 * SV_THREADS + (t >> 3)] = chunk_candidates(r.v[2], r.nx[2]);
+    sh.sbits[par][t] = 0;
+    sh.pbits[par][t] = 0;
+    if (MODE != 4 && have_next) load_tile(rx, rx_len, next_T0, r);   // MODE 4: no prefetch (registers)
     __syncthreads();
-    if (have_next) load_tile(rx, rx_len, next_T0, r);
-    candidate_bits(sh.l, sh.cb);
+    if (MODE == 2) {   // timing experiment: staging and candidate words only
+        if (w0 == 0x12345678u) sh.sbits[par][0] = w1;
+        __syncthreads();
+        return;
+    }
+    const uint64_t lo = sb + pos, hi = sb + L;
+    const uint32_t qlo = lo > T0 ? (uint32_t)(lo - T0) : 0u;
+    const uint32_t qhi = hi - T0 < SV_TILE ? (uint32_t)(hi - T0) : SV_TILE;
+    const uint32_t hrel = hi - T0 < (1u << 30) ? (uint32_t)(hi - T0) : (1u << 30);   // > any 16-bit-length frame end
+    uint32_t wtot;
+    const uint32_t first = wave_prefix(__builtin_popcount(w0) + __builtin_popcount(w1), wtot);
+    uint16_t* list = sh.list[w];
+    for (uint32_t base = 0; base < wtot; base += SV_WLIST) {
+        uint32_t k = first;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t m = h ? w1 : w0;
+            const uint32_t c = h ? t + SV_THREADS : t;
+            while (m) {
+                const uint32_t b = __builtin_ctz(m);
+                m &= m - 1;
+                if (k >= base && k < base + SV_WLIST) list[k - base] = (uint16_t)(16u * c + 4u * (b & 7u) + (b >> 3));
+                ++k;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t nl = wtot - base < SV_WLIST ? wtot - base : SV_WLIST;
+        for (uint32_t e = lane; e < nl && MODE != 1; e += 64) {   // MODE 1 (timing): lists only
+            const uint32_t q = list[e];
+            if (q < qlo || q >= qhi) continue;
+            uint32_t v = quick_verdict(sh.l, sh.cb, q, hrel);
+            if (v == SV_NO) continue;
+            if (v == SV_FULL) v = SV_PENDING;   // k_sieve_verify decides from HBM (keeps this loop lean)
+            if (v != SV_NO) atomicOr(&sh.sbits[par][q >> 5], 1u << (q & 31u));
+            if (v == SV_PENDING) atomicOr(&sh.pbits[par][q >> 5], 1u << (q & 31u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     __syncthreads();
-    const uint32_t sm = survivors(rx, rx_len, sh.l, sh.cb, T0, sb, L, pos);
-    before = block_prefix(__builtin_popcount(sm), sh.ws, tot);
-    return sm;
 }
 
-// COUNT: tcount[t] = survivors of tile t, the first SV_SLOT of them (tile
-// offsets) into slot[t].
-__global__ __launch_bounds__(SV_THREADS) void k_sieve_count(const uint8_t* __restrict__ rx, uint64_t rx_len,
+// Wave 0 records tile t's survivors (bitmaps of parity par) in position
+// order: up to SV_SLOT in the tile's slot; a tile with more reserves a run
+// of the pool and records its start in slot word 0.  Every survivor comes
+// from one snapshot of the bytes, so S is exact and sorted even while a
+// concurrent unmask rewrites the payloads (only false survivors depend on
+// payload bytes).  Bit 31 of an entry: verify from HBM.
+__device__ __forceinline__ void record_tile(const sieve_lds& sh, int par, uint64_t t, uint64_t* tcount,
+                                            uint32_t* slot, uint32_t* pool, unsigned long long* pool_n,
+                                            uint64_t pool_cap) {
+    const uint32_t lane = threadIdx.x;   // wave 0
+    const uint32_t* sw = sh.sbits[par] + 4 * lane;
+    const uint32_t* pw = sh.pbits[par] + 4 * lane;
+    const uint32_t n = __builtin_popcount(sw[0]) + __builtin_popcount(sw[1]) + __builtin_popcount(sw[2]) +
+                       __builtin_popcount(sw[3]);
+    uint32_t tot;
+    uint32_t k = wave_prefix(n, tot);
+    if (tot == 0) {
+        if (lane == 0) tcount[t] = 0;
+        return;
+    }
+    uint32_t* dst = slot + t * SV_SLOT;
+    uint32_t cap = SV_SLOT;
+    if (tot > SV_SLOT) {
+        uint64_t base = 0;
+        if (lane == 0) base = atomicAdd(pool_n, (unsigned long long)tot);
+        base = __shfl(base, 0);
+        if (lane == 0) dst[0] = (uint32_t)base;
+        dst = pool + base;
+        cap = base + tot <= pool_cap ? tot : 0;   // pool full: the survivor total exceeds capS, sieve off
+    }
+    if (lane == 0) tcount[t] = tot;
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        uint32_t m = sw[i];
+        const uint32_t pmk = pw[i];
+        while (m) {
+            const uint32_t b = __builtin_ctz(m);
+            m &= m - 1;
+            if (k < cap) dst[k] = (128u * lane + 32u * i + b) | (((pmk >> b) & 1u) << 31);
+            ++k;
+        }
+    }
+}
+
+// COUNT: tcount[t] = survivors of tile t, recorded by record_tile.
+template <int MODE>
+__global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_sieve_count(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                             const dseg* __restrict__ segs, const dmid* __restrict__ mid,
                                                             const uint64_t* __restrict__ npred, uint64_t sieve_min,
                                                             uint64_t* __restrict__ tcount, uint32_t* __restrict__ slot,
@@ -267,7 +375,7 @@ __global__ __launch_bounds__(SV_THREADS) void k_sieve_count(const uint8_t* __res
         *sv = z;
     }
     if (!want) return;
-    if (threadIdx.x < 8) sh.l[(SV_TILE + SV_HALO) / 4 + threadIdx.x] = 0;
+    if (threadIdx.x < 8) sh.l[(SV_TILE + SV_HALO) / 4 + threadIdx.x] = 0;   // read past the last halo chunk
     const uint64_t A0 = (sb + pos) & ~15ull;
     const uint64_t ntiles = (sb + L - A0 + SV_TILE - 1) / SV_TILE;
     for (uint64_t t = ntiles + blockIdx.x; t < ntiles_max; t += gridDim.x)
@@ -275,34 +383,19 @@ __global__ __launch_bounds__(SV_THREADS) void k_sieve_count(const uint8_t* __res
     tile_regs r;
     uint64_t t = blockIdx.x;
     if (t < ntiles) load_tile(rx, rx_len, A0 + t * SV_TILE, r);
-    for (; t < ntiles; t += gridDim.x) {
-        const uint64_t T0 = A0 + t * SV_TILE;
+    int par = 0;
+    for (; t < ntiles; t += gridDim.x, par ^= 1) {
         const uint64_t tn = t + gridDim.x;
-        uint32_t before, tot;
-        uint32_t m = sieve_tile(rx, rx_len, sh, r, T0, tn < ntiles, A0 + tn * SV_TILE, sb, L, pos, before, tot);
-        // Up to SV_SLOT survivors go to the tile's slot; a tile with more
-        // reserves a run of the pool and records its start in slot word 0.
-        // Every survivor is written from this one snapshot of the bytes, so
-        // S is exact and sorted even while a concurrent unmask rewrites the
-        // payloads (only false survivors depend on payload bytes).
-        uint32_t* dst = slot + t * SV_SLOT;
-        uint64_t cap = SV_SLOT;
-        if (tot > SV_SLOT) {
-            if (threadIdx.x == 0) sh.nover = (uint32_t)atomicAdd(pool_n, (unsigned long long)tot);
-            __syncthreads();
-            const uint64_t base = sh.nover;
-            __syncthreads();
-            if (threadIdx.x == 0) dst[0] = (uint32_t)base;
-            dst = pool + base;
-            cap = base + tot <= pool_cap ? tot : 0;   // pool full: the survivor total exceeds capS, sieve off
+        if (MODE == 3) {   // timing experiment: the loads alone
+            if (tn < ntiles) load_tile(rx, rx_len, A0 + tn * SV_TILE, r);
+            if (threadIdx.x == 0) tcount[t] = r.v[0].x == 0x12345678u && r.v[1].y == 7u ? 1u : 0u;
+            continue;
         }
-        if (threadIdx.x == 0) tcount[t] = tot;
-        uint32_t k = before;
-        while (m && k < cap) {
-            const uint32_t i = __builtin_ctz(m);
-            m &= m - 1;
-            dst[k++] = threadIdx.x * SV_PER + i;
-        }
+        if (MODE == 4 && t != blockIdx.x) load_tile(rx, rx_len, A0 + t * SV_TILE, r);
+        sieve_tile<MODE>(rx, rx_len, sh, r, par, A0 + t * SV_TILE, tn < ntiles, A0 + tn * SV_TILE, sb, L, pos);
+        // wave 0 records while the other waves stage the next tile (the
+        // bitmaps alternate by parity; the next barrier orders the rest)
+        if (threadIdx.x < 64) record_tile(sh, par, t, tcount, slot, pool, pool_n, pool_cap);
     }
 }
 
@@ -323,8 +416,47 @@ __global__ __launch_bounds__(256) void k_sieve_fill(const dseg* __restrict__ seg
         if (n == 0) continue;
         const uint64_t T0 = A0 + t * SV_TILE - sb;
         const uint32_t* src = n <= SV_SLOT ? slot + t * SV_SLOT : pool + slot[t * SV_SLOT];
-        for (uint64_t k = 0; k < n; ++k) S[b + k] = T0 + src[k];
+        for (uint64_t k = 0; k < n; ++k) {
+            const uint32_t e = src[k];
+            S[b + k] = (T0 + (e & 0x7FFFFFFFu)) | ((uint64_t)(e >> 31) << 63);
+        }
     }
+}
+
+// Finish the survivor test of entries whose chain left their tile (from
+// HBM, one thread per entry, every entry's loads in flight at once);
+// keep[j] = 1 for survivors, 0 otherwise and for j in [m_pre, capS).
+__global__ __launch_bounds__(256) void k_sieve_verify(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                      const dseg* __restrict__ segs, uint64_t* __restrict__ Spre,
+                                                      const uint64_t* __restrict__ m_pre, uint64_t capS,
+                                                      uint64_t* __restrict__ keep, const dsieve* __restrict__ sv) {
+    if (!sv->active || *m_pre > capS) return;
+    const uint64_t m = *m_pre, sb = segs[0].off, L = segs[0].len;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < capS; j += (uint64_t)gridDim.x * blockDim.x) {
+        if (j >= m) {
+            keep[j] = 0;
+            continue;
+        }
+        const uint64_t e = Spre[j];
+        if (!(e >> 63)) {
+            keep[j] = 1;
+            continue;
+        }
+        const uint64_t q = e & ~(1ull << 63);
+        keep[j] = survivor<false>(rx, rx_len, nullptr, 0, sb, L, sb + q) == SV_YES;
+        Spre[j] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sieve_compact(const uint64_t* __restrict__ Spre,
+                                                       const uint64_t* __restrict__ m_pre, uint64_t capS,
+                                                       const uint64_t* __restrict__ keep,
+                                                       const uint64_t* __restrict__ kbase, uint64_t* __restrict__ S,
+                                                       const dsieve* __restrict__ sv) {
+    if (!sv->active || *m_pre > capS) return;
+    const uint64_t m = *m_pre;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x)
+        if (keep[j]) S[kbase[j]] = Spre[j];
 }
 
 __device__ __forceinline__ bool sieve_on(const dsieve* sv, const uint64_t* m_total, uint64_t capS) {
@@ -457,13 +589,31 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     dsieve* sv = reinterpret_cast<dsieve*>(b.state);
     hipError_t e = hipMemsetAsync(b.pool_n, 0, 8, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sieve_count, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred, sieve_min(),
-                       b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), b.capS, ntm, sv);
-    if ((e = launch_exclusive_scan(b.tcount, b.tbase, ntm, b.tmp, b.m_total, st)) != hipSuccess) return e;
+    // $HVWS_SIEVE_MODE (timing experiments only, results then wrong): 1 lists
+    // without checks, 2 staging + candidate words, 3 loads alone; 4 = the
+    // product without the next tile's register prefetch (exact).
+    static const int mode = getenv("HVWS_SIEVE_MODE") ? atoi(getenv("HVWS_SIEVE_MODE")) : 0;
+#define HVWS_SIEVE_COUNT(M)                                                                                     \
+    hipLaunchKernelGGL(k_sieve_count<M>, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,    \
+                       sieve_min(), b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), \
+                       b.capS, ntm, sv)
+    switch (mode) {
+        case 1: HVWS_SIEVE_COUNT(1); break;
+        case 2: HVWS_SIEVE_COUNT(2); break;
+        case 3: HVWS_SIEVE_COUNT(3); break;
+        case 4: HVWS_SIEVE_COUNT(4); break;
+        default: HVWS_SIEVE_COUNT(0); break;
+    }
+#undef HVWS_SIEVE_COUNT
+    if ((e = launch_exclusive_scan(b.tcount, b.tbase, ntm, b.tmp, b.m_pre, st)) != hipSuccess) return e;
     const uint64_t fb = (ntm + 255) / 256;
     hipLaunchKernelGGL(k_sieve_fill, dim3((uint32_t)(fb < 8192 ? fb : 8192)), dim3(256), 0, st, segs, mid, b.tcount,
-                       b.tbase, b.slot, b.pool, b.S, b.m_total, b.capS, sv);
+                       b.tbase, b.slot, b.pool, b.Spre, b.m_pre, b.capS, sv);
     const uint32_t lg = (uint32_t)((b.capS + 255) / 256 < 8192 ? (b.capS + 255) / 256 : 8192);
+    // keep flags in `mark`, their scan in `rank` (both rewritten by the chain steps below)
+    hipLaunchKernelGGL(k_sieve_verify, dim3(lg), dim3(256), 0, st, rx, rx_len, segs, b.Spre, b.m_pre, b.capS, b.mark, sv);
+    if ((e = launch_exclusive_scan(b.mark, b.rank, b.capS, b.tmp, b.m_total, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sieve_compact, dim3(lg), dim3(256), 0, st, b.Spre, b.m_pre, b.capS, b.mark, b.rank, b.S, sv);
     hipLaunchKernelGGL(k_sieve_link, dim3(lg), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capS, b.J0,
                        b.mark, sv);
     uint32_t* Jin = b.J0;
