@@ -444,42 +444,64 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
             lo[u] = hi[u] = 0;
             if (inr[u]) ld16(rx, rx_len, sb + pos + (uint64_t)j * stride, lo[u], hi[u]);
         }
-        hdr h[SCAN_U];
-        bool whole[SCAN_U];
+        // Per prediction only what the records need is kept: the key and a
+        // packed (flags | hlen << 8 | viol << 16); a frame that holds has
+        // length = stride - hlen.  The first break's wholeness and size are
+        // taken while its header is parsed.  (Holding the parsed headers of
+        // all SCAN_U predictions cost 134 VGPRs, 3 waves per SIMD.)
+        uint32_t key[SCAN_U], pk[SCAN_U];
         uint32_t f = NPRED;
+        bool wf = false;
+        uint64_t sf = 0;
 #pragma unroll
         for (int u = 0; u < SCAN_U; ++u) {
             const uint32_t j = (uint32_t)u * 64u + lane;
             const uint64_t q = pos + (uint64_t)j * stride;
-            h[u] = parse_hdr(lo[u], hi[u]);
+            const hdr h = parse_hdr(lo[u], hi[u]);
             const uint64_t rq = inr[u] ? L - q : 0;
-            whole[u] = inr[u] && h[u].hlen <= rq && h[u].length <= rq - h[u].hlen;
-            const bool ok = whole[u] && (uint64_t)h[u].hlen + h[u].length == stride;
+            const bool whole = inr[u] && h.hlen <= rq && h.length <= rq - h.hlen;
+            const uint64_t sz = (uint64_t)h.hlen + h.length;
+            const bool ok = whole && sz == stride;
+            key[u] = h.key;
+            pk[u] = h.flags | (h.hlen << 8) | (h.viol << 16);
             const unsigned long long bad = __ballot(!ok);
-            if (f == NPRED && bad) f = (uint32_t)u * 64u + (uint32_t)(__ffsll((long long)bad) - 1);
+            if (f == NPRED && bad) {
+                const int lf = __ffsll((long long)bad) - 1;
+                f = (uint32_t)u * 64u + (uint32_t)lf;
+                wf = __shfl((int)whole, lf) != 0;
+                sf = __shfl(sz, lf);
+            }
         }
         uint32_t last_flags = 0, last_key = 0;
         uint64_t last_len = 0;
         bool any_masked = false;
-#pragma unroll
-        for (int u = 0; u < SCAN_U; ++u) {
+#pragma unroll 1
+        for (int u = 0; u < SCAN_U; ++u) {   // not unrolled: 4 records' stores in flight cost ~30 VGPRs
             const uint32_t j = (uint32_t)u * 64u + lane;
             const bool mine = j < f;
+            const uint32_t fl = pk[u] & 0xFFu, hl = (pk[u] >> 8) & 0xFFu;
             if (EMIT && mine) {
+                const uint64_t q = pos + (uint64_t)j * stride;
+                const uint64_t len = stride - hl;
                 frec v;
-                whole_frame_rec(v, pos + (uint64_t)j * stride, h[u], vmask);
+                v.hdr_off = (int64_t)q;
+                v.pay_off = q + hl;
+                v.pay_len = len;
+                v.length = len;
+                v.key = key[u];
+                v.info = fl | I_HDR | I_START | I_END | (len ? I_BODY : 0u) | invalid_bits(pk[u] >> 16, vmask);
                 emit(n + j, v);
             }
-            const unsigned long long mm = __ballot(mine && (h[u].flags & F_MASK));
+            const unsigned long long mm = __ballot(mine && (fl & F_MASK));
             if (mm) {
                 const int src = 63 - __clzll((long long)mm);
-                last_key = __shfl(h[u].key, src);
+                last_key = __shfl(key[u], src);
                 any_masked = true;
             }
             if (f > (uint32_t)u * 64u && f <= (uint32_t)u * 64u + 64u) {
                 const int src = (int)(f - 1 - (uint32_t)u * 64u);
-                last_flags = __shfl(h[u].flags, src);
-                last_len = __shfl(h[u].length, src);
+                last_flags = __shfl(fl, src);
+                last_len = stride - __shfl(hl, src);
             }
         }
         if (f > 0) {
@@ -499,18 +521,6 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
         }
         width = f * 2 < 2 ? 2 : (f * 2 < NPRED ? f * 2 : NPRED);
         if (pos >= L) break;
-        bool wf = false;
-        uint64_t sf = 0;
-        const uint32_t uf = f >> 6, lf = f & 63u;
-#pragma unroll
-        for (int u = 0; u < SCAN_U; ++u) {
-            const bool w = __shfl((int)whole[u], (int)lf) != 0;
-            const uint64_t sz = __shfl((uint64_t)h[u].hlen + h[u].length, (int)lf);
-            if ((uint32_t)u == uf) {
-                wf = w;
-                sf = sz;
-            }
-        }
         if (!wf) break;
         stride = sf;
     }

@@ -623,3 +623,25 @@ def test_sieve_pipelined_same_buffer(eng, sieve_low):
     for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
         assert np.array_equal(frames[f], exp_recs[f]), f
     assert _last_sieve(eng)[0] == 1
+
+
+def test_sieve_pipeline_host_inclusive(eng, sieve_low):
+    """hvws_pipeline over mixed traffic with every chunk sieved: frames straddle
+    the 2 MiB chunks, each chunk's scan starts from the carried state."""
+    plan = synth.mixed_plan(12 << 20, 97, hi=1 << 18)
+    host = H.synth_cpu(plan)
+    _, _, _, exp = _oracle_batch(host, [(0, plan.total)], None)
+    L = libhv_amd.lib()
+    pinned = L.hvws_host_alloc(eng.ctx, plan.total)
+    try:
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * plan.total).from_address(pinned))
+        arr[:] = host
+        carry = libhv_amd.WsParser()
+        L.websocket_parser_init(ctypes.byref(carry))
+        rc = L.hvws_pipeline(eng.ctx, pinned, plan.total, 2 << 20, ctypes.byref(carry))
+        assert rc == 0, L.hvws_last_error()
+        assert np.array_equal(arr, exp)
+        assert carry.state == 0
+        assert _last_sieve(eng)[0] == 1
+    finally:
+        L.hvws_host_free(eng.ctx, pinned)
