@@ -177,14 +177,19 @@ uint64_t hvws_set_sieve_min(uint64_t bytes);
  * chain; out[3] = segment offset where the exact walk resumed. */
 int hvws_last_sieve(hvws_ctx* ctx, uint64_t out[4]);
 
-/* Speculative frame table for large multi-segment batches: when the last
- * batch's per-segment record counts matched the uniform-stride estimates,
- * the next scan emits straight into the table at the estimated offsets and
- * the device checks it (one walk, no host round trip before EMIT); a failed
- * check re-scans exactly.  mode -1 = that automatic choice (default, or
- * $HVWS_SPEC unset), 0 = never speculate, 1 = always try first (tests).
- * Results never depend on it.  ctx NULL = the calling thread's context.
- * Returns the previous mode. */
+/* Speculative frame tables for large multi-segment batches.  SPEC: when the
+ * last batch's per-segment record counts matched the uniform-stride
+ * estimates, the next scan emits straight into the table at the estimated
+ * offsets and the device checks it (one walk, no host round trip before
+ * EMIT).  SLACK: otherwise (mixed sizes), one walk emits each segment's
+ * records into its own region of a scratch table (at most 1.5 x the last
+ * exact scan's largest segment count + 16), the device checks that every
+ * segment fit and compacts the records to the exact offsets (and whether the
+ * uniform estimates would have held: SPEC next time).  A failed check
+ * re-scans exactly (COUNT, wait, EMIT).  mode -1 = that automatic choice
+ * (default, or $HVWS_SPEC unset), 0 = never speculate, 1 = try SPEC first,
+ * 2 = try SLACK first (tests).  Results never depend on it.  ctx NULL = the
+ * calling thread's context.  Returns the previous mode. */
 int hvws_set_speculation(hvws_ctx* ctx, int mode);
 
 /* How the last hvws_scan on ctx found its frames (tests, benchmarks). */
@@ -193,7 +198,9 @@ enum {
     HVWS_PATH_COUNT_READ_EMIT = 1,  /* COUNT, wait for the count, EMIT */
     HVWS_PATH_SINGLE = 2,           /* one segment: one walk into an estimated table */
     HVWS_PATH_SPEC = 3,             /* speculative table checked exact on the device */
-    HVWS_PATH_SPEC_FAILED = 4       /* speculation rejected by the check, then COUNT/EMIT */
+    HVWS_PATH_SPEC_FAILED = 4,      /* speculation rejected by the check, then COUNT/EMIT */
+    HVWS_PATH_SLACK = 5,            /* mixed sizes: one EMIT walk into per-segment regions, compacted on the device */
+    HVWS_PATH_SLACK_FAILED = 6      /* a segment outgrew its region, then COUNT/EMIT */
 };
 int hvws_last_scan_path(hvws_ctx* ctx);
 /* Batches whose record bound (rx_len / 2 + 2 * nseg + 1) is at most

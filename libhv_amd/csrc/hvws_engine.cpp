@@ -148,9 +148,15 @@ struct hvws_ctx {
     hbuf h_status;
     uint64_t scan_seq = 0;
     bool spec_ok = false;
-    int spec_mode = -1;   // -1 auto, 0 never, 1 always try first ($HVWS_SPEC / hvws_set_speculation)
+    int spec_mode = -1;   // -1 auto, 0 never, 1 SPEC first, 2 SLACK first ($HVWS_SPEC / hvws_set_speculation)
+    // SLACK (mixed sizes, several segments): scratch table, exact bases, and
+    // the per-segment region cap from the last exact scan's largest segment
+    dbuf sl_hdr, sl_off, sl_len, sl_length, sl_key, sl_keyrot, sl_info, sl_bx;
+    uint64_t sl_cap = 0;       // records the scratch table holds
+    uint64_t slack_seg = 0;    // largest per-segment count of the last exact scan (0 = unknown)
     uint64_t fast_bound = 0;   // record bound below which COUNT -> EMIT needs no host wait; 0 = default
     int scan_path = -1;        // HVWS_PATH_* of the last scan
+    int prev_path = -1;        // ... and of the one before (set when a scan starts)
     uint64_t single_hint = 0;  // records of the last one-segment scan whose count was read
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
@@ -392,9 +398,21 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_
     }
     c->t_adjacent[c->t_cur] = after_scan;
     if (!after_scan && (e = hipEventRecord(tev[2], c->stream)) != hipSuccess) return e;
+    // Pipelined steps of mixed multi-segment batches: the unmask in pieces.
+    // The hardware dispatches a kernel queued on the second stream (the next
+    // batch's discovery) only once the unmask grid is fully launched, so its
+    // walk (~0.2 ms at c4) waited for the whole unmask; between pieces it is
+    // dispatched and overlaps.  On-device sweep: 4 pieces c4
+    // 1.73 -> 1.55 ms, but c3 21.3 -> 22.4 ms and c2 flat, so uniform batches
+    // (SPEC: a short scan) keep one launch.  $HVWS_UNMASK_PIECES overrides.
+    static const int env_pieces = getenv("HVWS_UNMASK_PIECES") ? atoi(getenv("HVWS_UNMASK_PIECES")) : -1;
+    const int path = c->prev_path;   // the current scan's path may not be settled yet
+    const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED ||
+                       path == HVWS_PATH_COUNT_READ_EMIT || path == HVWS_PATH_SPEC_FAILED;
+    const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 4u : 1u);
     if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
                            c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(), c->T().total.as<uint64_t>(),
-                           c->stream)) != hipSuccess)
+                           c->stream, pieces)) != hipSuccess)
         return e;
     if ((e = hipEventRecord(tev[3], c->stream)) != hipSuccess) return e;
     c->t_unmask[c->t_cur] = true;
@@ -415,6 +433,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     // The other table set: the previous batch's tables stay intact while its
     // unmask may still be running (pipelined steps).
     c->cur ^= 1;
+    c->prev_path = c->scan_path;
     if (c->cs == c->stream) c->piped = false;   // a later pipelined step re-arms the set events
     if (c->cs != c->stream && c->T().free_pending) {
         HIP_OR(hipStreamWaitEvent(c->cs, c->T().free_ev, 0), HVWS_EHIP);
@@ -449,6 +468,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.status = nullptr;
     sc.seq = 0;
     sc.sieve = nullptr;
+    sc.slack = frames_of(c);
+    sc.slack_cap = 0;
+    sc.bases_x = nullptr;
+    sc.est_u = nullptr;
     dspec_status* status_d = mapped<dspec_status>(c->h_status);
     const dspec_status* status_h = c->h_status.as<dspec_status>();
     if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
@@ -606,12 +629,61 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             if (done && unmask_into && unmasked) *unmasked = true;
             tiles_done = done;
         }
+        // Mixed sizes: one EMIT walk into per-segment regions of a scratch
+        // table, checked and compacted on the device (SCAN_SLACK).  Its check
+        // also tells whether the uniform estimates held (SPEC next time).
+        const bool slack_try = !done && c->spec_mode != 0 && c->spec_mode != 1 && c->slack_seg &&
+                               (c->spec_mode == 2 || !c->spec_ok);
+        if (slack_try) {
+            const uint64_t cap_seg = c->slack_seg + c->slack_seg / 2 + 16;
+            const uint64_t want = std::min<uint64_t>((uint64_t)nseg * cap_seg, bound) + 1;
+            if (want > c->sl_cap) {
+                const uint64_t n = want + want / 4;
+                for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length})
+                    HIP_OR(b->ensure(n * 8), HVWS_ENOMEM);
+                for (dbuf* b : {&c->sl_key, &c->sl_keyrot, &c->sl_info}) HIP_OR(b->ensure(n * 4), HVWS_ENOMEM);
+                c->sl_cap = n;
+            }
+            HIP_OR(c->sl_bx.ensure((uint64_t)nseg * 16 + 16), HVWS_ENOMEM);
+            // the frame table must hold the batch: the last count, with room
+            if (c->T().frame_cap < c->ts[c->cur ^ 1].frame_cap)
+                HIP_OR(ensure_frames(c, c->ts[c->cur ^ 1].frame_cap, /*exact=*/true), HVWS_ENOMEM);
+            sc.slack.hdr_off = c->sl_hdr.as<int64_t>();
+            sc.slack.pay_off = c->sl_off.as<uint64_t>();
+            sc.slack.pay_len = c->sl_len.as<uint64_t>();
+            sc.slack.length = c->sl_length.as<uint64_t>();
+            sc.slack.key = c->sl_key.as<uint32_t>();
+            sc.slack.keyrot = c->sl_keyrot.as<uint32_t>();
+            sc.slack.info = c->sl_info.as<uint32_t>();
+            sc.slack.cap = c->sl_cap;
+            sc.slack_cap = cap_seg;
+            sc.bases_x = c->sl_bx.as<uint64_t>();
+            sc.est_u = c->sl_bx.as<uint64_t>() + nseg + 1;
+            sc.seq = ++c->scan_seq;
+            HIP_OR(pass(SCAN_SLACK), HVWS_EHIP);
+            if ((rc = tiles()) != HVWS_OK) return rc;
+            if (unmask_into) {
+                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
+            }
+            if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
+            if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            done = (flags & SPEC_OK) != 0;
+            if (done) {
+                c->slack_seg = status_h->pad2[0];
+                c->spec_ok = (flags & SPEC_MATCH) != 0;   // uniform again: the next batch tries SPEC
+                if (unmask_into && unmasked) *unmasked = true;
+            }
+            c->scan_path = done ? HVWS_PATH_SLACK : HVWS_PATH_SLACK_FAILED;
+            tiles_done = done;
+        }
         if (!done) {
             sc.seq = ++c->scan_seq;
             HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
             HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
             c->spec_ok = (flags & SPEC_MATCH) != 0;
+            c->slack_seg = status_h->pad2[0];
             HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
             HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
         }
@@ -932,7 +1004,7 @@ hvws_ctx* hvws_ctx_create(int device) {
     // so no stale copy can sit in a device cache across reuses.
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
-    if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : -1);
+    if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess ||
@@ -966,6 +1038,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         t.release();
         if (t.free_ev) hipEventDestroy(t.free_ev);
     }
+    for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length, &c->sl_key, &c->sl_keyrot, &c->sl_info, &c->sl_bx})
+        b->release();
     for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
                     &c->sv_mark, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
         b->release();
@@ -1527,7 +1601,7 @@ int hvws_set_speculation(hvws_ctx* c, int mode) {
     if (!c) c = thread_ctx();
     if (!c) return HVWS_ENODEV;
     const int old = c->spec_mode;
-    c->spec_mode = mode < 0 ? -1 : (mode > 1 ? 1 : mode);
+    c->spec_mode = mode < 0 ? -1 : (mode > 2 ? 2 : mode);
     return old;
 }
 

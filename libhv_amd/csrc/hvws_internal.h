@@ -121,6 +121,10 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     dspec_status* status;    // device-mapped pinned host
     uint64_t      seq;
     const sieve_bufs* sieve; // SINGLE / its re-EMIT: frame sieve buffers, nullptr = no sieve
+    dframes   slack;         // SLACK: scratch table
+    uint64_t  slack_cap;     // SLACK: records per segment region at most
+    uint64_t* bases_x;       // SLACK: exact bases (nseg)
+    uint64_t* est_u;         // SLACK: uniform-stride estimates (nseg), for SPEC_MATCH
 };
 
 // Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
@@ -186,7 +190,12 @@ hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* seg
 // EMIT; otherwise *total is zeroed (the tile kernels and k_unmask then do
 // nothing) and the host re-runs COUNT + EMIT.  COUNT also runs the check,
 // to tell the host whether the next batch is worth speculating on.
-enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2, SCAN_SPEC = 3 };
+// SLACK (several segments of mixed sizes): one EMIT walk into per-segment
+// regions of a scratch table (sized by each segment's record bound, capped at
+// slack_cap), then a device check that every segment fit and a compaction into
+// the frame table at the exact bases; a segment that did not fit zeroes *total
+// and the host re-scans COUNT + EMIT.
+enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2, SCAN_SPEC = 3, SCAN_SLACK = 4 };
 hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
@@ -215,7 +224,8 @@ int unmask_variant_count();
 uint64_t unmask_tile(int variant);         // bytes per workgroup tile
 const char* unmask_name(int variant);
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
-                         const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st);
+                         const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st,
+                         uint32_t pieces = 1);
 hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
                              const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
                              uint64_t tile, uint64_t rx_len, hipStream_t st);

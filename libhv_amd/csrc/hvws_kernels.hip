@@ -220,7 +220,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        uint64_t spec_min, uint64_t* __restrict__ est,
                                                        const dseg* __restrict__ src_segs,
                                                        const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
-                                                       dcarry* __restrict__ carry_w, int probe_mixed) {
+                                                       dcarry* __restrict__ carry_w, int probe_mixed,
+                                                       uint64_t slack_cap, uint64_t* __restrict__ est_u) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = SCAN_THREADS / 64;
     for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
@@ -307,7 +308,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
             }
         }
         if (lane == 0) {
-            if (est) est[s] = e;
+            // SLACK (mixed sizes): the segment's region of the slack table --
+            // its record bound, at most slack_cap records
+            if (est) est[s] = slack_cap ? min(L / 2 + 3, slack_cap) : e;
+            if (est_u) est_u[s] = e;   // SLACK: the uniform estimate, to tell whether SPEC would hold
             dmid m;
             m.st = st;
             m.pos = pos;
@@ -766,32 +770,38 @@ __global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict_
                                                      const uint64_t* __restrict__ est, uint32_t nseg,
                                                      uint64_t* __restrict__ total, uint64_t cap,
                                                      dspec_status* __restrict__ status, uint64_t seq) {
-    __shared__ uint64_t s_sum[1024 / 64];
+    __shared__ uint64_t s_sum[1024 / 64], s_max[1024 / 64];
     __shared__ uint32_t s_bad[1024 / 64];
     const uint32_t t = threadIdx.x;
-    uint64_t sum = 0;
+    uint64_t sum = 0, mx = 0;
     uint32_t bad = 0;
     for (uint32_t i = t; i < nseg; i += 1024) {
         const uint64_t c = counts[i];
         sum += c;
+        mx = c > mx ? c : mx;
         bad |= c != est[i];
     }
     for (int o = 32; o > 0; o >>= 1) {
         sum += __shfl_xor(sum, o);
+        const uint64_t m2 = __shfl_xor(mx, o);
+        mx = m2 > mx ? m2 : mx;
         bad |= __shfl_xor(bad, o);
     }
     if ((t & 63u) == 0) {
         s_sum[t >> 6] = sum;
+        s_max[t >> 6] = mx;
         s_bad[t >> 6] = bad;
     }
     __syncthreads();
     if (t == 0) {
-        uint64_t all = 0;
+        uint64_t all = 0, amax = 0;
         uint32_t any_bad = 0;
         for (int w = 0; w < 1024 / 64; ++w) {
             all += s_sum[w];
+            amax = s_max[w] > amax ? s_max[w] : amax;
             any_bad |= s_bad[w];
         }
+        status->pad2[0] = amax;   // largest segment count: sizes the next slack table
         uint32_t flags = any_bad ? 0u : SPEC_MATCH;
         if (SPEC) {
             const bool ok = !any_bad && all <= cap;
@@ -802,6 +812,97 @@ __global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict_
         status->flags = flags;
         // last: the host polls seq (fine-grained pinned memory)
         __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// ----------------------------------------------------------- SLACK table
+// Mixed-size batches of many segments: one EMIT walk writes each segment's
+// records into its own region of a scratch table (k_head sized it: the
+// segment's record bound, at most a cap from the last batch's largest
+// segment count).  k_slack_check (one block) verifies every count fits its
+// region and scans the counts into the exact bases; k_slack_compact moves
+// the records into the frame table there.  A segment that did not fit
+// zeroes the count (downstream kernels do nothing) and the host re-scans
+// COUNT, read, EMIT -- so a mixed batch is discovered with one walk and no
+// host round trip before EMIT, like SPEC for uniform ones.
+__global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict__ counts,
+                                                      const uint64_t* __restrict__ est,
+                                                      const uint64_t* __restrict__ est_u, uint32_t nseg,
+                                                      uint64_t* __restrict__ bases_x, uint64_t* __restrict__ total,
+                                                      uint64_t cap, dspec_status* __restrict__ status, uint64_t seq) {
+    __shared__ uint64_t part[1024], pmax[1024 / 64];
+    __shared__ uint32_t pbad[1024 / 64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nseg + 1023u) / 1024u;
+    const uint32_t b = t * per;
+    const uint32_t e = min(nseg, b + per);
+    uint64_t sum = 0, mx = 0;
+    uint32_t bad = 0;
+    for (uint32_t i = b; i < e; ++i) {
+        const uint64_t c = counts[i];
+        sum += c;
+        mx = c > mx ? c : mx;
+        bad |= (c > est[i] ? 1u : 0u) | (c != est_u[i] ? 2u : 0u);   // 1: region overflow, 2: not uniform
+    }
+    part[t] = sum;
+    for (int o = 32; o > 0; o >>= 1) {   // max and flags: wave reductions, then 16 partials
+        const uint64_t m2 = __shfl_xor(mx, o);
+        mx = m2 > mx ? m2 : mx;
+        bad |= __shfl_xor(bad, o);
+    }
+    if ((t & 63u) == 0) {
+        pmax[t >> 6] = mx;
+        pbad[t >> 6] = bad;
+    }
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint32_t i = b; i < e; ++i) {
+        bases_x[i] = run;
+        run += counts[i];
+    }
+    if (t == 0) {
+        uint64_t amax = 0;
+        uint32_t any_bad = 0;
+        for (uint32_t k = 0; k < 1024u / 64; ++k) {
+            amax = pmax[k] > amax ? pmax[k] : amax;
+            any_bad |= pbad[k];
+        }
+        const uint64_t all = part[1023];
+        const bool ok = !(any_bad & 1u) && all <= cap;
+        *total = ok ? all : 0;
+        status->total = all;
+        status->flags = (ok ? SPEC_OK : 0u) | ((any_bad & 2u) ? 0u : SPEC_MATCH);
+        status->pad2[0] = amax;
+        __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// One block per segment: records [bases[s], +counts[s]) of the slack table
+// to [bases_x[s], ...) of the frame table; bases[s] then holds the exact base.
+__global__ __launch_bounds__(256) void k_slack_compact(dframes src, dframes dst, const uint64_t* __restrict__ counts,
+                                                       uint64_t* __restrict__ bases,
+                                                       const uint64_t* __restrict__ bases_x,
+                                                       const uint64_t* __restrict__ total, uint32_t nseg) {
+    if (*total == 0) return;   // rejected (or empty): the host re-scans
+    for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+        const uint64_t n = counts[s], a = bases[s], b = bases_x[s];
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            dst.hdr_off[b + i] = src.hdr_off[a + i];
+            dst.pay_off[b + i] = src.pay_off[a + i];
+            dst.pay_len[b + i] = src.pay_len[a + i];
+            dst.length[b + i] = src.length[a + i];
+            dst.key[b + i] = src.key[a + i];
+            dst.keyrot[b + i] = src.keyrot[a + i];
+            dst.info[b + i] = src.info[a + i];
+        }
+        __syncthreads();   // every thread has read bases[s]
+        if (threadIdx.x == 0) bases[s] = b;
     }
 }
 
@@ -1155,16 +1256,18 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
     auto head_count = [&](uint64_t* est) {
         hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
-                           sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, (int)(pass == SCAN_SINGLE && sieve));
+                           sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, (int)(pass == SCAN_SINGLE && sieve),
+                           pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
+                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
     };
-    auto emit = [&](int emit_counts) -> hipError_t {
+    auto emit = [&](int emit_counts, dframes fr) -> hipError_t {
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
                            (uint64_t*)nullptr, (const dseg*)nullptr, (const dcarry*)nullptr, (dseg*)nullptr,
-                           (dcarry*)nullptr, 0);
+                           (dcarry*)nullptr, 0, (uint64_t)0, (uint64_t*)nullptr);
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         if (sieve) {
@@ -1181,12 +1284,12 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         hipError_t e;
         if (sieve && (e = launch_sieve(rx, rx_len, segs, sc.mid, sc.npred, *sc.sieve, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st)) != hipSuccess) return e;
-        if ((e = emit(1)) != hipSuccess) return e;
+        if ((e = emit(1, fr)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
     } else if (pass == SCAN_SPEC) {
         head_count(sc.est);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
-        if (hipError_t e = emit(1); e != hipSuccess) return e;
+        if (hipError_t e = emit(1, fr); e != hipSuccess) return e;
         hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
                            sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
@@ -1198,8 +1301,16 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         if (sc.status)
             hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
                                sc.status, sc.seq);
+    } else if (pass == SCAN_SLACK) {
+        head_count(sc.est);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
+        if (hipError_t e = emit(1, sc.slack); e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_slack_check, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.est_u, nseg, sc.bases_x, total, fr.cap,
+                           sc.status, sc.seq);
+        hipLaunchKernelGGL(k_slack_compact, dim3(nseg < 65535u ? nseg : 65535u), dim3(256), 0, st, sc.slack, fr, counts,
+                           bases, sc.bases_x, total, nseg);
     } else {
-        if (hipError_t e = emit(0); e != hipSuccess) return e;
+        if (hipError_t e = emit(0, fr); e != hipSuccess) return e;
     }
     return hipGetLastError();
 }
@@ -1311,13 +1422,21 @@ static uint64_t max_tiles_per_launch(int threads) {
 }
 
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
-                         const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st) {
+                         const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st,
+                         uint32_t pieces) {
     if (rx_len == 0) return hipSuccess;
     if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
     const uint64_t tile = unmask_tile(variant);
     const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
     const int threads = kGeoms[variant].threads;
-    const uint64_t cap = max_tiles_per_launch(threads);
+    // pieces > 1: several launches over consecutive tile ranges, so kernels
+    // queued on another stream (the next batch's discovery) are dispatched
+    // between them instead of after the whole grid.
+    uint64_t cap = max_tiles_per_launch(threads);
+    if (pieces > 1) {
+        const uint64_t per = (ntiles_all + pieces - 1) / pieces;
+        cap = per < cap ? (per ? per : 1) : cap;
+    }
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
 #define HVWS_K k_unmask

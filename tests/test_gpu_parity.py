@@ -159,9 +159,10 @@ def _oracle_batch(buf: np.ndarray, segs, carries):
 # (fast-bound threshold, speculation mode).  The default sends these small
 # batches COUNT -> EMIT with no wait; threshold 1 forces the large-batch
 # path, without speculation (COUNT, read, EMIT) and with it (speculative
-# EMIT checked on the device, exact re-scan when the check fails).
+# EMIT checked on the device, exact re-scan when the check fails): SPEC
+# (uniform estimates) and SLACK (per-segment regions, compacted).
 SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1),
-              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1)]
+              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1), ("slack", 1, 2), ("pipelined_slack", 1, 2)]
 
 
 def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, mode):
@@ -403,24 +404,29 @@ def test_speculative_table_rejected(eng):
 
 
 def test_speculation_adapts(eng):
-    """Automatic mode: a uniform batch scanned exactly teaches the context to
-    speculate on the next one; a mixed batch then fails the check once and
-    turns it off again.  Results stay exact throughout."""
+    """Automatic mode: SPEC for uniform traffic, SLACK for mixed, switching by
+    what the last batch's check saw; a SLACK region sized by a lighter batch
+    fails once and is re-sized by the exact re-scan.  Results stay exact."""
     L = libhv_amd.lib()
     rng = random.Random(5)
-    ubuf, usegs, ucarry = _cut_uniform(rng, 600, 1024, 11)
-    mplan = synth.mixed_plan(4 << 20, 19, hi=1 << 16).split(11)
+    ubuf, usegs, ucarry = _cut_uniform(rng, 300, 1024, 11)          # ~27 records per segment
+    mplan = synth.mixed_plan(4 << 20, 19, hi=1 << 14).split(11)     # >100 records per segment
     mbuf = H.synth_cpu(mplan)
     uexp = _oracle_batch(ubuf, usegs, ucarry)
     mexp = _oracle_batch(mbuf, mplan.segments, None)
+    assert max(np.bincount(np.searchsorted(np.array([o for o, _ in mplan.segments]), mexp[0]["hdr_off"].clip(0),
+                                           side="right") - 1)) > 1.5 * 28 + 16
     auto = ("auto", 1, -1)
-    seq = [(ubuf, usegs, ucarry, uexp, 1), (ubuf, usegs, ucarry, uexp, 3), (mbuf, mplan.segments, None, mexp, 4),
-           (mbuf, mplan.segments, None, mexp, 1), (ubuf, usegs, ucarry, uexp, 1), (ubuf, usegs, ucarry, uexp, 3)]
+    # reset (exact, mixed) -> ubuf: SLACK (sees uniform) -> ubuf: SPEC -> mbuf:
+    # SPEC fails, SLACK (regions sized by ubuf) fails -> mbuf: SLACK -> ubuf:
+    # SLACK (uniform again) -> ubuf: SPEC
+    seq = [(ubuf, usegs, ucarry, uexp, 5), (ubuf, usegs, ucarry, uexp, 3), (mbuf, mplan.segments, None, mexp, 6),
+           (mbuf, mplan.segments, None, mexp, 5), (ubuf, usegs, ucarry, uexp, 5), (ubuf, usegs, ucarry, uexp, 3)]
     L.hvws_set_speculation(eng.ctx, 0)   # forget what earlier tests taught the context
     _step_checked(eng, mbuf, mplan.segments, None, *mexp, ("reset", 1, 0))
-    for buf, segs, carries, exp, want in seq:
+    for i, (buf, segs, carries, exp, want) in enumerate(seq):
         path = _step_checked(eng, buf, segs, carries, *exp, auto)
-        assert path == want, (path, want)
+        assert path == want, (i, path, want)
 
 
 def test_pipelined_steps_back_to_back(eng):
@@ -645,3 +651,21 @@ def test_sieve_pipeline_host_inclusive(eng, sieve_low):
         assert _last_sieve(eng)[0] == 1
     finally:
         L.hvws_host_free(eng.ctx, pinned)
+
+
+def test_slack_table_mixed_segments(eng):
+    """Mixed sizes over many segments: one EMIT walk into per-segment regions,
+    compacted on the device (HVWS_PATH_SLACK); a later batch whose segments
+    outgrow their regions fails the check and is re-scanned exactly."""
+    L = libhv_amd.lib()
+    small = synth.mixed_plan(3 << 20, 101, lo=1000, hi=1 << 16).split(29)
+    sbuf = H.synth_cpu(small)
+    dense = synth.mixed_plan(3 << 20, 102, lo=1, hi=300).split(5)   # many more frames per segment
+    dbuf = H.synth_cpu(dense)
+    sexp = _oracle_batch(sbuf, small.segments, None)
+    dexp = _oracle_batch(dbuf, dense.segments, None)
+    L.hvws_set_speculation(eng.ctx, 0)
+    _step_checked(eng, sbuf, small.segments, None, *sexp, ("exact", 1, 0))   # learns the region size
+    assert _step_checked(eng, sbuf, small.segments, None, *sexp, ("slack", 1, 2)) == 5
+    assert _step_checked(eng, dbuf, dense.segments, None, *dexp, ("slack", 1, 2)) == 6
+    assert _step_checked(eng, dbuf, dense.segments, None, *dexp, ("slack", 1, 2)) == 5   # sized from the re-scan
