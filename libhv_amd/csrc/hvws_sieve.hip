@@ -64,51 +64,36 @@ __device__ __forceinline__ bool sieve_wanted(const dseg* segs, const dmid* mid, 
 
 __device__ __forceinline__ bool plausible(const hdr& h) { return h.viol == 0 && (h.length >> 48) == 0; }
 
-// 16 bytes at byte offset p of the LDS tile.
-__device__ __forceinline__ void lds_ld16(const uint32_t* l, uint32_t p, uint64_t& lo, uint64_t& hi) {
-    const uint32_t w = p >> 2, sh = p & 3u;
-    const uint32_t a0 = l[w], a1 = l[w + 1], a2 = l[w + 2], a3 = l[w + 3], a4 = l[w + 4];
-    const uint32_t b0 = __builtin_amdgcn_alignbyte(a1, a0, sh), b1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
-    const uint32_t b2 = __builtin_amdgcn_alignbyte(a3, a2, sh), b3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
-    lo = (uint64_t)b0 | ((uint64_t)b1 << 32);
-    hi = (uint64_t)b2 | ((uint64_t)b3 << 32);
-}
-
-// Survivor test of the candidate at absolute a (segment [sb, sb + L)): a
-// whole frame with a plausible header whose next SV_DEPTH headers are
-// plausible, or end the stream (exactly, or with a header or frame cut by
-// the segment end).  LOCAL: headers are read from the staged tile only, and
-// the answer is SV_PENDING when the chain leaves it (k_sieve_verify finishes
-// those from HBM, off the tile loop's critical path).
-enum : uint32_t { SV_NO = 0, SV_YES = 1, SV_PENDING = 2 };
-
-template <bool LOCAL>
-__device__ uint32_t survivor(const uint8_t* rx, uint64_t rx_len, const uint32_t* l, uint64_t T0, uint64_t sb,
-                             uint64_t L, uint64_t a) {
-    const uint64_t end = sb + L;
-    auto staged = [&](uint64_t x) { return x >= T0 && x - T0 + 16 <= SV_TILE + SV_HALO; };
+// Survivor test of the candidate at segment offset q (k_sieve_verify, from
+// HBM): a whole frame with a plausible header whose next SV_DEPTH headers are
+// plausible, or end the stream (exactly, or with a header or frame cut by the
+// segment end).
+__device__ bool survivor(const uint8_t* rx, uint64_t rx_len, uint64_t sb, uint64_t L, uint64_t q) {
+    const uint64_t end = sb + L, a = sb + q;
     auto load = [&](uint64_t x) {
         uint64_t lo, hi;
-        if (LOCAL) lds_ld16(l, (uint32_t)(x - T0), lo, hi);
-        else ld16(rx, rx_len, x, lo, hi);
+        ld16(rx, rx_len, x, lo, hi);
         return parse_hdr(lo, hi);
     };
     hdr h = load(a);
     const uint64_t r0 = end - a;
-    if (!plausible(h) || h.hlen > r0 || h.length > r0 - h.hlen) return SV_NO;
+    if (!plausible(h) || h.hlen > r0 || h.length > r0 - h.hlen) return false;
     uint64_t x = a + h.hlen + h.length;
 #pragma unroll 1
     for (int d = 0; d < SV_DEPTH; ++d) {
         const uint64_t r = end - x;
-        if (r < 14) return SV_YES;   // end of stream, or a header that may be cut by it
-        if (LOCAL && !staged(x)) return SV_PENDING;
+        if (r < 14) return true;   // end of stream, or a header that may be cut by it
         h = load(x);
-        if (!plausible(h)) return SV_NO;
-        if (h.length > r - h.hlen) return SV_YES;   // frame cut by the segment end
+        if (!plausible(h)) return false;
+        if (h.length > r - h.hlen) return true;   // frame cut by the segment end
         x += h.hlen + h.length;
     }
-    return SV_YES;
+    return true;
 }
+
+// Verdicts of the tile pass (quick_verdict): rejected, a survivor without a
+// doubt, or pending -- k_sieve_verify decides from HBM.
+enum : uint32_t { SV_NO = 0, SV_YES = 1, SV_PENDING = 2 };
 
 // Tile staging in two halves so the next tile's loads can be in flight while
 // the current tile is sieved: each thread loads 16-B chunks c = t, t + 256
@@ -193,9 +178,9 @@ __device__ __forceinline__ uint32_t cand_bit(const uint32_t* cb, uint32_t q) {
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* l, uint32_t p) { return (l[p >> 2] >> (8 * (p & 3u))) & 0xFFu; }
 
 // Verdict from the staged bytes and the candidate bitmap where that is
-// enough: SV_NO and SV_PENDING as survivor<true> would answer, SV_FULL when
-// survivor<true> must decide.  Every rejection is implied by survivor<true>
-// rejecting: control frames must be FIN and <= 125 bytes, lengths minimal
+// enough: SV_NO, SV_PENDING, or SV_FULL when only the full test can decide
+// (the tile pass hands those to k_sieve_verify too).  Every rejection is
+// implied by survivor() rejecting: control frames must be FIN and <= 125 bytes, lengths minimal
 // and < 2^48, and a header the chain reaches must be a candidate -- followed
 // through the bitmap for 7-bit lengths while the next header is staged.
 // A plausible 16-bit-length candidate whose next header lies beyond the
@@ -443,7 +428,7 @@ __global__ __launch_bounds__(256) void k_sieve_verify(const uint8_t* __restrict_
             continue;
         }
         const uint64_t q = e & ~(1ull << 63);
-        keep[j] = survivor<false>(rx, rx_len, nullptr, 0, sb, L, sb + q) == SV_YES;
+        keep[j] = survivor(rx, rx_len, sb, L, q);
         Spre[j] = q;
     }
 }
@@ -589,9 +574,10 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     dsieve* sv = reinterpret_cast<dsieve*>(b.state);
     hipError_t e = hipMemsetAsync(b.pool_n, 0, 8, st);
     if (e != hipSuccess) return e;
-    // $HVWS_SIEVE_MODE (timing experiments only, results then wrong): 1 lists
-    // without checks, 2 staging + candidate words, 3 loads alone; 4 = the
-    // product without the next tile's register prefetch (exact).
+    // $HVWS_SIEVE_MODE (timing experiments only): 1 lists without checks,
+    // 2 staging + candidate words, 3 loads alone -- these find no survivors,
+    // so the chain is empty and the exact walk does everything (results stay
+    // exact, only slow); 4 = without the next tile's register prefetch.
     static const int mode = getenv("HVWS_SIEVE_MODE") ? atoi(getenv("HVWS_SIEVE_MODE")) : 0;
 #define HVWS_SIEVE_COUNT(M)                                                                                     \
     hipLaunchKernelGGL(k_sieve_count<M>, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,    \
