@@ -499,14 +499,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         }
         return e;
     };
-    auto read_count = [&](uint64_t& n) -> int {
-        HIP_OR(hipMemcpyAsync(c->h_total.p, c->T().total.p, 8, hipMemcpyDeviceToHost, c->cs), HVWS_EHIP);
-        HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
-        n = *c->h_total.as<uint64_t>();
-        if (n >= 0xFFFFFFF0ull)
-            return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
-        return HVWS_OK;
-    };
     // k_spec_check's verdict for the pass just issued (after a wait on the
     // stream or for the published status): the record count and the SPEC_* flags.
     auto read_status = [&](uint64_t& n, uint32_t& flags) -> int {
@@ -576,11 +568,31 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         }
         HIP_OR(pass(SCAN_SINGLE), HVWS_EHIP);
         if (bound > c->T().frame_cap) {
-            int rc = read_count(nfr);
-            if (rc) return rc;
-            if (nfr > c->T().frame_cap) {
+            // The table was sized by an estimate.  The device checks the count
+            // against it (over capacity zeroes the count, so the tile kernels
+            // and an unmask queued behind do nothing) and publishes it; the
+            // tiles and the unmask are queued before the host waits, so the
+            // device runs on instead of idling through a host round trip.
+            int rc;
+            uint32_t flags = 0;
+            sc.seq = ++c->scan_seq;
+            HIP_OR(launch_cap_check(c->T().total.as<uint64_t>(), c->T().frame_cap, status_d, sc.seq, c->cs), HVWS_EHIP);
+            if ((rc = tiles()) != HVWS_OK) return rc;
+            if (unmask_into) {
+                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
+            }
+            if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
+            if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            if (flags & SPEC_OK) {
+                tiles_done = true;
+                if (unmask_into && unmasked) *unmasked = true;
+            } else {   // overflowed: re-emit into an exact table (the caller unmasks)
                 HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
                 HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
+                HIP_OR(launch_offsets(c->T().counts.as<uint64_t>(), c->T().bases.as<uint64_t>(), 1,
+                                      c->T().total.as<uint64_t>(), c->cs),
+                       HVWS_EHIP);
             }
             c->nfr_known = true;
             c->single_hint = nfr;

@@ -201,6 +201,8 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
+// *total > cap: *total = 0; publishes the count to status (SPEC_OK if within cap).
+hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st);
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
                              uint32_t* tile_first, uint64_t ntiles, uint64_t tile, hipStream_t st);
 // Small batches, whole path in one launch (one wave per segment): records

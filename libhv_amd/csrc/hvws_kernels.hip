@@ -906,6 +906,24 @@ __global__ __launch_bounds__(256) void k_slack_compact(dframes src, dframes dst,
     }
 }
 
+// One-segment scans whose table was sized by an estimate: over capacity
+// zeroes the count (downstream kernels then do nothing; the host re-emits);
+// the true count goes to pinned host memory with the scan's sequence number.
+__global__ void k_cap_check(uint64_t* __restrict__ total, uint64_t cap, dspec_status* __restrict__ status,
+                            uint64_t seq) {
+    const uint64_t v = *total;
+    const bool ok = v <= cap;
+    if (!ok) *total = 0;
+    status->total = v;
+    status->flags = ok ? SPEC_OK : 0u;
+    __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, st, total, cap, status, seq);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------- k_tile_index
 // tile_first[t] = first frame k with off[k] + len[k] > t*tile (t <= ntiles).
 // Two kernels: k_tile_scatter has each frame k write the tiles whose start
