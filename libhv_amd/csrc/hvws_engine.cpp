@@ -212,6 +212,7 @@ namespace {
 constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
 constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
 constexpr uint64_t kSingleMin = 1ull << 20;   // records: smallest one-stream table before its count is known
+constexpr uint64_t kSlackMaxRecords = 1ull << 26;   // SLACK scratch table at most (48 B each: 3.2 GB)
 // Small-batch path (k_small): batches up to kSmallBatch bytes whose segments
 // are each at most kSmallSegment bytes run as one launch.
 constexpr uint64_t kSmallBatch = 64ull << 20;
@@ -560,10 +561,16 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             } else {
                 HIP_OR(c->h_sv.ensure(sizeof(dsieve) + 32), HVWS_ENOMEM);
                 if (!c->sv_ev) HIP_OR(hipEventCreateWithFlags(&c->sv_ev, hipEventDisableTiming), HVWS_EHIP);
-                const int rc = ensure_sieve(c, rx_len, svb);
-                if (rc) return rc;
-                sc.sieve = &svb;
-                c->sv_ran = true;
+                if (ensure_sieve(c, rx_len, svb) == HVWS_OK) {
+                    sc.sieve = &svb;
+                    c->sv_ran = true;
+                } else {   // no room for the sieve's tables: walk instead (results are the same)
+                    (void)hipGetLastError();
+                    for (dbuf* b : {&c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_Spre, &c->sv_S,
+                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_rank, &c->sv_tmp})
+                        b->release();
+                    c->sv_ran = false;
+                }
             }
         }
         HIP_OR(pass(SCAN_SINGLE), HVWS_EHIP);
@@ -644,18 +651,26 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         // Mixed sizes: one EMIT walk into per-segment regions of a scratch
         // table, checked and compacted on the device (SCAN_SLACK).  Its check
         // also tells whether the uniform estimates held (SPEC next time).
-        const bool slack_try = !done && c->spec_mode != 0 && c->spec_mode != 1 && c->slack_seg &&
-                               (c->spec_mode == 2 || !c->spec_ok);
-        if (slack_try) {
-            const uint64_t cap_seg = c->slack_seg + c->slack_seg / 2 + 16;
-            const uint64_t want = std::min<uint64_t>((uint64_t)nseg * cap_seg, bound) + 1;
-            if (want > c->sl_cap) {
-                const uint64_t n = want + want / 4;
-                for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length})
-                    HIP_OR(b->ensure(n * 8), HVWS_ENOMEM);
-                for (dbuf* b : {&c->sl_key, &c->sl_keyrot, &c->sl_info}) HIP_OR(b->ensure(n * 4), HVWS_ENOMEM);
-                c->sl_cap = n;
+        const uint64_t cap_seg = c->slack_seg + c->slack_seg / 2 + 16;
+        const uint64_t want = std::min<uint64_t>((uint64_t)nseg * cap_seg, bound) + 1;
+        bool slack_try = !done && c->spec_mode != 0 && c->spec_mode != 1 && c->slack_seg &&
+                         (c->spec_mode == 2 || !c->spec_ok) && want <= kSlackMaxRecords;
+        if (slack_try && want > c->sl_cap) {
+            // a scratch table that cannot be had is no error: scan exactly instead
+            const uint64_t n = want + want / 4;
+            bool ok = true;
+            for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length}) ok = ok && b->ensure(n * 8) == hipSuccess;
+            for (dbuf* b : {&c->sl_key, &c->sl_keyrot, &c->sl_info}) ok = ok && b->ensure(n * 4) == hipSuccess;
+            c->sl_cap = ok ? n : 0;
+            if (!ok) {
+                (void)hipGetLastError();
+                for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length, &c->sl_key, &c->sl_keyrot,
+                                &c->sl_info})
+                    b->release();
             }
+            slack_try = ok;
+        }
+        if (slack_try) {
             HIP_OR(c->sl_bx.ensure((uint64_t)nseg * 16 + 16), HVWS_ENOMEM);
             // the frame table must hold the batch: the last count, with room
             if (c->T().frame_cap < c->ts[c->cur ^ 1].frame_cap)
