@@ -25,7 +25,12 @@ pytestmark = pytest.mark.gpu
 GOLD = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs.json")))
 
 
-def _run(eng, plan, nseg, golden=None):
+def _run(eng, plan, nseg, golden=None, sieve=None, path2=None):
+    """sieve: assert the frame sieve's chain covered every frame (one segment);
+    path2: the HVWS_PATH_* the second step must take."""
+    L = libhv_amd.lib()
+    if sieve:
+        L.hvws_set_sieve_min(0)   # default threshold; contexts forget "uniform, skip the sieve"
     plan.split(nseg)
     dp = libhv_amd.DevicePlan(eng, plan)
     rx = eng.alloc(plan.total + 64)
@@ -35,6 +40,10 @@ def _run(eng, plan, nseg, golden=None):
             assert f"{eng.digest(rx, plan.total):016x}" == golden["digest_masked"]
         eng.step(rx, plan.total, plan.segments)
         assert eng.synth(rx, plan.total, plan.seed, dp, 2) == 0      # plaintext + untouched headers
+        if sieve:
+            out = (ctypes.c_uint64 * 4)()
+            assert L.hvws_last_sieve(eng.ctx, out) == 0
+            assert out[0] == 1 and out[2] == plan.n and out[3] == plan.total, list(out)
         assert libhv_amd.lib().hvws_frame_count(eng.ctx) == plan.n
         first, cnt = eng.segment_frames(len(plan.segments))
         assert int(cnt.sum()) == plan.n
@@ -44,6 +53,8 @@ def _run(eng, plan, nseg, golden=None):
         assert all(c.state == 0 and c.require == 0 for c in carry)
         eng.step(rx, plan.total, plan.segments)
         assert eng.synth(rx, plan.total, plan.seed, dp, 1) == 0      # masked again, byte-exact
+        if path2 is not None:
+            assert L.hvws_last_scan_path(eng.ctx) == path2
     finally:
         dp.free()
         rx.free()
@@ -61,7 +72,10 @@ def test_config3_1m_x_64k(eng, nseg):
 
 @pytest.mark.parametrize("nseg", [1, 1024])
 def test_config4_mixed(eng, nseg):
-    _run(eng, synth.config_plan("c4", seed=1), nseg, GOLD["c4"])
+    """One stream: the frame sieve discovers all 74 701 frames; 1024
+    connections: the second step takes the SLACK table (one walk)."""
+    _run(eng, synth.config_plan("c4", seed=1), nseg, GOLD["c4"], sieve=nseg == 1,
+         path2=5 if nseg == 1024 else None)
 
 
 def test_config1_through_websocketparser_8k_chunks():
