@@ -161,8 +161,9 @@ struct hvws_ctx {
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
     // after each sieved scan (read as hints by the next one).
-    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_rank, sv_cnt, sv_tmp;
-    uint64_t sv_cap = 0;
+    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_rank, sv_cnt, sv_tmp;
+    uint64_t sv_cap = 0, sv_capc = 0;
+    uint64_t sv_hint_pre = 0, sv_hint_surv = 0;   // counts of the latest sieved scan read back
     hbuf h_sv;
     uint32_t sv_skip = 0;      // one-stream scans left before the sieve is tried again on uniform traffic
     bool sv_ran = false;       // the last scan launched the sieve
@@ -340,8 +341,15 @@ bool sieve_state_ready(hvws_ctx* c) { return c->sv_ran && c->sv_ev && hipEventQu
 // the sieve off (the exact walk runs) and the next one gets room.
 int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     const uint64_t* h = c->h_sv.as<uint64_t>();
-    // entries (before HBM verification) of the last sieved scan
-    const uint64_t seen = sieve_state_ready(c) ? h[sizeof(dsieve) / 8 + 3] : 0;
+    // entries before HBM verification, and survivors, of the latest sieved
+    // scan whose state has landed (pipelined steps run ahead of it)
+    if (sieve_state_ready(c)) {
+        const uint64_t pre = h[sizeof(dsieve) / 8 + 3], surv = h[sizeof(dsieve) / 8];
+        const bool counted = surv <= pre && pre <= c->sv_cap;   // else it overflowed and never counted survivors
+        c->sv_hint_pre = pre;
+        c->sv_hint_surv = counted ? surv : 0;
+    }
+    const uint64_t seen = c->sv_hint_pre, seen_s = c->sv_hint_surv;
     // Capacity from the last sieved scan's entry count when there is one (the
     // chain steps and their scans run over the whole capacity), else one
     // entry per KiB of the batch.
@@ -349,19 +357,27 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
                         : std::max<uint64_t>(1ull << 20, rx_len / 1024);
     cap = std::min<uint64_t>(cap, 0xFFFFFFF0ull);
     c->sv_cap = cap;
+    // chain arrays: from the last survivor count (the chain steps scale with it)
+    // (no usable count -- none yet, or the last scan overflowed its entries and
+    // never counted survivors -- means the full capacity)
+    const uint64_t capc = seen_s ? std::min<uint64_t>(cap, std::max<uint64_t>(1ull << 16, seen_s + seen_s / 4 + 1024))
+                                 : cap;
+    c->sv_capc = capc;
     const uint64_t ntm = sieve_tiles_max(rx_len);
     const uint64_t nmax = std::max(cap, ntm);
     HIP_OR(c->sv_state.ensure(sizeof(dsieve)), HVWS_ENOMEM);
     HIP_OR(c->sv_tcount.ensure(ntm * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_tbase.ensure(ntm * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_slot.ensure(sieve_slot_words(rx_len) * 4), HVWS_ENOMEM);
-    HIP_OR(c->sv_S.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_S.ensure(capc * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_Spre.ensure(cap * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_pool.ensure(cap * 4), HVWS_ENOMEM);
-    HIP_OR(c->sv_J0.ensure(cap * 4), HVWS_ENOMEM);
-    HIP_OR(c->sv_J1.ensure(cap * 4), HVWS_ENOMEM);
-    HIP_OR(c->sv_mark.ensure(cap * 8), HVWS_ENOMEM);
-    HIP_OR(c->sv_rank.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_keep.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_kbase.ensure(cap * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_J0.ensure(capc * 4), HVWS_ENOMEM);
+    HIP_OR(c->sv_J1.ensure(capc * 4), HVWS_ENOMEM);
+    HIP_OR(c->sv_mark.ensure(capc * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_rank.ensure(capc * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_cnt.ensure(32), HVWS_ENOMEM);
     HIP_OR(c->sv_tmp.ensure((4 * ((nmax + 1023) / 1024) + 64) * 8), HVWS_ENOMEM);
     b.state = c->sv_state.as<dsieve>();
@@ -381,6 +397,9 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     b.npath = c->sv_cnt.as<uint64_t>() + 1;
     b.tmp = c->sv_tmp.as<uint64_t>();
     b.capS = cap;
+    b.capC = capc;
+    b.keep = c->sv_keep.as<uint64_t>();
+    b.kbase = c->sv_kbase.as<uint64_t>();
     return HVWS_OK;
 }
 
@@ -552,6 +571,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             c->sv_gen = sieve_generation();
             c->sv_skip = 0;
             c->sv_ran = false;
+            c->sv_hint_pre = c->sv_hint_surv = 0;
         }
         if (rx_len >= sieve_min()) {
             if (sieve_state_ready(c) && c->h_sv.as<dsieve>()->active == 0 && c->sv_skip == 0) c->sv_skip = 15;
@@ -566,7 +586,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                     c->sv_ran = true;
                 } else {   // no room for the sieve's tables: walk instead (results are the same)
                     (void)hipGetLastError();
-                    for (dbuf* b : {&c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_Spre, &c->sv_S,
+                    for (dbuf* b : {&c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
+                                    &c->sv_Spre, &c->sv_S,
                                     &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_rank, &c->sv_tmp})
                         b->release();
                     c->sv_ran = false;
@@ -1067,7 +1088,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     }
     for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length, &c->sl_key, &c->sl_keyrot, &c->sl_info, &c->sl_bx})
         b->release();
-    for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
+    for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
+                    &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
                     &c->sv_mark, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
         b->release();
     c->h_sv.release();
@@ -1608,7 +1630,7 @@ int hvws_last_sieve(hvws_ctx* c, uint64_t out[4]) {
     HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
     const dsieve* d = c->h_sv.as<dsieve>();
     const uint64_t* n = reinterpret_cast<const uint64_t*>(c->h_sv.as<uint8_t>() + sizeof(dsieve));
-    out[0] = d->active ? (n[3] <= c->sv_cap ? 1 : 2) : 0;
+    out[0] = d->active ? (n[3] <= c->sv_cap && n[0] <= c->sv_capc ? 1 : 2) : 0;
     out[1] = d->active ? n[0] : 0;
     out[2] = d->use ? d->npath : 0;
     out[3] = d->use ? d->pend : 0;

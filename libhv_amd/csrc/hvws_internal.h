@@ -155,17 +155,20 @@ struct sieve_bufs {
     uint32_t* slot;      // first survivors of each tile      (sieve_slot_words)
     uint32_t* pool;      // survivors of tiles with more      (capS)
     uint64_t* pool_n;    // pool entries used
+    uint64_t* keep;      // 1 = survivor after HBM verification (capS)
+    uint64_t* kbase;     // exclusive scan of keep            (capS)
     uint64_t* Spre;      // survivors before HBM verification (capS)
     uint64_t* m_pre;     // entries of Spre
-    uint64_t* S;         // survivor segment offsets, sorted  (capS)
-    uint32_t* J0;        // successor / doubling tables       (capS each)
+    uint64_t* S;         // survivor segment offsets, sorted  (capC)
+    uint32_t* J0;        // successor / doubling tables       (capC each)
     uint32_t* J1;
-    uint64_t* mark;      // 1 = on the chain                  (capS)
-    uint64_t* rank;      // exclusive scan of mark            (capS)
+    uint64_t* mark;      // 1 = on the chain                  (capC)
+    uint64_t* rank;      // exclusive scan of mark            (capC)
     uint64_t* m_total;   // survivors
     uint64_t* npath;     // chain frames
     uint64_t* tmp;       // scan scratch (>= 4 * ceil(max(capS, tiles) / 1024) + 64 words)
-    uint64_t  capS;      // < 2^32
+    uint64_t  capS;      // entries before verification, < 2^32
+    uint64_t  capC;      // survivors / chain nodes, <= capS
 };
 uint64_t sieve_tiles_max(uint64_t rx_len);
 uint64_t sieve_slot_words(uint64_t rx_len);

@@ -437,11 +437,11 @@ __global__ __launch_bounds__(256) void k_sieve_compact(const uint64_t* __restric
                                                        const uint64_t* __restrict__ m_pre, uint64_t capS,
                                                        const uint64_t* __restrict__ keep,
                                                        const uint64_t* __restrict__ kbase, uint64_t* __restrict__ S,
-                                                       const dsieve* __restrict__ sv) {
+                                                       uint64_t capC, const dsieve* __restrict__ sv) {
     if (!sv->active || *m_pre > capS) return;
     const uint64_t m = *m_pre;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x)
-        if (keep[j]) S[kbase[j]] = Spre[j];
+        if (keep[j] && kbase[j] < capC) S[kbase[j]] = Spre[j];
 }
 
 __device__ __forceinline__ bool sieve_on(const dsieve* sv, const uint64_t* m_total, uint64_t capS) {
@@ -595,32 +595,36 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     const uint64_t fb = (ntm + 255) / 256;
     hipLaunchKernelGGL(k_sieve_fill, dim3((uint32_t)(fb < 8192 ? fb : 8192)), dim3(256), 0, st, segs, mid, b.tcount,
                        b.tbase, b.slot, b.pool, b.Spre, b.m_pre, b.capS, sv);
+    // Pre-verification entries use capacity capS; the survivors and the chain
+    // arrays capC (about the survivor count: the doubling rounds and the mark
+    // scan run over it).  More survivors than capC: the sieve stands down.
     const uint32_t lg = (uint32_t)((b.capS + 255) / 256 < 8192 ? (b.capS + 255) / 256 : 8192);
-    // keep flags in `mark`, their scan in `rank` (both rewritten by the chain steps below)
-    hipLaunchKernelGGL(k_sieve_verify, dim3(lg), dim3(256), 0, st, rx, rx_len, segs, b.Spre, b.m_pre, b.capS, b.mark, sv);
-    if ((e = launch_exclusive_scan(b.mark, b.rank, b.capS, b.tmp, b.m_total, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sieve_compact, dim3(lg), dim3(256), 0, st, b.Spre, b.m_pre, b.capS, b.mark, b.rank, b.S, sv);
-    hipLaunchKernelGGL(k_sieve_link, dim3(lg), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capS, b.J0,
+    const uint32_t lc = (uint32_t)((b.capC + 255) / 256 < 8192 ? (b.capC + 255) / 256 : 8192);
+    hipLaunchKernelGGL(k_sieve_verify, dim3(lg), dim3(256), 0, st, rx, rx_len, segs, b.Spre, b.m_pre, b.capS, b.keep, sv);
+    if ((e = launch_exclusive_scan(b.keep, b.kbase, b.capS, b.tmp, b.m_total, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sieve_compact, dim3(lg), dim3(256), 0, st, b.Spre, b.m_pre, b.capS, b.keep, b.kbase, b.S, b.capC,
+                       sv);
+    hipLaunchKernelGGL(k_sieve_link, dim3(lc), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capC, b.J0,
                        b.mark, sv);
     uint32_t* Jin = b.J0;
     uint32_t* Jout = b.J1;
-    const uint32_t rounds = jump_rounds(b.capS);
+    const uint32_t rounds = jump_rounds(b.capC);
     for (uint32_t r = 0; r < rounds; ++r) {
-        hipLaunchKernelGGL(k_sieve_jump, dim3(lg < 1024 ? lg : 1024), dim3(256), 0, st, Jin, Jout, b.mark, b.m_total,
-                           b.capS, sv, r);
+        hipLaunchKernelGGL(k_sieve_jump, dim3(lc < 1024 ? lc : 1024), dim3(256), 0, st, Jin, Jout, b.mark, b.m_total,
+                           b.capC, sv, r);
         uint32_t* t = Jin;
         Jin = Jout;
         Jout = t;
     }
-    e = launch_exclusive_scan(b.mark, b.rank, b.capS, b.tmp, b.npath, st);
+    e = launch_exclusive_scan(b.mark, b.rank, b.capC, b.tmp, b.npath, st);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
 hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid,
                              const sieve_bufs& b, dframes fr, uint32_t vmask, hipStream_t st) {
-    const uint32_t lg = (uint32_t)((b.capS + 255) / 256 < 8192 ? (b.capS + 255) / 256 : 8192);
-    hipLaunchKernelGGL(k_sieve_emit, dim3(lg), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capS,
+    const uint32_t lc = (uint32_t)((b.capC + 255) / 256 < 8192 ? (b.capC + 255) / 256 : 8192);
+    hipLaunchKernelGGL(k_sieve_emit, dim3(lc), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capC,
                        b.mark, b.rank, b.npath, fr, vmask, reinterpret_cast<dsieve*>(b.state));
     return hipGetLastError();
 }
