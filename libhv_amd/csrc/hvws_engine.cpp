@@ -427,8 +427,8 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_
     // (SPEC: a short scan) keep one launch.  $HVWS_UNMASK_PIECES overrides.
     static const int env_pieces = getenv("HVWS_UNMASK_PIECES") ? atoi(getenv("HVWS_UNMASK_PIECES")) : -1;
     const int path = c->prev_path;   // the current scan's path may not be settled yet
-    const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED ||
-                       path == HVWS_PATH_COUNT_READ_EMIT || path == HVWS_PATH_SPEC_FAILED;
+    const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED || path == HVWS_PATH_SPEC_FAILED ||
+                       (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 4u : 1u);
     if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
                            c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(), c->T().total.as<uint64_t>(),
