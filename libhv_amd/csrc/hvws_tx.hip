@@ -232,7 +232,7 @@ __device__ __forceinline__ void build_chunk(uint8_t* __restrict__ out, uint64_t 
     }
 }
 
-template <int U, bool SWZ, bool NT>
+template <int U, bool SWZ, bool NT, bool SF>
 __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64_t out_len,
                                                const uint8_t* __restrict__ pay, uint64_t plen,
                                                const uint64_t* __restrict__ pay_off,
@@ -247,7 +247,11 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
     const uint64_t k_lo = tile_first[t];
-    if (k_lo < n && base + TILE <= out_len) {
+    // SF: both ends of the tile's frame range load together, and a tile that
+    // more than one frame touches goes straight to staging (no dependent
+    // load of its first frame's record to find out it is not one payload).
+    const uint64_t k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
+    if (k_lo < n && base + TILE <= out_len && (!SF || k_hi == k_lo + 1)) {
         const uint32_t fl = flags[k_lo];
         const uint64_t ln = len[k_lo];
         const uint64_t ps = out_off[k_lo] + tx_hdr_len(fl, ln);
@@ -290,7 +294,6 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
             return;
         }
     }
-    const uint64_t k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
     if (nf && nf <= BUILD_MAXF && base + TILE <= out_len) {
         // Boundary tile: the tile's frames staged in LDS; chunks inside one
@@ -415,31 +418,35 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 }
 
 // Build geometries: X(index, chunks per thread, XCD order, nontemporal
-// realigning loads); 0 is the default.  On-device sweep (profiles/,
-// DESIGN.md): 256 x 2 linear reaches the copy ceiling; larger tiles lose
-// occupancy to the boundary-tile registers, and the XCD-contiguous order that
-// helps the in-place unmask halves this out-of-place stream.
-#define HVWS_BUILD_GEOMS(X) \
-    X(0, 2, false, false)   \
-    X(1, 4, false, false)   \
-    X(2, 1, false, false)   \
-    X(3, 2, true, false)    \
-    X(4, 2, false, true)    \
-    X(5, 8, false, false)
+// realigning loads, stage-first); 0 is the default.  On-device sweeps
+// (profiles/): 256 x 2 linear reaches the copy ceiling; larger
+// tiles lose occupancy to the boundary-tile registers, and the XCD-contiguous
+// order that helps the in-place unmask halves this out-of-place stream.
+// Stage-first (index 0 vs 6, profiles/r1an_raw): c2 0.64 -> 0.60 ms, c3
+// 20.93 -> 20.50 ms.
+#define HVWS_BUILD_GEOMS(X)       \
+    X(0, 2, false, false, true)   \
+    X(1, 4, false, false, false)  \
+    X(2, 1, false, false, false)  \
+    X(3, 2, true, false, false)   \
+    X(4, 2, false, true, false)   \
+    X(5, 8, false, false, false)  \
+    X(6, 2, false, false, false)  \
+    X(7, 4, false, false, true)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 6) ? x : 0;
+        return (x >= 0 && x < 8) ? x : 0;
     }();
     return v;
 }
 uint64_t build_tile(int v) {
     switch (v) {
-#define X(I, U, S, N) \
-    case I:           \
+#define X(I, U, S, N, F) \
+    case I:              \
         return 256ull * U * 16u;
         HVWS_BUILD_GEOMS(X)
 #undef X
@@ -450,9 +457,9 @@ uint64_t build_tile(int v) {
 
 const char* build_kernel_name() {
     switch (build_variant()) {
-#define X(I, U, S, N) \
-    case I:           \
-        return "k_build<" #U "," #S "," #N ">";
+#define X(I, U, S, N, F) \
+    case I:              \
+        return "k_build<" #U "," #S "," #N "," #F ">";
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
@@ -472,9 +479,9 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
         const uint64_t nt = min(per_launch, ntiles - t0);
         switch (v) {
-#define X(I, U, S, N)                                                                                          \
+#define X(I, U, S, N, F)                                                                                       \
     case I:                                                                                                    \
-        hipLaunchKernelGGL((k_build<U, S, N>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off, \
+        hipLaunchKernelGGL((k_build<U, S, N, F>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off, \
                            len, flags, mask, out_off, size, tile_first, n, t0, nt);                            \
         break;
             HVWS_BUILD_GEOMS(X)
