@@ -1005,8 +1005,14 @@ __global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_
     if (t > ntiles) return;
     const uint64_t nfr = *nfr_p;
     const uint64_t x = t * tile;
+    // tile_first[t] is not cleared between batches: k_tile_scatter writes
+    // every tile whose start lies before the last frame's end, except the
+    // tiles of very long frames.  An entry is taken only if it is this
+    // batch's answer (the first frame ending after x); anything else -- a
+    // stale or never-written entry -- is searched for.
     uint32_t k = tile_first[t];
-    if (k == TILE_MARK) {
+    const bool valid = k < nfr && off[k] + len[k] > x && (k == 0 || off[k - 1] + len[k - 1] <= x);
+    if (!valid) {
         uint64_t lo = 0, hi = nfr;
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
@@ -1354,9 +1360,7 @@ hipError_t launch_unmask_tiles(const uint64_t* off, const uint64_t* len, const u
                                uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
                                uint64_t tile, uint64_t rx_len, hipStream_t st) {
     const uint64_t n = ntiles + 1;
-    // fill whole 16-B words (one fill kernel instead of an aligned body + tail)
-    hipError_t e = hipMemsetD32Async(tile_first, TILE_MARK, (n + 3) & ~3ull, st);
-    if (e != hipSuccess) return e;
+    // no fill: k_tile_fix_class checks every entry (see there)
     hipLaunchKernelGGL(k_tile_scatter, dim3(2048), dim3(256), 0, st, off, len, (uint64_t)0, nfr_dev, tile_first,
                        ntiles, tile);
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
