@@ -106,6 +106,10 @@ int   hvws_d2h(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async
 int   hvws_memset(hvws_ctx* ctx, void* dst, int v, uint64_t n);
 int   hvws_d2d(hvws_ctx* ctx, void* dst, const void* src, uint64_t n);  /* async, ctx stream */
 int   hvws_sync(hvws_ctx* ctx);
+/* Tests only: hold back work queued on the ctx stream after this call for
+ * `usec` microseconds without occupying the device (a host function on the
+ * stream), e.g. to keep an unmask waiting while the second stream runs on. */
+int   hvws_debug_stall(hvws_ctx* ctx, uint32_t usec);
 
 /* ---- the hot path, device resident ---------------------------------- */
 /* Frame discovery + header parse for every segment.  Waits for the device
@@ -176,6 +180,13 @@ uint64_t hvws_set_sieve_min(uint64_t bytes);
  * table held (walked instead); out[1] = survivors; out[2] = frames on the
  * chain; out[3] = segment offset where the exact walk resumed. */
 int hvws_last_sieve(hvws_ctx* ctx, uint64_t out[4]);
+
+/* Verify after every scan that frame ends (pay_off + pay_len) never
+ * decrease over the table -- the invariant the unmask tile index is built on
+ * -- and fail the scan with HVWS_EINVAL otherwise.  Costs one device sync
+ * per scan; for tests (process-wide; default off, or $HVWS_CHECK_TABLES=1).
+ * Returns the previous setting. */
+int hvws_set_table_checks(int on);
 
 /* Speculative frame tables for large multi-segment batches.  SPEC: when the
  * last batch's per-segment record counts matched the uniform-stride

@@ -93,6 +93,7 @@ _SIGS = {
     "hvws_d2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_memset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]),
     "hvws_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "hvws_debug_stall": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     "hvws_scan": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32],
@@ -157,6 +158,7 @@ _SIGS = {
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_spec_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_sieve_min": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "hvws_set_table_checks": (ctypes.c_int, [ctypes.c_int]),
     "hvws_last_sieve": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),

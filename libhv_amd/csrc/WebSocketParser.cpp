@@ -95,7 +95,7 @@ size_t replay_messages(WebSocketParser* wp, const char* base, uint64_t base_off,
         }
     }
     void* keep = parser->data;
-    *parser = out;
+    hvws::copy_parser(*parser, out);
     parser->data = keep;
     return len;
 }
@@ -142,7 +142,7 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
         segs[i].off = total;
         segs[i].len = len[i];
         total += len[i];
-        carry[i] = *parsers[i]->parser;
+        hvws::copy_parser(carry[i], *parsers[i]->parser);
     }
     char* stage = hvws::pinned_stage(total);
     for (int i = 0; i < n; ++i)
@@ -156,9 +156,12 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
     if ((nf > 0 && hvws_get_frames(c, frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
         hvws_get_segment_frames(c, first.data(), count.data()) != HVWS_OK)
         hvws::fatal("frame table read-back");
+    // Every segment leaves the (thread's, reusable) stage before any callback
+    // runs: an onMessage that feeds again on this thread restages it.
+    for (int i = 0; i < n; ++i)
+        if (len[i]) memcpy(const_cast<char*>(data[i]), stage + segs[i].off, len[i]);   // in place, like the reference
     for (int i = 0; i < n; ++i) {
         char* dst = const_cast<char*>(data[i]);
-        if (len[i]) memcpy(dst, stage + segs[i].off, len[i]);   // in place, like the reference
         carry[i].data = parsers[i]->parser->data;
         const size_t used =
             replay_messages(parsers[i], dst, segs[i].off, frames.data() + first[i], (size_t)count[i], carry[i], len[i]);

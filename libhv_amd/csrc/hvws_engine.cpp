@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <vector>
@@ -201,6 +202,9 @@ struct hvws_ctx {
     int t_cur = 0;        // ring slot of the last scan
     int variant = 0;   // k_unmask geometry the tile index was built for
     bool nfr_known = false;   // else c->nfr is an upper bound, the count is on the device
+    // table invariant check (hvws_set_table_checks)
+    dbuf chk;
+    hbuf h_chk;
     // host copy of the last scan's results (readback_all)
     hbuf h_readback;
     bool hcache_valid = false;
@@ -219,6 +223,15 @@ constexpr uint64_t kSlackMaxRecords = 1ull << 26;   // SLACK scratch table at mo
 constexpr uint64_t kSmallBatch = 64ull << 20;
 constexpr uint64_t kSmallSegment = 1ull << 20;
 constexpr uint64_t kSmallHostRecords = 1ull << 20;   // records returned through pinned memory
+int g_table_checks = -1;   // -1: from $HVWS_CHECK_TABLES on first use
+bool table_checks() {
+    if (__atomic_load_n(&g_table_checks, __ATOMIC_RELAXED) < 0) {
+        const char* e = getenv("HVWS_CHECK_TABLES");
+        int want = e && atoi(e) ? 1 : 0, unset = -1;
+        __atomic_compare_exchange_n(&g_table_checks, &unset, want, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+    }
+    return __atomic_load_n(&g_table_checks, __ATOMIC_RELAXED) > 0;
+}
 }  // namespace
 
 namespace {
@@ -262,7 +275,7 @@ void to_dcarry(const websocket_parser& p, dcarry& d) {
     d.started = 0;
     // Validation state of a partial header lives in the struct's padding
     // byte after mask_offset (offset 13), invisible to the reference API.
-    d.viol = reinterpret_cast<const uint8_t*>(&p)[offsetof(websocket_parser, mask_offset) + 1];
+    d.viol = reinterpret_cast<const uint8_t*>(&p)[kViolByte];
 }
 
 void from_dcarry(const dcarry& d, websocket_parser& p) {
@@ -273,7 +286,7 @@ void from_dcarry(const dcarry& d, websocket_parser& p) {
     p.length = d.length;
     p.require = d.require;
     p.offset = d.offset;
-    reinterpret_cast<uint8_t*>(&p)[offsetof(websocket_parser, mask_offset) + 1] = (uint8_t)d.viol;
+    reinterpret_cast<uint8_t*>(&p)[kViolByte] = (uint8_t)d.viol;
 }
 
 int check_ctx(hvws_ctx* c) {
@@ -530,6 +543,17 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
         return HVWS_OK;
     };
+    // A rejected check in pipelined mode.  The speculative unmask was queued
+    // on c->stream, behind the previous batch's unmask, and reads this set's
+    // tile index and count when it runs, not when it was queued.  The exact
+    // re-scan rewrites those tables on c->cs; unordered, a still-waiting
+    // speculative unmask would see the re-scan's tiles and XOR for real, and
+    // the caller's unmask would then XOR the payloads back.  So the re-scan
+    // waits for it (the set's free event, recorded right after it).
+    auto join_rejected = [&]() -> int {
+        if (unmask_into && c->cs != c->stream) HIP_OR(hipStreamWaitEvent(c->cs, c->T().free_ev, 0), HVWS_EHIP);
+        return HVWS_OK;
+    };
     c->variant = unmask_variant();
     const uint64_t tile = unmask_tile(c->variant);
     const uint64_t ntiles = (rx_len + tile - 1) / tile;
@@ -616,6 +640,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 tiles_done = true;
                 if (unmask_into && unmasked) *unmasked = true;
             } else {   // overflowed: re-emit into an exact table (the caller unmasks)
+                if ((rc = join_rejected()) != HVWS_OK) return rc;
                 HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
                 HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
                 HIP_OR(launch_offsets(c->T().counts.as<uint64_t>(), c->T().bases.as<uint64_t>(), 1,
@@ -667,6 +692,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             c->spec_ok = done;
             c->scan_path = done ? HVWS_PATH_SPEC : HVWS_PATH_SPEC_FAILED;
             if (done && unmask_into && unmasked) *unmasked = true;
+            if (!done && (rc = join_rejected()) != HVWS_OK) return rc;
             tiles_done = done;
         }
         // Mixed sizes: one EMIT walk into per-segment regions of a scratch
@@ -721,6 +747,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 c->slack_seg = status_h->pad2[0];
                 c->spec_ok = (flags & SPEC_MATCH) != 0;   // uniform again: the next batch tries SPEC
                 if (unmask_into && unmasked) *unmasked = true;
+            } else if ((rc = join_rejected()) != HVWS_OK) {
+                return rc;
             }
             c->scan_path = done ? HVWS_PATH_SLACK : HVWS_PATH_SLACK_FAILED;
             tiles_done = done;
@@ -742,6 +770,19 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         if (rc) return rc;
     }
     if (!(unmasked && *unmasked)) HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+    if (table_checks()) {   // the tile index's invariant (k_ends_check), tests only: one sync
+        HIP_OR(c->chk.ensure(8), HVWS_ENOMEM);
+        HIP_OR(c->h_chk.ensure(8), HVWS_ENOMEM);
+        HIP_OR(hipMemsetAsync(c->chk.p, 0, 8, c->cs), HVWS_EHIP);
+        HIP_OR(launch_ends_check(c->T().f_off.as<uint64_t>(), c->T().f_len.as<uint64_t>(), c->T().total.as<uint64_t>(),
+                                 c->chk.as<unsigned long long>(), c->cs),
+               HVWS_EHIP);
+        HIP_OR(hipMemcpyAsync(c->h_chk.p, c->chk.p, 8, hipMemcpyDeviceToHost, c->cs), HVWS_EHIP);
+        HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
+        if (const uint64_t bad = *c->h_chk.as<uint64_t>())
+            return set_err(HVWS_EINVAL, "frame table: %llu record ends before its predecessor's (scan path %d)",
+                           (unsigned long long)bad, c->scan_path);
+    }
     c->nseg = nseg;
     c->nfr = nfr;
     c->rx = d_rx;
@@ -1017,6 +1058,8 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
 thread_local int t_device = -1;
 thread_local hvws_ctx* t_ctx = nullptr;
 
+void stall_fn(void* usec) { usleep((useconds_t)(uintptr_t)usec); }
+
 }  // namespace
 
 // ===================================================================== C ABI
@@ -1104,6 +1147,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     c->h_segs.release();
     for (hbuf& b : c->h_up) b.release();
     c->h_total.release();
+    c->chk.release();
+    c->h_chk.release();
     for (auto& ev : c->ev)
         if (ev) hipEventDestroy(ev);
     for (auto& row : c->tev)
@@ -1191,6 +1236,13 @@ int hvws_sync(hvws_ctx* c) {
     if (rc) return rc;
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->sstream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_debug_stall(hvws_ctx* c, uint32_t usec) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    HIP_OR(hipLaunchHostFunc(c->stream, stall_fn, (void*)(uintptr_t)usec), HVWS_EHIP);
     return HVWS_OK;
 }
 
@@ -1621,6 +1673,12 @@ uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
 
 uint64_t hvws_set_sieve_min(uint64_t bytes) { return set_sieve_min(bytes); }
 
+int hvws_set_table_checks(int on) {
+    const int prev = table_checks() ? 1 : 0;
+    __atomic_store_n(&g_table_checks, on ? 1 : 0, __ATOMIC_RELAXED);
+    return prev;
+}
+
 int hvws_last_sieve(hvws_ctx* c, uint64_t out[4]) {
     if (!c) c = thread_ctx();
     if (!c || !out) return set_err(HVWS_EINVAL, "hvws_last_sieve: NULL argument");
@@ -1727,14 +1785,15 @@ void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask,
               websocket_parser& carry_out, int& started) {
     hvws_ctx* c = thread_ctx();
     hvws_segment seg = {0, (uint64_t)len};
-    websocket_parser cin = carry;
+    websocket_parser cin;
+    copy_parser(cin, carry);
     if (hvws_rx_batch(c, (uint8_t*)buf, len, &seg, &cin, 1, unmask ? 1 : 0) != HVWS_OK) fatal("hvws_rx_batch");
     const int64_t n = hvws_frame_count(c);
     frames.resize((size_t)n);
     if (n > 0 && hvws_get_frames(c, frames.data(), 0, (uint64_t)n) != HVWS_OK) fatal("hvws_get_frames");
     int st = 0;
     if (hvws_get_carry(c, nullptr, &st) != HVWS_OK) fatal("hvws_get_carry");
-    carry_out = cin;
+    copy_parser(carry_out, cin);
     started = st;
 }
 

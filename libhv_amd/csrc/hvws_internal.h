@@ -2,9 +2,21 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
+#include <string.h>
+
+#include "websocket_parser.h"
 
 namespace hvws {
+
+// With validation on, the state of a header split across reads lives in the
+// padding byte after websocket_parser.mask_offset (the reference never reads
+// it).  Copies of the struct inside the library go through memcpy: a struct
+// assignment may copy member by member and drop the padding.
+constexpr size_t kViolByte = offsetof(websocket_parser, mask_offset) + 1;
+static_assert(offsetof(websocket_parser, length) > kViolByte, "validation byte must be padding");
+inline void copy_parser(websocket_parser& dst, const websocket_parser& src) { memcpy(&dst, &src, sizeof dst); }
 
 // Parser states (reference enum at http/websocket_parser.c:34-40).
 enum : uint32_t { S_START = 0, S_HEAD = 1, S_LENGTH = 2, S_MASK = 3, S_BODY = 4 };
@@ -206,6 +218,8 @@ hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg
                           hipStream_t st);
 // *total > cap: *total = 0; publishes the count to status (SPEC_OK if within cap).
 hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st);
+hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uint64_t* nfr_dev,
+                             unsigned long long* bad, hipStream_t st);
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
                              uint32_t* tile_first, uint64_t ntiles, uint64_t tile, hipStream_t st);
 // Small batches, whole path in one launch (one wave per segment): records

@@ -924,6 +924,32 @@ hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status,
     return hipGetLastError();
 }
 
+// Table invariant the tile index stands on: frame ends off[k] + len[k] are
+// non-decreasing over the whole table.  Every producer keeps it by
+// construction -- a segment's records are written in stream order, each
+// inside its own segment (a carried-in frame's record first, at the segment
+// start), segments are sorted and disjoint and their record bases come from
+// an exclusive scan in segment order (EMIT, SPEC, SLACK's compaction, the
+// sieve's ranked chain).  k_tile_scatter then has one writer per tile, and
+// k_tile_fix_class's two-load validity test and its binary search are exact.
+// k_ends_check verifies it (hvws_set_table_checks, tests): bad[0] counts the
+// records whose end lies before their predecessor's.
+__global__ void k_ends_check(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                             const uint64_t* __restrict__ nfr_p, unsigned long long* __restrict__ bad) {
+    const uint64_t nfr = *nfr_p;
+    unsigned long long n = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; k < nfr;
+         k += (uint64_t)gridDim.x * blockDim.x)
+        n += off[k - 1] + len[k - 1] > off[k] + len[k];
+    if (n) atomicAdd(bad, n);
+}
+
+hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uint64_t* nfr_dev,
+                             unsigned long long* bad, hipStream_t st) {
+    hipLaunchKernelGGL(k_ends_check, dim3(1024), dim3(256), 0, st, off, len, nfr_dev, bad);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------- k_tile_index
 // tile_first[t] = first frame k with off[k] + len[k] > t*tile (t <= ntiles).
 // Two kernels: k_tile_scatter has each frame k write the tiles whose start

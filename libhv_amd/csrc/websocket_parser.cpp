@@ -124,8 +124,7 @@ size_t websocket_parser_execute(websocket_parser* parser, const websocket_parser
     p->offset = out.offset;
     p->data = keep;
     // partial-header validation state (padding byte after mask_offset; see hvws_set_validation)
-    reinterpret_cast<uint8_t*>(p)[offsetof(websocket_parser, mask_offset) + 1] =
-        reinterpret_cast<const uint8_t*>(&out)[offsetof(websocket_parser, mask_offset) + 1];
+    reinterpret_cast<uint8_t*>(p)[kViolByte] = reinterpret_cast<const uint8_t*>(&out)[kViolByte];
     if (out.state != S_START && started && !pending_has_record) p->mask_offset = 0;
     else p->mask_offset = mo;
     return len;

@@ -138,3 +138,45 @@ def test_feed_many_config1_event_loop():
     _loop(random.Random(4), conns)
     _check(conns)
     assert sum(len(c.sink.msgs) for c in conns) == 1000
+
+
+def test_feed_many_reentrant_callback():
+    """An onMessage that feeds another connection on the same loop thread
+    (which restages, and here regrows, the thread's pinned stage) while the
+    outer batch is still being replayed: every connection, the inner one
+    included, must still see exactly the reference's results."""
+    L = libhv_amd.lib()
+    rng = random.Random(21)
+    conns = []
+    for _ in range(8):
+        data = S.rand_stream(rng, rng.randint(4, 10), max_len=2000)
+        conns.append(Conn(data, [len(data)]))
+    inner_data = S.rand_stream(rng, 30, max_len=70000)   # larger than the outer batch
+    inner = Conn(inner_data, [len(inner_data)])
+    fired = []
+
+    def on0(user, op, data, n):
+        conns[0].sink._on(user, op, data, n)
+        if not fired:
+            fired.append(1)
+            hs = (ctypes.c_void_p * 1)(inner.h)
+            ds = (ctypes.c_void_p * 1)(ctypes.addressof(inner.buf))
+            ls = (ctypes.c_size_t * 1)(len(inner.data))
+            rets = (ctypes.c_int * 1)()
+            assert L.hvws_wsp_feed_many(hs, ds, ls, 1, rets) == 1
+            inner.rets.append(rets[0])
+            inner.chunks = []
+
+    conns[0].cb = libhv_amd.MSG_CB(on0)
+    L.hvws_wsp_set_sink(conns[0].h, conns[0].cb, None)
+    # every connection ready in the same poll iteration, connection 0 first
+    n = len(conns)
+    hs = (ctypes.c_void_p * n)(*[c.h for c in conns])
+    ds = (ctypes.c_void_p * n)(*[ctypes.addressof(c.buf) for c in conns])
+    ls = (ctypes.c_size_t * n)(*[len(c.data) for c in conns])
+    rets = (ctypes.c_int * n)()
+    assert L.hvws_wsp_feed_many(hs, ds, ls, n, rets) == n
+    for i, c in enumerate(conns):
+        c.rets.append(rets[i])
+    assert fired, "connection 0 delivered no message"
+    _check(conns + [inner])

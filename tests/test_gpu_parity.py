@@ -479,6 +479,96 @@ def test_pipelined_steps_back_to_back(eng):
             assert cout[k].fields() == exp_carry[k].fields(), k
 
 
+def _piped_after_stall(eng, learn, target, spec_learn, spec_target, bound=1, stall_us=150_000):
+    """Pipelined step of `learn`, then a host stall on the context stream (a
+    stand-in for a long previous unmask: everything queued there after it
+    waits), then a pipelined step of `target` whose check is rejected.
+    The pair runs twice and the second is checked: the first sizes the
+    target's table set, so the re-scan reallocates nothing (a reallocation's
+    hipFree would synchronise the device and hide the race).
+    Returns (target bytes after its step, target frames, target's path)."""
+    L = libhv_amd.lib()
+    old_b = L.hvws_set_fast_bound(eng.ctx, bound)
+    try:
+        lbuf, lsegs = learn
+        tbuf, tsegs = target
+        for rep in range(2):
+            L.hvws_set_speculation(eng.ctx, spec_learn)
+            dl, dt = eng.to_device(lbuf), eng.to_device(tbuf)
+            eng.step_resident(dl, len(lbuf), lsegs, None)
+            L.hvws_set_speculation(eng.ctx, spec_target)
+            if rep:
+                libhv_amd._check(L.hvws_debug_stall(eng.ctx, stall_us), "hvws_debug_stall")
+            eng.step_resident(dt, len(tbuf), tsegs, None)
+            path = L.hvws_last_scan_path(eng.ctx)
+            eng.sync()
+            got = dt.download(len(tbuf))
+            frames = eng.frames()
+            dl.free()
+            dt.free()
+    finally:
+        L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
+        L.hvws_set_speculation(eng.ctx, -1)
+    return got, frames, path
+
+
+def test_pipelined_rejected_check_waits_for_queued_unmask():
+    """A pipelined step whose speculative check is rejected (SPEC, SLACK, or a
+    one-stream table that overflowed its estimate) has already queued its
+    speculative unmask on the context stream, behind the previous batch's
+    unmask.  The exact re-scan runs on the second stream and rewrites the same
+    tile index: it must wait for that unmask, or the unmask (running late)
+    sees the new tiles and XORs for real and the caller's unmask XORs the
+    payloads back.  A host stall on the context stream holds the queued unmask
+    back for 150 ms so the window is certain to be open."""
+    rng = random.Random(606)
+    lplan = synth.uniform_plan(600, 1024, 608).split(9)   # uniform traffic first
+    lbuf = H.synth_cpu(lplan)
+    mplan = synth.mixed_plan(4 << 20, 607, hi=1 << 15).split(9)
+    mbuf = H.synth_cpu(mplan)
+    mexp_recs, _, _, mexp = _oracle_batch(mbuf, mplan.segments, None)
+
+    def check(got, frames, path, want_path, exp, exp_recs):
+        assert path == want_path, path
+        assert np.array_equal(got, exp)
+        assert len(frames) == len(exp_recs)
+        for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
+            assert np.array_equal(frames[f], exp_recs[f]), f
+
+    # SPEC rejected (mixed target after uniform traffic, SPEC forced)
+    with libhv_amd.Engine(0) as fresh:
+        got, frames, path = _piped_after_stall(fresh, (lbuf, lplan.segments), (mbuf, mplan.segments), 1, 1)
+        check(got, frames, path, 4, mexp, mexp_recs)   # HVWS_PATH_SPEC_FAILED
+
+    # SLACK rejected: regions sized by a light batch, a dense one outgrows them
+    small = synth.mixed_plan(3 << 20, 609, lo=1000, hi=1 << 16).split(29)
+    sbuf = H.synth_cpu(small)
+    dense = synth.mixed_plan(3 << 20, 610, lo=1, hi=300).split(5)
+    dbuf = H.synth_cpu(dense)
+    drecs, _, _, dexp = _oracle_batch(dbuf, dense.segments, None)
+    with libhv_amd.Engine(0) as fresh:
+        got, frames, path = _piped_after_stall(fresh, (sbuf, small.segments), (dbuf, dense.segments), 0, 2)
+        check(got, frames, path, 6, dexp, drecs)       # HVWS_PATH_SLACK_FAILED
+
+    # one stream whose table overflowed the first estimate (2^20 records)
+    k = b"\x11\x22\x33\x44"
+    frames_in = []
+    for _ in range(1_100_000):
+        if rng.random() < 0.8:
+            frames_in.append((0x2 | 0x10, b"", None))
+        else:
+            frames_in.append((0x1 | 0x10 | 0x20, rng.randbytes(rng.randint(1, 9)), k))
+    obuf = np.frombuffer(H.build_frames_ref(frames_in), np.uint8).copy()
+    orecs, _, _, oexp = _oracle_batch(obuf, [(0, len(obuf))], None)
+    # learn: one stream of 64 KiB frames whose record bound exceeds the table
+    # guess, so its count is read and the next guess is back to 2^20
+    splan = synth.uniform_plan(64, 65536, 611)
+    sl = H.synth_cpu(splan)
+    with libhv_amd.Engine(0) as fresh:
+        got, frames, path = _piped_after_stall(fresh, (sl, [(0, len(sl))]), (obuf, [(0, len(obuf))]), -1, -1)
+        check(got, frames, path, 2, oexp, orecs)       # HVWS_PATH_SINGLE (re-emitted)
+
+
 def test_single_segment_table_overflow():
     """One segment with more records than the first one-stream table guess
     (2^20): the pass overflows, the count is read, the segment is re-emitted
@@ -669,3 +759,35 @@ def test_slack_table_mixed_segments(eng):
     assert _step_checked(eng, sbuf, small.segments, None, *sexp, ("slack", 1, 2)) == 5
     assert _step_checked(eng, dbuf, dense.segments, None, *dexp, ("slack", 1, 2)) == 6
     assert _step_checked(eng, dbuf, dense.segments, None, *dexp, ("slack", 1, 2)) == 5   # sized from the re-scan
+
+
+def test_slack_carried_partial_frames_ends_monotone(eng):
+    """SLACK over segments that each continue a frame carried in from an
+    earlier batch (cut inside headers and payloads) and end inside one: the
+    compacted table must equal the oracle's and its frame ends must never
+    decrease -- the invariant k_tile_scatter / k_tile_fix_class rely on
+    (every scan of the session also runs k_ends_check, conftest.py)."""
+    L = libhv_amd.lib()
+    assert L.hvws_set_table_checks(1) == 1
+    rng = random.Random(707)
+    parts, segs, carries = [], [], []
+    at = 0
+    for _ in range(23):
+        data = S.rand_stream(rng, rng.randint(20, 60), max_len=rng.choice([300, 5000, 70000]))
+        a = rng.randint(1, len(data) // 3)
+        b = rng.randint(2 * len(data) // 3, len(data) - 1)
+        _, st, _, _ = H.scan_segment(data[:a])
+        parts.append(data[a:b])
+        segs.append((at, b - a))
+        carries.append(st)
+        at += b - a
+    buf = np.frombuffer(b"".join(parts), np.uint8).copy()
+    exp = _oracle_batch(buf, segs, carries)
+    L.hvws_set_speculation(eng.ctx, 0)
+    _step_checked(eng, buf, segs, carries, *exp, ("exact", 1, 0))          # learns the region size
+    for mode in (("slack", 1, 2), ("pipelined_slack", 1, 2)):
+        assert _step_checked(eng, buf, segs, carries, *exp, mode) == 5, mode   # HVWS_PATH_SLACK
+        f = eng.frames()
+        ends = f["pay_off"] + f["pay_len"]
+        assert np.all(ends[1:] >= ends[:-1])
+    L.hvws_set_speculation(eng.ctx, -1)
