@@ -1096,10 +1096,18 @@ hvws_ctx* hvws_ctx_create(int device) {
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
+    // The pipelined scan stream at the highest priority: a scan kernel of
+    // ~1000 workgroups queued while an unmask grid is being dispatched waits
+    // for that whole grid at normal priority, but is dispatched beside it at
+    // high priority (scripts/dispatch_probe.hip).  $HVWS_SCAN_PRIORITY=0: normal.
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    const char* sp_env = getenv("HVWS_SCAN_PRIORITY");
+    const int scan_prio = sp_env && atoi(sp_env) == 0 ? prio_least : prio_greatest;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithPriority(&c->sstream, hipStreamNonBlocking, scan_prio) != hipSuccess) {
         set_err(HVWS_EHIP, "stream creation failed");
         hvws_ctx_destroy(c);
         return nullptr;

@@ -1027,9 +1027,9 @@ __global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_
                                  const uint32_t* __restrict__ keyrot, const uint64_t* __restrict__ nfr_p,
                                  uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
                                  uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile, uint64_t rx_len) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
     const uint64_t nfr = *nfr_p;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
+         t += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t x = t * tile;
     // tile_first[t] is not cleared between batches: k_tile_scatter writes
     // every tile whose start lies before the last frame's end, except the
@@ -1048,7 +1048,7 @@ __global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_
         k = (uint32_t)lo;
         tile_first[t] = k;
     }
-    if (t == ntiles) return;   // sentinel entry: index only
+    if (t == ntiles) continue;   // sentinel entry: index only
     const uint64_t xe = x + tile < rx_len ? x + tile : rx_len;
     uint32_t kind = TILE_GENERAL, key = 0;
     if (k >= nfr || off[k] >= xe) {
@@ -1059,6 +1059,7 @@ __global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_
     }
     tile_key[t] = key;
     tile_kind[t] = (uint8_t)kind;
+    }
 }
 
 // -------------------------------------------------------------- k_unmask
@@ -1389,7 +1390,8 @@ hipError_t launch_unmask_tiles(const uint64_t* off, const uint64_t* len, const u
     // no fill: k_tile_fix_class checks every entry (see there)
     hipLaunchKernelGGL(k_tile_scatter, dim3(2048), dim3(256), 0, st, off, len, (uint64_t)0, nfr_dev, tile_first,
                        ntiles, tile);
-    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    const uint64_t nb = (n + 255) / 256;
+    const uint32_t blocks = nb > 65536u ? 65536u : (uint32_t)nb;
     hipLaunchKernelGGL(k_tile_fix_class, dim3(blocks), dim3(256), 0, st, off, len, keyrot, nfr_dev, tile_first,
                        tile_key, tile_kind, ntiles, tile, rx_len);
     return hipGetLastError();
