@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--sweep-unmask", action="store_true",
                     help="rank 0: time every k_unmask geometry on the same batch (design record)")
     ap.add_argument("--no-tx", action="store_true", help="skip the transmit-side (hvws_build_frames) measurement")
+    ap.add_argument("--validate", action="store_true",
+                    help="RFC 6455 header validation on (hvws_set_validation, all classes; off = reference behaviour)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
     return ap.parse_args()
@@ -252,6 +254,8 @@ def main():
     # previous step's unmask; every step still scans and unmasks the whole
     # batch (the same buffer: headers are never modified, payloads toggle).
     step = eng.step if args.serial else eng.step_resident
+    if args.validate:
+        libhv_amd.lib().hvws_set_validation(eng.ctx, 0x3F)   # HVWS_V_ALL
     for _ in range(args.warmup):
         step(rx, plan.total, segs)
     barrier()
@@ -314,6 +318,8 @@ def main():
         extra["stream_ceiling_GBps"] = round(ceiling, 1)
         extra["scan_ms_mean"] = round(float(np.mean(scan_ms)), 3)
         extra["step_call"] = "hvws_step" if args.serial else "hvws_step_resident (discovery overlaps the previous unmask)"
+        if args.validate:
+            extra["validation"] = "HVWS_V_ALL"
         extra["other_step_call_ms"] = round(other_ms, 3) if other_ms is not None else None
         extra["scan_path"] = {0: "count_emit", 1: "count_read_emit", 2: "single", 3: "speculative",
                               4: "speculative_rejected"}.get(scan_path, scan_path)
