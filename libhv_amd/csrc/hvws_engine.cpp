@@ -170,6 +170,10 @@ struct hvws_ctx {
     bool sv_ran = false;       // the last scan launched the sieve
     hipEvent_t sv_ev = nullptr;   // h_sv holds the last sieved scan's state once this has completed
     uint64_t sv_gen = 0;       // sieve_generation() the history below belongs to
+    // hvws_pipeline: its three device slots and their events, kept across
+    // calls (a per-call hipMalloc/hipFree pair cost the first call ~2x)
+    dbuf pipe_slot[3], pipe_segs;
+    hipEvent_t pipe_ev[9] = {};
     // staging for host-memory entry points
     dbuf stage;
     dbuf xor_stage;
@@ -1145,6 +1149,9 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         b->release();
     c->h_sv.release();
     if (c->sv_ev) hipEventDestroy(c->sv_ev);
+    for (dbuf* b : {&c->pipe_slot[0], &c->pipe_slot[1], &c->pipe_slot[2], &c->pipe_segs}) b->release();
+    for (hipEvent_t ev : c->pipe_ev)
+        if (ev) hipEventDestroy(ev);
     for (dbuf* b : {&c->segs, &c->carry_in, &c->stage, &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad,
                     &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->d_small_in, &c->d_small_slots})
         b->release();
@@ -1455,19 +1462,23 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
     chunk = (chunk + 15) & ~15ull;
     const uint64_t nchunks = (len + chunk - 1) / chunk;
     if (nchunks == 0) return HVWS_OK;
-    // Three device slots: H2D(k+1) and D2H(k-1) overlap compute(k).
-    dbuf slot[3];
-    hipEvent_t in_done[3], comp_done[3], out_done[3];
-    for (int i = 0; i < 3; ++i) {
-        HIP_OR(slot[i].ensure(chunk + 64), HVWS_ENOMEM);
-        hipEventCreateWithFlags(&in_done[i], hipEventDisableTiming);
-        hipEventCreateWithFlags(&comp_done[i], hipEventDisableTiming);
-        hipEventCreateWithFlags(&out_done[i], hipEventDisableTiming);
-    }
-    // every chunk's segment {0, n}, resident before the loop
-    dbuf pipe_segs;
-    HIP_OR(pipe_segs.ensure(nchunks * sizeof(dseg)), HVWS_ENOMEM);
+    // Three device slots: H2D(k+1) and D2H(k-1) overlap compute(k).  Slots
+    // and events live in the context (grow-only), so repeated calls pay no
+    // allocation; earlier work on the context's streams is finished first
+    // (an earlier call's copies may still use the slots).
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);   // h_segs may still feed an earlier copy
+    HIP_OR(hipStreamSynchronize(c->copy_in), HVWS_EHIP);
+    HIP_OR(hipStreamSynchronize(c->copy_out), HVWS_EHIP);
+    dbuf* slot = c->pipe_slot;
+    for (int i = 0; i < 3; ++i) HIP_OR(slot[i].ensure(chunk + 64), HVWS_ENOMEM);
+    for (hipEvent_t& ev : c->pipe_ev)
+        if (!ev) HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), HVWS_EHIP);
+    hipEvent_t* in_done = c->pipe_ev;
+    hipEvent_t* comp_done = c->pipe_ev + 3;
+    hipEvent_t* out_done = c->pipe_ev + 6;
+    // every chunk's segment {0, n}, resident before the loop
+    dbuf& pipe_segs = c->pipe_segs;
+    HIP_OR(pipe_segs.ensure(nchunks * sizeof(dseg)), HVWS_ENOMEM);
     HIP_OR(c->h_segs.ensure(nchunks * sizeof(dseg)), HVWS_ENOMEM);
     for (uint64_t k = 0; k < nchunks; ++k) c->h_segs.as<dseg>()[k] = dseg{0, std::min(chunk, len - k * chunk)};
     HIP_OR(hipMemcpyAsync(pipe_segs.p, c->h_segs.p, nchunks * sizeof(dseg), hipMemcpyHostToDevice, c->stream),
@@ -1527,15 +1538,9 @@ int hvws_pipeline(hvws_ctx* c, uint8_t* h_rx, uint64_t len, uint64_t chunk, webs
     hipStreamSynchronize(c->copy_in);
     hipStreamSynchronize(c->copy_out);
     hipStreamSynchronize(c->stream);
-    for (int i = 0; i < 3; ++i) {
-        hipEventDestroy(in_done[i]);
-        hipEventDestroy(comp_done[i]);
-        hipEventDestroy(out_done[i]);
-        slot[i].release();
-    }
-    pipe_segs.release();
     carry->data = keep;
-    // The slots are gone: forget the scan that referenced them.
+    // The last scan referenced a slot, which the next call overwrites:
+    // forget it (hvws_unmask would refuse it anyway).
     c->have_scan = false;
     if (e != hipSuccess) return set_err(HVWS_EHIP, "pipeline: %s", hipGetErrorString(e));
     return out_rc;
