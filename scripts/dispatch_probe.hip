@@ -93,13 +93,17 @@ __global__ __launch_bounds__(256) void k_big_v(uint8_t* d, uint64_t ntiles, uint
 // Persistent variant: `grid` workgroups loop over the tiles.
 __global__ __launch_bounds__(256) void k_big_persistent(u32x4* d, uint64_t ntiles, span* s) {
     stamp_begin(s);
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        u32x4* b = d + t * 1024;
+    uint8_t* db = reinterpret_cast<uint8_t*>(d);
+    for (uint64_t i = blockIdx.x; i < ntiles; i += gridDim.x) {   // gridDim a multiple of 8: XCD order kept
+        const uint64_t base = xcd_tile(i, ntiles) * 16384u;
         u32x4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(b + u * 256 + threadIdx.x);
+        for (int u = 0; u < 4; ++u)
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(db + base + ((uint64_t)u * 256 + threadIdx.x) * 16u));
 #pragma unroll
-        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u] ^ 0x5A5A5A5Au, b + u * 256 + threadIdx.x);
+        for (int u = 0; u < 4; ++u)
+            __builtin_nontemporal_store(v[u] ^ 0x5A5A5A5Au,
+                                        reinterpret_cast<u32x4*>(db + base + ((uint64_t)u * 256 + threadIdx.x) * 16u));
     }
     stamp_end(s);
 }
@@ -183,9 +187,11 @@ int main(int argc, char** argv) {
     // `chain` scan kernels on B (waits for its table set's free event), the
     // host waits for the chain's 5th kernel (the check), the big grid on A
     // waits for the chain's end event; set free event recorded after the big grid.
-    for (int variant = 0; variant < 6; ++variant) {
+    for (int variant = 0; variant < 10; ++variant) {
         const bool high = variant & 1, setwait = variant < 2 || variant >= 4;
         const bool wide = variant >= 4;   // chain kernels shaped like the engine's: 1024 x 256 threads
+        // variants 6-9: the big grid persistent, 6 or 7 workgroups per CU (wave slots left free)
+        const int pers = variant >= 8 ? 7 : (variant >= 6 ? 6 : 0);
         hipStream_t B = high ? Bh : Bn;
         const int nstep = 6, chain = 7;
         hipEvent_t scan_done[nstep], check[nstep], freev[2];
@@ -211,7 +217,10 @@ int main(int argc, char** argv) {
             }
             CK(hipEventRecord(scan_done[k], B));
             CK(hipStreamWaitEvent(A, scan_done[k], 0));
-            hipLaunchKernelGGL(k_big_t<true>, dim3(ntiles), dim3(256), 0, A, d, ntiles, bigs + k * ntiles);
+            if (pers)
+                hipLaunchKernelGGL(k_big_persistent, dim3(ncu * pers), dim3(256), 0, A, d, ntiles, bigs + k * ntiles);
+            else
+                hipLaunchKernelGGL(k_big_t<true>, dim3(ntiles), dim3(256), 0, A, d, ntiles, bigs + k * ntiles);
             CK(hipEventRecord(freev[k & 1], A));
             CK(hipEventSynchronize(check[k]));
         }
@@ -221,12 +230,14 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(bh.data(), bigs, nstep * ntiles * sizeof(span), hipMemcpyDeviceToHost));
         CK(hipFree(bigs));
         unsigned long long z = h[0].t0;
-        printf("pipeline emulation, %s prio, %s set-free wait, chain kernels %s:\n", high ? "high" : "normal",
-               setwait ? "with" : "without", wide ? "1024 x 256" : "16-64 x 64");
+        printf("pipeline emulation, %s prio, %s set-free wait, chain kernels %s, big grid %s:\n", high ? "high" : "normal",
+               setwait ? "with" : "without", wide ? "1024 x 256" : "16-64 x 64",
+               pers == 0 ? "one workgroup per tile" : (pers == 6 ? "persistent 6/CU" : "persistent 7/CU"));
         for (int k = 0; k < nstep; ++k) {
             span b{~0ull, 0ull};
-            for (uint64_t i = 0; i < ntiles; ++i) {
-                if (!(i % 512u == 0 || i + 256u >= ntiles)) continue;
+            const uint64_t gk = pers ? (uint64_t)ncu * pers : ntiles;
+            for (uint64_t i = 0; i < gk; ++i) {
+                if (!(i % 512u == 0 || i + 256u >= gk)) continue;
                 const span& x = bh[k * ntiles + i];
                 b.t0 = x.t0 < b.t0 ? x.t0 : b.t0;
                 b.t1 = x.t1 > b.t1 ? x.t1 : b.t1;
