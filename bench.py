@@ -316,7 +316,9 @@ def main():
         eng.sync()
         ceiling = 2 * (plan.total & ~15) * reps / (time.perf_counter() - t) / 1e9
         extra["stream_ceiling_GBps"] = round(ceiling, 1)
-        extra["scan_ms_mean"] = round(float(np.mean(scan_ms)), 3)
+        # pipelined steps record no scan-side timing markers (-1; include/hvws.h)
+        scan_rec = [t for t in scan_ms if t >= 0]
+        extra["scan_ms_mean"] = round(float(np.mean(scan_rec)), 3) if scan_rec else None
         extra["step_call"] = "hvws_step" if args.serial else "hvws_step_resident (discovery overlaps the previous unmask)"
         if args.validate:
             extra["validation"] = "HVWS_V_ALL"

@@ -145,7 +145,8 @@ int     hvws_get_carry(hvws_ctx* ctx, websocket_parser* out, int* started);
 
 /* Device time (ms, HIP events on the ctx stream) of the last scan and
  * unmask: out[0] = scan kernels (count + offsets + emit + tile index),
- * out[1] = unmask kernel. */
+ * out[1] = unmask kernel.  A pipelined step (hvws_step_resident) records the
+ * unmask's events only: its out[0] is -1 ($HVWS_STEP_EVENTS=2 records both). */
 int hvws_last_times(hvws_ctx* ctx, float out[2]);
 /* The same for each of the last min(max_steps, 32) scans, oldest first:
  * out[2*i] = scan ms, out[2*i+1] = unmask ms (-1 if the step had none).
@@ -202,6 +203,22 @@ int hvws_set_table_checks(int on);
  * 2 = try SLACK first (tests).  Results never depend on it.  ctx NULL = the
  * calling thread's context.  Returns the previous mode. */
 int hvws_set_speculation(hvws_ctx* ctx, int mode);
+
+/* SPEC scans as one persistent launch (k_pscan: discovery, the device check
+ * and the unmask tile index, phases separated by grid barriers) instead of a
+ * chain of ~10 kernels, so a pipelined step's discovery runs beside the
+ * previous unmask.  mode 1 = on ($HVWS_PSCAN=1), 0 = the chain (default:
+ * measured slower).  Results never depend on it.  Returns the previous mode, or the
+ * number of workgroups the last scan launched when mode is -1 (query; 0 =
+ * that scan used the chain). */
+int hvws_set_one_launch_scan(hvws_ctx* ctx, int mode);
+
+/* One-walk passes (SPEC, SLACK): mode -1 = adaptive (default: the grid-wide
+ * k_verify pair and k_head<true> run only when the last check saw a segment
+ * with >= spec_min predicted frames; otherwise k_head<false>, the offsets and
+ * one walk that also records the carried-in frame), 0 = never, 1 = always.
+ * Results never depend on it.  Returns the previous mode. */
+int hvws_set_walk_verify(hvws_ctx* ctx, int mode);
 
 /* How the last hvws_scan on ctx found its frames (tests, benchmarks). */
 enum {

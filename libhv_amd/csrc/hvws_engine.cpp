@@ -99,13 +99,14 @@ struct tset {
     dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total, sc_est;
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first, tile_key, tile_kind;
+    dbuf pbar;   // grid-barrier words of the one-launch scan (k_pscan)
     uint64_t frame_cap = 0;
     hipEvent_t free_ev = nullptr;   // recorded after the last kernel reading the set (pipelined steps)
     bool free_pending = false;
     void release() {
         for (dbuf* b : {&carry_out, &counts, &bases, &total, &sc_mid, &sc_npred, &sc_pbase, &sc_fail, &sc_masked,
                         &sc_total, &sc_est, &f_hdr, &f_off, &f_len, &f_length, &f_key, &f_keyrot, &f_info,
-                        &tile_first, &tile_key, &tile_kind})
+                        &tile_first, &tile_key, &tile_kind, &pbar})
             b->release();
         frame_cap = 0;
     }
@@ -149,7 +150,16 @@ struct hvws_ctx {
     hbuf h_status;
     uint64_t scan_seq = 0;
     bool spec_ok = false;
+    // The last check saw a segment with >= spec_min predicted frames: the
+    // next one-walk pass keeps the grid-wide k_verify pair (else head + walk).
+    bool verify_hint = true;
+    int verify_mode = -1;   // hvws_set_walk_verify: -1 adaptive (the hint), 0 never, 1 always
     int spec_mode = -1;   // -1 auto, 0 never, 1 SPEC first, 2 SLACK first ($HVWS_SPEC / hvws_set_speculation)
+    // SPEC as one persistent launch (k_pscan) of pscan_blocks workgroups;
+    // 0 = the kernel chain ($HVWS_PSCAN=0 / hvws_set_one_launch_scan)
+    uint32_t pscan_blocks = 0;
+    int pscan_mode = -1;   // -1 not yet decided
+    bool pscan_ran = false;   // the last scan used it (hvws_last_scan_path reports SPEC either way)
     // SLACK (mixed sizes, several segments): scratch table, exact bases, and
     // the per-segment region cap from the last exact scan's largest segment
     dbuf sl_hdr, sl_off, sl_len, sl_length, sl_key, sl_keyrot, sl_info, sl_bx;
@@ -202,6 +212,7 @@ struct hvws_ctx {
     hipEvent_t tev[kTimeRing][4] = {};
     bool t_unmask[kTimeRing] = {};
     bool t_adjacent[kTimeRing] = {};   // unmask started at the scan's end event
+    uint8_t t_rec[kTimeRing] = {};      // which of the slot's 4 events were recorded (bit i)
     uint64_t t_seq = 0;   // scans recorded so far
     int t_cur = 0;        // ring slot of the last scan
     int variant = 0;   // k_unmask geometry the tile index was built for
@@ -307,23 +318,53 @@ T* mapped(hbuf& b) {
     return reinterpret_cast<T*>(d);
 }
 
+// Which per-step timing events are recorded: 2 = scan begin/end and unmask
+// begin/end, 1 = the unmask's only, 0 = none.  Default: 2 for serial steps,
+// 1 for pipelined ones (hvws_step_resident) -- each timing marker is a packet
+// the command processor runs between kernels, and the scan-side pair cost a
+// pipelined c2 step ~9 us (0.465 -> 0.456 ms, profiles/r2d_raw); a pipelined
+// scan's span includes its wait for the previous unmask anyway.
+// $HVWS_STEP_EVENTS forces a mode.
+int step_events(const hvws_ctx* c) {
+    static const int v = [] {
+        const char* e = getenv("HVWS_STEP_EVENTS");
+        return e ? atoi(e) : -1;
+    }();
+    return v >= 0 ? v : (c->cs != c->stream ? 1 : 2);
+}
+
+// Record timing event i (0 scan begin, 1 scan end, 2 unmask begin, 3 unmask
+// end) of the current ring slot if this mode keeps it.
+hipError_t tev_record(hvws_ctx* c, int i, hipStream_t st) {
+    const int m = step_events(c);
+    if (m <= 0 || (m == 1 && i < 2)) return hipSuccess;
+    c->t_rec[c->t_cur] |= (uint8_t)(1u << i);
+    return hipEventRecord(c->tev[c->t_cur][i], st);
+}
+
 // Next slot of the timing ring: record the scan-begin event there.
 hipError_t begin_timed_scan(hvws_ctx* c) {
     c->t_cur = (int)(c->t_seq % hvws_ctx::kTimeRing);
     c->t_unmask[c->t_cur] = false;
+    c->t_rec[c->t_cur] = 0;
     ++c->t_seq;
-    return hipEventRecord(c->tev[c->t_cur][0], c->cs);
+    return tev_record(c, 0, c->cs);
 }
 
-// out[0] = scan ms, out[1] = unmask ms (-1: no unmask) of the step in ring `slot`.
+// out[0] = scan ms, out[1] = unmask ms (-1: no unmask, or not recorded) of
+// the step in ring `slot`.
 int step_times_at(hvws_ctx* c, int slot, float* out) {
     hipEvent_t* e = c->tev[slot];
+    const uint8_t r = c->t_rec[slot];
     out[0] = out[1] = -1.0f;
-    HIP_OR(hipEventSynchronize(e[1]), HVWS_EHIP);
-    HIP_OR(hipEventElapsedTime(&out[0], e[0], e[1]), HVWS_EHIP);
-    if (c->t_unmask[slot]) {
+    if ((r & 3u) == 3u) {
+        HIP_OR(hipEventSynchronize(e[1]), HVWS_EHIP);
+        HIP_OR(hipEventElapsedTime(&out[0], e[0], e[1]), HVWS_EHIP);
+    }
+    const int start = c->t_adjacent[slot] ? 1 : 2;
+    if (c->t_unmask[slot] && (r & (1u << start)) && (r & 8u)) {
         HIP_OR(hipEventSynchronize(e[3]), HVWS_EHIP);
-        HIP_OR(hipEventElapsedTime(&out[1], c->t_adjacent[slot] ? e[1] : e[2], e[3]), HVWS_EHIP);
+        HIP_OR(hipEventElapsedTime(&out[1], e[start], e[3]), HVWS_EHIP);
     }
     return HVWS_OK;
 }
@@ -420,12 +461,36 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     return HVWS_OK;
 }
 
+// Workgroups of the one-launch SPEC scan: 2 per CU (all resident at once
+// even beside an unmask grid that holds every other slot), or the kernel
+// chain (0) when disabled or when the occupancy query cannot vouch for it.
+uint32_t pscan_blocks(hvws_ctx* c) {
+    if (c->pscan_mode < 0) {
+        const char* e = getenv("HVWS_PSCAN");
+        c->pscan_mode = e ? (atoi(e) != 0) : 0;
+    }
+    if (!c->pscan_mode) return 0;
+    if (!c->pscan_blocks) {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
+            return 0;
+        const int per = pscan_blocks_per_cu();   // advisory; over-reports by one on ROCm 7.2 (cdna guide sec. 1)
+        if (per < 3) return 0;
+        uint32_t want = 2u * (uint32_t)ncu;
+        if (const char* b = getenv("HVWS_PSCAN_BLOCKS")) {
+            const long v = atol(b);
+            if (v > 0 && v <= 2L * ncu) want = (uint32_t)v;
+        }
+        c->pscan_blocks = want;
+    }
+    return c->pscan_blocks;
+}
+
 // Scan with the carry-in already resident in c->carry_in (device).
 // Unmask kernel launch with its timing events (no argument checks).
 // after_scan: queued right behind the scan's end event, which then doubles
 // as the unmask's start (one timing marker fewer).
 hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
-    hipEvent_t* tev = c->tev[c->t_cur];
     hipError_t e;
     const bool piped = c->cs != c->stream;
     if (piped) {   // the scan ran on the side stream: join it
@@ -433,8 +498,9 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_
         if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
     }
+    if (step_events(c) < 2) after_scan = false;   // no scan-end event to start from
     c->t_adjacent[c->t_cur] = after_scan;
-    if (!after_scan && (e = hipEventRecord(tev[2], c->stream)) != hipSuccess) return e;
+    if (!after_scan && (e = tev_record(c, 2, c->stream)) != hipSuccess) return e;
     // Pipelined steps of mixed multi-segment batches: the unmask in pieces.
     // The hardware dispatches a kernel queued on the second stream (the next
     // batch's discovery) only once the unmask grid is fully launched, so its
@@ -451,7 +517,7 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_
                            c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(), c->T().total.as<uint64_t>(),
                            c->stream, pieces)) != hipSuccess)
         return e;
-    if ((e = hipEventRecord(tev[3], c->stream)) != hipSuccess) return e;
+    if ((e = tev_record(c, 3, c->stream)) != hipSuccess) return e;
     c->t_unmask[c->t_cur] = true;
     if (piped) {   // the next pipelined scan into this set waits for this unmask
         if ((e = hipEventRecord(c->T().free_ev, c->stream)) != hipSuccess) return e;
@@ -509,6 +575,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.slack_cap = 0;
     sc.bases_x = nullptr;
     sc.est_u = nullptr;
+    sc.no_verify = 0;
     dspec_status* status_d = mapped<dspec_status>(c->h_status);
     const dspec_status* status_h = c->h_status.as<dspec_status>();
     if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
@@ -522,18 +589,20 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     c->up_src_segs = nullptr;
     c->up_src_carry = nullptr;
     bool slot_released = up_slot < 0;
+    auto release_slot = [&]() -> hipError_t {
+        if (slot_released) return hipSuccess;
+        slot_released = true;
+        const hipError_t e2 = hipEventRecord(c->up_ev[up_slot], c->cs);
+        c->up_pending[up_slot] = e2 == hipSuccess;
+        return e2;
+    };
     auto pass = [&](int which) {
         const hipError_t e = launch_scan(which, d_rx, rx_len, segs, nseg, cin, c->T().carry_out.as<dcarry>(),
                                          c->T().counts.as<uint64_t>(), c->T().bases.as<uint64_t>(), c->T().total.as<uint64_t>(), sc,
                                          frames_of(c), c->vmask, c->cs);
         sc.src_segs = nullptr;
         sc.src_carry = nullptr;
-        if (e == hipSuccess && !slot_released) {
-            slot_released = true;
-            const hipError_t e2 = hipEventRecord(c->up_ev[up_slot], c->cs);
-            c->up_pending[up_slot] = e2 == hipSuccess;
-            return e2;
-        }
+        if (e == hipSuccess) return release_slot();
         return e;
     };
     // k_spec_check's verdict for the pass just issued (after a wait on the
@@ -543,6 +612,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                                                     (unsigned long long)status_h->seq, (unsigned long long)sc.seq);
         n = status_h->total;
         flags = status_h->flags;
+        if (flags & SPEC_ERR) return set_err(HVWS_EHIP, "one-launch scan: a grid barrier timed out (seq %llu)",
+                                             (unsigned long long)sc.seq);
         if (n >= 0xFFFFFFF0ull)
             return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
         return HVWS_OK;
@@ -578,6 +649,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const uint64_t bound = rx_len / 2 + 2 * (uint64_t)nseg + 1;
     uint64_t nfr = bound;
     c->nfr_known = false;
+    c->pscan_ran = false;
     bool tiles_done = false;
     if (nseg == 1) {
         c->scan_path = HVWS_PATH_SINGLE;
@@ -635,7 +707,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             HIP_OR(launch_cap_check(c->T().total.as<uint64_t>(), c->T().frame_cap, status_d, sc.seq, c->cs), HVWS_EHIP);
             if ((rc = tiles()) != HVWS_OK) return rc;
             if (unmask_into) {
-                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+                HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
@@ -684,14 +756,46 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             if (c->T().frame_cap < c->ts[c->cur ^ 1].frame_cap)
                 HIP_OR(ensure_frames(c, c->ts[c->cur ^ 1].frame_cap, /*exact=*/true), HVWS_ENOMEM);
             sc.seq = ++c->scan_seq;
-            HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
-            if ((rc = tiles()) != HVWS_OK) return rc;
+            sc.no_verify = (c->verify_mode < 0 ? c->verify_hint : c->verify_mode != 0) ? 0u : 1u;
+            if (const uint32_t pb = pscan_blocks(c)) {
+                // one launch: SPEC pass + tile index + classes (k_pscan)
+                HIP_OR(c->T().pbar.ensure(sizeof(dpbar)), HVWS_ENOMEM);
+                pscan_args a;
+                a.rx = d_rx;
+                a.rx_len = rx_len;
+                a.segs = segs;
+                a.carry_in = cin;
+                a.carry_out = c->T().carry_out.as<dcarry>();
+                a.counts = c->T().counts.as<uint64_t>();
+                a.bases = c->T().bases.as<uint64_t>();
+                a.total = c->T().total.as<uint64_t>();
+                a.sc = sc;
+                a.fr = frames_of(c);
+                a.spec_min = spec_min();
+                a.tile_first = c->T().tile_first.as<uint32_t>();
+                a.tile_key = c->T().tile_key.as<uint32_t>();
+                a.tile_kind = c->T().tile_kind.as<uint8_t>();
+                a.ntiles = ntiles;
+                a.tile = tile;
+                a.bar = c->T().pbar.as<dpbar>();
+                a.nseg = nseg;
+                a.vmask = c->vmask;
+                HIP_OR(launch_pscan(a, pb, c->cs), HVWS_EHIP);
+                HIP_OR(release_slot(), HVWS_EHIP);
+                sc.src_segs = nullptr;
+                sc.src_carry = nullptr;
+                c->pscan_ran = true;
+            } else {
+                HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
+                if ((rc = tiles()) != HVWS_OK) return rc;
+            }
             if (unmask_into) {
-                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+                HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            c->verify_hint = status_h->pad2[1] != 0;
             done = (flags & SPEC_OK) != 0;
             c->spec_ok = done;
             c->scan_path = done ? HVWS_PATH_SPEC : HVWS_PATH_SPEC_FAILED;
@@ -738,14 +842,16 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             sc.bases_x = c->sl_bx.as<uint64_t>();
             sc.est_u = c->sl_bx.as<uint64_t>() + nseg + 1;
             sc.seq = ++c->scan_seq;
+            sc.no_verify = (c->verify_mode < 0 ? c->verify_hint : c->verify_mode != 0) ? 0u : 1u;
             HIP_OR(pass(SCAN_SLACK), HVWS_EHIP);
             if ((rc = tiles()) != HVWS_OK) return rc;
             if (unmask_into) {
-                HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+                HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            c->verify_hint = status_h->pad2[1] != 0;
             done = (flags & SPEC_OK) != 0;
             if (done) {
                 c->slack_seg = status_h->pad2[0];
@@ -759,9 +865,11 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         }
         if (!done) {
             sc.seq = ++c->scan_seq;
+            sc.no_verify = 0;
             HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
             HIP_OR(hipStreamSynchronize(c->cs), HVWS_EHIP);
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
+            c->verify_hint = status_h->pad2[1] != 0;
             c->spec_ok = (flags & SPEC_MATCH) != 0;
             c->slack_seg = status_h->pad2[0];
             HIP_OR(ensure_frames(c, nfr + 1), HVWS_ENOMEM);
@@ -773,7 +881,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         int rc = tiles();
         if (rc) return rc;
     }
-    if (!(unmasked && *unmasked)) HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->cs), HVWS_EHIP);
+    if (!(unmasked && *unmasked)) HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
     if (table_checks()) {   // the tile index's invariant (k_ends_check), tests only: one sync
         HIP_OR(c->chk.ensure(8), HVWS_ENOMEM);
         HIP_OR(c->h_chk.ensure(8), HVWS_ENOMEM);
@@ -1000,7 +1108,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
                         (drec*)(ho_d + nseg), hcap, ho_d, user_mapped ? user_mapped : hp_d + o_data, unmask,
                         c->vmask, c->stream),
            HVWS_EHIP);
-    HIP_OR(hipEventRecord(c->tev[c->t_cur][1], c->stream), HVWS_EHIP);
+    HIP_OR(tev_record(c, 1, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (!user_mapped && unmask && len) memcpy(h_rx, hp + o_data, len);
     // host cache in segment order
@@ -1100,6 +1208,7 @@ hvws_ctx* hvws_ctx_create(int device) {
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
+    if (const char* wv = getenv("HVWS_WALK_VERIFY")) c->verify_mode = atoi(wv) < 0 ? -1 : (atoi(wv) ? 1 : 0);
     // The pipelined scan stream at the highest priority: a scan kernel of
     // ~1000 workgroups queued while an unmask grid is being dispatched waits
     // for that whole grid at normal priority, but is dispatched beside it at
@@ -1714,6 +1823,23 @@ uint64_t hvws_set_fast_bound(hvws_ctx* c, uint64_t records) {
     if (!c) return 0;
     const uint64_t old = c->fast_bound ? c->fast_bound : kFastFrameBound;
     c->fast_bound = records;
+    return old;
+}
+
+int hvws_set_one_launch_scan(hvws_ctx* c, int mode) {
+    if (!c) c = thread_ctx();
+    if (!c) return -1;
+    if (mode < 0) return c->pscan_ran ? (int)c->pscan_blocks : 0;
+    const int old = c->pscan_mode < 0 ? (getenv("HVWS_PSCAN") ? atoi(getenv("HVWS_PSCAN")) != 0 : 0) : c->pscan_mode;
+    c->pscan_mode = mode ? 1 : 0;
+    return old;
+}
+
+int hvws_set_walk_verify(hvws_ctx* c, int mode) {
+    if (!c) c = thread_ctx();
+    if (!c) return HVWS_ENODEV;
+    const int old = c->verify_mode;
+    c->verify_mode = mode < 0 ? -1 : (mode ? 1 : 0);
     return old;
 }
 

@@ -110,7 +110,8 @@ struct dspec_status {
 };
 enum : uint32_t {
     SPEC_MATCH = 1u,   // every segment's record count equals k_head's estimate
-    SPEC_OK = 2u       // SCAN_SPEC: the speculative table is the exact table (match and within capacity)
+    SPEC_OK = 2u,      // SCAN_SPEC: the speculative table is the exact table (match and within capacity)
+    SPEC_ERR = 4u      // one-launch scan: a grid barrier timed out (results void)
 };
 
 struct sieve_bufs;
@@ -137,6 +138,37 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint64_t  slack_cap;     // SLACK: records per segment region at most
     uint64_t* bases_x;       // SLACK: exact bases (nseg)
     uint64_t* est_u;         // SLACK: uniform-stride estimates (nseg), for SPEC_MATCH
+    uint32_t  no_verify;     // SPEC/SLACK: head + walk only (no k_verify pair, no k_head<true>)
+};
+
+// Grid-barrier words of the one-launch scan (k_pscan), zeroed before each launch.
+struct dpbar {
+    uint32_t count;   // arrivals: barrier k completes at k x workgroups
+    uint32_t err;     // a barrier timed out
+    uint32_t pad[14];
+};
+
+// Everything the one-launch SPEC scan reads and writes (kernel argument).
+struct pscan_args {
+    const uint8_t* rx;
+    uint64_t       rx_len;
+    const dseg*    segs;
+    const dcarry*  carry_in;
+    dcarry*        carry_out;
+    uint64_t*      counts;
+    uint64_t*      bases;
+    uint64_t*      total;
+    scan_scratch   sc;
+    dframes        fr;
+    uint64_t       spec_min;
+    uint32_t*      tile_first;
+    uint32_t*      tile_key;
+    uint8_t*       tile_kind;
+    uint64_t       ntiles;
+    uint64_t       tile;
+    dpbar*         bar;
+    uint32_t       nseg;
+    uint32_t       vmask;
 };
 
 // Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
@@ -216,6 +248,12 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
+// The SPEC pass + tile index/classes as one persistent launch (k_pscan) of
+// `blocks` workgroups, all of which must be resident at once (<= 2 per CU);
+// zeroes a.bar first.  The check verdict is published like k_spec_check's.
+hipError_t launch_pscan(const pscan_args& a, uint32_t blocks, hipStream_t st);
+int pscan_blocks_per_cu();
+uint32_t pscan_threads();
 // *total > cap: *total = 0; publishes the count to status (SPEC_OK if within cap).
 hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st);
 hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uint64_t* nfr_dev,

@@ -210,8 +210,13 @@ uint64_t set_spec_min(uint64_t v) {
     return old;
 }
 
+enum : uint32_t {
+    HEAD_ZERO_LM = 1u,     // also clear last_masked (no k_head<true> follows)
+    HEAD_NO_VERIFY = 2u    // no k_verify follows (see head_body)
+};
+
 template <bool EMIT>
-__global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict__ rx, uint64_t rx_len,
+__device__ __forceinline__ void head_body(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                        const dseg* __restrict__ segs, uint32_t nseg,
                                                        const dcarry* __restrict__ carry_in, dmid* __restrict__ mid,
                                                        uint64_t* __restrict__ npred, uint64_t* __restrict__ first_fail,
@@ -221,10 +226,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        const dseg* __restrict__ src_segs,
                                                        const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
                                                        dcarry* __restrict__ carry_w, int probe_mixed,
-                                                       uint64_t slack_cap, uint64_t* __restrict__ est_u) {
+                                                       uint64_t slack_cap, uint64_t* __restrict__ est_u,
+                                          uint32_t w0, uint32_t wn, uint32_t hflags) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wpb = SCAN_THREADS / 64;
-    for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
+    for (uint32_t s = w0; s < nseg; s += wn) {
         dseg sg;
         dcarry st;
         if (src_segs) {
@@ -320,25 +325,46 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
             m.pad = mixed;   // read by the frame sieve (hvws_sieve.hip)
             mid[s] = m;
             npred[s] = np;
-            if (!EMIT) first_fail[s] = np;
-            else last_masked[s] = 0;
+            // HEAD_NO_VERIFY: no k_verify follows; the walk takes every frame
+            // (first_fail 0), npred keeps the candidate count as a hint
+            if (!EMIT) first_fail[s] = (hflags & HEAD_NO_VERIFY) ? 0 : np;
+            if (EMIT || (hflags & HEAD_ZERO_LM)) last_masked[s] = 0;
         }
     }
 }
 
+template <bool EMIT>
+__global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                       const dseg* __restrict__ segs, uint32_t nseg,
+                                                       const dcarry* __restrict__ carry_in, dmid* __restrict__ mid,
+                                                       uint64_t* __restrict__ npred, uint64_t* __restrict__ first_fail,
+                                                       uint64_t* __restrict__ last_masked,
+                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
+                                                       uint64_t spec_min, uint64_t* __restrict__ est,
+                                                       const dseg* __restrict__ src_segs,
+                                                       const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
+                                                       dcarry* __restrict__ carry_w, int probe_mixed,
+                                                       uint64_t slack_cap, uint64_t* __restrict__ est_u,
+                                                       uint32_t hflags) {
+    const uint32_t wpb = SCAN_THREADS / 64;
+    head_body<EMIT>(rx, rx_len, segs, nseg, carry_in, mid, npred, first_fail, last_masked, bases, fr, vmask, spec_min, est,
+                    src_segs, src_carry, segs_w, carry_w, probe_mixed, slack_cap, est_u,
+                    blockIdx.x * wpb + (threadIdx.x >> 6), gridDim.x * wpb, hflags);
+}
+
 // --------------------------------------------------------------- k_verify
 template <bool EMIT>
-__global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, uint64_t rx_len,
+__device__ __forceinline__ void verify_body(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                 const dseg* __restrict__ segs, uint32_t nseg,
                                                 const dmid* __restrict__ mid, const uint64_t* __restrict__ pbase,
-                                                const uint64_t* __restrict__ total_pred,
+                                                uint64_t total,
                                                 uint64_t* __restrict__ first_fail,
                                                 uint64_t* __restrict__ last_masked,
-                                                const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
-    const uint64_t total = *total_pred;
+                                                const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
+                                            uint32_t bid, uint32_t nb) {
     if (total == 0) return;
-    const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
-    const uint64_t g0 = (uint64_t)blockIdx.x * per;
+    const uint64_t per = (total + nb - 1) / nb;
+    const uint64_t g0 = (uint64_t)bid * per;
     const uint64_t g1 = g0 + per < total ? g0 + per : total;
     if (g0 >= g1) return;
     // segment holding g0: last s with pbase[s] <= g0 (pbase is non-decreasing)
@@ -414,6 +440,18 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, 
             atomicMax((unsigned long long*)&last_masked[ms], (unsigned long long)mmax);
         }
     }
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                const dseg* __restrict__ segs, uint32_t nseg,
+                                                const dmid* __restrict__ mid, const uint64_t* __restrict__ pbase,
+                                                const uint64_t* __restrict__ total_pred,
+                                                uint64_t* __restrict__ first_fail,
+                                                uint64_t* __restrict__ last_masked,
+                                                const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask) {
+    verify_body<EMIT>(rx, rx_len, segs, nseg, mid, pbase, *total_pred, first_fail, last_masked, bases, fr, vmask,
+                      blockIdx.x, gridDim.x);
 }
 
 // Whole frames from segment offset `pos` on (wave-wide speculative walk,
@@ -539,21 +577,24 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
 }
 
 // ----------------------------------------------------------------- k_walk
+// carry_rec (EMIT, one-launch scan): also write the record of the frame
+// carried in from the previous batch (k_head<true>'s job in the kernel
+// chain), re-running the exact state machine from the carried-in state.
 template <bool EMIT>
-__global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict__ rx, uint64_t rx_len,
-                                                       const dseg* __restrict__ segs, uint32_t nseg,
-                                                       const dmid* __restrict__ mid,
-                                                       const uint64_t* __restrict__ npred,
-                                                       const uint64_t* __restrict__ first_fail,
-                                                       const uint64_t* __restrict__ last_masked,
-                                                       dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
-                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
-                                                       int emit_counts, const dsieve* __restrict__ sv,
-                                                       const uint64_t* __restrict__ sv_S) {
+__device__ __forceinline__ void walk_body(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                          const dseg* __restrict__ segs, uint32_t nseg,
+                                          const dmid* __restrict__ mid,
+                                          const uint64_t* __restrict__ npred,
+                                          const uint64_t* __restrict__ first_fail,
+                                          const uint64_t* __restrict__ last_masked,
+                                          dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
+                                          const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
+                                          int emit_counts, const dsieve* __restrict__ sv,
+                                          const uint64_t* __restrict__ sv_S, const dcarry* __restrict__ carry_rec,
+                                          uint32_t w0, uint32_t wn) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wpb = SCAN_THREADS / 64;
 
-    for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < nseg; s += gridDim.x * wpb) {
+    for (uint32_t s = w0; s < nseg; s += wn) {
         const uint64_t sb = segs[s].off;
         const uint64_t L = segs[s].len;
         const dmid m = mid[s];
@@ -561,6 +602,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
         uint64_t pos = m.pos;
         uint64_t n = m.n_a;
         const uint64_t obase = EMIT ? bases[s] : 0;
+        if (EMIT && carry_rec && m.n_a) {
+            dcarry c0 = carry_rec[s];
+            c0.started = 0;
+            uint64_t p0 = 0;
+            frec r;
+            scalar_frame(rx + sb, L, c0, p0, r, vmask);
+            if (lane == 0) store_frame(fr, obase, sb, r);
+        }
 
         // Skip the prefix k_verify proved; restore the fields the reference
         // leaves behind after its last frame (Q14).
@@ -611,6 +660,23 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
             if (EMIT) carry_out[s] = st;
         }
     }
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                       const dseg* __restrict__ segs, uint32_t nseg,
+                                                       const dmid* __restrict__ mid,
+                                                       const uint64_t* __restrict__ npred,
+                                                       const uint64_t* __restrict__ first_fail,
+                                                       const uint64_t* __restrict__ last_masked,
+                                                       dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
+                                                       const uint64_t* __restrict__ bases, dframes fr, uint32_t vmask,
+                                                       int emit_counts, const dsieve* __restrict__ sv,
+                                                       const uint64_t* __restrict__ sv_S,
+                                                       const dcarry* __restrict__ carry_rec) {
+    const uint32_t wpb = SCAN_THREADS / 64;
+    walk_body<EMIT>(rx, rx_len, segs, nseg, mid, npred, first_fail, last_masked, carry_out, counts, bases, fr, vmask,
+                    emit_counts, sv, sv_S, carry_rec, blockIdx.x * wpb + (threadIdx.x >> 6), gridDim.x * wpb);
 }
 
 // ----------------------------------------------------------------- k_small
@@ -731,19 +797,19 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // ------------------------------------------------------------- k_offsets
 // Exclusive scan of counts[0..nseg) into bases[], total into *total.  One
 // block of 1024 threads; each thread owns a contiguous run.
-__global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ counts,
-                                                  uint64_t* __restrict__ bases, uint32_t nseg,
-                                                  uint64_t* __restrict__ total) {
-    __shared__ uint64_t part[1024];
+template <uint32_t NT>
+__device__ __forceinline__ void offsets_body(const uint64_t* __restrict__ counts, uint64_t* __restrict__ bases,
+                                             uint32_t nseg, uint64_t* __restrict__ total) {
+    __shared__ uint64_t part[NT];
     const uint32_t t = threadIdx.x;
-    const uint32_t per = (nseg + 1023u) / 1024u;
+    const uint32_t per = (nseg + NT - 1u) / NT;
     const uint32_t b = t * per;
     const uint32_t e = min(nseg, b + per);
     uint64_t sum = 0;
     for (uint32_t i = b; i < e; ++i) sum += counts[i];
     part[t] = sum;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+    for (uint32_t d = 1; d < NT; d <<= 1) {
         uint64_t v = t >= d ? part[t - d] : 0;
         __syncthreads();
         part[t] += v;
@@ -754,7 +820,13 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ c
         bases[i] = run;
         run += counts[i];
     }
-    if (t == 1023u) *total = part[1023];
+    if (t == NT - 1u) *total = part[NT - 1u];
+}
+
+__global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ counts,
+                                                  uint64_t* __restrict__ bases, uint32_t nseg,
+                                                  uint64_t* __restrict__ total) {
+    offsets_body<1024>(counts, bases, nseg, total);
 }
 
 // ----------------------------------------------------------- k_spec_check
@@ -765,21 +837,24 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ c
 // host re-scans exactly).  COUNT (observe only): report whether the
 // estimates would have held, leave *total alone.  Results go to pinned host
 // memory (status), tagged with the scan's sequence number.
-template <bool SPEC>
-__global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict__ counts,
-                                                     const uint64_t* __restrict__ est, uint32_t nseg,
+template <bool SPEC, uint32_t NT>
+__device__ __forceinline__ void spec_check_body(const uint64_t* __restrict__ counts,
+                                                     const uint64_t* __restrict__ est,
+                                                     const uint64_t* __restrict__ npred, uint32_t nseg,
                                                      uint64_t* __restrict__ total, uint64_t cap,
-                                                     dspec_status* __restrict__ status, uint64_t seq) {
-    __shared__ uint64_t s_sum[1024 / 64], s_max[1024 / 64];
-    __shared__ uint32_t s_bad[1024 / 64];
+                                                     dspec_status* __restrict__ status, uint64_t seq,
+                                                     bool publish) {
+    __shared__ uint64_t s_sum[NT / 64], s_max[NT / 64];
+    __shared__ uint32_t s_bad[NT / 64];
     const uint32_t t = threadIdx.x;
     uint64_t sum = 0, mx = 0;
     uint32_t bad = 0;
-    for (uint32_t i = t; i < nseg; i += 1024) {
+    for (uint32_t i = t; i < nseg; i += NT) {
         const uint64_t c = counts[i];
         sum += c;
         mx = c > mx ? c : mx;
         bad |= c != est[i];
+        if (npred && npred[i]) bad |= 2u;   // a long uniform run (the next scan keeps k_verify)
     }
     for (int o = 32; o > 0; o >>= 1) {
         sum += __shfl_xor(sum, o);
@@ -796,12 +871,14 @@ __global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict_
     if (t == 0) {
         uint64_t all = 0, amax = 0;
         uint32_t any_bad = 0;
-        for (int w = 0; w < 1024 / 64; ++w) {
+        for (uint32_t w = 0; w < NT / 64; ++w) {
             all += s_sum[w];
             amax = s_max[w] > amax ? s_max[w] : amax;
             any_bad |= s_bad[w];
         }
         status->pad2[0] = amax;   // largest segment count: sizes the next slack table
+        status->pad2[1] = (any_bad & 2u) ? 1u : 0u;   // some segment had >= spec_min predicted frames
+        any_bad &= 1u;
         uint32_t flags = any_bad ? 0u : SPEC_MATCH;
         if (SPEC) {
             const bool ok = !any_bad && all <= cap;
@@ -811,8 +888,17 @@ __global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict_
         status->total = all;
         status->flags = flags;
         // last: the host polls seq (fine-grained pinned memory)
-        __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (publish) __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+template <bool SPEC>
+__global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict__ counts,
+                                                     const uint64_t* __restrict__ est,
+                                                     const uint64_t* __restrict__ npred, uint32_t nseg,
+                                                     uint64_t* __restrict__ total, uint64_t cap,
+                                                     dspec_status* __restrict__ status, uint64_t seq) {
+    spec_check_body<SPEC, 1024>(counts, est, npred, nseg, total, cap, status, seq, true);
 }
 
 // ----------------------------------------------------------- SLACK table
@@ -827,7 +913,8 @@ __global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict_
 // host round trip before EMIT, like SPEC for uniform ones.
 __global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict__ counts,
                                                       const uint64_t* __restrict__ est,
-                                                      const uint64_t* __restrict__ est_u, uint32_t nseg,
+                                                      const uint64_t* __restrict__ est_u,
+                                                      const uint64_t* __restrict__ npred, uint32_t nseg,
                                                       uint64_t* __restrict__ bases_x, uint64_t* __restrict__ total,
                                                       uint64_t cap, dspec_status* __restrict__ status, uint64_t seq) {
     __shared__ uint64_t part[1024], pmax[1024 / 64];
@@ -843,6 +930,7 @@ __global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict
         sum += c;
         mx = c > mx ? c : mx;
         bad |= (c > est[i] ? 1u : 0u) | (c != est_u[i] ? 2u : 0u);   // 1: region overflow, 2: not uniform
+        if (npred[i]) bad |= 4u;                                       // 4: a long uniform run (keep k_verify)
     }
     part[t] = sum;
     for (int o = 32; o > 0; o >>= 1) {   // max and flags: wave reductions, then 16 partials
@@ -879,6 +967,7 @@ __global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict
         status->total = all;
         status->flags = (ok ? SPEC_OK : 0u) | ((any_bad & 2u) ? 0u : SPEC_MATCH);
         status->pad2[0] = amax;
+        status->pad2[1] = (any_bad & 4u) ? 1u : 0u;
         __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -963,11 +1052,10 @@ hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uin
 constexpr uint32_t TILE_MARK = 0xFFFFFFFFu;
 constexpr uint64_t TILE_SPAN_MAX = 64;
 
-__global__ void k_tile_scatter(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t nfr_v,
-                               const uint64_t* __restrict__ nfr_p, uint32_t* __restrict__ tile_first, uint64_t ntiles,
-                               uint64_t tile) {
-    const uint64_t nfr = nfr_p ? *nfr_p : nfr_v;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nfr; k += (uint64_t)gridDim.x * blockDim.x) {
+__device__ __forceinline__ void tile_scatter_body(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                                                  uint64_t nfr, uint32_t* __restrict__ tile_first, uint64_t ntiles,
+                                                  uint64_t tile, uint64_t k0, uint64_t kstep) {
+    for (uint64_t k = k0; k < nfr; k += kstep) {
         const uint64_t lo = k ? off[k - 1] + len[k - 1] : 0;
         const uint64_t hi = off[k] + len[k];
         if (hi <= lo) continue;
@@ -977,6 +1065,13 @@ __global__ void k_tile_scatter(const uint64_t* __restrict__ off, const uint64_t*
         if (t1 <= t0 || t1 - t0 > TILE_SPAN_MAX) continue;
         for (uint64_t t = t0; t < t1; ++t) tile_first[t] = (uint32_t)k;
     }
+}
+
+__global__ void k_tile_scatter(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t nfr_v,
+                               const uint64_t* __restrict__ nfr_p, uint32_t* __restrict__ tile_first, uint64_t ntiles,
+                               uint64_t tile) {
+    tile_scatter_body(off, len, nfr_p ? *nfr_p : nfr_v, tile_first, ntiles, tile,
+                      (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
 }
 
 __global__ void k_tile_fixup(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t nfr_v,
@@ -1023,13 +1118,12 @@ __global__ void k_tile_class(const uint64_t* __restrict__ off, const uint64_t* _
 
 // k_tile_fixup + k_tile_class in one pass over the tiles (the scan's unmask
 // tiles): resolve a tile k_tile_scatter left marked, then classify it.
-__global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
-                                 const uint32_t* __restrict__ keyrot, const uint64_t* __restrict__ nfr_p,
-                                 uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
-                                 uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile, uint64_t rx_len) {
-    const uint64_t nfr = *nfr_p;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
-         t += (uint64_t)gridDim.x * blockDim.x) {
+__device__ __forceinline__ void fix_class_body(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                                               const uint32_t* __restrict__ keyrot, uint64_t nfr,
+                                               uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
+                                               uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile,
+                                               uint64_t rx_len, uint64_t t0, uint64_t tstep) {
+    for (uint64_t t = t0; t <= ntiles; t += tstep) {
     const uint64_t x = t * tile;
     // tile_first[t] is not cleared between batches: k_tile_scatter writes
     // every tile whose start lies before the last frame's end, except the
@@ -1060,6 +1154,152 @@ __global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_
     tile_key[t] = key;
     tile_kind[t] = (uint8_t)kind;
     }
+}
+
+__global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                                 const uint32_t* __restrict__ keyrot, const uint64_t* __restrict__ nfr_p,
+                                 uint32_t* __restrict__ tile_first, uint32_t* __restrict__ tile_key,
+                                 uint8_t* __restrict__ tile_kind, uint64_t ntiles, uint64_t tile, uint64_t rx_len) {
+    fix_class_body(off, len, keyrot, *nfr_p, tile_first, tile_key, tile_kind, ntiles, tile, rx_len,
+                   (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
+}
+
+// ---------------------------------------------------------------- k_pscan
+//
+// The SPEC pass as ONE launch (pipelined and serial steps of uniform batches
+// alike).  As a chain of ~10 kernels the next batch's discovery could not
+// overlap the current unmask: a wide kernel queued on the second stream is
+// dispatched only once the unmask grid has been fully launched, so every
+// dependent kernel of the chain after the first waited for the unmask to
+// drain (profiles/r2b_raw/c2_piped_trace.txt).  One persistent launch of G
+// workgroups (2 per CU at most, all resident) is dispatched beside the unmask
+// grid once, and its phases are separated by grid barriers instead of kernel
+// boundaries:
+//   A  head<false> + est (+ zero-copy upload, last_masked cleared)   | barrier
+//   B  block 0: npred -> pbase, total_pred; block 1: est -> bases, total | barrier
+//   V  (only if some segment is long) verify<false> | barrier | verify<true> | barrier
+//   W  walk<true> (+ the carried-in frame's record: k_head<true>'s part)  | barrier
+//   C  block 0: spec check (status fields); all: tile scatter            | barrier
+//   T  tile fixup + classes; block 0 publishes the status sequence number
+// The bodies are the chain's kernels' own code (head_body, verify_body, ...),
+// so records, counts, carry and tiles are the chain's bit for bit.
+//
+// Visibility: a phase's outputs are plain stores; every workgroup's thread 0
+// makes an agent-scope release fence before it arrives at the barrier's
+// counter and an acquire fence after the count is complete (the 8 XCDs have
+// private L2s; cdna_hip_programming.md sec. 6 G16).  Values another
+// workgroup wrote in this launch that are read at a uniform address (totals)
+// are read with atomic loads, so they never come from the scalar cache.
+// Spins are bounded (~seconds): a barrier that cannot complete (a workgroup
+// never resident) sets err, every later barrier then passes at once, the
+// tiles are classified empty (the queued unmask does nothing) and the host
+// gets SPEC_ERR.  The barrier words are zeroed by the host before each launch.
+constexpr uint32_t PSCAN_THREADS = 256;
+constexpr uint32_t PSCAN_SPIN_MAX = 1u << 22;
+
+__device__ __forceinline__ bool pscan_sync(dpbar* __restrict__ b, uint32_t target) {
+    __shared__ uint32_t s_ok;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(&b->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t ok = 1;
+        for (uint32_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(&b->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if (__hip_atomic_load(&b->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                ok = 0;
+                break;
+            }
+            if (spin >= PSCAN_SPIN_MAX) {
+                __hip_atomic_fetch_or(&b->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+__device__ __forceinline__ uint64_t ld_shared_u64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(PSCAN_THREADS) void k_pscan(pscan_args a) {
+    const uint32_t G = gridDim.x, bid = blockIdx.x;
+    const uint32_t wpb = PSCAN_THREADS / 64;
+    const uint32_t w0 = bid * wpb + (threadIdx.x >> 6), wn = G * wpb;
+    scan_scratch& sc = a.sc;
+    dpbar* bar = a.bar;
+    uint32_t nbar = 0;
+    bool ok = true;
+    auto sync = [&]() { ok = pscan_sync(bar, ++nbar * G) && ok; };
+
+    // A: first whole frame, stride and estimate of every segment
+    head_body<false>(a.rx, a.rx_len, a.segs, a.nseg, a.carry_in, sc.mid, sc.npred, sc.first_fail, sc.last_masked,
+                     a.bases, a.fr, a.vmask, a.spec_min, sc.est, sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0,
+                     0, nullptr, w0, wn, HEAD_ZERO_LM);
+    sync();
+    // B: the two exclusive scans
+    if (bid == 0) offsets_body<PSCAN_THREADS>(sc.npred, sc.pbase, a.nseg, sc.total_pred);
+    if (bid == (G > 1 ? 1u : 0u)) {
+        __syncthreads();
+        offsets_body<PSCAN_THREADS>(sc.est, a.bases, a.nseg, a.total);
+    }
+    sync();
+    // V: grid-wide verification of long uniform runs (none at c2/c3 shapes)
+    const uint64_t tp = ok ? ld_shared_u64(sc.total_pred) : 0;
+    if (tp) {
+        verify_body<false>(a.rx, a.rx_len, a.segs, a.nseg, sc.mid, sc.pbase, tp, sc.first_fail, sc.last_masked, a.bases,
+                           a.fr, a.vmask, bid, G);
+        sync();
+        verify_body<true>(a.rx, a.rx_len, a.segs, a.nseg, sc.mid, sc.pbase, tp, sc.first_fail, sc.last_masked, a.bases,
+                          a.fr, a.vmask, bid, G);
+        sync();
+    }
+    // W: the walk, records at the estimated bases
+    walk_body<true>(a.rx, a.rx_len, a.segs, a.nseg, sc.mid, sc.npred, sc.first_fail, sc.last_masked, a.carry_out,
+                    a.counts, a.bases, a.fr, a.vmask, 1, nullptr, nullptr, a.carry_in, w0, wn);
+    sync();
+    // C: the check (block 0; zeroes *total when the table is not exact) beside
+    // the tile scatter over the estimated count (a rejected table's entries
+    // are harmless: T classifies every tile with the checked count)
+    // (capped at the table: a rejected estimate can exceed what was allocated)
+    const uint64_t est_raw = ok ? ld_shared_u64(a.total) : 0;
+    const uint64_t est_total = est_raw < a.fr.cap ? est_raw : a.fr.cap;
+    if (bid == 0)
+        spec_check_body<true, PSCAN_THREADS>(a.counts, sc.est, sc.npred, a.nseg, a.total, a.fr.cap, sc.status, sc.seq, false);
+    tile_scatter_body(a.fr.pay_off, a.fr.pay_len, est_total, a.tile_first, a.ntiles, a.tile,
+                      (uint64_t)bid * PSCAN_THREADS + threadIdx.x, (uint64_t)G * PSCAN_THREADS);
+    sync();
+    // T: tile fixup and classes with the checked count
+    const uint64_t nfr = ok ? ld_shared_u64(a.total) : 0;
+    fix_class_body(a.fr.pay_off, a.fr.pay_len, a.fr.keyrot, nfr, a.tile_first, a.tile_key, a.tile_kind, a.ntiles, a.tile,
+                   a.rx_len, (uint64_t)bid * PSCAN_THREADS + threadIdx.x, (uint64_t)G * PSCAN_THREADS);
+    if (bid == 0 && threadIdx.x == 0) {
+        if (!ok || __hip_atomic_load(&bar->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sc.status->flags = SPEC_ERR;
+        __hip_atomic_store(&sc.status->seq, sc.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+uint32_t pscan_threads() { return PSCAN_THREADS; }
+
+hipError_t launch_pscan(const pscan_args& a, uint32_t blocks, hipStream_t st) {
+    if (a.nseg == 0 || blocks == 0) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(a.bar, 0, sizeof(dpbar), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pscan, dim3(blocks), dim3(PSCAN_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+// Workgroups of k_pscan that can be resident at once per CU (occupancy query).
+int pscan_blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pscan, PSCAN_THREADS, 0) != hipSuccess) return 0;
+    return n;
 }
 
 // -------------------------------------------------------------- k_unmask
@@ -1309,7 +1549,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
                            sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, (int)(pass == SCAN_SINGLE && sieve),
                            pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
-                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr);
+                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, 0u);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
@@ -1318,7 +1558,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
                            (uint64_t*)nullptr, (const dseg*)nullptr, (const dcarry*)nullptr, (dseg*)nullptr,
-                           (dcarry*)nullptr, 0, (uint64_t)0, (uint64_t*)nullptr);
+                           (dcarry*)nullptr, 0, (uint64_t)0, (uint64_t*)nullptr, 0u);
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         if (sieve) {
@@ -1327,8 +1567,23 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         }
         hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, emit_counts,
-                           sv, sv_S);
+                           sv, sv_S, (const dcarry*)nullptr);
         return hipSuccess;
+    };
+    // One-walk passes (SPEC, SLACK) when the last check saw no long uniform
+    // run: k_head<false> alone (no k_verify pair, no npred scan), then the
+    // walk also writes the carried-in frame's record, so no k_head<true>:
+    // 4 kernels fewer.  The walk is exact whatever the segments hold.
+    auto head_walk = [&](uint64_t* est, dframes fr) {
+        hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
+                           sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0,
+                           pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
+                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, est, bases, nseg, total);
+        hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+                           sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 1,
+                           (const dsieve*)nullptr, (const uint64_t*)nullptr, carry_in);
     };
     if (pass == SCAN_SINGLE) {
         head_count(nullptr);
@@ -1338,26 +1593,34 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         if ((e = emit(1, fr)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
     } else if (pass == SCAN_SPEC) {
-        head_count(sc.est);
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
-        if (hipError_t e = emit(1, fr); e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
+        if (sc.no_verify) {
+            head_walk(sc.est, fr);
+        } else {
+            head_count(sc.est);
+            hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
+            if (hipError_t e = emit(1, fr); e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.npred, nseg, total, fr.cap,
                            sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
         head_count(sc.status ? sc.est : nullptr);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0,
-                           (const dsieve*)nullptr, (const uint64_t*)nullptr);
+                           (const dsieve*)nullptr, (const uint64_t*)nullptr, (const dcarry*)nullptr);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
         if (sc.status)
-            hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(1024), 0, st, counts, sc.est, nseg, total, fr.cap,
-                               sc.status, sc.seq);
+            hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.npred, nseg, total,
+                               fr.cap, sc.status, sc.seq);
     } else if (pass == SCAN_SLACK) {
-        head_count(sc.est);
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
-        if (hipError_t e = emit(1, sc.slack); e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_slack_check, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.est_u, nseg, sc.bases_x, total, fr.cap,
-                           sc.status, sc.seq);
+        if (sc.no_verify) {
+            head_walk(sc.est, sc.slack);
+        } else {
+            head_count(sc.est);
+            hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
+            if (hipError_t e = emit(1, sc.slack); e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_slack_check, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.est_u, sc.npred, nseg, sc.bases_x,
+                           total, fr.cap, sc.status, sc.seq);
         hipLaunchKernelGGL(k_slack_compact, dim3(nseg < 65535u ? nseg : 65535u), dim3(256), 0, st, sc.slack, fr, counts,
                            bases, sc.bases_x, total, nseg);
     } else {

@@ -161,15 +161,27 @@ def _oracle_batch(buf: np.ndarray, segs, carries):
 # path, without speculation (COUNT, read, EMIT) and with it (speculative
 # EMIT checked on the device, exact re-scan when the check fails): SPEC
 # (uniform estimates) and SLACK (per-segment regions, compacted).
-SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1),
-              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1), ("slack", 1, 2), ("pipelined_slack", 1, 2)]
+# SPEC runs as the kernel chain (default) and as the one-launch scan
+# ("_one_launch": k_pscan, hvws_set_one_launch_scan 1); the fourth field is
+# that mode.  The one-walk passes (SPEC, SLACK) run adaptively (default), with
+# the k_verify pair forced ("_verify", fifth field 1) and without it
+# ("_noverify", 0: head + walk, the walk records the carried-in frame).
+SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1), ("speculate_one_launch", 1, 1, 1),
+              ("speculate_verify", 1, 1, 0, 1), ("speculate_noverify", 1, 1, 0, 0),
+              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1), ("pipelined_speculate_one_launch", 1, 1, 1),
+              ("slack", 1, 2), ("slack_noverify", 1, 2, 0, 0), ("pipelined_slack", 1, 2),
+              ("pipelined_slack_verify", 1, 2, 0, 1)]
 
 
 def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, mode):
     L = libhv_amd.lib()
-    _, bound, spec = mode
+    bound, spec = mode[1], mode[2]
+    one_launch = mode[3] if len(mode) > 3 else 0
+    verify = mode[4] if len(mode) > 4 else -1
     old_b = L.hvws_set_fast_bound(eng.ctx, bound)
     old_s = L.hvws_set_speculation(eng.ctx, spec)
+    old_p = L.hvws_set_one_launch_scan(eng.ctx, one_launch)
+    old_v = L.hvws_set_walk_verify(eng.ctx, verify)
     try:
         rx = eng.to_device(buf)
         if mode[0].startswith("pipelined"):
@@ -181,9 +193,15 @@ def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp
         cout, started = eng.carry(len(segs))
         rx.free()
         path = L.hvws_last_scan_path(eng.ctx)
+        launched = L.hvws_set_one_launch_scan(eng.ctx, -1)
     finally:
         L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
         L.hvws_set_speculation(eng.ctx, old_s)
+        L.hvws_set_one_launch_scan(eng.ctx, old_p)
+        L.hvws_set_walk_verify(eng.ctx, old_v)
+    # a SPEC scan used the one-launch kernel exactly when it was on
+    if path in (3, 4):
+        assert (launched > 0) == bool(one_launch), (mode, path, launched)
     assert len(frames) == len(exp_recs), mode
     for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
         assert np.array_equal(frames[f], exp_recs[f]), (mode, f)
@@ -391,6 +409,8 @@ def test_speculative_table_uniform(eng):
         buf, segs, carries = _cut_uniform(rng, nframes, size, nseg)
         paths = _compare_batch(eng, buf, segs, carries)
         assert paths["speculate"] == 3, paths   # HVWS_PATH_SPEC
+        assert paths["speculate_one_launch"] == 3, paths
+        assert paths["pipelined_speculate_one_launch"] == 3, paths
         assert paths["count_read"] == 1, paths
 
 
@@ -401,6 +421,7 @@ def test_speculative_table_rejected(eng):
     host = H.synth_cpu(plan)
     paths = _compare_batch(eng, host, plan.segments)
     assert paths["speculate"] == 4, paths       # HVWS_PATH_SPEC_FAILED
+    assert paths["speculate_one_launch"] == 4, paths
 
 
 def test_speculation_adapts(eng):
