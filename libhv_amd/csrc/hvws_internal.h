@@ -139,6 +139,8 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint64_t* bases_x;       // SLACK: exact bases (nseg)
     uint64_t* est_u;         // SLACK: uniform-stride estimates (nseg), for SPEC_MATCH
     uint32_t  no_verify;     // SPEC/SLACK: head + walk only (no k_verify pair, no k_head<true>)
+    hipStream_t tail_st;     // SPEC: run the check on this stream after tail_ev (recorded behind the walk)
+    hipEvent_t  tail_ev;
 };
 
 // Grid-barrier words of the one-launch scan (k_pscan), zeroed before each launch.
@@ -282,7 +284,7 @@ uint64_t unmask_tile(int variant);         // bytes per workgroup tile
 const char* unmask_name(int variant);
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
                          const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st,
-                         uint32_t pieces = 1);
+                         uint32_t pieces = 1, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uint32_t* keyrot, const uint64_t* nfr_dev,
                              const uint32_t* tile_first, uint32_t* tile_key, uint8_t* tile_kind, uint64_t ntiles,
                              uint64_t tile, uint64_t rx_len, hipStream_t st);

@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <hip/hip_ext.h>
+
 #include "hvws_dev.h"
 
 namespace hvws {
@@ -1600,7 +1602,14 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
             hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
             if (hipError_t e = emit(1, fr); e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.npred, nseg, total, fr.cap,
+        hipStream_t cst = st;
+        if (sc.tail_st) {   // the check (and the caller's tile kernels) on the unmask stream
+            hipError_t e = hipEventRecord(sc.tail_ev, st);
+            if (e == hipSuccess) e = hipStreamWaitEvent(sc.tail_st, sc.tail_ev, 0);
+            if (e != hipSuccess) return e;
+            cst = sc.tail_st;
+        }
+        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, cst, counts, sc.est, sc.npred, nseg, total, fr.cap,
                            sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
         head_count(sc.status ? sc.est : nullptr);
@@ -1734,9 +1743,12 @@ static uint64_t max_tiles_per_launch(int threads) {
     return by_items < 0x7FFFFFFFull ? by_items : 0x7FFFFFFFull;
 }
 
+#define HVWS_GEOM_CASE_EXT(i, t, u, s) \
+    case i: hipExtLaunchKernelGGL((HVWS_K<t, u, s>), HVWS_EXT_ARGS); break;
+
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
                          const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st,
-                         uint32_t pieces) {
+                         uint32_t pieces, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (rx_len == 0) return hipSuccess;
     if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
     const uint64_t tile = unmask_tile(variant);
@@ -1750,14 +1762,27 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         const uint64_t per = (ntiles_all + pieces - 1) / pieces;
         cap = per < cap ? (per ? per : 1) : cap;
     }
+    // Timing events ride on the dispatch packets themselves (start of the
+    // first launch, end of the last): a separate hipEventRecord marker
+    // between the tile kernels and the unmask cost ~12 us of idle device per
+    // pipelined c2 step (profiles/r2g_raw).
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
+        const hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
+        const hipEvent_t e1 = tile0 + ntiles >= ntiles_all ? ev_stop : nullptr;
 #define HVWS_K k_unmask
 #define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, fr.keyrot, \
                   tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
-        switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
+#define HVWS_EXT_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, e0, e1, 0u, rx, rx_len, fr.pay_off, fr.pay_len, \
+                      fr.keyrot, tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
+        if (e0 || e1) {
+            switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE_EXT) default: return hipErrorInvalidValue; }
+        } else {
+            switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE) default: return hipErrorInvalidValue; }
+        }
 #undef HVWS_K
 #undef HVWS_ARGS
+#undef HVWS_EXT_ARGS
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
