@@ -159,10 +159,7 @@ struct hvws_ctx {
     // 0 = the kernel chain ($HVWS_PSCAN=0 / hvws_set_one_launch_scan)
     uint32_t pscan_blocks = 0;
     int pscan_mode = -1;   // -1 not yet decided
-    bool pscan_ran = false;
-    // pipelined SPEC: check + tile kernels on the unmask stream ($HVWS_TAIL=0: on the scan stream)
-    bool tail_mode = true;
-    bool tail_on_stream = false;   // the current scan did that   // the last scan used it (hvws_last_scan_path reports SPEC either way)
+    bool pscan_ran = false;   // the last scan used it (hvws_last_scan_path reports SPEC either way)
     // SLACK (mixed sizes, several segments): scratch table, exact bases, and
     // the per-segment region cap from the last exact scan's largest segment
     dbuf sl_hdr, sl_off, sl_len, sl_length, sl_key, sl_keyrot, sl_info, sl_bx;
@@ -378,13 +375,11 @@ int step_times_at(hvws_ctx* c, int slot, float* out) {
 // costs ~10 us of device idle between the check and the tile kernels).  A
 // stream that drains without publishing is an error, never a hang.
 int wait_status(hvws_ctx* c, uint64_t seq) {
-    // the stream the check was queued on (the unmask stream when the tail moved there)
-    hipStream_t cst = c->tail_on_stream ? c->stream : c->cs;
     const dspec_status* st = c->h_status.as<dspec_status>();
     for (uint64_t spin = 0;; ++spin) {
         if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
         if ((spin & 1023) == 1023) {
-            const hipError_t q = hipStreamQuery(cst);
+            const hipError_t q = hipStreamQuery(c->cs);
             if (q == hipSuccess) {
                 if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
                 return set_err(HVWS_EHIP, "scan check did not publish (seq %llu)", (unsigned long long)seq);
@@ -497,11 +492,9 @@ uint32_t pscan_blocks(hvws_ctx* c) {
 hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
     hipError_t e;
     const bool piped = c->cs != c->stream;
-    if (piped) {   // the scan ran on the side stream: join it (unless its tail already did)
-        if (!c->tail_on_stream) {
-            if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
-        }
+    if (piped) {   // the scan ran on the side stream: join it
+        if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
     }
     (void)after_scan;
     c->t_adjacent[c->t_cur] = false;
@@ -582,8 +575,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.bases_x = nullptr;
     sc.est_u = nullptr;
     sc.no_verify = 0;
-    sc.tail_st = nullptr;
-    sc.tail_ev = nullptr;
     dspec_status* status_d = mapped<dspec_status>(c->h_status);
     const dspec_status* status_h = c->h_status.as<dspec_status>();
     if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
@@ -643,14 +634,11 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     HIP_OR(c->T().tile_first.ensure((ntiles + 8) * 4), HVWS_ENOMEM);
     HIP_OR(c->T().tile_key.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
     HIP_OR(c->T().tile_kind.ensure(ntiles + 16), HVWS_ENOMEM);
-    // tail_on_stream: the scan's tail (check, tile index) runs on the unmask
-    // stream (pipelined SPEC steps, below)
-    c->tail_on_stream = false;
     auto tiles = [&]() -> int {
         HIP_OR(launch_unmask_tiles(c->T().f_off.as<uint64_t>(), c->T().f_len.as<uint64_t>(), c->T().f_keyrot.as<uint32_t>(),
                                    c->T().total.as<uint64_t>(), c->T().tile_first.as<uint32_t>(), c->T().tile_key.as<uint32_t>(),
                                    c->T().tile_kind.as<uint8_t>(), ntiles, tile, rx_len,
-                                   c->tail_on_stream ? c->stream : c->cs),
+                                   c->cs),
                HVWS_EHIP);
         return HVWS_OK;
     };
@@ -769,17 +757,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 HIP_OR(ensure_frames(c, c->ts[c->cur ^ 1].frame_cap, /*exact=*/true), HVWS_ENOMEM);
             sc.seq = ++c->scan_seq;
             sc.no_verify = (c->verify_mode < 0 ? c->verify_hint : c->verify_mode != 0) ? 0u : 1u;
-            // Pipelined: the check and the tile kernels go on the unmask
-            // stream behind the walk's event.  That stream reaches the event
-            // when the previous unmask ends, and by then the walk (dispatched
-            // beside that unmask) has finished: the wait is already
-            // satisfied, where waiting on the scan's last kernel cost ~24 us
-            // of idle device per step (the cross-queue barrier resolves late).
-            if (unmask_into && c->cs != c->stream && c->tail_mode) {
-                sc.tail_st = c->stream;
-                sc.tail_ev = c->scan_done;
-                c->tail_on_stream = true;
-            }
             if (const uint32_t pb = pscan_blocks(c)) {
                 // one launch: SPEC pass + tile index + classes (k_pscan)
                 HIP_OR(c->T().pbar.ensure(sizeof(dpbar)), HVWS_ENOMEM);
@@ -803,7 +780,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 a.bar = c->T().pbar.as<dpbar>();
                 a.nseg = nseg;
                 a.vmask = c->vmask;
-                c->tail_on_stream = false;
                 HIP_OR(launch_pscan(a, pb, c->cs), HVWS_EHIP);
                 HIP_OR(release_slot(), HVWS_EHIP);
                 sc.src_segs = nullptr;
@@ -814,7 +790,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 if ((rc = tiles()) != HVWS_OK) return rc;
             }
             if (unmask_into) {
-                HIP_OR(tev_record(c, 1, c->tail_on_stream ? c->stream : c->cs), HVWS_EHIP);
+                HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
@@ -823,8 +799,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             done = (flags & SPEC_OK) != 0;
             c->spec_ok = done;
             c->scan_path = done ? HVWS_PATH_SPEC : HVWS_PATH_SPEC_FAILED;
-            sc.tail_st = nullptr;
-            if (!done) c->tail_on_stream = false;   // the exact re-scan's tail runs on cs again
             if (done && unmask_into && unmasked) *unmasked = true;
             if (!done && (rc = join_rejected()) != HVWS_OK) return rc;
             tiles_done = done;
@@ -1234,7 +1208,6 @@ hvws_ctx* hvws_ctx_create(int device) {
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
-    if (const char* tm = getenv("HVWS_TAIL")) c->tail_mode = atoi(tm) != 0;
     if (const char* wv = getenv("HVWS_WALK_VERIFY")) c->verify_mode = atoi(wv) < 0 ? -1 : (atoi(wv) ? 1 : 0);
     // The pipelined scan stream at the highest priority: a scan kernel of
     // ~1000 workgroups queued while an unmask grid is being dispatched waits

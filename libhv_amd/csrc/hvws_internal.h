@@ -139,8 +139,6 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint64_t* bases_x;       // SLACK: exact bases (nseg)
     uint64_t* est_u;         // SLACK: uniform-stride estimates (nseg), for SPEC_MATCH
     uint32_t  no_verify;     // SPEC/SLACK: head + walk only (no k_verify pair, no k_head<true>)
-    hipStream_t tail_st;     // SPEC: run the check on this stream after tail_ev (recorded behind the walk)
-    hipEvent_t  tail_ev;
 };
 
 // Grid-barrier words of the one-launch scan (k_pscan), zeroed before each launch.

@@ -1602,15 +1602,8 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
             hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
             if (hipError_t e = emit(1, fr); e != hipSuccess) return e;
         }
-        hipStream_t cst = st;
-        if (sc.tail_st) {   // the check (and the caller's tile kernels) on the unmask stream
-            hipError_t e = hipEventRecord(sc.tail_ev, st);
-            if (e == hipSuccess) e = hipStreamWaitEvent(sc.tail_st, sc.tail_ev, 0);
-            if (e != hipSuccess) return e;
-            cst = sc.tail_st;
-        }
-        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, cst, counts, sc.est, sc.npred, nseg, total, fr.cap,
-                           sc.status, sc.seq);
+        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.npred, nseg, total,
+                           fr.cap, sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
         head_count(sc.status ? sc.est : nullptr);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
