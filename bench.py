@@ -296,7 +296,7 @@ def main():
     alg_bytes = 2 * P + HB
     achieved = alg_bytes / (mean_unmask * 1e-3) / 1e9
 
-    kname = libhv_amd.lib().hvws_unmask_kernel_name().decode()
+    kname = libhv_amd.lib().hvws_unmask_kernel_name_for(plan.total).decode()
     traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
@@ -349,7 +349,7 @@ def main():
                         eng.stream_xor(rx, plan.total & ~15, 0x5A5A5A5A)
                     eng.sync()
                     stimes.setdefault(name, []).append((time.perf_counter() - t) / 2)
-            L.hvws_set_unmask_variant(0)
+            L.hvws_set_unmask_variant(-1)
             ok = eng.synth(rx, plan.total, plan.seed, dp, 2 if passes % 2 else 1) == 0
             sweep = {n: (round(alg_bytes / (float(np.median(t)) * 1e-3) / 1e9, 1) if ok else None)
                      for n, t in times.items()}

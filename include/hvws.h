@@ -154,9 +154,15 @@ int hvws_last_times(hvws_ctx* ctx, float out[2]);
  * error).  Lets a caller time a run of asynchronous steps afterwards. */
 int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
 
-/* Name of the k_unmask geometry in use (e.g. "k_unmask<256,8,xcd>"). */
+/* k_unmask geometry.  By default it follows the batch size: 512 threads x 2
+ * chunks in linear tile order below 16 GiB, 256 x 4 in XCD-contiguous order
+ * from there (measured).  hvws_unmask_kernel_name: the name
+ * of the forced geometry, or of the large-batch one; ..._for: the geometry a
+ * batch of rx_len bytes runs with (e.g. "k_unmask<256,4,xcd>"). */
 const char* hvws_unmask_kernel_name(void);
-/* Select another k_unmask geometry for later scans (tuning; process-wide). */
+const char* hvws_unmask_kernel_name_for(uint64_t rx_len);
+/* Force a k_unmask geometry for later scans (tuning; process-wide); -1 =
+ * back to the choice by batch size. */
 int hvws_set_unmask_variant(int variant);
 
 /* Uniform runs of at least `frames` predicted frames in one segment are

@@ -628,7 +628,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         if (unmask_into && c->cs != c->stream) HIP_OR(hipStreamWaitEvent(c->cs, c->T().free_ev, 0), HVWS_EHIP);
         return HVWS_OK;
     };
-    c->variant = unmask_variant();
+    c->variant = unmask_variant_for(rx_len);
     const uint64_t tile = unmask_tile(c->variant);
     const uint64_t ntiles = (rx_len + tile - 1) / tile;
     HIP_OR(c->T().tile_first.ensure((ntiles + 8) * 4), HVWS_ENOMEM);
@@ -1531,7 +1531,7 @@ int hvws_stream_xor(hvws_ctx* c, uint8_t* d, uint64_t n, uint32_t pattern) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (((uintptr_t)d & 15u) != 0) return set_err(HVWS_EINVAL, "buffer must be 16-byte aligned");
-    HIP_OR(launch_stream_xor(unmask_variant(), d, n, pattern, c->stream), HVWS_EHIP);
+    HIP_OR(launch_stream_xor(unmask_variant_for(n), d, n, pattern, c->stream), HVWS_EHIP);
     return HVWS_OK;
 }
 
@@ -1791,6 +1791,8 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
 
 const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant()); }
 
+const char* hvws_unmask_kernel_name_for(uint64_t rx_len) { return unmask_name(unmask_variant_for(rx_len)); }
+
 uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
 
 uint64_t hvws_set_sieve_min(uint64_t bytes) { return set_sieve_min(bytes); }
@@ -1852,8 +1854,8 @@ int hvws_set_speculation(hvws_ctx* c, int mode) {
 }
 
 int hvws_set_unmask_variant(int v) {
-    if (set_unmask_variant(v) < 0) return set_err(HVWS_EINVAL, "unmask variant %d out of range [0,%d)", v,
-                                                  unmask_variant_count());
+    if (set_unmask_variant(v) < -1) return set_err(HVWS_EINVAL, "unmask variant %d out of range [-1,%d)", v,
+                                                   unmask_variant_count());
     return HVWS_OK;
 }
 

@@ -275,8 +275,9 @@ hipError_t launch_encode_keys(const uint8_t* keys, const uint64_t* key_off, cons
 uint64_t spec_min();
 uint64_t set_spec_min(uint64_t v);   // 0 = default; returns the previous value
 // k_unmask geometry variants (threads x chunks/thread, XCD-ordered tiles)
-int unmask_variant();                      // process default ($HVWS_UNMASK or 0)
-int set_unmask_variant(int v);             // -1 if out of range
+int unmask_variant();                      // the forced geometry, else the large-batch default
+int unmask_variant_for(uint64_t rx_len);   // the geometry a batch of rx_len bytes runs with
+int set_unmask_variant(int v);             // -1 = by batch size; -2 if out of range
 int unmask_variant_count();
 uint64_t unmask_tile(int variant);         // bytes per workgroup tile
 const char* unmask_name(int variant);

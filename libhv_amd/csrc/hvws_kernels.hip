@@ -1694,21 +1694,46 @@ struct unmask_geom {
     X(11, 512, 2, false)
 #define HVWS_GEOM_ENTRY(i, t, u, s) {t, u, s},
 static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
-static int g_geom = -1;
+
+// Geometry by batch size unless one is chosen ($HVWS_UNMASK, or
+// hvws_set_unmask_variant; -1 = back to this choice).  Pipelined steps,
+// interleaved runs on one box (profiles/r2l_raw): 512 x 2 in linear tile
+// order against the XCD-contiguous 256 x 4 -- c2 (1 GiB) 0.4195 vs 0.425
+// ms/step, c4 (4.3 GB, 1024 segments) 1.383 vs 1.510 ms; at c3 (68.7 GB) the
+// XCD-contiguous order wins, 20.92 vs 22.76 ms.  The single-step sweep over
+// uniform batches (profiles/r2c_raw/size_sweep.jsonl) puts the crossover at
+// 16 GiB.
+constexpr int kGeomSmall = 11;                        // 512 x 2, linear
+constexpr int kGeomLarge = 0;                         // 256 x 4, XCD-contiguous
+constexpr uint64_t kGeomLinearMax = 16ull << 30;     // bytes
+
+static int g_geom_forced = -2;   // -2: not yet read from the environment; -1: by size
+
+static int forced_geom() {
+    if (g_geom_forced == -2) {
+        const char* e = getenv("HVWS_UNMASK");
+        int v = e ? atoi(e) : -1;
+        if (v < -1 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) v = -1;
+        g_geom_forced = v;
+    }
+    return g_geom_forced;
+}
 
 int unmask_variant() {
-    if (g_geom < 0) {
-        const char* e = getenv("HVWS_UNMASK");
-        int v = e ? atoi(e) : 0;
-        if (v < 0 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) v = 0;
-        g_geom = v;
-    }
-    return g_geom;
+    const int f = forced_geom();
+    return f >= 0 ? f : kGeomLarge;
+}
+
+int unmask_variant_for(uint64_t rx_len) {
+    const int f = forced_geom();
+    if (f >= 0) return f;
+    return rx_len < kGeomLinearMax ? kGeomSmall : kGeomLarge;
 }
 
 int set_unmask_variant(int v) {
-    if (v < 0 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) return -1;
-    g_geom = v;
+    if (v < -1 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) return -2;
+    (void)forced_geom();
+    g_geom_forced = v;
     return v;
 }
 

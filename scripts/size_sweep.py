@@ -55,7 +55,7 @@ def main():
         for v in variants:
             L.hvws_set_unmask_variant(v)
             names[v] = L.hvws_unmask_kernel_name().decode()
-        L.hvws_set_unmask_variant(0)
+        L.hvws_set_unmask_variant(-1)
         out = {"gib": gib, "frames": n, "alg_bytes": alg,
                "GBps": {names[v]: round(alg / (float(np.median(times[v])) * 1e-3) / 1e9, 1) for v in variants}}
         print(json.dumps(out), flush=True)

@@ -352,6 +352,50 @@ def test_batch_dense_tiny_frames(eng, spec_min):
         _compare_batch(eng, buf, [(pad, len(data) - pad)])
 
 
+def test_unmask_geometries(eng):
+    """Every compiled k_unmask geometry (the engine picks one by batch size:
+    include/hvws.h hvws_set_unmask_variant) on batches with every tile class:
+    dense tiny frames (boundary chunks), mixed sizes with fragments and pings,
+    64 KiB frames (single-payload tiles), unmasked frames (empty tiles) --
+    bytes and frames bit-exact against the oracle."""
+    L = libhv_amd.lib()
+    rng = random.Random(4242)
+    k = b"\x9a\x5c\x33\xe1"
+    dense = [(0x2 | 0x10 | 0x20, rng.randbytes(rng.randint(0, 30)), rng.randbytes(4)) for _ in range(3000)]
+    cases = [np.frombuffer(bytes(5) + H.build_frames_ref(dense), np.uint8).copy()]
+    mplan = synth.mixed_plan(6 << 20, 4243, hi=1 << 18).split(13)
+    cases.append(H.synth_cpu(mplan))
+    uplan = synth.uniform_plan(40, 65536, 4244).split(3)
+    cases.append(H.synth_cpu(uplan))
+    plain = [(0x2 | 0x10, rng.randbytes(70000), None), (0x1 | 0x10 | 0x20, rng.randbytes(50000), k)] * 4
+    cases.append(np.frombuffer(H.build_frames_ref(plain), np.uint8).copy())
+    segss = [[(5, len(cases[0]) - 5)], mplan.segments, uplan.segments, [(0, len(cases[3]))]]
+    nvar = 0
+    while L.hvws_set_unmask_variant(nvar) == 0:
+        nvar += 1
+    assert nvar >= 12, nvar
+    try:
+        for buf, segs in zip(cases, segss):
+            exp_recs, _, _, exp = _oracle_batch(buf, segs, None)
+            for v in range(nvar):
+                assert L.hvws_set_unmask_variant(v) == 0
+                rx = eng.to_device(buf)
+                eng.step(rx, len(buf), segs, None)
+                got = rx.download(len(buf))
+                frames = eng.frames()
+                rx.free()
+                name = L.hvws_unmask_kernel_name().decode()
+                assert np.array_equal(got, exp), name
+                assert len(frames) == len(exp_recs), name
+                for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
+                    assert np.array_equal(frames[f], exp_recs[f]), (name, f)
+    finally:
+        L.hvws_set_unmask_variant(-1)
+    # by size: small batches run the linear geometry, 16 GiB and up the XCD-contiguous one
+    assert L.hvws_unmask_kernel_name_for(1 << 30).decode() == "k_unmask<512,2,linear>"
+    assert L.hvws_unmask_kernel_name_for(64 << 30).decode() == "k_unmask<256,4,xcd>"
+
+
 def test_long_segment_speculation_breaks(eng, spec_min):
     """Uniform runs verified in parallel, broken by a different size at many
     positions (the prefix verifier must stop exactly at the first break)."""
