@@ -505,12 +505,14 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_
     // walk (~0.2 ms at c4) waited for the whole unmask; between pieces it is
     // dispatched and overlaps.  On-device sweep: 4 pieces c4
     // 1.73 -> 1.55 ms, but c3 21.3 -> 22.4 ms and c2 flat, so uniform batches
-    // (SPEC: a short scan) keep one launch.  $HVWS_UNMASK_PIECES overrides.
+    // (SPEC: a short scan) keep one launch.  With the 512 x 2 linear geometry
+    // (round 2, profiles/r2n_raw) c4 ran 1.429 / 1.405 / 1.377 / 1.366 ms at
+    // 1 / 2 / 4 / 8 pieces: 8.  $HVWS_UNMASK_PIECES overrides.
     static const int env_pieces = getenv("HVWS_UNMASK_PIECES") ? atoi(getenv("HVWS_UNMASK_PIECES")) : -1;
     const int path = c->prev_path;   // the current scan's path may not be settled yet
     const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED || path == HVWS_PATH_SPEC_FAILED ||
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
-    const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 4u : 1u);
+    const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
     if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
                            c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(), c->T().total.as<uint64_t>(),
                            c->stream, pieces, timed ? c->tev[c->t_cur][2] : nullptr,
