@@ -28,29 +28,53 @@ __device__ __forceinline__ uint32_t tx_hdr_byte(uint32_t flags, uint64_t n, uint
 }
 
 // ---- device-wide exclusive scan of u64 (block sums, scan of sums, add) ----
-constexpr int SCAN_B = 1024;
+// 256-thread workgroups, 4 consecutive elements per thread (1024 per block).
+// Workgroups of 1024 threads waited 125-200 us each for a CU with 16 free
+// wave slots while a pipelined unmask held the device (the frame sieve's
+// scans, profiles/r2o_raw), against ~5 us alone.
+constexpr int SCAN_T = 256;
+constexpr int SCAN_I = 4;
+constexpr int SCAN_B = SCAN_T * SCAN_I;
 
-__global__ __launch_bounds__(SCAN_B) void k_scan_blocks(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
-                                                        uint64_t n, uint64_t* __restrict__ block_sums) {
-    __shared__ uint64_t s[SCAN_B];
-    const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
-    const uint64_t v = i < n ? in[i] : 0;
-    s[threadIdx.x] = v;
+__global__ __launch_bounds__(SCAN_T) void k_scan_blocks(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                        uint64_t n, uint64_t* __restrict__ block_sums,
+                                                        uint64_t* __restrict__ total_if_one) {
+    __shared__ uint64_t s[SCAN_T];
+    const uint32_t t = threadIdx.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)t * SCAN_I;
+    uint64_t v[SCAN_I], sum = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+        v[k] = i0 + k < n ? in[i0 + k] : 0;
+        sum += v[k];
+    }
+    s[t] = sum;
     __syncthreads();
-    for (int d = 1; d < SCAN_B; d <<= 1) {
-        const uint64_t a = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+    for (int d = 1; d < SCAN_T; d <<= 1) {
+        const uint64_t a = t >= (unsigned)d ? s[t - d] : 0;
         __syncthreads();
-        s[threadIdx.x] += a;
+        s[t] += a;
         __syncthreads();
     }
-    if (i < n) out[i] = s[threadIdx.x] - v;   // exclusive within the block
-    if (threadIdx.x == SCAN_B - 1) block_sums[blockIdx.x] = s[SCAN_B - 1];
+    uint64_t run = s[t] - sum;   // exclusive within the block
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+        if (i0 + k < n) out[i0 + k] = run;
+        run += v[k];
+    }
+    if (t == SCAN_T - 1) {
+        block_sums[blockIdx.x] = s[t];
+        if (total_if_one) *total_if_one = s[t];   // one block: its sum is the total
+    }
 }
 
-__global__ __launch_bounds__(SCAN_B) void k_add_block_base(uint64_t* __restrict__ out, uint64_t n,
+__global__ __launch_bounds__(SCAN_T) void k_add_block_base(uint64_t* __restrict__ out, uint64_t n,
                                                            const uint64_t* __restrict__ block_base) {
-    const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
-    if (i < n) out[i] += block_base[blockIdx.x];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_I;
+    const uint64_t b = block_base[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k)
+        if (i0 + k < n) out[i0 + k] += b;
 }
 
 // ------------------------------------------------------------- k_build
@@ -382,16 +406,12 @@ hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, 
     const uint64_t nb = (n + SCAN_B - 1) / SCAN_B;
     uint64_t* sums = tmp;
     uint64_t* base = tmp + nb;
-    hipLaunchKernelGGL(k_scan_blocks, dim3((uint32_t)nb), dim3(SCAN_B), 0, st, in, out, n, sums);
-    if (nb == 1) {
-        hipError_t e = hipMemsetAsync(base, 0, 8, st);
-        if (e != hipSuccess) return e;
-        e = hipMemcpyAsync(total, sums, 8, hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return e;
-    } else {
+    hipLaunchKernelGGL(k_scan_blocks, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, in, out, n, sums,
+                       nb == 1 ? total : (uint64_t*)nullptr);
+    if (nb > 1) {
         hipError_t e = launch_exclusive_scan(sums, base, nb, tmp + 2 * nb, total, st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_add_block_base, dim3((uint32_t)nb), dim3(SCAN_B), 0, st, out, n, base);
+        hipLaunchKernelGGL(k_add_block_base, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, out, n, base);
     }
     return hipGetLastError();
 }
