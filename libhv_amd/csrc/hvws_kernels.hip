@@ -825,10 +825,15 @@ __device__ __forceinline__ void offsets_body(const uint64_t* __restrict__ counts
     if (t == NT - 1u) *total = part[NT - 1u];
 }
 
-__global__ __launch_bounds__(1024) void k_offsets(const uint64_t* __restrict__ counts,
-                                                  uint64_t* __restrict__ bases, uint32_t nseg,
-                                                  uint64_t* __restrict__ total) {
-    offsets_body<1024>(counts, bases, nseg, total);
+// Single-block kernels of the scan chains run as 256-thread workgroups: a
+// 1024-thread one (16 waves on one CU) waited tens of us for slots beside a
+// pipelined unmask (k_offsets 6 -> 66 us in profiles/r2h_raw/c2_trace.csv).
+constexpr uint32_t ONE_BLOCK = 256;
+
+__global__ __launch_bounds__(ONE_BLOCK) void k_offsets(const uint64_t* __restrict__ counts,
+                                                       uint64_t* __restrict__ bases, uint32_t nseg,
+                                                       uint64_t* __restrict__ total) {
+    offsets_body<ONE_BLOCK>(counts, bases, nseg, total);
 }
 
 // ----------------------------------------------------------- k_spec_check
@@ -895,12 +900,12 @@ __device__ __forceinline__ void spec_check_body(const uint64_t* __restrict__ cou
 }
 
 template <bool SPEC>
-__global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict__ counts,
+__global__ __launch_bounds__(ONE_BLOCK) void k_spec_check(const uint64_t* __restrict__ counts,
                                                      const uint64_t* __restrict__ est,
                                                      const uint64_t* __restrict__ npred, uint32_t nseg,
                                                      uint64_t* __restrict__ total, uint64_t cap,
                                                      dspec_status* __restrict__ status, uint64_t seq) {
-    spec_check_body<SPEC, 1024>(counts, est, npred, nseg, total, cap, status, seq, true);
+    spec_check_body<SPEC, ONE_BLOCK>(counts, est, npred, nseg, total, cap, status, seq, true);
 }
 
 // ----------------------------------------------------------- SLACK table
@@ -913,16 +918,16 @@ __global__ __launch_bounds__(1024) void k_spec_check(const uint64_t* __restrict_
 // zeroes the count (downstream kernels do nothing) and the host re-scans
 // COUNT, read, EMIT -- so a mixed batch is discovered with one walk and no
 // host round trip before EMIT, like SPEC for uniform ones.
-__global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict__ counts,
+__global__ __launch_bounds__(ONE_BLOCK) void k_slack_check(const uint64_t* __restrict__ counts,
                                                       const uint64_t* __restrict__ est,
                                                       const uint64_t* __restrict__ est_u,
                                                       const uint64_t* __restrict__ npred, uint32_t nseg,
                                                       uint64_t* __restrict__ bases_x, uint64_t* __restrict__ total,
                                                       uint64_t cap, dspec_status* __restrict__ status, uint64_t seq) {
-    __shared__ uint64_t part[1024], pmax[1024 / 64];
-    __shared__ uint32_t pbad[1024 / 64];
+    __shared__ uint64_t part[ONE_BLOCK], pmax[ONE_BLOCK / 64];
+    __shared__ uint32_t pbad[ONE_BLOCK / 64];
     const uint32_t t = threadIdx.x;
-    const uint32_t per = (nseg + 1023u) / 1024u;
+    const uint32_t per = (nseg + ONE_BLOCK - 1u) / ONE_BLOCK;
     const uint32_t b = t * per;
     const uint32_t e = min(nseg, b + per);
     uint64_t sum = 0, mx = 0;
@@ -935,7 +940,7 @@ __global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict
         if (npred[i]) bad |= 4u;                                       // 4: a long uniform run (keep k_verify)
     }
     part[t] = sum;
-    for (int o = 32; o > 0; o >>= 1) {   // max and flags: wave reductions, then 16 partials
+    for (int o = 32; o > 0; o >>= 1) {   // max and flags: wave reductions, then one partial per wave
         const uint64_t m2 = __shfl_xor(mx, o);
         mx = m2 > mx ? m2 : mx;
         bad |= __shfl_xor(bad, o);
@@ -945,7 +950,7 @@ __global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict
         pbad[t >> 6] = bad;
     }
     __syncthreads();
-    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+    for (uint32_t d = 1; d < ONE_BLOCK; d <<= 1) {
         const uint64_t v = t >= d ? part[t - d] : 0;
         __syncthreads();
         part[t] += v;
@@ -959,11 +964,11 @@ __global__ __launch_bounds__(1024) void k_slack_check(const uint64_t* __restrict
     if (t == 0) {
         uint64_t amax = 0;
         uint32_t any_bad = 0;
-        for (uint32_t k = 0; k < 1024u / 64; ++k) {
+        for (uint32_t k = 0; k < ONE_BLOCK / 64; ++k) {
             amax = pmax[k] > amax ? pmax[k] : amax;
             any_bad |= pbad[k];
         }
-        const uint64_t all = part[1023];
+        const uint64_t all = part[ONE_BLOCK - 1u];
         const bool ok = !(any_bad & 1u) && all <= cap;
         *total = ok ? all : 0;
         status->total = all;
@@ -1552,7 +1557,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, (int)(pass == SCAN_SINGLE && sieve),
                            pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
                            pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, 0u);
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
     };
@@ -1582,7 +1587,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0,
                            pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
                            pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY);
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, est, bases, nseg, total);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, est, bases, nseg, total);
         hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 1,
                            (const dsieve*)nullptr, (const uint64_t*)nullptr, carry_in);
@@ -1593,35 +1598,35 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         if (sieve && (e = launch_sieve(rx, rx_len, segs, sc.mid, sc.npred, *sc.sieve, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(bases, 0, (size_t)nseg * 8, st)) != hipSuccess) return e;
         if ((e = emit(1, fr)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, counts, bases, nseg, total);
     } else if (pass == SCAN_SPEC) {
         if (sc.no_verify) {
             head_walk(sc.est, fr);
         } else {
             head_count(sc.est);
-            hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
+            hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, sc.est, bases, nseg, total);
             if (hipError_t e = emit(1, fr); e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.npred, nseg, total,
+        hipLaunchKernelGGL(k_spec_check<true>, dim3(1), dim3(ONE_BLOCK), 0, st, counts, sc.est, sc.npred, nseg, total,
                            fr.cap, sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
         head_count(sc.status ? sc.est : nullptr);
         hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0,
                            (const dsieve*)nullptr, (const uint64_t*)nullptr, (const dcarry*)nullptr);
-        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+        hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, counts, bases, nseg, total);
         if (sc.status)
-            hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.npred, nseg, total,
+            hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(ONE_BLOCK), 0, st, counts, sc.est, sc.npred, nseg, total,
                                fr.cap, sc.status, sc.seq);
     } else if (pass == SCAN_SLACK) {
         if (sc.no_verify) {
             head_walk(sc.est, sc.slack);
         } else {
             head_count(sc.est);
-            hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, sc.est, bases, nseg, total);
+            hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, sc.est, bases, nseg, total);
             if (hipError_t e = emit(1, sc.slack); e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_slack_check, dim3(1), dim3(1024), 0, st, counts, sc.est, sc.est_u, sc.npred, nseg, sc.bases_x,
+        hipLaunchKernelGGL(k_slack_check, dim3(1), dim3(ONE_BLOCK), 0, st, counts, sc.est, sc.est_u, sc.npred, nseg, sc.bases_x,
                            total, fr.cap, sc.status, sc.seq);
         hipLaunchKernelGGL(k_slack_compact, dim3(nseg < 65535u ? nseg : 65535u), dim3(256), 0, st, sc.slack, fr, counts,
                            bases, sc.bases_x, total, nseg);
@@ -1633,7 +1638,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
 
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st) {
-    hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, st, counts, bases, nseg, total);
+    hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, counts, bases, nseg, total);
     return hipGetLastError();
 }
 
