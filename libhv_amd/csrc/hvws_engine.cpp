@@ -213,7 +213,6 @@ struct hvws_ctx {
     static constexpr int kTimeRing = 32;
     hipEvent_t tev[kTimeRing][4] = {};
     bool t_unmask[kTimeRing] = {};
-    bool t_adjacent[kTimeRing] = {};   // unmask started at the scan's end event
     uint8_t t_rec[kTimeRing] = {};      // which of the slot's 4 events were recorded (bit i)
     uint64_t t_seq = 0;   // scans recorded so far
     int t_cur = 0;        // ring slot of the last scan
@@ -363,10 +362,9 @@ int step_times_at(hvws_ctx* c, int slot, float* out) {
         HIP_OR(hipEventSynchronize(e[1]), HVWS_EHIP);
         HIP_OR(hipEventElapsedTime(&out[0], e[0], e[1]), HVWS_EHIP);
     }
-    const int start = c->t_adjacent[slot] ? 1 : 2;
-    if (c->t_unmask[slot] && (r & (1u << start)) && (r & 8u)) {
+    if (c->t_unmask[slot] && (r & 4u) && (r & 8u)) {
         HIP_OR(hipEventSynchronize(e[3]), HVWS_EHIP);
-        HIP_OR(hipEventElapsedTime(&out[1], e[start], e[3]), HVWS_EHIP);
+        HIP_OR(hipEventElapsedTime(&out[1], e[2], e[3]), HVWS_EHIP);
     }
     return HVWS_OK;
 }
@@ -488,18 +486,15 @@ uint32_t pscan_blocks(hvws_ctx* c) {
     return c->pscan_blocks;
 }
 
-// Unmask kernel launch with its timing events (no argument checks);
-// after_scan: queued right behind the scan (kept for the call sites; the
-// events now ride on the unmask's own dispatch either way).
-hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
+// Unmask kernel launch with its timing events (no argument checks).  The
+// events ride on the unmask's own dispatch (launch_unmask).
+hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     hipError_t e;
     const bool piped = c->cs != c->stream;
     if (piped) {   // the scan ran on the side stream: join it
         if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
     }
-    (void)after_scan;
-    c->t_adjacent[c->t_cur] = false;
     const bool timed = step_events(c) >= 1;
     // Pipelined steps of mixed multi-segment batches: the unmask in pieces.
     // The hardware dispatches a kernel queued on the second stream (the next
@@ -720,7 +715,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             if ((rc = tiles()) != HVWS_OK) return rc;
             if (unmask_into) {
                 HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
-                HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
@@ -803,7 +798,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             }
             if (unmask_into) {
                 HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
-                HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
@@ -859,7 +854,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             if ((rc = tiles()) != HVWS_OK) return rc;
             if (unmask_into) {
                 HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
-                HIP_OR(issue_unmask(c, unmask_into, rx_len, true), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len), HVWS_EHIP);
             }
             if ((rc = wait_status(c, sc.seq)) != HVWS_OK) return rc;
             if ((rc = read_status(nfr, flags)) != HVWS_OK) return rc;
@@ -1167,15 +1162,14 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     return HVWS_OK;
 }
 
-// Unmask launch.  after_scan: queued right behind the scan's end event,
-// which then doubles as the unmask's start (one timing marker fewer).
-int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool after_scan) {
+// Unmask launch after a scan of the same buffer.
+int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (!c->have_scan) return set_err(HVWS_EINVAL, "hvws_unmask without a preceding hvws_scan");
     if (d_rx != c->rx || rx_len != c->rx_len)
         return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
-    HIP_OR(issue_unmask(c, d_rx, rx_len, after_scan), HVWS_EHIP);
+    HIP_OR(issue_unmask(c, d_rx, rx_len), HVWS_EHIP);
     return HVWS_OK;
 }
 
@@ -1392,7 +1386,7 @@ int hvws_scan(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, const hvws_segm
     return scan_device_carry(c, d_rx, rx_len, nseg);
 }
 
-int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) { return unmask_impl(c, d_rx, rx_len, false); }
+int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) { return unmask_impl(c, d_rx, rx_len); }
 
 int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
                        const websocket_parser* carry_in, uint32_t nseg) {
@@ -1414,7 +1408,7 @@ int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_s
     c->cs = c->sstream;
     bool unmasked = false;
     rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked);
-    if (rc == HVWS_OK && !unmasked) rc = unmask_impl(c, d_rx, rx_len, false);
+    if (rc == HVWS_OK && !unmasked) rc = unmask_impl(c, d_rx, rx_len);
     c->cs = c->stream;
     return rc;
 }
@@ -1428,7 +1422,7 @@ int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* s
     if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
     bool unmasked = false;
     if ((rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked)) != HVWS_OK) return rc;
-    return unmasked ? HVWS_OK : unmask_impl(c, d_rx, rx_len, true);
+    return unmasked ? HVWS_OK : unmask_impl(c, d_rx, rx_len);
 }
 
 int64_t hvws_frame_count(hvws_ctx* c) {
@@ -1561,7 +1555,7 @@ int hvws_rx_batch(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* 
     bool unmasked = false;
     if ((rc = scan_device_carry(c, d, len, nseg, unmask ? d : nullptr, &unmasked)) != HVWS_OK) return rc;
     if (unmask) {
-        if (!unmasked && (rc = unmask_impl(c, d, len, true)) != HVWS_OK) return rc;
+        if (!unmasked && (rc = unmask_impl(c, d, len)) != HVWS_OK) return rc;
         if (len) HIP_OR(hipMemcpyAsync(h_rx, d, len, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     }
     // one round trip for the results (the D2H of the bytes above is ordered before it)

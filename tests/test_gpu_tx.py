@@ -71,6 +71,22 @@ def test_build_random_vs_reference(eng, seed):
     assert off.tolist() == list(np.cumsum([0] + sizes[:-1]))
 
 
+@pytest.mark.parametrize("seed", [21, 22])
+def test_build_small_frames_vs_reference(eng, seed):
+    """Small frames only (every output <= 2026 bytes, 1 KiB-class frames:
+    every output tile a boundary tile), misaligned payload offsets, all
+    length classes up to the 16-bit one, tiny frames sharing output chunks;
+    frame by frame against the reference."""
+    rng = np.random.default_rng(seed)
+    lens = np.concatenate([rng.integers(0, 20, 300), rng.integers(120, 130, 100), rng.integers(1000, 2019, 300)])
+    rng.shuffle(lens)
+    frames = _frames(rng, len(lens), lens=lens)
+    got, off = _gpu_build(eng, frames, gap_rng=rng, with_off=True)
+    assert got == H.build_frames_ref(frames)
+    sizes = [len(H.build_frames_ref([f])) for f in frames]
+    assert off.tolist() == list(np.cumsum([0] + sizes[:-1]))
+
+
 def test_build_length_edges(eng):
     rng = np.random.default_rng(7)
     for p_mask in (0.0, 1.0, 0.5):
