@@ -267,7 +267,7 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
                         uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
-                        hipStream_t st);
+                        hipStream_t st, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 // Batched handshake digest (hvws_keys.hip): accept[32*i..] = base64(SHA-1(key_i + GUID)), 28 chars + 4 zero bytes.
 hipError_t launch_encode_keys(const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len, uint64_t n,
                               uint8_t* accept, hipStream_t st);

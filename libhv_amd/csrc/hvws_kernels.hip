@@ -789,10 +789,12 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
                         uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
-                        hipStream_t st) {
+                        hipStream_t st, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (nseg == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_small, dim3(nseg), dim3(64), 0, st, rx, rx_len, segs, carry_in, slot_base, slots, rec_total,
-                       h_rec, h_rec_cap, h_out, h_rx, unmask, vmask);
+    // timing events on the dispatch itself: no marker packets around a
+    // launch whose whole round trip is the latency FeedRecvData pays
+    hipExtLaunchKernelGGL(k_small, dim3(nseg), dim3(64), 0, st, ev_start, ev_stop, 0u, rx, rx_len, segs, carry_in,
+                          slot_base, slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask);
     return hipGetLastError();
 }
 
