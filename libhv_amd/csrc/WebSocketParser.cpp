@@ -28,6 +28,32 @@ void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask,
 }  // namespace hvws
 
 namespace {
+// Gather (to_stage) or scatter the n chunks through the pinned stage, split
+// into byte-balanced runs of chunks over the host copy pool.
+void stage_copy(char* stage, const hvws_segment* segs, const char* const* data, const size_t* len, int n,
+                uint64_t total, bool to_stage) {
+    auto one = [&](int i) {
+        if (!len[i]) return;
+        if (to_stage) memcpy(stage + segs[i].off, data[i], len[i]);
+        else memcpy(const_cast<char*>(data[i]), stage + segs[i].off, len[i]);
+    };
+    const int w = total >= hvws::kParCopyMin ? hvws::copy_width() : 1;
+    if (w <= 1) {
+        for (int i = 0; i < n; ++i) one(i);
+        return;
+    }
+    std::vector<int> cut(1, 0);   // run r covers chunks [cut[r], cut[r+1])
+    const uint64_t share = (total + w - 1) / w;
+    for (int i = 0; i < n; ++i)
+        if (segs[i].off + len[i] >= share * cut.size() && i + 1 < n) cut.push_back(i + 1);
+    cut.push_back(n);
+    hvws::par_for((int)cut.size() - 1, [&](int r) {
+        for (int i = cut[r]; i < cut[r + 1]; ++i) one(i);
+    });
+}
+}  // namespace
+
+namespace {
 const int kMaxReserve = 1 << 24;   // MAX_PAYLOAD_LENGTH, reference WebSocketParser.cpp:6
 }
 
@@ -145,8 +171,7 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
         hvws::copy_parser(carry[i], *parsers[i]->parser);
     }
     char* stage = hvws::pinned_stage(total);
-    for (int i = 0; i < n; ++i)
-        if (len[i]) memcpy(stage + segs[i].off, data[i], len[i]);
+    stage_copy(stage, segs.data(), data, len, n, total, true);
     hvws_ctx* c = hvws::thread_ctx();
     if (hvws_rx_batch(c, (uint8_t*)stage, total, segs.data(), carry.data(), (uint32_t)n, 1) != HVWS_OK)
         hvws::fatal("hvws_rx_batch");
@@ -158,8 +183,7 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
         hvws::fatal("frame table read-back");
     // Every segment leaves the (thread's, reusable) stage before any callback
     // runs: an onMessage that feeds again on this thread restages it.
-    for (int i = 0; i < n; ++i)
-        if (len[i]) memcpy(const_cast<char*>(data[i]), stage + segs[i].off, len[i]);   // in place, like the reference
+    stage_copy(stage, segs.data(), data, len, n, total, false);   // in place, like the reference
     for (int i = 0; i < n; ++i) {
         char* dst = const_cast<char*>(data[i]);
         carry[i].data = parsers[i]->parser->data;

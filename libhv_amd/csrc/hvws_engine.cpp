@@ -1098,7 +1098,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
         hb[s] = nslots;
         nslots += segs[s].len / 2 + 3;   // carried-in frame + >= 2 bytes per frame + tail
     }
-    if (!user_mapped && len) memcpy(hp + o_data, h_rx, len);
+    if (!user_mapped && len) par_memcpy(hp + o_data, h_rx, len);
     const uint64_t hcap = std::min<uint64_t>(nslots, kSmallHostRecords);
     HIP_OR(c->d_small_slots.ensure(nslots * sizeof(drec) + 64), HVWS_ENOMEM);
     HIP_OR(c->h_small_out.ensure((uint64_t)nseg * sizeof(dsmall_out) + hcap * sizeof(drec) + 64), HVWS_ENOMEM);
@@ -1123,7 +1123,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     if (timed) c->t_rec[c->t_cur] |= 3u;
     else HIP_OR(tev_record(c, 1, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
-    if (!user_mapped && unmask && len) memcpy(h_rx, hp + o_data, len);
+    if (!user_mapped && unmask && len) par_memcpy(h_rx, hp + o_data, len);
     // host cache in segment order
     uint64_t total = 0;
     for (uint32_t s = 0; s < nseg; ++s) total += ho[s].count;

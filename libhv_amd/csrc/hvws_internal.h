@@ -6,6 +6,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <functional>
+
 #include "websocket_parser.h"
 
 namespace hvws {
@@ -268,6 +270,13 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
                         uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
                         hipStream_t st, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
+// copy_width() threads (the caller included; serial when another caller
+// holds the pool); par_memcpy splits copies of >= kParCopyMin bytes.
+constexpr uint64_t kParCopyMin = 1ull << 20;
+int copy_width();
+void par_for(int n, const std::function<void(int)>& fn);
+void par_memcpy(void* dst, const void* src, uint64_t n);
 // Batched handshake digest (hvws_keys.hip): accept[32*i..] = base64(SHA-1(key_i + GUID)), 28 chars + 4 zero bytes.
 hipError_t launch_encode_keys(const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len, uint64_t n,
                               uint8_t* accept, hipStream_t st);

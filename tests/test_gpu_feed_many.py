@@ -180,3 +180,19 @@ def test_feed_many_reentrant_callback():
         c.rets.append(rets[i])
     assert fired, "connection 0 delivered no message"
     _check(conns + [inner])
+
+
+def test_feed_many_large_poll_iteration():
+    """Poll iterations of ~2 MiB (256 connections x 8 KiB reads): the gather
+    into and scatter out of the pinned stage split over the host copy pool
+    (hvws_hostpool.cpp, batches >= 1 MiB).  Chunks land back in the right
+    connections' buffers and every connection matches the reference."""
+    rng = random.Random(31)
+    conns = []
+    for _ in range(256):
+        data = S.rand_stream(rng, rng.randint(4, 12), max_len=rng.choice([600, 9000]))
+        chunks = [8192] * (len(data) // 8192) + ([len(data) % 8192] if len(data) % 8192 else [])
+        conns.append(Conn(data, chunks))
+    _loop(random.Random(5), conns)
+    assert sum(len(c.data) for c in conns) > 2 << 20
+    _check(conns)
