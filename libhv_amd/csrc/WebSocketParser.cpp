@@ -10,9 +10,11 @@
 //   end:    on FIN, onMessage(opcode, message)                        (:39-50)
 #include "WebSocketParser.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <unordered_set>
 #include <vector>
 
@@ -158,9 +160,33 @@ int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, con
     return n;
 }
 
+namespace {
+// $HVWS_FEED_TIMES=1: per-phase host time of feed_distinct, printed at exit (diagnostic)
+struct feed_times {
+    double ph[5] = {0, 0, 0, 0, 0};
+    long calls = 0;
+    bool on = getenv("HVWS_FEED_TIMES") && atoi(getenv("HVWS_FEED_TIMES"));
+    ~feed_times() {
+        if (on && calls)
+            fprintf(stderr, "[feed_times] calls=%ld us/call: carry %.1f gather %.1f gpu %.1f scatter %.1f replay %.1f\n",
+                    calls, ph[0] / calls, ph[1] / calls, ph[2] / calls, ph[3] / calls, ph[4] / calls);
+    }
+} g_ft;
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
 static int feed_distinct(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
                          int* rets) {
     if (n <= 0) return 0;
+    double t0 = g_ft.on ? now_us() : 0, t1;
+    auto lap = [&](int k) {
+        if (!g_ft.on) return;
+        t1 = now_us();
+        g_ft.ph[k] += t1 - t0;
+        t0 = t1;
+    };
     std::vector<hvws_segment> segs((size_t)n);
     std::vector<websocket_parser> carry((size_t)n);
     uint64_t total = 0;
@@ -170,8 +196,10 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
         total += len[i];
         hvws::copy_parser(carry[i], *parsers[i]->parser);
     }
+    lap(0);
     char* stage = hvws::pinned_stage(total);
     stage_copy(stage, segs.data(), data, len, n, total, true);
+    lap(1);
     hvws_ctx* c = hvws::thread_ctx();
     if (hvws_rx_batch(c, (uint8_t*)stage, total, segs.data(), carry.data(), (uint32_t)n, 1) != HVWS_OK)
         hvws::fatal("hvws_rx_batch");
@@ -181,9 +209,11 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
     if ((nf > 0 && hvws_get_frames(c, frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
         hvws_get_segment_frames(c, first.data(), count.data()) != HVWS_OK)
         hvws::fatal("frame table read-back");
+    lap(2);
     // Every segment leaves the (thread's, reusable) stage before any callback
     // runs: an onMessage that feeds again on this thread restages it.
     stage_copy(stage, segs.data(), data, len, n, total, false);   // in place, like the reference
+    lap(3);
     for (int i = 0; i < n; ++i) {
         char* dst = const_cast<char*>(data[i]);
         carry[i].data = parsers[i]->parser->data;
@@ -191,6 +221,8 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
             replay_messages(parsers[i], dst, segs[i].off, frames.data() + first[i], (size_t)count[i], carry[i], len[i]);
         if (rets) rets[i] = (int)used;
     }
+    lap(4);
+    g_ft.calls += g_ft.on;
     return n;
 }
 
