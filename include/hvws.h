@@ -146,7 +146,10 @@ int     hvws_get_carry(hvws_ctx* ctx, websocket_parser* out, int* started);
 /* Device time (ms, HIP events on the ctx stream) of the last scan and
  * unmask: out[0] = scan kernels (count + offsets + emit + tile index),
  * out[1] = unmask kernel.  A pipelined step (hvws_step_resident) records the
- * unmask's events only: its out[0] is -1 ($HVWS_STEP_EVENTS=2 records both). */
+ * unmask's events only: its out[0] is -1 ($HVWS_STEP_EVENTS=2 records both).
+ * The small-batch path (reads of an event loop) records none unless
+ * $HVWS_STEP_EVENTS=2: out[0] = out[1] = -1 (an event-carrying launch costs
+ * ~10 us of a ~30 us read). */
 int hvws_last_times(hvws_ctx* ctx, float out[2]);
 /* The same for each of the last min(max_steps, 32) scans, oldest first:
  * out[2*i] = scan ms, out[2*i+1] = unmask ms (-1 if the step had none).
@@ -306,6 +309,14 @@ uint32_t hvws_set_validation(hvws_ctx* ctx, uint32_t classes);
  * reference-API entry points.  Returns the previous limit.  Results are identical
  * either way; only latency differs. */
 uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
+
+/* Small batches whose segments are all <= 32 KiB (total <= 1 MiB; an event
+ * loop's reads) are read by the device straight from pinned host memory, each
+ * segment staged in LDS, with no H2D copy ahead of the launch (on = 1, the
+ * default; $HVWS_SMALL_ZC=0 turns it off for new contexts).  ctx NULL = the
+ * calling thread's context.  Returns the previous setting.  Results are
+ * identical either way; only latency differs. */
+int hvws_set_small_zero_copy(hvws_ctx* ctx, int on);
 
 /* Host-inclusive streaming unmask of a large pinned host buffer holding
  * frames back to back from one stream: chunked H2D -> scan -> unmask -> D2H,

@@ -165,6 +165,7 @@ _SIGS = {
     "hvws_last_sieve": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
+    "hvws_set_small_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),
     "hvws_set_unmask_variant": (ctypes.c_int, [ctypes.c_int]),
     # reference ABI (include/websocket_parser.h, include/wsdef.h)

@@ -195,6 +195,12 @@ struct hvws_ctx {
     hbuf h_feed;   // hvws_feed_many's gather buffer (reference-API thread contexts)
     dbuf d_small_in, d_small_slots;
     uint64_t small_limit = 0;   // bytes; 0 = default
+    // k_small's record counter lives on the device and only ever grows; a
+    // call's records start at small_ctr_base
+    dbuf d_small_ctr;
+    uint64_t small_ctr_base = 0;
+    bool small_ctr_dirty = true;   // unknown value (first use, failed call): zero it
+    int small_zc = 1;              // $HVWS_SMALL_ZC / hvws_set_small_zero_copy
     uint32_t vmask = 0;         // protocol validation classes (V_*); 0 = reference behaviour
     // transmit side (hvws_build_frames)
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat;
@@ -1080,6 +1086,14 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     const uint64_t o_data = (o_slot + (uint64_t)nseg * 8 + 255) & ~255ull;
     uint8_t* user_mapped = host_mapped(h_rx);   // pinned caller buffer: read and write it directly
     const uint64_t pkt = user_mapped ? o_data : o_data + len;
+    // Segments of event-loop size are staged in LDS by k_small; small
+    // batches of them may also go zero-copy (the kernel reads the packet and
+    // the bytes from pinned host memory, no H2D copy ahead of the launch).
+    uint64_t max_seg = 0;
+    for (uint32_t s = 0; s < nseg; ++s) max_seg = std::max<uint64_t>(max_seg, segs[s].len);
+    const bool stage = max_seg <= kStageSegment;
+    const bool zc = stage && c->small_zc && len <= kZcBatch;
+    const uint32_t stage_lds = stage ? (uint32_t)(((max_seg + 15) & ~15ull) + 16) : 0u;
     // The pinned packet may still be the source of an in-flight copy.
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     HIP_OR(c->h_small_in.ensure(o_data + len + 64), HVWS_ENOMEM);
@@ -1107,26 +1121,44 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     dsmall_out* ho_d = mapped<dsmall_out>(c->h_small_out);
     uint8_t* hp_d = mapped<uint8_t>(c->h_small_in);
     if (!ho_d || !hp_d) return set_err(HVWS_EHIP, "pinned buffers not device-mapped");
-    uint8_t* d = c->d_small_in.as<uint8_t>();
-    HIP_OR(hipMemcpyAsync(d, hp, pkt, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
-    if (user_mapped && len) HIP_OR(hipMemcpyAsync(d + o_data, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
-    // timing events ride on the k_small dispatch (against marker packets:
-    // per-read latency unchanged at ~45 us, profiles/r2aa_raw)
-    const bool timed = step_events(c) >= 2;
-    HIP_OR(begin_timed_scan(c, !timed), HVWS_EHIP);
-    HIP_OR(launch_small(d + o_data, len, (const dseg*)(d + o_segs), (const dcarry*)(d + o_carry), nseg,
-                        (const uint64_t*)(d + o_slot), c->d_small_slots.as<drec>(), (unsigned long long*)d,
+    // Record counter: device memory, only ever grows; this call's records
+    // start at small_ctr_base (no per-call reset operation).
+    HIP_OR(c->d_small_ctr.ensure(64), HVWS_ENOMEM);
+    unsigned long long* ctr = c->d_small_ctr.as<unsigned long long>();
+    if (c->small_ctr_dirty) {
+        HIP_OR(hipMemsetAsync(ctr, 0, 8, c->stream), HVWS_EHIP);
+        c->small_ctr_base = 0;
+        c->small_ctr_dirty = false;
+    }
+    const uint64_t ctr_base = c->small_ctr_base;
+    c->small_ctr_dirty = true;   // until this call's record total is known
+    uint8_t* d = hp_d;           // zero-copy: the kernel reads the pinned packet in place
+    if (!zc) {
+        d = c->d_small_in.as<uint8_t>();
+        HIP_OR(hipMemcpyAsync(d, hp, pkt, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
+        if (user_mapped && len)
+            HIP_OR(hipMemcpyAsync(d + o_data, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
+    }
+    const uint8_t* d_rx = zc ? (user_mapped ? user_mapped : hp_d + o_data) : d + o_data;
+    // No timing events unless $HVWS_STEP_EVENTS >= 2 asks for them: an
+    // event-carrying launch costs a per-read call ~10 us of ~38 (r2an).
+    static const bool timed_env = getenv("HVWS_STEP_EVENTS") && atoi(getenv("HVWS_STEP_EVENTS")) >= 2;
+    const bool timed = timed_env;
+    HIP_OR(begin_timed_scan(c, false), HVWS_EHIP);
+    HIP_OR(launch_small(d_rx, len, (const dseg*)(d + o_segs), (const dcarry*)(d + o_carry), nseg,
+                        (const uint64_t*)(d + o_slot), c->d_small_slots.as<drec>(), ctr, ctr_base,
                         (drec*)(ho_d + nseg), hcap, ho_d, user_mapped ? user_mapped : hp_d + o_data, unmask,
-                        c->vmask, c->stream, timed ? c->tev[c->t_cur][0] : nullptr,
+                        c->vmask, stage_lds, c->stream, timed ? c->tev[c->t_cur][0] : nullptr,
                         timed ? c->tev[c->t_cur][1] : nullptr),
            HVWS_EHIP);
     if (timed) c->t_rec[c->t_cur] |= 3u;
-    else HIP_OR(tev_record(c, 1, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (!user_mapped && unmask && len) par_memcpy(h_rx, hp + o_data, len);
     // host cache in segment order
     uint64_t total = 0;
     for (uint32_t s = 0; s < nseg; ++s) total += ho[s].count;
+    c->small_ctr_base = ctr_base + total;
+    c->small_ctr_dirty = false;
     c->hcache.resize(total);
     c->hfirst.resize(nseg);
     c->hcount.resize(nseg);
@@ -1219,6 +1251,7 @@ hvws_ctx* hvws_ctx_create(int device) {
     // so no stale copy can sit in a device cache across reuses.
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
+    if (const char* zc = getenv("HVWS_SMALL_ZC")) c->small_zc = atoi(zc) ? 1 : 0;
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
     if (const char* wv = getenv("HVWS_WALK_VERIFY")) c->verify_mode = atoi(wv) < 0 ? -1 : (atoi(wv) ? 1 : 0);
     // The pipelined scan stream at the highest priority: a scan kernel of
@@ -1799,6 +1832,13 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
     if (!c) c = hvws::thread_ctx();   // the calling thread's reference-API context
     const uint64_t old = c->small_limit ? c->small_limit : kSmallBatch;
     c->small_limit = bytes;
+    return old;
+}
+
+int hvws_set_small_zero_copy(hvws_ctx* c, int on) {
+    if (!c) c = hvws::thread_ctx();
+    const int old = c->small_zc;
+    c->small_zc = on ? 1 : 0;
     return old;
 }
 

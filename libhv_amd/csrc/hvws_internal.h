@@ -265,11 +265,17 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
 // Small batches, whole path in one launch (one wave per segment): records
 // into slots[slot_base[s]..], then compacted into h_rec (pinned host) when
 // they fit h_rec_cap; results into h_out[s]; unmasked chunks into h_rx
-// (pinned host, same layout as rx).  *rec_total must be 0 on entry.
+// (pinned host, same layout as rx).  *rec_total (device) must equal rec_base
+// on entry and advances by the records written.  stage_lds != 0: each segment
+// is staged in stage_lds bytes of LDS (>= its 16-aligned span + 16); rx,
+// segs, carry_in and slot_base may then be pinned host memory read in place
+// (zero-copy).
+constexpr uint64_t kStageSegment = 32ull << 10;   // largest segment k_small stages in LDS
+constexpr uint64_t kZcBatch = 1ull << 20;         // largest batch sent zero-copy
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
-                        const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
-                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
-                        hipStream_t st, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+                        const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, uint64_t rec_base,
+                        drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
+                        uint32_t stage_lds, hipStream_t st, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 // Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
 // copy_width() threads (the caller included; serial when another caller
 // holds the pool); par_memcpy splits copies of >= kParCopyMin bytes.

@@ -686,23 +686,193 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_walk(const uint8_t* __restrict
 // Small batches (an event loop's reads, FeedRecvData): one wavefront per
 // segment runs the whole hot path in a single launch -- the carried-in frame
 // (exact state machine), the speculative walk and the tail (the same device
-// code as the COUNT/EMIT kernels), records into a slot the host sized from the
-// segment length, then the XOR of the segment's masked payload bytes -- and
-// writes its results straight into pinned host memory: the changed 16-byte
-// chunks, the records (compacted by one atomic per segment), the count and the
-// carry.  One H2D copy, one launch and one sync replace the ~15 operations of
-// the general path, whose fixed cost dominates reads of a few KiB.
+// code as the COUNT/EMIT kernels), records, then the XOR of the segment's
+// masked payload bytes -- and writes its results straight into pinned host
+// memory: the changed 16-byte chunks, the records (compacted by one atomic per
+// segment), the count and the carry.  One launch and one sync (plus one H2D
+// copy unless zero-copy) replace the ~15 operations of the general path,
+// whose fixed cost dominates reads of a few KiB.
+//
+// A read's time is a chain of dependent memory round trips (~1 us each to HBM,
+// several us across PCIe), so STAGE (segments <= kZcSegment) first pulls the
+// whole segment into LDS in one round of 16-byte loads; the walk, the tail and
+// the XOR then read LDS, and the records stay in LDS (the first SMALL_LREC of
+// them; more spill to the device slot).  `rx` handed to the body is a flat
+// pointer biased so absolute offsets in [sb, se) land in LDS, with rx_len = se
+// (bytes past the segment end never decide a result: a header that reaches
+// past it is incomplete whatever those bytes hold).  The source is device
+// memory (after the H2D copy) or, zero-copy, the pinned host buffer itself.
+constexpr uint32_t SMALL_LREC = 512;      // records kept in LDS (20 KiB)
+constexpr uint32_t SMALL_BY_RECORD = 64;  // up to this many records: record-major XOR
+
+// Bytes [lo, hi) of a 64-bit word (bounds clamped to [0, 8]).
+__device__ __forceinline__ uint64_t byte_range(int64_t lo, int64_t hi) {
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > 8 ? 8 : hi;
+    if (hi <= lo) return 0;
+    const uint64_t h = hi >= 8 ? ~0ull : ((1ull << (8 * hi)) - 1);
+    return h & ~((1ull << (8 * lo)) - 1);
+}
+
+// k_small's XOR of segment [sb, se): records via rec(i) (sorted by payload
+// offset), n of them.  The key stream is periodic in absolute offsets, so a
+// chunk's mask is the key word rotated for the chunk start, cut to the bytes
+// each masked payload covers.  STAGE: XOR the LDS copy (lds holds offset sb16
+// at 0), then a pass of host stores only -- no load between the stores (a
+// vector-memory load waits for every older store's round trip).
+template <bool STAGE, typename Rec>
+__device__ __forceinline__ void small_xor(Rec rec, uint64_t n, uint64_t sb, uint64_t se, const uint8_t* src,
+                                          uint8_t* lds, uint8_t* __restrict__ h_rx) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t sb16 = sb & ~15ull;
+    uint64_t k_lo = 0;      // chunks rise, so the first live record never moves back
+    uint64_t changed = 0;   // STAGE: bit i = this lane's i-th chunk changed (<= 33 per lane)
+    uint32_t i = 0;
+    if (STAGE && n <= SMALL_BY_RECORD) {
+        // Record-major: the wave walks the records in order, every lane
+        // XORing chunks of the current payload (a broadcast LDS read per
+        // record instead of a per-chunk search).  A chunk two payloads share
+        // is updated by both, in program order (one wave's LDS accesses do not
+        // pass each other).  Every chunk is then stored back.
+        for (uint64_t k = 0; k < n; ++k) {
+            const drec f = rec(k);
+            if (!(f.info & F_MASK) || f.pay_len == 0) continue;
+            const uint32_t phase = (f.info >> 8) & 3u;
+            const uint64_t pe = f.pay_off + f.pay_len;
+            for (uint64_t c = (f.pay_off & ~15ull) + (uint64_t)lane * 16u; c < pe; c += 64u * 16u) {
+                const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + c - f.pay_off) & 3u));
+                const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                const int64_t a = (int64_t)(f.pay_off > c ? f.pay_off - c : 0);
+                const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
+                const uint64_t mlo = kk & byte_range(a, e), mhi = kk & byte_range(a - 8, e - 8);
+                *reinterpret_cast<u32x4*>(lds + (c - sb16)) ^=
+                    u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+            }
+        }
+        changed = ~0ull;
+    } else
+    for (uint64_t c = sb16 + (uint64_t)lane * 16u; c < se; c += 64u * 16u, ++i) {
+        uint64_t k = k_lo, k_end = n;   // first record whose payload ends after c
+        while (k < k_end) {
+            const uint64_t mid = (k + k_end) >> 1;
+            const drec m = rec(mid);
+            if (m.pay_off + m.pay_len > c) k_end = mid;
+            else k = mid + 1;
+        }
+        k_lo = k;
+        uint64_t mlo = 0, mhi = 0;
+        for (; k < n; ++k) {
+            const drec f = rec(k);
+            if (f.pay_off >= c + 16) break;
+            if (!(f.info & F_MASK) || f.pay_len == 0) continue;
+            const uint32_t phase = (f.info >> 8) & 3u;
+            const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + c - f.pay_off) & 3u));
+            const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+            const int64_t a = (int64_t)(f.pay_off > c ? f.pay_off - c : 0);
+            const uint64_t pe = f.pay_off + f.pay_len;
+            const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
+            mlo |= kk & byte_range(a, e);
+            mhi |= kk & byte_range(a - 8, e - 8);
+            if (e == 16) break;   // this payload runs past the chunk
+        }
+        if (!(mlo | mhi)) continue;   // no masked byte (or a zero key): bytes unchanged
+        const u32x4 m4 = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+        const bool whole = c >= sb && c + 16 <= se;
+        if (STAGE) {
+            changed |= 1ull << i;
+            u32x4* p = reinterpret_cast<u32x4*>(lds + (c - sb16));
+            if (whole) {
+                *p ^= m4;
+            } else {   // chunk shared with a neighbouring segment: own bytes only
+                for (uint32_t b = 0; b < 16; ++b) {
+                    const uint64_t x = c + b;
+                    if (x >= sb && x < se) lds[x - sb16] ^= (uint8_t)((b < 8 ? mlo >> (8 * b) : mhi >> (8 * (b - 8))) & 0xFFu);
+                }
+            }
+        } else if (whole) {
+            u32x4 v = *reinterpret_cast<const u32x4*>(src + c);
+            *reinterpret_cast<u32x4*>(h_rx + c) = v ^ m4;
+        } else {
+            for (uint32_t b = 0; b < 16; ++b) {
+                const uint64_t x = c + b;
+                const uint32_t kb = (uint32_t)((b < 8 ? mlo >> (8 * b) : mhi >> (8 * (b - 8))) & 0xFFu);
+                if (x >= sb && x < se && kb) h_rx[x] = src[x] ^ (uint8_t)kb;
+            }
+        }
+    }
+    if (!STAGE) return;
+    i = 0;
+    for (uint64_t c = sb16 + (uint64_t)lane * 16u; c < se; c += 64u * 16u, ++i) {
+        if (!((changed >> i) & 1u)) continue;
+        if (c >= sb && c + 16 <= se) {
+            *reinterpret_cast<u32x4*>(h_rx + c) = *reinterpret_cast<const u32x4*>(lds + (c - sb16));
+        } else {
+            for (uint32_t b = 0; b < 16; ++b) {
+                const uint64_t x = c + b;
+                if (x >= sb && x < se) h_rx[x] = lds[x - sb16];
+            }
+        }
+    }
+}
+
+template <bool STAGE>
 __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                               const dseg* __restrict__ segs, const dcarry* __restrict__ carry_in,
                                               const uint64_t* __restrict__ slot_base, drec* __restrict__ slots,
                                               unsigned long long* __restrict__ rec_total, drec* __restrict__ h_rec,
                                               uint64_t h_rec_cap, dsmall_out* __restrict__ h_out,
-                                              uint8_t* __restrict__ h_rx, int unmask, uint32_t vmask) {
+                                              uint8_t* __restrict__ h_rx, int unmask, uint32_t vmask,
+                                              uint64_t rec_base) {
+    extern __shared__ u32x4 lds_seg[];
+    __shared__ drec lrec[SMALL_LREC];
     const uint32_t s = blockIdx.x;
     const uint32_t lane = threadIdx.x;
-    const uint64_t sb = segs[s].off, L = segs[s].len;
-    drec* slot = slots + slot_base[s];
+    // independent loads, one round trip
+    const dseg sg = segs[s];
     dcarry st = carry_in[s];
+    drec* slot = slots + slot_base[s];
+    const uint64_t sb = sg.off, L = sg.len, se = sb + L;
+
+    const uint8_t* src = rx;
+    uint64_t src_len = rx_len;
+    uint8_t* lds = reinterpret_cast<uint8_t*>(lds_seg);
+    const uint64_t sb16 = sb & ~15ull;
+    if (STAGE) {
+        // Whole 16-byte chunks: SB independent loads per lane in flight, then
+        // their LDS stores (a load -> store -> load chain would pay the full
+        // memory latency per chunk: ~1.5 us each across PCIe).
+        constexpr int SB = 8;
+        for (uint64_t c0 = sb16 + (uint64_t)lane * 16u; c0 < se; c0 += 64u * 16u * SB) {
+            u32x4 v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const uint64_t c = c0 + (uint64_t)u * 1024u;
+                v[u] = c >= sb && c + 16 <= se ? *reinterpret_cast<const u32x4*>(rx + c) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const uint64_t c = c0 + (uint64_t)u * 1024u;
+                if (c >= sb && c + 16 <= se) *reinterpret_cast<u32x4*>(lds + (c - sb16)) = v[u];
+            }
+        }
+        // The (at most two) chunks the segment shares with a neighbour: lane 0
+        // the first, lane 1 the last, their bytes loaded together.
+        const uint64_t c_last = (se - 1) & ~15ull;
+        const uint64_t ce = lane == 0 ? sb16 : c_last;
+        const bool partial = L && lane < 2 && (lane == 0 || c_last != sb16) && (ce < sb || ce + 16 > se);
+        if (partial) {
+            uint8_t b16[16];
+#pragma unroll
+            for (int b = 0; b < 16; ++b) b16[b] = ce + b >= sb && ce + b < se ? rx[ce + b] : 0;
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                if (ce + b >= sb && ce + b < se) lds[ce + b - sb16] = b16[b];
+        }
+        __syncthreads();
+        src = lds - sb16;
+        src_len = se;
+    }
+
     st.started = 0;
     uint64_t pos = 0, n = 0;
     auto emit = [&](uint64_t idx, const frec& v) {
@@ -713,70 +883,43 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
         o.length = v.length;
         o.key = v.key;
         o.info = v.info;
-        slot[idx] = o;
+        if (idx < SMALL_LREC) lrec[idx] = o;
+        else slot[idx] = o;
     };
     if (st.state != S_START) {
         frec r;
-        if (scalar_frame(rx + sb, L, st, pos, r, vmask)) {
+        if (scalar_frame(src + sb, L, st, pos, r, vmask)) {
             if (lane == 0) emit(0, r);
             n = 1;
         }
     }
-    walk_frames<true>(rx, rx_len, sb, L, st, pos, n, vmask, emit);
+    walk_frames<true>(src, src_len, sb, L, st, pos, n, vmask, emit);
     __threadfence_block();
     __syncthreads();
 
+    // The record base first: a returning global atomic issued after the
+    // host stores below would wait for all of them to complete (vmcnt counts
+    // loads and stores in order on CDNA).
+    uint64_t base = 0;
+    if (lane == 0 && n) base = atomicAdd(rec_total, (unsigned long long)n) - rec_base;
+
     if (unmask && n) {
-        const uint64_t se = sb + L;
-        for (uint64_t c = (sb & ~15ull) + (uint64_t)lane * 16u; c < se; c += 64u * 16u) {
-            uint64_t k = 0, k_end = n;   // first record whose payload ends after c
-            while (k < k_end) {
-                const uint64_t mid = (k + k_end) >> 1;
-                if (slot[mid].pay_off + slot[mid].pay_len > c) k_end = mid;
-                else k = mid + 1;
-            }
-            uint64_t mlo = 0, mhi = 0;
-            for (; k < n; ++k) {
-                const drec f = slot[k];
-                if (f.pay_off >= c + 16) break;
-                if (!(f.info & F_MASK) || f.pay_len == 0) continue;
-                const uint32_t phase = (f.info >> 8) & 3u;
-                const uint64_t pe = f.pay_off + f.pay_len;
-                if (f.pay_off <= c && c + 16 <= pe) {   // whole chunk inside this payload
-                    const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + (c - f.pay_off)) & 3u));
-                    mlo = mhi = (uint64_t)kw | ((uint64_t)kw << 32);
-                    break;
-                }
-                const uint64_t a = f.pay_off > c ? f.pay_off : c;
-                const uint64_t e = pe < c + 16 ? pe : c + 16;
-                for (uint64_t x = a; x < e; ++x) {
-                    const uint64_t kb = (f.key >> (8u * (uint32_t)((phase + (x - f.pay_off)) & 3u))) & 0xFFu;
-                    const uint32_t b = (uint32_t)(x - c);
-                    if (b < 8) mlo |= kb << (8 * b);
-                    else mhi |= kb << (8 * (b - 8));
-                }
-            }
-            if (!(mlo | mhi)) continue;   // no masked byte (or a zero key): bytes unchanged
-            if (c >= sb && c + 16 <= se) {
-                u32x4 v = *reinterpret_cast<const u32x4*>(rx + c);
-                v ^= u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
-                *reinterpret_cast<u32x4*>(h_rx + c) = v;
-            } else {   // chunk shared with a neighbouring segment: own bytes only
-                for (uint32_t b = 0; b < 16; ++b) {
-                    const uint64_t x = c + b;
-                    if (x < sb || x >= se) continue;
-                    const uint32_t kb = (uint32_t)((b < 8 ? mlo >> (8 * b) : mhi >> (8 * (b - 8))) & 0xFFu);
-                    if (kb) h_rx[x] = rx[x] ^ (uint8_t)kb;
-                }
-            }
+        if (n <= SMALL_LREC) {
+            small_xor<STAGE>([&](uint64_t i) { return lrec[i]; }, n, sb, se, src, lds, h_rx);
+        } else {   // > SMALL_LREC records (frames of a few bytes): all of them in the device slot
+            for (uint64_t i = lane; i < SMALL_LREC; i += 64) slot[i] = lrec[i];
+            __threadfence_block();
+            __syncthreads();
+            small_xor<STAGE>([&](uint64_t i) { return slot[i]; }, n, sb, se, src, lds, h_rx);
         }
     }
 
-    uint64_t base = 0;
-    if (lane == 0 && n) base = atomicAdd(rec_total, (unsigned long long)n);
     base = __shfl(base, 0);
-    if (base + n <= h_rec_cap)
-        for (uint64_t i = lane; i < n; i += 64) h_rec[base + i] = slot[i];
+    if (base + n <= h_rec_cap) {
+        const uint64_t nl = n < SMALL_LREC ? n : SMALL_LREC;
+        for (uint64_t i = lane; i < nl; i += 64) h_rec[base + i] = lrec[i];
+        for (uint64_t i = SMALL_LREC + lane; i < n; i += 64) h_rec[base + i] = slot[i];
+    }
     if (lane == 0) {
         dsmall_out o;
         o.first = base;
@@ -787,14 +930,27 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
 }
 
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
-                        const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, drec* h_rec,
-                        uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
-                        hipStream_t st, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                        const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, uint64_t rec_base,
+                        drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
+                        uint32_t stage_lds, hipStream_t st, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (nseg == 0) return hipSuccess;
-    // timing events on the dispatch itself: no marker packets around a
-    // launch whose whole round trip is the latency FeedRecvData pays
-    hipExtLaunchKernelGGL(k_small, dim3(nseg), dim3(64), 0, st, ev_start, ev_stop, 0u, rx, rx_len, segs, carry_in,
-                          slot_base, slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask);
+    // Timing events, when asked for, ride on the dispatch itself (no marker
+    // packets); without them the plain launch is cheaper still.
+    const bool ev = ev_start || ev_stop;
+    if (stage_lds && ev)
+        hipExtLaunchKernelGGL(k_small<true>, dim3(nseg), dim3(64), stage_lds, st, ev_start, ev_stop, 0u, rx, rx_len,
+                              segs, carry_in, slot_base, slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask,
+                              rec_base);
+    else if (stage_lds)
+        hipLaunchKernelGGL(k_small<true>, dim3(nseg), dim3(64), stage_lds, st, rx, rx_len, segs, carry_in, slot_base,
+                           slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask, rec_base);
+    else if (ev)
+        hipExtLaunchKernelGGL(k_small<false>, dim3(nseg), dim3(64), 0, st, ev_start, ev_stop, 0u, rx, rx_len, segs,
+                              carry_in, slot_base, slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask,
+                              rec_base);
+    else
+        hipLaunchKernelGGL(k_small<false>, dim3(nseg), dim3(64), 0, st, rx, rx_len, segs, carry_in, slot_base, slots,
+                           rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask, rec_base);
     return hipGetLastError();
 }
 

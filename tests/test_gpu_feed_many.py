@@ -15,21 +15,27 @@ import wsharness as H
 
 pytestmark = pytest.mark.gpu
 
-@pytest.fixture(params=["small", "general"], autouse=True)
+@pytest.fixture(params=["small", "small_copy", "general"], autouse=True)
 def rx_path(request):
-    """Run every case through both host-batch paths: the single-launch
-    small-batch kernel (default for reads this size) and the general
+    """Run every case through the three host-batch paths: the single-launch
+    small-batch kernel (default for reads this size; zero-copy for segments
+    <= 32 KiB), the same kernel behind an H2D copy, and the general
     COUNT/EMIT/unmask sequence.  Results must be identical."""
     L = libhv_amd.lib()
-    limit = 0 if request.param == "small" else (1 << 64) - 1
+    limit = 0 if request.param.startswith("small") else (1 << 64) - 1
+    zc = 0 if request.param == "small_copy" else 1
     L.hvws_set_small_batch_limit(None, limit)
+    L.hvws_set_small_zero_copy(None, zc)
     eng = request.getfixturevalue("eng") if "eng" in request.fixturenames else None
     if eng:
         L.hvws_set_small_batch_limit(eng.ctx, limit)
+        L.hvws_set_small_zero_copy(eng.ctx, zc)
     yield request.param
     L.hvws_set_small_batch_limit(None, 0)
+    L.hvws_set_small_zero_copy(None, 1)
     if eng:
         L.hvws_set_small_batch_limit(eng.ctx, 0)
+        L.hvws_set_small_zero_copy(eng.ctx, 1)
 
 
 def _clamp(chunks, n):
@@ -195,4 +201,22 @@ def test_feed_many_large_poll_iteration():
         conns.append(Conn(data, chunks))
     _loop(random.Random(5), conns)
     assert sum(len(c.data) for c in conns) > 2 << 20
+    _check(conns)
+
+
+@pytest.mark.parametrize("read", [8192, 32768, 8191])
+def test_feed_many_record_density(read):
+    """k_small's XOR paths by records per segment: few long payloads (record-
+    major), a few hundred (chunk-major, records in LDS) and more than its LDS
+    record area holds (tiny frames, records in the device slot); reads of
+    8191 bytes put segment ends and starts inside 16-byte chunks."""
+    rng = random.Random(read)
+    conns = []
+    for max_len in (3000, 40, 4):
+        for _ in range(4):
+            data = S.rand_stream(rng, rng.randint(40, 3000) if max_len < 100 else rng.randint(10, 40),
+                                 max_len=max_len)
+            chunks = [read] * (len(data) // read) + ([len(data) % read] if len(data) % read else [])
+            conns.append(Conn(data, chunks))
+    _loop(random.Random(read + 1), conns)
     _check(conns)
