@@ -218,6 +218,12 @@ def max_over_ranks(dist, seconds: float) -> float:
 def main():
     args = parse()
     rank, world, local, dist = init_dist()
+    if world > 1:
+        # N > 1: the replicas' timed steps only.  The CPU baseline is taken at
+        # N = 1 (rank 0), and so are the host-inclusive and transmit legs.
+        args.cpu_seconds = 0
+        args.host_gib = 0
+        args.no_tx = True
     import torch
 
     import libhv_amd
