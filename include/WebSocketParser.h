@@ -57,4 +57,12 @@ typedef std::shared_ptr<WebSocketParser> WebSocketParserPtr;
 HV_EXPORT int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
                              int* rets);
 
+/* Pipelined form for an event loop (see hvws_feeder in hvws.h): starts this
+ * poll iteration's reads on the GPU and replays the previous submission's
+ * callbacks meanwhile.  Returns n, or -1 when called from inside one of the
+ * feeder's own callbacks. */
+struct hvws_feeder;
+HV_EXPORT int hvws_feeder_submit(hvws_feeder* f, WebSocketParser* const* parsers, const char* const* data,
+                                 const size_t* len, int n, int* rets);
+
 #endif

@@ -334,6 +334,27 @@ void  hvws_wsp_state(void* h, uint64_t out[8]);
 /* n handles fed in one GPU round trip (see hvws_feed_many in WebSocketParser.h) */
 int   hvws_wsp_feed_many(void* const* handles, const char* const* data, const size_t* len, int n, int* rets);
 
+/* Pipelined event-loop feed.  A feeder owns a
+ * worker thread with its own context, stream and pinned stage.  Each submit
+ * starts the device half of this poll iteration's reads (gather, one GPU round
+ * trip, unmasked bytes written back in place) on the worker and, meanwhile,
+ * replays the PREVIOUS submission's message logic and onMessage callbacks on
+ * the calling thread.  Effects per parser are those of hvws_feed_many, one
+ * submission late: the callbacks and rets[] of submission k arrive during
+ * submit k+1 (or flush).  The caller keeps submission k's buffers and its
+ * rets array alive and untouched until then.  Submitting 0 reads = flush.
+ * A parser whose feed returned short must be closed (as libhv does); its
+ * results already in flight are then undefined.  Not callable from inside
+ * the feeder's own callbacks (returns -1).  new() binds the calling thread's
+ * device; free() flushes. */
+typedef struct hvws_feeder hvws_feeder;
+hvws_feeder* hvws_feeder_new(void);
+void hvws_feeder_free(hvws_feeder* f);
+int  hvws_feeder_flush(hvws_feeder* f);
+/* hvws_feeder_submit over hvws_wsp_* handles (C++: hvws_feeder_submit in WebSocketParser.h) */
+int  hvws_wsp_feeder_submit(hvws_feeder* f, void* const* handles, const char* const* data, const size_t* len, int n,
+                            int* rets);
+
 /* Device used by the reference-API entry points on the calling thread
  * (default: $HVWS_DEVICE or 0). */
 int hvws_set_thread_device(int device);

@@ -155,6 +155,14 @@ _SIGS = {
         [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
          ctypes.POINTER(ctypes.c_int)],
     ),
+    "hvws_feeder_new": (ctypes.c_void_p, []),
+    "hvws_feeder_free": (None, [ctypes.c_void_p]),
+    "hvws_feeder_flush": (ctypes.c_int, [ctypes.c_void_p]),
+    "hvws_wsp_feeder_submit": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+         ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
+    ),
     "hvws_set_thread_device": (ctypes.c_int, [ctypes.c_int]),
     "hvws_thread_release": (None, []),
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
@@ -187,6 +195,7 @@ _SIGS = {
 # C++ drop-in symbols (include/WebSocketParser.h)
 CXX_SYMBOLS = (
     "_Z14hvws_feed_manyPKP15WebSocketParserPKPKcPKmiPi",
+    "_Z18hvws_feeder_submitP11hvws_feederPKP15WebSocketParserPKPKcPKmiPi",
     "_ZN15WebSocketParserC1Ev",
     "_ZN15WebSocketParserD1Ev",
     "_ZN15WebSocketParser12FeedRecvDataEPKcm",

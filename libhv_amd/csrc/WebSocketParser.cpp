@@ -14,7 +14,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -25,6 +30,7 @@ namespace hvws {
 [[noreturn]] void fatal(const char* what);
 hvws_ctx* thread_ctx();
 char* pinned_stage(uint64_t bytes);
+void ctx_copy_settings(hvws_ctx* dst, const hvws_ctx* src);
 void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
               websocket_parser& carry_out, int& started);
 }  // namespace hvws
@@ -163,13 +169,14 @@ int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, con
 namespace {
 // $HVWS_FEED_TIMES=1: per-phase host time of feed_distinct, printed at exit (diagnostic)
 struct feed_times {
-    double ph[5] = {0, 0, 0, 0, 0};
+    double ph[6] = {0, 0, 0, 0, 0, 0};   // carry, gather, gpu, scatter, replay, feeder wait
     long calls = 0;
     bool on = getenv("HVWS_FEED_TIMES") && atoi(getenv("HVWS_FEED_TIMES"));
     ~feed_times() {
         if (on && calls)
-            fprintf(stderr, "[feed_times] calls=%ld us/call: carry %.1f gather %.1f gpu %.1f scatter %.1f replay %.1f\n",
-                    calls, ph[0] / calls, ph[1] / calls, ph[2] / calls, ph[3] / calls, ph[4] / calls);
+            fprintf(stderr, "[feed_times] calls=%ld us/call: carry %.1f gather %.1f gpu %.1f scatter %.1f replay %.1f "
+                    "feeder-wait %.1f\n",
+                    calls, ph[0] / calls, ph[1] / calls, ph[2] / calls, ph[3] / calls, ph[4] / calls, ph[5] / calls);
     }
 } g_ft;
 double now_us() {
@@ -177,9 +184,42 @@ double now_us() {
 }
 }  // namespace
 
-static int feed_distinct(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
-                         int* rets) {
-    if (n <= 0) return 0;
+namespace {
+// One distinct-parser run of a poll iteration: its reads, the carries going
+// in (then the states coming out) and the frame records of every segment.
+struct feed_batch {
+    std::vector<WebSocketParser*> parsers;
+    std::vector<const char*> data;
+    std::vector<size_t> len;
+    int* rets = nullptr;
+    std::vector<hvws_segment> segs;
+    std::vector<websocket_parser> carry;
+    std::vector<hvws_frame> frames;
+    std::vector<uint64_t> first, count;
+    uint64_t total = 0;
+    int n() const { return (int)parsers.size(); }
+    void set(WebSocketParser* const* p, const char* const* d, const size_t* l, int k, int* r) {
+        parsers.assign(p, p + k);
+        data.assign(d, d + k);
+        len.assign(l, l + k);
+        rets = r;
+        segs.resize((size_t)k);
+        carry.resize((size_t)k);
+        total = 0;
+        for (int i = 0; i < k; ++i) {
+            segs[i].off = total;
+            segs[i].len = len[i];
+            total += len[i];
+        }
+    }
+};
+
+// The device half of a run, on the calling thread's context and pinned stage:
+// gather the reads, one hvws_rx_batch, read the frame table back, and write
+// the unmasked bytes back into the callers' buffers.  Touches no parser:
+// b.carry must already hold the carries going in.
+void gpu_part(feed_batch& b) {
+    const int n = b.n();
     double t0 = g_ft.on ? now_us() : 0, t1;
     auto lap = [&](int k) {
         if (!g_ft.on) return;
@@ -187,42 +227,215 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
         g_ft.ph[k] += t1 - t0;
         t0 = t1;
     };
-    std::vector<hvws_segment> segs((size_t)n);
-    std::vector<websocket_parser> carry((size_t)n);
-    uint64_t total = 0;
-    for (int i = 0; i < n; ++i) {
-        segs[i].off = total;
-        segs[i].len = len[i];
-        total += len[i];
-        hvws::copy_parser(carry[i], *parsers[i]->parser);
-    }
-    lap(0);
-    char* stage = hvws::pinned_stage(total);
-    stage_copy(stage, segs.data(), data, len, n, total, true);
+    char* stage = hvws::pinned_stage(b.total);
+    stage_copy(stage, b.segs.data(), b.data.data(), b.len.data(), n, b.total, true);
     lap(1);
     hvws_ctx* c = hvws::thread_ctx();
-    if (hvws_rx_batch(c, (uint8_t*)stage, total, segs.data(), carry.data(), (uint32_t)n, 1) != HVWS_OK)
+    if (hvws_rx_batch(c, (uint8_t*)stage, b.total, b.segs.data(), b.carry.data(), (uint32_t)n, 1) != HVWS_OK)
         hvws::fatal("hvws_rx_batch");
     const int64_t nf = hvws_frame_count(c);
-    std::vector<hvws_frame> frames((size_t)(nf > 0 ? nf : 0));
-    std::vector<uint64_t> first((size_t)n), count((size_t)n);
-    if ((nf > 0 && hvws_get_frames(c, frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
-        hvws_get_segment_frames(c, first.data(), count.data()) != HVWS_OK)
+    b.frames.resize((size_t)(nf > 0 ? nf : 0));
+    b.first.resize((size_t)n);
+    b.count.resize((size_t)n);
+    if ((nf > 0 && hvws_get_frames(c, b.frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
+        hvws_get_segment_frames(c, b.first.data(), b.count.data()) != HVWS_OK)
         hvws::fatal("frame table read-back");
     lap(2);
     // Every segment leaves the (thread's, reusable) stage before any callback
     // runs: an onMessage that feeds again on this thread restages it.
-    stage_copy(stage, segs.data(), data, len, n, total, false);   // in place, like the reference
+    stage_copy(stage, b.segs.data(), b.data.data(), b.len.data(), n, b.total, false);   // in place, like the reference
     lap(3);
-    for (int i = 0; i < n; ++i) {
-        char* dst = const_cast<char*>(data[i]);
-        carry[i].data = parsers[i]->parser->data;
-        const size_t used =
-            replay_messages(parsers[i], dst, segs[i].off, frames.data() + first[i], (size_t)count[i], carry[i], len[i]);
-        if (rets) rets[i] = (int)used;
+}
+
+// The host half, on the loop thread: the reference's message logic and
+// onMessage callbacks, connection by connection in submission order.
+void replay_part(feed_batch& b) {
+    double t0 = g_ft.on ? now_us() : 0;
+    for (int i = 0; i < b.n(); ++i) {
+        char* dst = const_cast<char*>(b.data[i]);
+        b.carry[i].data = b.parsers[i]->parser->data;
+        const size_t used = replay_messages(b.parsers[i], dst, b.segs[i].off, b.frames.data() + b.first[i],
+                                            (size_t)b.count[i], b.carry[i], b.len[i]);
+        if (b.rets) b.rets[i] = (int)used;
     }
-    lap(4);
+    if (g_ft.on) g_ft.ph[4] += now_us() - t0;
+}
+}  // namespace
+
+static int feed_distinct(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
+                         int* rets) {
+    if (n <= 0) return 0;
+    double t0 = g_ft.on ? now_us() : 0;
+    feed_batch b;   // local: an onMessage may feed again on this thread
+    b.set(parsers, data, len, n, rets);
+    for (int i = 0; i < n; ++i) hvws::copy_parser(b.carry[i], *parsers[i]->parser);
+    if (g_ft.on) g_ft.ph[0] += now_us() - t0;
+    gpu_part(b);
+    replay_part(b);
     g_ft.calls += g_ft.on;
+    return n;
+}
+
+// ------------------------------------------------------------ pipelined feed
+// hvws_feeder: the device half of poll iteration k
+// (gather, GPU round trip, write-back) runs on the feeder's worker thread,
+// on that thread's own context, stream and pinned stage, while the loop
+// thread replays iteration k-1's message logic and onMessage callbacks.
+// Callbacks arrive one submission late; their order is hvws_feed_many's.
+struct hvws_feeder {
+    int device = 0;
+    hvws_ctx* src = nullptr;         // creating thread's context (settings), until the worker started
+    bool started = false;
+    std::thread worker;
+    std::mutex m;
+    std::condition_variable cv;
+    feed_batch slot[2];
+    int next = 0;                    // slot the next run fills (the other one may be pending)
+    std::atomic<feed_batch*> job{nullptr};   // handed to the worker, device half not finished
+    feed_batch* pending = nullptr;   // device half issued, callbacks not replayed yet
+    bool stop = false;
+    bool in_replay = false;
+    uint64_t inline_bytes = 0;       // runs up to this size skip the worker ($HVWS_FEEDER_INLINE)
+    std::unordered_map<WebSocketParser*, int> pend_idx;   // parser -> index in *pending
+};
+
+namespace {
+// Hand-offs spin briefly before blocking: an event loop submits every poll
+// iteration, and a futex wake-up costs ~10-20 us against ~30-50 us round trips.
+constexpr int kFeederSpinUs = 200;
+
+template <class Pred>
+bool spin_until(Pred p) {
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(kFeederSpinUs);
+    for (int i = 0;; ++i) {
+        if (p()) return true;
+        if ((i & 63) == 63 && std::chrono::steady_clock::now() > t_end) return false;
+        __builtin_ia32_pause();
+    }
+}
+
+void feeder_main(hvws_feeder* f) {
+    hvws_set_thread_device(f->device);
+    {
+        std::lock_guard<std::mutex> lk(f->m);
+        hvws::ctx_copy_settings(hvws::thread_ctx(), f->src);
+        f->src = nullptr;
+        f->started = true;
+    }
+    f->cv.notify_all();
+    for (;;) {
+        feed_batch* b = nullptr;
+        if (!spin_until([&] { return (b = f->job.load(std::memory_order_acquire)) != nullptr; })) {
+            std::unique_lock<std::mutex> lk(f->m);
+            f->cv.wait(lk, [&] { return (b = f->job.load(std::memory_order_acquire)) != nullptr || f->stop; });
+            if (!b) break;
+        }
+        gpu_part(*b);
+        {
+            std::lock_guard<std::mutex> lk(f->m);
+            f->job.store(nullptr, std::memory_order_release);
+        }
+        f->cv.notify_all();
+    }
+    hvws_thread_release();
+}
+
+void feeder_wait_idle(hvws_feeder* f) {
+    const double t0 = g_ft.on ? now_us() : 0;
+    if (!spin_until([f] { return f->job.load(std::memory_order_acquire) == nullptr; })) {
+        std::unique_lock<std::mutex> lk(f->m);
+        f->cv.wait(lk, [f] { return f->job.load(std::memory_order_acquire) == nullptr; });
+    }
+    if (g_ft.on) g_ft.ph[5] += now_us() - t0;
+}
+
+void feeder_replay_pending(hvws_feeder* f) {
+    if (!f->pending) return;
+    f->in_replay = true;
+    replay_part(*f->pending);
+    f->in_replay = false;
+    f->pending = nullptr;
+    f->pend_idx.clear();
+}
+
+// One run of distinct parsers: start its device half, then replay the
+// previous run while it is in flight.
+void feeder_run(hvws_feeder* f, WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
+                int* rets) {
+    feed_batch& b = f->slot[f->next];
+    f->next ^= 1;
+    b.set(parsers, data, len, n, rets);
+    // The previous run's device half has produced its carries; a parser it
+    // holds continues from there (its own state is only written by the
+    // replay below), any other parser from its own state.
+    feeder_wait_idle(f);
+    for (int i = 0; i < n; ++i) {
+        auto it = f->pending ? f->pend_idx.find(parsers[i]) : f->pend_idx.end();
+        if (it != f->pend_idx.end()) hvws::copy_parser(b.carry[i], f->pending->carry[it->second]);
+        else hvws::copy_parser(b.carry[i], *parsers[i]->parser);
+    }
+    g_ft.calls += g_ft.on;
+    if (b.total <= f->inline_bytes) {
+        // Too small for the hand-off to pay: the device half on this thread
+        // (its own context), then the previous run's replay.
+        gpu_part(b);
+    } else {
+        {
+            std::lock_guard<std::mutex> lk(f->m);
+            f->job.store(&b, std::memory_order_release);
+        }
+        f->cv.notify_all();
+    }
+    feeder_replay_pending(f);
+    f->pending = &b;
+    for (int i = 0; i < n; ++i) f->pend_idx[parsers[i]] = i;
+}
+}  // namespace
+
+extern "C" hvws_feeder* hvws_feeder_new(void) {
+    hvws_feeder* f = new hvws_feeder();
+    if (const char* e = getenv("HVWS_FEEDER_INLINE")) f->inline_bytes = strtoull(e, nullptr, 0);
+    f->src = hvws::thread_ctx();
+    f->device = hvws_ctx_device(f->src);
+    f->worker = std::thread(feeder_main, f);
+    std::unique_lock<std::mutex> lk(f->m);
+    f->cv.wait(lk, [f] { return f->started; });
+    return f;
+}
+
+extern "C" int hvws_feeder_flush(hvws_feeder* f) {
+    if (!f) return -1;
+    if (f->in_replay) return -1;   // from inside one of its own callbacks
+    feeder_wait_idle(f);
+    feeder_replay_pending(f);
+    return 0;
+}
+
+extern "C" void hvws_feeder_free(hvws_feeder* f) {
+    if (!f) return;
+    hvws_feeder_flush(f);
+    {
+        std::lock_guard<std::mutex> lk(f->m);
+        f->stop = true;
+    }
+    f->cv.notify_all();
+    f->worker.join();
+    delete f;
+}
+
+int hvws_feeder_submit(hvws_feeder* f, WebSocketParser* const* parsers, const char* const* data, const size_t* len,
+                       int n, int* rets) {
+    if (!f || n < 0 || f->in_replay) return -1;
+    if (n == 0) return hvws_feeder_flush(f);
+    // as hvws_feed_many: a parser seen twice starts a new run
+    int done = 0;
+    while (done < n) {
+        int end = done;
+        std::unordered_set<WebSocketParser*> seen;
+        while (end < n && seen.insert(parsers[end]).second) ++end;
+        feeder_run(f, parsers + done, data + done, len + done, end - done, rets ? rets + done : nullptr);
+        done = end;
+    }
     return n;
 }
 
@@ -257,6 +470,13 @@ int hvws_wsp_feed_many(void* const* handles, const char* const* data, const size
     std::vector<WebSocketParser*> ps((size_t)(n > 0 ? n : 0));
     for (int i = 0; i < n; ++i) ps[i] = &((wsp_handle*)handles[i])->p;
     return hvws_feed_many(ps.data(), data, len, n, rets);
+}
+
+int hvws_wsp_feeder_submit(hvws_feeder* f, void* const* handles, const char* const* data, const size_t* len, int n,
+                           int* rets) {
+    std::vector<WebSocketParser*> ps((size_t)(n > 0 ? n : 0));
+    for (int i = 0; i < n; ++i) ps[i] = &((wsp_handle*)handles[i])->p;
+    return hvws_feeder_submit(f, ps.data(), data, len, n, rets);
 }
 
 void hvws_wsp_state(void* h, uint64_t out[8]) {

@@ -201,6 +201,7 @@ struct hvws_ctx {
     uint64_t small_ctr_base = 0;
     bool small_ctr_dirty = true;   // unknown value (first use, failed call): zero it
     int small_zc = 1;              // $HVWS_SMALL_ZC / hvws_set_small_zero_copy
+    uint64_t zc_batch = kZcBatch;  // largest zero-copy batch ($HVWS_ZC_BATCH)
     uint32_t vmask = 0;         // protocol validation classes (V_*); 0 = reference behaviour
     // transmit side (hvws_build_frames)
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat;
@@ -1092,7 +1093,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     uint64_t max_seg = 0;
     for (uint32_t s = 0; s < nseg; ++s) max_seg = std::max<uint64_t>(max_seg, segs[s].len);
     const bool stage = max_seg <= kStageSegment;
-    const bool zc = stage && c->small_zc && len <= kZcBatch;
+    const bool zc = stage && c->small_zc && len <= c->zc_batch;
     const uint32_t stage_lds = stage ? (uint32_t)(((max_seg + 15) & ~15ull) + 16) : 0u;
     // The pinned packet may still be the source of an in-flight copy.
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
@@ -1252,6 +1253,7 @@ hvws_ctx* hvws_ctx_create(int device) {
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
     if (const char* zc = getenv("HVWS_SMALL_ZC")) c->small_zc = atoi(zc) ? 1 : 0;
+    if (const char* zb = getenv("HVWS_ZC_BATCH")) c->zc_batch = strtoull(zb, nullptr, 0);
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
     if (const char* wv = getenv("HVWS_WALK_VERIFY")) c->verify_mode = atoi(wv) < 0 ? -1 : (atoi(wv) ? 1 : 0);
     // The pipelined scan stream at the highest priority: a scan kernel of
@@ -1947,6 +1949,15 @@ hvws_ctx* thread_ctx() {
     t_ctx = hvws_ctx_create(dev);
     if (!t_ctx) fatal("cannot open a HIP device context");
     return t_ctx;
+}
+
+// A feeder's worker context takes the per-context knobs of the thread that
+// made the feeder (small-batch path, zero-copy, validation classes).
+void ctx_copy_settings(hvws_ctx* dst, const hvws_ctx* src) {
+    dst->small_limit = src->small_limit;
+    dst->small_zc = src->small_zc;
+    dst->zc_batch = src->zc_batch;
+    dst->vmask = src->vmask;
 }
 
 // Per-thread pinned staging for batched host entry points.

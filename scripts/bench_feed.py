@@ -5,6 +5,9 @@ n connections each deliver 8 KiB reads (event/hevent.h:16 HLOOP_READ_BUFSIZE)
 of a stream of masked 1 KiB binary frames.  One "poll iteration" hands every
 connection's next read to the parser:
   * gpu_many : one hvws_wsp_feed_many call (one GPU round trip per iteration);
+  * gpu_pipe : one hvws_wsp_feeder_submit per iteration (pipelined: iteration
+               k's GPU round trip overlaps iteration k-1's callback replay;
+               the final flush is inside the timed region);
   * gpu_each : WebSocketParser::FeedRecvData per connection (a round trip each);
   * cpu_ref  : the reference frame parser + restated WebSocketParser callbacks
                (oracle/_ref), per connection, one core.
@@ -38,7 +41,7 @@ def main():
     R = H.ref() if H.have_ref() else H.oracle()
     kind = "reference" if H.have_ref() else "port"
     conns = [int(x) for x in os.environ.get("CONNS", "1,16,256,1024,4096").split(",")]
-    modes = os.environ.get("MODES", "gpu_many,gpu_each,gpu_many_general,gpu_each_general,cpu_ref").split(",")
+    modes = os.environ.get("MODES", "gpu_many,gpu_pipe,gpu_each,gpu_many_general,gpu_each_general,cpu_ref").split(",")
     for n in conns:
         per_conn = READ * iters
         frames = per_conn // 1032 + 2
@@ -77,18 +80,31 @@ def main():
                 for i in range(n):
                     ds[i] = scratch[i].ctypes.data
                 warm = [L.hvws_wsp_new() for _ in range(n)]
-                L.hvws_wsp_feed_many((ctypes.c_void_p * n)(*warm), ds, lens, n, rets)
+                # gpu_pipe_inline: runs <= 256 KiB do their device half on the loop thread
+                os.environ["HVWS_FEEDER_INLINE"] = str(256 << 10) if mode == "gpu_pipe_inline" else "0"
+                feeder = L.hvws_feeder_new() if mode.startswith("gpu_pipe") else None
+                if feeder:
+                    L.hvws_wsp_feeder_submit(feeder, (ctypes.c_void_p * n)(*warm), ds, lens, n, rets)
+                    L.hvws_feeder_flush(feeder)
+                else:
+                    L.hvws_wsp_feed_many((ctypes.c_void_p * n)(*warm), ds, lens, n, rets)
                 for h in warm:
                     L.hvws_wsp_free(h)
                 t0 = time.perf_counter()
                 for it in range(iters):
                     ds_np[:] = base + np.uint64(it * READ)
-                    if mode.startswith("gpu_many"):
+                    if feeder:
+                        L.hvws_wsp_feeder_submit(feeder, hv, ds, lens, n, rets)
+                    elif mode.startswith("gpu_many"):
                         L.hvws_wsp_feed_many(hv, ds, lens, n, rets)
                     else:
                         for i in range(n):
                             L.hvws_wsp_feed(hs[i], ds[i], READ)
+                if feeder:
+                    L.hvws_feeder_flush(feeder)
                 dt = time.perf_counter() - t0
+                if feeder:
+                    L.hvws_feeder_free(feeder)
                 for h in hs:
                     L.hvws_wsp_free(h)
             res[mode] = {

@@ -65,8 +65,13 @@ class Conn:
         self.rets = []
 
 
-def _loop(rng, conns, max_batch=None, dup=False):
+def _loop(rng, conns, max_batch=None, dup=False, feeder=False):
+    """One poll iteration per pass: the ready connections' next reads go to
+    hvws_wsp_feed_many, or (feeder=True) to a pipelined hvws_feeder, whose
+    rets for a submission arrive during the next submit or the final flush."""
     L = libhv_amd.lib()
+    f = L.hvws_feeder_new() if feeder else None
+    subs = []
     pending = [c for c in conns if c.chunks]
     while pending:
         ready = [c for c in pending if rng.random() < 0.7] or pending[:1]
@@ -85,10 +90,18 @@ def _loop(rng, conns, max_batch=None, dup=False):
             ls[i] = k
             c.at += k
         rets = (ctypes.c_int * n)()
-        assert L.hvws_wsp_feed_many(hs, ds, ls, n, rets) == n
+        if f:
+            assert L.hvws_wsp_feeder_submit(f, hs, ds, ls, n, rets) == n
+        else:
+            assert L.hvws_wsp_feed_many(hs, ds, ls, n, rets) == n
+        subs.append((ready, rets))
+        pending = [c for c in conns if c.chunks]
+    if f:
+        assert L.hvws_feeder_flush(f) == 0
+        L.hvws_feeder_free(f)
+    for ready, rets in subs:
         for i, c in enumerate(ready):
             c.rets.append(rets[i])
-        pending = [c for c in conns if c.chunks]
 
 
 def _check(conns):
@@ -104,8 +117,9 @@ def _check(conns):
         L.hvws_wsp_free(c.h)
 
 
+@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_feed_many_matches_sequential_reference(seed):
+def test_feed_many_matches_sequential_reference(seed, feeder):
     rng = random.Random(seed)
     conns = []
     for _ in range(rng.randint(5, 60)):
@@ -113,11 +127,12 @@ def test_feed_many_matches_sequential_reference(seed):
         chunks = S.rand_chunks(rng, len(data), rng.choice(["rand", "small", "one"]))
         c = Conn(data, chunks)
         conns.append(c)
-    _loop(rng, conns)
+    _loop(rng, conns, feeder=feeder)
     _check(conns)
 
 
-def test_feed_many_repeated_connection_in_batch():
+@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
+def test_feed_many_repeated_connection_in_batch(feeder):
     rng = random.Random(9)
     conns = []
     for _ in range(12):
@@ -125,7 +140,7 @@ def test_feed_many_repeated_connection_in_batch():
         chunks = S.rand_chunks(rng, len(data), "small")
         c = Conn(data, chunks)
         conns.append(c)
-    _loop(rng, conns, dup=True)
+    _loop(rng, conns, dup=True, feeder=feeder)
     _check(conns)
 
 
@@ -188,7 +203,8 @@ def test_feed_many_reentrant_callback():
     _check(conns + [inner])
 
 
-def test_feed_many_large_poll_iteration():
+@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
+def test_feed_many_large_poll_iteration(feeder):
     """Poll iterations of ~2 MiB (256 connections x 8 KiB reads): the gather
     into and scatter out of the pinned stage split over the host copy pool
     (hvws_hostpool.cpp, batches >= 1 MiB).  Chunks land back in the right
@@ -199,7 +215,7 @@ def test_feed_many_large_poll_iteration():
         data = S.rand_stream(rng, rng.randint(4, 12), max_len=rng.choice([600, 9000]))
         chunks = [8192] * (len(data) // 8192) + ([len(data) % 8192] if len(data) % 8192 else [])
         conns.append(Conn(data, chunks))
-    _loop(random.Random(5), conns)
+    _loop(random.Random(5), conns, feeder=feeder)
     assert sum(len(c.data) for c in conns) > 2 << 20
     _check(conns)
 
@@ -219,4 +235,41 @@ def test_feed_many_record_density(read):
             chunks = [read] * (len(data) // read) + ([len(data) % read] if len(data) % read else [])
             conns.append(Conn(data, chunks))
     _loop(random.Random(read + 1), conns)
+    _check(conns)
+
+
+def test_feeder_callbacks_one_submission_late():
+    """A feeder replays submission k's callbacks during submit k+1 (or flush):
+    nothing is delivered by the first submit, everything by the flush; a
+    submit from inside one of its own callbacks is refused (-1)."""
+    L = libhv_amd.lib()
+    rng = random.Random(41)
+    conns = [Conn(S.rand_stream(rng, 6, max_len=500), [0]) for _ in range(5)]
+    f = L.hvws_feeder_new()
+    inner = []
+
+    def on0(user, op, data, n):
+        conns[0].sink._on(user, op, data, n)
+        if not inner:
+            h = (ctypes.c_void_p * 1)(conns[1].h)
+            d = (ctypes.c_void_p * 1)(ctypes.addressof(conns[1].buf))
+            ln = (ctypes.c_size_t * 1)(1)
+            inner.append(L.hvws_wsp_feeder_submit(f, h, d, ln, 1, None))
+            inner.append(L.hvws_feeder_flush(f))
+
+    conns[0].cb = libhv_amd.MSG_CB(on0)
+    L.hvws_wsp_set_sink(conns[0].h, conns[0].cb, None)
+    n = len(conns)
+    hs = (ctypes.c_void_p * n)(*[c.h for c in conns])
+    ds = (ctypes.c_void_p * n)(*[ctypes.addressof(c.buf) for c in conns])
+    ls = (ctypes.c_size_t * n)(*[len(c.data) for c in conns])
+    rets = (ctypes.c_int * n)()
+    assert L.hvws_wsp_feeder_submit(f, hs, ds, ls, n, rets) == n
+    assert all(not c.sink.msgs for c in conns) and list(rets) == [0] * n
+    assert L.hvws_wsp_feeder_submit(f, hs, ds, ls, 0, None) == 0   # 0 reads = flush
+    assert inner == [-1, -1]
+    for i, c in enumerate(conns):
+        c.fed = [len(c.data)]
+        c.rets = [rets[i]]
+    L.hvws_feeder_free(f)
     _check(conns)
