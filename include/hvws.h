@@ -318,6 +318,22 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
  * identical either way; only latency differs. */
 int hvws_set_small_zero_copy(hvws_ctx* ctx, int on);
 
+/* Registered pinned host memory: hvws_host_alloc'ed ranges are registered
+ * automatically; hvws_host_register pins and registers caller memory (an
+ * event loop's read buffers), hvws_host_unregister undoes it. */
+int hvws_host_register(hvws_ctx* ctx, void* p, uint64_t bytes);
+int hvws_host_unregister(hvws_ctx* ctx, void* p);
+
+/* hvws_rx_batch over n separate reads that live in registered pinned memory
+ * (no gather into a staging buffer, no copies: the kernel reads every read
+ * where it is and unmasks it in place).  Each read is at most 32 KiB, the
+ * total at most the small-batch limit (64 MiB by default), and reads must not
+ * overlap.  Read i is segment i: hvws_get_segment_frames / hvws_get_frames
+ * report its frames with hdr_off / pay_off relative to reads[i]; carry is
+ * in/out per read.  HVWS_EINVAL (nothing done) if a read is not registered. */
+int hvws_rx_reads(hvws_ctx* ctx, char* const* reads, const uint64_t* lens, websocket_parser* carry, uint32_t n,
+                  int unmask);
+
 /* Host-inclusive streaming unmask of a large pinned host buffer holding
  * frames back to back from one stream: chunked H2D -> scan -> unmask -> D2H,
  * double-buffered over two streams.  carry is in/out. */

@@ -155,6 +155,13 @@ _SIGS = {
         [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
          ctypes.POINTER(ctypes.c_int)],
     ),
+    "hvws_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "hvws_host_unregister": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "hvws_rx_reads": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_uint32,
+         ctypes.c_int],
+    ),
     "hvws_feeder_new": (ctypes.c_void_p, []),
     "hvws_feeder_free": (None, [ctypes.c_void_p]),
     "hvws_feeder_flush": (ctypes.c_int, [ctypes.c_void_p]),

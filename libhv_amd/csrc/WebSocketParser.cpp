@@ -31,6 +31,7 @@ namespace hvws {
 hvws_ctx* thread_ctx();
 char* pinned_stage(uint64_t bytes);
 void ctx_copy_settings(hvws_ctx* dst, const hvws_ctx* src);
+bool is_pinned(const void* p, uint64_t len);
 void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
               websocket_parser& carry_out, int& started);
 }  // namespace hvws
@@ -63,6 +64,7 @@ void stage_copy(char* stage, const hvws_segment* segs, const char* const* data, 
 
 namespace {
 const int kMaxReserve = 1 << 24;   // MAX_PAYLOAD_LENGTH, reference WebSocketParser.cpp:6
+const size_t kMappedRead = 32 << 10;   // largest read hvws_rx_reads takes in place
 }
 
 WebSocketParser::WebSocketParser() {
@@ -197,6 +199,7 @@ struct feed_batch {
     std::vector<hvws_frame> frames;
     std::vector<uint64_t> first, count;
     uint64_t total = 0;
+    bool mapped = false;   // reads taken in place (hvws_rx_reads): record offsets are per read
     int n() const { return (int)parsers.size(); }
     void set(WebSocketParser* const* p, const char* const* d, const size_t* l, int k, int* r) {
         parsers.assign(p, p + k);
@@ -227,12 +230,22 @@ void gpu_part(feed_batch& b) {
         g_ft.ph[k] += t1 - t0;
         t0 = t1;
     };
-    char* stage = hvws::pinned_stage(b.total);
-    stage_copy(stage, b.segs.data(), b.data.data(), b.len.data(), n, b.total, true);
-    lap(1);
     hvws_ctx* c = hvws::thread_ctx();
-    if (hvws_rx_batch(c, (uint8_t*)stage, b.total, b.segs.data(), b.carry.data(), (uint32_t)n, 1) != HVWS_OK)
-        hvws::fatal("hvws_rx_batch");
+    static_assert(sizeof(size_t) == sizeof(uint64_t), "read lengths pass as uint64_t");
+    // Reads in registered pinned memory (an event loop whose read buffers come
+    // from hvws_host_alloc / hvws_host_register) go to the device where they
+    // are: no gather, no write-back.  Anything else goes through the stage.
+    b.mapped = n && b.len[0] <= kMappedRead && hvws::is_pinned(b.data[0], b.len[0]) &&
+               hvws_rx_reads(c, const_cast<char* const*>(b.data.data()), (const uint64_t*)b.len.data(),
+                             b.carry.data(), (uint32_t)n, 1) == HVWS_OK;
+    char* stage = nullptr;
+    if (!b.mapped) {
+        stage = hvws::pinned_stage(b.total);
+        stage_copy(stage, b.segs.data(), b.data.data(), b.len.data(), n, b.total, true);
+        lap(1);
+        if (hvws_rx_batch(c, (uint8_t*)stage, b.total, b.segs.data(), b.carry.data(), (uint32_t)n, 1) != HVWS_OK)
+            hvws::fatal("hvws_rx_batch");
+    }
     const int64_t nf = hvws_frame_count(c);
     b.frames.resize((size_t)(nf > 0 ? nf : 0));
     b.first.resize((size_t)n);
@@ -243,7 +256,7 @@ void gpu_part(feed_batch& b) {
     lap(2);
     // Every segment leaves the (thread's, reusable) stage before any callback
     // runs: an onMessage that feeds again on this thread restages it.
-    stage_copy(stage, b.segs.data(), b.data.data(), b.len.data(), n, b.total, false);   // in place, like the reference
+    if (!b.mapped) stage_copy(stage, b.segs.data(), b.data.data(), b.len.data(), n, b.total, false);   // in place, like the reference
     lap(3);
 }
 
@@ -254,7 +267,7 @@ void replay_part(feed_batch& b) {
     for (int i = 0; i < b.n(); ++i) {
         char* dst = const_cast<char*>(b.data[i]);
         b.carry[i].data = b.parsers[i]->parser->data;
-        const size_t used = replay_messages(b.parsers[i], dst, b.segs[i].off, b.frames.data() + b.first[i],
+        const size_t used = replay_messages(b.parsers[i], dst, b.mapped ? 0 : b.segs[i].off, b.frames.data() + b.first[i],
                                             (size_t)b.count[i], b.carry[i], b.len[i]);
         if (b.rets) b.rets[i] = (int)used;
     }

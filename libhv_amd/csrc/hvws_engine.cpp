@@ -10,6 +10,9 @@
 
 #include <algorithm>
 #include <vector>
+#include <mutex>
+#include <shared_mutex>
+#include <atomic>
 
 #include "hvws.h"
 #include "hvws_internal.h"
@@ -1072,7 +1075,7 @@ bool small_eligible(hvws_ctx* c, uint64_t len, const hvws_segment* segs, uint32_
 
 // hvws_rx_batch for small batches: one H2D copy, k_small, one sync.
 int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment* segs, websocket_parser* carry,
-                   uint32_t nseg, int unmask) {
+                   uint32_t nseg, int unmask, uint8_t* dev_base = nullptr) {
     for (uint32_t s = 0; s < nseg; ++s) {
         if (segs[s].off > len || segs[s].len > len - segs[s].off)
             return set_err(HVWS_EINVAL, "segment %u [%llu,+%llu) outside the %llu-byte buffer", s,
@@ -1085,7 +1088,9 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     const uint64_t o_carry = o_segs + (uint64_t)nseg * sizeof(dseg);
     const uint64_t o_slot = o_carry + (uint64_t)nseg * sizeof(dcarry);
     const uint64_t o_data = (o_slot + (uint64_t)nseg * 8 + 255) & ~255ull;
-    uint8_t* user_mapped = host_mapped(h_rx);   // pinned caller buffer: read and write it directly
+    // pinned caller buffer: read and write it directly.  dev_base (hvws_rx_reads):
+    // the segments are the callers' registered pinned reads, offsets from dev_base.
+    uint8_t* user_mapped = dev_base ? dev_base : host_mapped(h_rx);
     const uint64_t pkt = user_mapped ? o_data : o_data + len;
     // Segments of event-loop size are staged in LDS by k_small; small
     // batches of them may also go zero-copy (the kernel reads the packet and
@@ -1093,12 +1098,17 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     uint64_t max_seg = 0;
     for (uint32_t s = 0; s < nseg; ++s) max_seg = std::max<uint64_t>(max_seg, segs[s].len);
     const bool stage = max_seg <= kStageSegment;
-    const bool zc = stage && c->small_zc && len <= c->zc_batch;
+    const bool zc = dev_base || (stage && c->small_zc && len <= c->zc_batch);
+    if (dev_base && !stage) return set_err(HVWS_EINVAL, "registered reads must be at most %llu bytes each",
+                                           (unsigned long long)kStageSegment);
     const uint32_t stage_lds = stage ? (uint32_t)(((max_seg + 15) & ~15ull) + 16) : 0u;
     // The pinned packet may still be the source of an in-flight copy.
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
-    HIP_OR(c->h_small_in.ensure(o_data + len + 64), HVWS_ENOMEM);
-    HIP_OR(c->d_small_in.ensure(o_data + len + 64), HVWS_ENOMEM);
+    // The packet carries the bytes only when the caller's buffer is not
+    // device-mapped; the device copy exists only without zero-copy.  (With
+    // dev_base, len spans all the reads' addresses, not bytes to move.)
+    HIP_OR(c->h_small_in.ensure(o_data + (user_mapped ? 0 : len) + 64), HVWS_ENOMEM);
+    if (!zc) HIP_OR(c->d_small_in.ensure(o_data + len + 64), HVWS_ENOMEM);
     uint8_t* hp = c->h_small_in.as<uint8_t>();
     memset(hp, 0, 64);
     dseg* hs = (dseg*)(hp + o_segs);
@@ -1199,6 +1209,60 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
         }
     }
     return HVWS_OK;
+}
+
+// ------------------------------------------- registered pinned host memory
+// Ranges the device can read and write in place (hvws_host_alloc,
+// hvws_host_register).  hvws_rx_reads looks every read up here; a
+// thread-local last hit makes the common case (many reads out of one pinned
+// arena) one compare per read.
+struct pinned_range {
+    uintptr_t lo, hi;
+    uint8_t* dev;
+    bool registered;   // hipHostRegister'ed (unregister on removal), else hipHostMalloc'ed
+};
+std::shared_mutex g_pin_m;
+std::vector<pinned_range> g_pins;     // sorted by lo, disjoint
+std::atomic<uint64_t> g_pin_gen{1};   // bumped on every removal
+
+void pin_add(void* p, uint64_t bytes, uint8_t* dev, bool registered) {
+    std::unique_lock<std::shared_mutex> lk(g_pin_m);
+    const pinned_range r{(uintptr_t)p, (uintptr_t)p + bytes, dev, registered};
+    g_pins.insert(std::upper_bound(g_pins.begin(), g_pins.end(), r,
+                                   [](const pinned_range& a, const pinned_range& b) { return a.lo < b.lo; }),
+                  r);
+}
+
+// Removes the range starting at p; returns it (lo == 0 if none).
+pinned_range pin_remove(void* p) {
+    std::unique_lock<std::shared_mutex> lk(g_pin_m);
+    for (auto it = g_pins.begin(); it != g_pins.end(); ++it)
+        if (it->lo == (uintptr_t)p) {
+            const pinned_range r = *it;
+            g_pins.erase(it);
+            g_pin_gen.fetch_add(1);
+            return r;
+        }
+    return pinned_range{0, 0, nullptr, false};
+}
+
+// Device address of [p, p+len) if it lies inside one registered range.
+uint8_t* pinned_dev(const void* p, uint64_t len) {
+    thread_local pinned_range last{0, 0, nullptr, false};
+    thread_local uint64_t last_gen = 0;
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t gen = g_pin_gen.load(std::memory_order_acquire);
+    if (last_gen != gen || a < last.lo || a + len > last.hi) {
+        std::shared_lock<std::shared_mutex> lk(g_pin_m);
+        auto it = std::upper_bound(g_pins.begin(), g_pins.end(), a,
+                                   [](uintptr_t v, const pinned_range& r) { return v < r.lo; });
+        if (it == g_pins.begin()) return nullptr;
+        --it;
+        if (a + len > it->hi) return nullptr;
+        last = *it;
+        last_gen = gen;
+    }
+    return last.dev + (a - last.lo);
 }
 
 // Unmask launch after a scan of the same buffer.
@@ -1365,13 +1429,109 @@ void* hvws_host_alloc(hvws_ctx* c, uint64_t bytes) {
         set_err(HVWS_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
         return nullptr;
     }
+    if (uint8_t* dev = host_mapped(p)) pin_add(p, bytes ? bytes : 16, dev, false);
     return p;
 }
 
 void hvws_host_free(hvws_ctx* c, void* p) {
     if (!c || !p) return;
     hipSetDevice(c->device);
+    pin_remove(p);
     hipHostFree(p);
+}
+
+int hvws_host_register(hvws_ctx* c, void* p, uint64_t bytes) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!p || !bytes) return set_err(HVWS_EINVAL, "empty range");
+    HIP_OR(hipHostRegister(p, bytes, hipHostRegisterMapped), HVWS_EHIP);
+    uint8_t* dev = host_mapped(p);
+    if (!dev) {
+        hipHostUnregister(p);
+        return set_err(HVWS_EHIP, "registered range not device-mapped");
+    }
+    pin_add(p, bytes, dev, true);
+    return HVWS_OK;
+}
+
+int hvws_host_unregister(hvws_ctx* c, void* p) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    const pinned_range r = pin_remove(p);
+    if (!r.lo || !r.registered) return set_err(HVWS_EINVAL, "not a range from hvws_host_register");
+    HIP_OR(hipHostUnregister(p), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_rx_reads(hvws_ctx* c, char* const* reads, const uint64_t* lens, websocket_parser* carry, uint32_t n,
+                  int unmask) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (n && (!reads || !lens)) return set_err(HVWS_EINVAL, "null read table");
+    // device address of every read; the batch goes to k_small in address order
+    std::vector<uint8_t*> dev(n);
+    bool sorted = true;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (lens[i] > kStageSegment)
+            return set_err(HVWS_EINVAL, "read %u: %llu bytes (at most %llu)", i, (unsigned long long)lens[i],
+                           (unsigned long long)kStageSegment);
+        if (!(dev[i] = pinned_dev(reads[i], lens[i])))
+            return set_err(HVWS_EINVAL, "read %u is not in registered pinned memory", i);
+        if (i && dev[i] < dev[i - 1]) sorted = false;
+    }
+    std::vector<uint32_t> ord(n);
+    for (uint32_t i = 0; i < n; ++i) ord[i] = i;
+    if (!sorted) std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return dev[a] < dev[b]; });
+    uint8_t* base = n ? (uint8_t*)((uintptr_t)dev[ord[0]] & ~(uintptr_t)15) : nullptr;
+    std::vector<hvws_segment> segs(n);
+    std::vector<websocket_parser> cin(carry ? n : 0);
+    uint64_t span = 0, total = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t i = ord[k];
+        segs[k].off = (uint64_t)(dev[i] - base);
+        segs[k].len = lens[i];
+        if (k && segs[k].off < segs[k - 1].off + segs[k - 1].len)
+            return set_err(HVWS_EINVAL, "reads %u and %u overlap", ord[k - 1], i);
+        span = segs[k].off + lens[i];
+        total += lens[i];
+        if (carry) copy_parser(cin[k], carry[i]);
+    }
+    const uint64_t limit = c->small_limit && c->small_limit != ~0ull ? c->small_limit : kSmallBatch;
+    if (total > limit) return set_err(HVWS_EINVAL, "%llu bytes of reads (at most %llu per call)",
+                                      (unsigned long long)total, (unsigned long long)limit);
+    if ((rc = rx_batch_small(c, nullptr, span, segs.data(), carry ? cin.data() : nullptr, n, unmask, base)) != HVWS_OK)
+        return rc;
+    // results back in caller order, offsets relative to each read
+    std::vector<hvws_frame> recs(c->hcache.size());
+    std::vector<uint64_t> first(n), count(n);
+    std::vector<dcarry> hc(n);
+    uint64_t at = 0;
+    std::vector<uint32_t> pos(n);   // caller index -> address-order position
+    for (uint32_t k = 0; k < n; ++k) pos[ord[k]] = k;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t k = pos[i];
+        const uint64_t cnt = c->hcount[k], rb = segs[k].off;
+        first[i] = at;
+        count[i] = cnt;
+        hc[i] = c->hcarry[k];
+        for (uint64_t j = 0; j < cnt; ++j) {
+            hvws_frame r = c->hcache[c->hfirst[k] + j];
+            if (r.hdr_off >= 0) r.hdr_off -= (int64_t)rb;
+            r.pay_off -= rb;
+            recs[at + j] = r;
+        }
+        at += cnt;
+        if (carry) {
+            void* keep = carry[i].data;
+            copy_parser(carry[i], cin[k]);
+            carry[i].data = keep;
+        }
+    }
+    c->hcache.swap(recs);
+    c->hfirst.swap(first);
+    c->hcount.swap(count);
+    c->hcarry.swap(hc);
+    return HVWS_OK;
 }
 
 int hvws_h2d(hvws_ctx* c, void* dst, const void* src, uint64_t n) {
@@ -1959,6 +2119,9 @@ void ctx_copy_settings(hvws_ctx* dst, const hvws_ctx* src) {
     dst->zc_batch = src->zc_batch;
     dst->vmask = src->vmask;
 }
+
+// True when [p, p+len) lies in registered pinned memory (hvws_rx_reads can take it).
+bool is_pinned(const void* p, uint64_t len) { return pinned_dev(p, len) != nullptr; }
 
 // Per-thread pinned staging for batched host entry points.
 char* pinned_stage(uint64_t bytes) {

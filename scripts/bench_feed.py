@@ -8,6 +8,12 @@ connection's next read to the parser:
   * gpu_pipe : one hvws_wsp_feeder_submit per iteration (pipelined: iteration
                k's GPU round trip overlaps iteration k-1's callback replay;
                the final flush is inside the timed region);
+  * *_pinned : the connections' read buffers are slices of one pinned arena
+               (hvws_host_alloc), so the reads go to the device in place
+               (hvws_rx_reads: no gather into / write-back from a stage);
+               connection-major (each connection's stream contiguous);
+  * *_ring   : the same, iteration-major (one poll iteration's reads side by
+               side, as a ring of read buffers);
   * gpu_each : WebSocketParser::FeedRecvData per connection (a round trip each);
   * cpu_ref  : the reference frame parser + restated WebSocketParser callbacks
                (oracle/_ref), per connection, one core.
@@ -42,6 +48,7 @@ def main():
     kind = "reference" if H.have_ref() else "port"
     conns = [int(x) for x in os.environ.get("CONNS", "1,16,256,1024,4096").split(",")]
     modes = os.environ.get("MODES", "gpu_many,gpu_pipe,gpu_each,gpu_many_general,gpu_each_general,cpu_ref").split(",")
+    eng = libhv_amd.Engine(0) if any(m.endswith(("_pinned", "_ring")) for m in modes) else None
     for n in conns:
         per_conn = READ * iters
         frames = per_conn // 1032 + 2
@@ -56,6 +63,22 @@ def main():
             # *_general: the COUNT/EMIT/unmask sequence instead of the single-launch small-batch kernel
             L.hvws_set_small_batch_limit(None, (1 << 64) - 1 if mode.endswith("_general") else 0)
             bufs = [np.array(s[:per_conn], copy=True) for s in streams]
+            arena = None
+            ring = mode.endswith("_ring")
+            if mode.endswith("_pinned") or ring:
+                # _pinned: connection i's whole stream at arena + i * per_conn;
+                # _ring: iteration-major, the reads of one poll iteration side by
+                # side (read `it` of connection i at arena + (it * n + i) * READ)
+                arena = L.hvws_host_alloc(eng.ctx, n * per_conn)
+                whole = np.ctypeslib.as_array((ctypes.c_uint8 * (n * per_conn)).from_address(arena))
+                for i in range(n):
+                    if ring:
+                        for it in range(iters):
+                            whole[(it * n + i) * READ:(it * n + i + 1) * READ] = bufs[i][it * READ:(it + 1) * READ]
+                    else:
+                        whole[i * per_conn:(i + 1) * per_conn] = bufs[i]
+                if not ring:
+                    bufs = [whole[i * per_conn:(i + 1) * per_conn] for i in range(n)]
             if mode == "cpu_ref":
                 hs = [R.msgp_new() for _ in range(n)]
                 t0 = time.perf_counter()
@@ -73,10 +96,15 @@ def main():
                 ds = (ctypes.c_void_p * n)()
                 # read pointers for iteration `it` = base + it * READ, set in one
                 # numpy add (a per-connection Python loop would add ~0.5 us each)
-                base = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+                if ring:
+                    base = np.array([arena + i * READ for i in range(n)], dtype=np.uint64)
+                    step = n * READ
+                else:
+                    base = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+                    step = READ
                 ds_np = np.frombuffer(ds, dtype=np.uint64)
                 # warm-up iteration on a scratch copy (allocations, first launch)
-                scratch = [b.copy() for b in bufs]
+                scratch = [np.array(b[:READ], copy=True) for b in bufs]   # pageable: the warm-up takes the staging path
                 for i in range(n):
                     ds[i] = scratch[i].ctypes.data
                 warm = [L.hvws_wsp_new() for _ in range(n)]
@@ -92,7 +120,7 @@ def main():
                     L.hvws_wsp_free(h)
                 t0 = time.perf_counter()
                 for it in range(iters):
-                    ds_np[:] = base + np.uint64(it * READ)
+                    ds_np[:] = base + np.uint64(it * step)
                     if feeder:
                         L.hvws_wsp_feeder_submit(feeder, hv, ds, lens, n, rets)
                     elif mode.startswith("gpu_many"):
@@ -105,6 +133,9 @@ def main():
                 dt = time.perf_counter() - t0
                 if feeder:
                     L.hvws_feeder_free(feeder)
+            if arena:
+                bufs = None
+                L.hvws_host_free(eng.ctx, arena)
                 for h in hs:
                     L.hvws_wsp_free(h)
             res[mode] = {
