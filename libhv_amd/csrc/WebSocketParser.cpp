@@ -315,7 +315,7 @@ struct hvws_feeder {
 namespace {
 // Hand-offs spin briefly before blocking: an event loop submits every poll
 // iteration, and a futex wake-up costs ~10-20 us against ~30-50 us round trips.
-constexpr int kFeederSpinUs = 200;
+constexpr int kFeederSpinUs = 50;
 
 template <class Pred>
 bool spin_until(Pred p) {

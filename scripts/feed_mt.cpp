@@ -6,11 +6,16 @@
 // connection's next 8 KiB read (event/hevent.h:16) to the parser:
 //   gpu : hvws_feed_many (this library; one GPU round trip per thread per
 //         iteration, each thread on its own context and stream)
+//   gpupipe : hvws_feeder_submit (the device half of iteration k on the
+//         thread's feeder worker while the loop thread replays k-1)
+//   gpupin, gpupinpipe : the same two with every connection's stream in a
+//         pinned arena (hvws_host_alloc), so the reads go to the device in
+//         place (hvws_rx_reads)
 //   ref : the reference frame parser + message layer (oracle/_ref), per
 //         connection, on the same threads
 // Prints one JSON line: aggregate payload GiB/s and per-iteration latency.
 //
-//   feed_mt <gpu|ref> <threads> <connections per thread> <iterations>
+//   feed_mt <gpu|gpupipe|gpupin|gpupinpipe|ref> <threads> <connections per thread> <iterations>
 #include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -67,7 +72,10 @@ int main(int argc, char** argv) {
         fprintf(stderr, "usage: feed_mt <gpu|ref> <threads> <connections/thread> <iterations>\n");
         return 2;
     }
-    const bool gpu = strcmp(argv[1], "gpu") == 0;
+    const std::string mode = argv[1];
+    const bool gpu = mode.compare(0, 3, "gpu") == 0;
+    const bool pipe = mode == "gpupipe" || mode == "gpupinpipe";
+    const bool pin = mode == "gpupin" || mode == "gpupinpipe";
     const int T = atoi(argv[2]), C = atoi(argv[3]), I = atoi(argv[4]);
     RefApi ref = {};
     if (!gpu) {
@@ -93,6 +101,20 @@ int main(int argc, char** argv) {
         th.emplace_back([&, t] {
             if (gpu) hvws_set_thread_device(0);
             std::vector<std::string>& ss = streams[t];
+            // pinned: the thread's streams copied into one arena, connection-major
+            hvws_ctx* actx = nullptr;
+            char* arena = nullptr;
+            const size_t stride = kRead * (I + 1);
+            if (pin) {
+                actx = hvws_ctx_create(0);
+                arena = (char*)hvws_host_alloc(actx, stride * C);
+                if (!arena) {
+                    fprintf(stderr, "hvws_host_alloc: %s\n", hvws_last_error());
+                    exit(1);
+                }
+                for (int c = 0; c < C; ++c) memcpy(arena + (size_t)c * stride, ss[c].data(), stride);
+            }
+            hvws_feeder* feeder = pipe ? hvws_feeder_new() : nullptr;
             std::vector<WebSocketParser> ps(gpu ? C : 0);
             std::vector<void*> rs;
             uint64_t got = 0;
@@ -110,21 +132,29 @@ int main(int argc, char** argv) {
             std::vector<int> rets(C);
             for (int c = 0; c < C && gpu; ++c) pp[c] = &ps[c];
             auto iter = [&](int it) {
-                for (int c = 0; c < C; ++c) dd[c] = &ss[c][(size_t)it * kRead];
-                if (gpu) {
+                for (int c = 0; c < C; ++c)
+                    dd[c] = pin ? arena + (size_t)c * stride + (size_t)it * kRead : &ss[c][(size_t)it * kRead];
+                if (feeder) {
+                    hvws_feeder_submit(feeder, pp.data(), dd.data(), ll.data(), C, rets.data());
+                } else if (gpu) {
                     hvws_feed_many(pp.data(), dd.data(), ll.data(), C, rets.data());
                 } else {
                     for (int c = 0; c < C; ++c) ref.feed(rs[c], dd[c], kRead);
                 }
             };
             iter(0);   // warm-up: contexts, allocations, first launch
+            if (feeder) hvws_feeder_flush(feeder);
             ready++;
             while (!go.load()) std::this_thread::yield();
             const auto t0 = std::chrono::steady_clock::now();
             for (int it = 1; it <= I; ++it) iter(it);
+            if (feeder) hvws_feeder_flush(feeder);   // the last iteration's callbacks, inside the timed region
             secs[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             delivered[t] = got;
             for (void* r : rs) ref.free_(r);
+            if (feeder) hvws_feeder_free(feeder);
+            if (arena) hvws_host_free(actx, arena);
+            if (actx) hvws_ctx_destroy(actx);
             if (gpu) hvws_thread_release();
         });
     }
@@ -141,7 +171,7 @@ int main(int argc, char** argv) {
     printf("{\"bench\": \"feed_mt\", \"mode\": \"%s\", \"threads\": %d, \"connections_per_thread\": %d, "
            "\"iterations\": %d, \"read_bytes\": %zu, \"iteration_us\": %.1f, \"GiBps_payload\": %.3f, "
            "\"message_bytes\": %llu}\n",
-           gpu ? "gpu" : "ref", T, C, I, kRead, wall / I * 1e6, payload / wall / (1 << 30),
+           mode.c_str(), T, C, I, kRead, wall / I * 1e6, payload / wall / (1 << 30),
            (unsigned long long)msg_bytes);
     return 0;
 }
