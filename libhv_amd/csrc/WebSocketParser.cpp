@@ -174,6 +174,15 @@ struct feed_times {
     double ph[6] = {0, 0, 0, 0, 0, 0};   // carry, gather, gpu, scatter, replay, feeder wait
     long calls = 0;
     bool on = getenv("HVWS_FEED_TIMES") && atoi(getenv("HVWS_FEED_TIMES"));
+    std::mutex m;   // the loop thread and feeder workers add to the same counters
+    void add(int k, double us) {
+        std::lock_guard<std::mutex> lk(m);
+        ph[k] += us;
+    }
+    void call() {
+        std::lock_guard<std::mutex> lk(m);
+        ++calls;
+    }
     ~feed_times() {
         if (on && calls)
             fprintf(stderr, "[feed_times] calls=%ld us/call: carry %.1f gather %.1f gpu %.1f scatter %.1f replay %.1f "
@@ -227,7 +236,7 @@ void gpu_part(feed_batch& b) {
     auto lap = [&](int k) {
         if (!g_ft.on) return;
         t1 = now_us();
-        g_ft.ph[k] += t1 - t0;
+        g_ft.add(k, t1 - t0);
         t0 = t1;
     };
     hvws_ctx* c = hvws::thread_ctx();
@@ -271,7 +280,7 @@ void replay_part(feed_batch& b) {
                                             (size_t)b.count[i], b.carry[i], b.len[i]);
         if (b.rets) b.rets[i] = (int)used;
     }
-    if (g_ft.on) g_ft.ph[4] += now_us() - t0;
+    if (g_ft.on) g_ft.add(4, now_us() - t0);
 }
 }  // namespace
 
@@ -282,10 +291,10 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
     feed_batch b;   // local: an onMessage may feed again on this thread
     b.set(parsers, data, len, n, rets);
     for (int i = 0; i < n; ++i) hvws::copy_parser(b.carry[i], *parsers[i]->parser);
-    if (g_ft.on) g_ft.ph[0] += now_us() - t0;
+    if (g_ft.on) g_ft.add(0, now_us() - t0);
     gpu_part(b);
     replay_part(b);
-    g_ft.calls += g_ft.on;
+    if (g_ft.on) g_ft.call();
     return n;
 }
 
@@ -359,7 +368,7 @@ void feeder_wait_idle(hvws_feeder* f) {
         std::unique_lock<std::mutex> lk(f->m);
         f->cv.wait(lk, [f] { return f->job.load(std::memory_order_acquire) == nullptr; });
     }
-    if (g_ft.on) g_ft.ph[5] += now_us() - t0;
+    if (g_ft.on) g_ft.add(5, now_us() - t0);
 }
 
 void feeder_replay_pending(hvws_feeder* f) {
@@ -387,7 +396,7 @@ void feeder_run(hvws_feeder* f, WebSocketParser* const* parsers, const char* con
         if (it != f->pend_idx.end()) hvws::copy_parser(b.carry[i], f->pending->carry[it->second]);
         else hvws::copy_parser(b.carry[i], *parsers[i]->parser);
     }
-    g_ft.calls += g_ft.on;
+    if (g_ft.on) g_ft.call();
     if (b.total <= f->inline_bytes) {
         // Too small for the hand-off to pay: the device half on this thread
         // (its own context), then the previous run's replay.

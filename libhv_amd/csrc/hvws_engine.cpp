@@ -1468,6 +1468,7 @@ int hvws_rx_reads(hvws_ctx* c, char* const* reads, const uint64_t* lens, websock
     int rc = check_ctx(c);
     if (rc) return rc;
     if (n && (!reads || !lens)) return set_err(HVWS_EINVAL, "null read table");
+    if (n == 0) return set_err(HVWS_EINVAL, "no reads");
     // device address of every read; the batch goes to k_small in address order
     std::vector<uint8_t*> dev(n);
     bool sorted = true;
