@@ -195,6 +195,9 @@ struct hvws_ctx {
     dbuf synth_sizes, synth_tiles, synth_bad;
     // small-batch path (k_small): upload packet, record slots, pinned results
     hbuf h_small_in, h_small_out;
+    hbuf h_small_done;             // per-segment completion words k_small writes last
+    uint64_t small_seq = 0;        // value the current call's completion words carry
+    int small_poll = 1;            // $HVWS_SMALL_POLL: poll those words instead of syncing the stream
     hbuf h_feed;   // hvws_feed_many's gather buffer (reference-API thread contexts)
     dbuf d_small_in, d_small_slots;
     uint64_t small_limit = 0;   // bytes; 0 = default
@@ -1155,15 +1158,50 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     // event-carrying launch costs a per-read call ~10 us of ~38 (r2an).
     static const bool timed_env = getenv("HVWS_STEP_EVENTS") && atoi(getenv("HVWS_STEP_EVENTS")) >= 2;
     const bool timed = timed_env;
+    // Completion: each wave releases its stores to system scope and then
+    // writes its segment's word with this call's sequence number; the host
+    // polls the words (in segment order) instead of waiting for the stream,
+    // which also waits for the kernel's end-of-pipe release and signal.
+    uint64_t* done_d = nullptr;
+    const volatile uint64_t* done_h = nullptr;
+    const uint64_t seq = ++c->small_seq;
+    if (c->small_poll) {
+        HIP_OR(c->h_small_done.ensure((uint64_t)nseg * 8 + 64), HVWS_ENOMEM);
+        done_d = mapped<uint64_t>(c->h_small_done);
+        done_h = c->h_small_done.as<uint64_t>();
+        if (!done_d) return set_err(HVWS_EHIP, "pinned completion words not device-mapped");
+    }
     HIP_OR(begin_timed_scan(c, false), HVWS_EHIP);
     HIP_OR(launch_small(d_rx, len, (const dseg*)(d + o_segs), (const dcarry*)(d + o_carry), nseg,
                         (const uint64_t*)(d + o_slot), c->d_small_slots.as<drec>(), ctr, ctr_base,
                         (drec*)(ho_d + nseg), hcap, ho_d, user_mapped ? user_mapped : hp_d + o_data, unmask,
-                        c->vmask, stage_lds, c->stream, timed ? c->tev[c->t_cur][0] : nullptr,
+                        c->vmask, stage_lds, done_d, seq, c->stream, timed ? c->tev[c->t_cur][0] : nullptr,
                         timed ? c->tev[c->t_cur][1] : nullptr),
            HVWS_EHIP);
     if (timed) c->t_rec[c->t_cur] |= 3u;
-    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    if (done_h) {
+        // Spin on the words; every ~64 polls ask the stream, so a kernel that
+        // faulted (or was never dispatched) ends the wait with its error.
+        uint32_t s = 0, spins = 0;
+        while (s < nseg) {
+            if (done_h[s] == seq) {
+                ++s;
+                continue;
+            }
+            if ((++spins & 63u) == 0) {
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q == hipSuccess) {   // finished: every word is written
+                    if (done_h[s] != seq) return set_err(HVWS_EHIP, "k_small finished without completing segment %u", s);
+                    continue;
+                }
+                if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "k_small: %s", hipGetErrorString(q));
+            }
+            __builtin_ia32_pause();
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    } else {
+        HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    }
     if (!user_mapped && unmask && len) par_memcpy(h_rx, hp + o_data, len);
     // host cache in segment order
     uint64_t total = 0;
@@ -1316,6 +1354,8 @@ hvws_ctx* hvws_ctx_create(int device) {
     // so no stale copy can sit in a device cache across reuses.
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
+    c->h_small_done.flags = hipHostMallocCoherent;
+    if (const char* sp = getenv("HVWS_SMALL_POLL")) c->small_poll = atoi(sp) ? 1 : 0;
     if (const char* zc = getenv("HVWS_SMALL_ZC")) c->small_zc = atoi(zc) ? 1 : 0;
     if (const char* zb = getenv("HVWS_ZC_BATCH")) c->zc_batch = strtoull(zb, nullptr, 0);
     if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
@@ -1377,6 +1417,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         b->release();
     c->h_tx.release();
     c->h_small_in.release();
+    c->h_small_done.release();
     c->h_small_out.release();
     c->h_feed.release();
     c->h_segs.release();

@@ -275,7 +275,8 @@ constexpr uint64_t kZcBatch = 1ull << 20;         // largest batch sent zero-cop
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, uint64_t rec_base,
                         drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
-                        uint32_t stage_lds, hipStream_t st, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+                        uint32_t stage_lds, uint64_t* h_done, uint64_t seq, hipStream_t st,
+                        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 // Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
 // copy_width() threads (the caller included; serial when another caller
 // holds the pool); par_memcpy splits copies of >= kParCopyMin bytes.

@@ -822,7 +822,7 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
                                               unsigned long long* __restrict__ rec_total, drec* __restrict__ h_rec,
                                               uint64_t h_rec_cap, dsmall_out* __restrict__ h_out,
                                               uint8_t* __restrict__ h_rx, int unmask, uint32_t vmask,
-                                              uint64_t rec_base) {
+                                              uint64_t rec_base, uint64_t* __restrict__ h_done, uint64_t seq) {
     extern __shared__ u32x4 lds_seg[];
     __shared__ drec lrec[SMALL_LREC];
     const uint32_t s = blockIdx.x;
@@ -927,12 +927,20 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
         o.st = st;
         h_out[s] = o;
     }
+    if (h_done) {
+        // Completion word the host polls instead of synchronising the stream:
+        // every store of this wave above (bytes, records, h_out) is released
+        // to system scope first, so seeing `seq` means seeing all of them.
+        __threadfence_system();
+        if (lane == 0) __hip_atomic_store(h_done + s, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dcarry* carry_in, uint32_t nseg,
                         const uint64_t* slot_base, drec* slots, unsigned long long* rec_total, uint64_t rec_base,
                         drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
-                        uint32_t stage_lds, hipStream_t st, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                        uint32_t stage_lds, uint64_t* h_done, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
+                        hipEvent_t ev_stop) {
     if (nseg == 0) return hipSuccess;
     // Timing events, when asked for, ride on the dispatch itself (no marker
     // packets); without them the plain launch is cheaper still.
@@ -940,17 +948,17 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     if (stage_lds && ev)
         hipExtLaunchKernelGGL(k_small<true>, dim3(nseg), dim3(64), stage_lds, st, ev_start, ev_stop, 0u, rx, rx_len,
                               segs, carry_in, slot_base, slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask,
-                              rec_base);
+                              rec_base, h_done, seq);
     else if (stage_lds)
         hipLaunchKernelGGL(k_small<true>, dim3(nseg), dim3(64), stage_lds, st, rx, rx_len, segs, carry_in, slot_base,
-                           slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask, rec_base);
+                           slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask, rec_base, h_done, seq);
     else if (ev)
         hipExtLaunchKernelGGL(k_small<false>, dim3(nseg), dim3(64), 0, st, ev_start, ev_stop, 0u, rx, rx_len, segs,
                               carry_in, slot_base, slots, rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask,
-                              rec_base);
+                              rec_base, h_done, seq);
     else
         hipLaunchKernelGGL(k_small<false>, dim3(nseg), dim3(64), 0, st, rx, rx_len, segs, carry_in, slot_base, slots,
-                           rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask, rec_base);
+                           rec_total, h_rec, h_rec_cap, h_out, h_rx, unmask, vmask, rec_base, h_done, seq);
     return hipGetLastError();
 }
 
