@@ -159,3 +159,38 @@ def test_feed_recv_data_rejects(path, seed):
     hlen = 2 + {126: 2, 127: 8}.get(b1 & 127, 0) + (4 if b1 & 128 else 0)
     assert rets == [off + hlen - 1]
     assert msgs == omsgs
+
+
+@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
+def test_batched_feed_rejects(path, feeder):
+    """hvws_feed_many and a feeder (whose worker context takes the creating
+    thread's validation classes) reject each connection's first violating
+    header exactly as that connection's own FeedRecvData does."""
+    L = libhv_amd.lib()
+    L.hvws_set_validation(None, V.V_ALL)
+    cases = []
+    for seed in (21, 22, 23, 24):
+        good, bad, _ = _valid_then_bad(seed)
+        cases.append(good + bad)
+    cases.append(_valid_then_bad(25)[0])   # a connection with no violation
+    exp = [H.run_messages("gpu", d, [len(d)])[:2] for d in cases]
+    n = len(cases)
+    sinks = [H.MsgLog() for _ in cases]
+    cbs = [libhv_amd.MSG_CB(s._on) for s in sinks]
+    hs = [L.hvws_wsp_new() for _ in cases]
+    for h, cb in zip(hs, cbs):
+        L.hvws_wsp_set_sink(h, cb, None)
+    bufs = [ctypes.create_string_buffer(d, len(d)) for d in cases]
+    hv = (ctypes.c_void_p * n)(*hs)
+    ds = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    ls = (ctypes.c_size_t * n)(*[len(d) for d in cases])
+    rets = (ctypes.c_int * n)()
+    if feeder:
+        f = L.hvws_feeder_new()
+        assert L.hvws_wsp_feeder_submit(f, hv, ds, ls, n, rets) == n
+        L.hvws_feeder_free(f)
+    else:
+        assert L.hvws_wsp_feed_many(hv, ds, ls, n, rets) == n
+    for i in range(n):
+        assert (sinks[i].msgs, [rets[i]]) == exp[i], i
+        L.hvws_wsp_free(hs[i])
