@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-tx", action="store_true", help="skip the transmit-side (hvws_build_frames) measurement")
     ap.add_argument("--validate", action="store_true",
                     help="RFC 6455 header validation on (hvws_set_validation, all classes; off = reference behaviour)")
+    ap.add_argument("--feed-conns", type=int, default=1024,
+                    help="event-loop leg: connections per poll iteration (0: skip)")
+    ap.add_argument("--feed-iters", type=int, default=20, help="event-loop leg: poll iterations (8 KiB reads each)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
     return ap.parse_args()
@@ -183,6 +186,103 @@ def pcie_ceiling(device: int, nbytes: int = 1 << 30, piece: int = 64 << 20, reps
             "concurrent_GBps_per_direction": round(nbytes / t_both / 1e9, 2), "bytes": nbytes, "piece": piece}
 
 
+FEED_READ = 8192   # event/hevent.h:16 HLOOP_READ_BUFSIZE
+
+
+def event_loop_leg(eng, device: int, conns: int, iters: int, seed: int):
+    """SURVEY 8(f) row 1 inside the run: `conns` connections each deliver
+    `iters` 8 KiB reads of a stream of masked 1 KiB binary frames (device
+    synth); one poll iteration hands every connection's next read over.
+    Read buffers are one pinned arena (hvws_host_alloc), a poll iteration's
+    reads side by side, so the reads go to the kernel in place (hvws_rx_reads).
+    Timed: hvws_feeder_submit per iteration + the final flush (pipelined), and
+    hvws_wsp_feed_many per iteration (synchronous), each over a whole pass with
+    fresh parsers after one untimed pass of each.  Returns (result dict, the masked
+    streams for the CPU reference, their payload bytes)."""
+    import libhv_amd
+    from libhv_amd import synth
+
+    L = libhv_amd.lib()
+    L.hvws_set_thread_device(device)
+    per = FEED_READ * iters
+    fp = synth.uniform_plan(conns * (per // 1032 + 2), 1024, seed).split(conns)
+    dpf = libhv_amd.DevicePlan(eng, fp)
+    buf = eng.alloc(fp.total + 64)
+    eng.synth(buf, fp.total, fp.seed, dpf, 0)
+    host = buf.download(fp.total)
+    buf.free()
+    dpf.free()
+    streams = np.stack([host[o:o + per] for o, _ in fp.segments])   # (conns, per), masked
+    arena = L.hvws_host_alloc(eng.ctx, conns * per)
+    ring = np.ctypeslib.as_array((ctypes.c_uint8 * (conns * per)).from_address(arena))
+    ring.reshape(iters, conns, FEED_READ)[:] = streams.reshape(conns, iters, FEED_READ).transpose(1, 0, 2)
+    lens = (ctypes.c_size_t * conns)(*([FEED_READ] * conns))
+    rets = (ctypes.c_int * conns)()
+    ds = (ctypes.c_void_p * conns)()
+    ds_np = np.frombuffer(ds, dtype=np.uint64)
+    base = np.uint64(arena) + np.arange(conns, dtype=np.uint64) * np.uint64(FEED_READ)
+
+    feeder = L.hvws_feeder_new()   # one feeder (its worker context stays warm across passes)
+
+    def one_pass(pipelined: bool) -> float:
+        hs = [L.hvws_wsp_new() for _ in range(conns)]
+        hv = (ctypes.c_void_p * conns)(*hs)
+        t = time.perf_counter()
+        for it in range(iters):
+            ds_np[:] = base + np.uint64(it * conns * FEED_READ)
+            if pipelined:
+                L.hvws_wsp_feeder_submit(feeder, hv, ds, lens, conns, rets)
+            else:
+                L.hvws_wsp_feed_many(hv, ds, lens, conns, rets)
+        if pipelined:
+            L.hvws_feeder_flush(feeder)
+        dt = time.perf_counter() - t
+        for h in hs:
+            L.hvws_wsp_free(h)
+        assert all(r == FEED_READ for r in rets), "event-loop leg: a read was not consumed"
+        return dt
+
+    # each pass unmasks (or re-masks) every read in place: the same work;
+    # one untimed pass per mode first (contexts, staging, first launches)
+    one_pass(True)
+    one_pass(False)
+    t_pipe = one_pass(True)
+    t_sync = one_pass(False)
+    L.hvws_feeder_free(feeder)
+    L.hvws_host_free(eng.ctx, arena)
+    pay = conns * iters * FEED_READ * 1024 / 1032
+    res = {
+        "connections": conns, "read_bytes": FEED_READ, "iterations": iters, "frames": "masked 1 KiB binary",
+        "pipelined_us_per_iteration": round(t_pipe / iters * 1e6, 1),
+        "GiBps_payload": round(pay / t_pipe / 2**30, 3),
+        "batched_us_per_iteration": round(t_sync / iters * 1e6, 1),
+        "batched_GiBps_payload": round(pay / t_sync / 2**30, 3),
+        "api": "hvws_feeder_submit (pipelined) / hvws_feed_many over hvws_host_alloc read buffers (hvws_rx_reads)",
+    }
+    return res, streams, pay
+
+
+def cpu_event_loop(streams: np.ndarray, iters: int, pay: float):
+    """The reference parser + WebSocketParser message layer on one core over
+    the same reads, connection by connection per poll iteration."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wsharness as H
+
+    R = H.ref() if H.have_ref() else H.oracle()
+    bufs = np.array(streams, copy=True)
+    conns = bufs.shape[0]
+    hs = [R.msgp_new() for _ in range(conns)]
+    addr = [bufs[i].ctypes.data for i in range(conns)]
+    t = time.perf_counter()
+    for it in range(iters):
+        for i in range(conns):
+            R.msgp_feed(hs[i], addr[i] + it * FEED_READ, FEED_READ)
+    dt = time.perf_counter() - t
+    for h in hs:
+        R.msgp_free(h)
+    return {"us_per_iteration": round(dt / iters * 1e6, 1), "GiBps_payload": round(pay / dt / 2**30, 3), "cores": 1}
+
+
 def init_dist():
     """(rank, world, local_rank, dist-or-None).  One process per GPU; gloo
     carries only the barrier and the timing reduction (no data collectives)."""
@@ -224,6 +324,7 @@ def main():
         args.cpu_seconds = 0
         args.host_gib = 0
         args.no_tx = True
+        args.feed_conns = 0
     import torch
 
     import libhv_amd
@@ -445,6 +546,11 @@ def main():
     dp.free()
     rx.free()
 
+    feed_streams = None
+    if rank == 0 and args.feed_conns > 0:
+        extra["event_loop"], feed_streams, feed_pay = event_loop_leg(eng, device, args.feed_conns, args.feed_iters,
+                                                                     plan.seed + 7)
+
     if rank == 0:
         cpu = None
         if sample is not None:
@@ -459,6 +565,8 @@ def main():
                 "decode_only": {"value": round(cpu_decode_only(sample, plan, args.cpu_seconds / 4), 3), "cores": 1,
                                 "note": "websocket_decode over the sample's masked payload spans"},
             }
+            if feed_streams is not None:
+                cpu["event_loop"] = cpu_event_loop(feed_streams, args.feed_iters, feed_pay)
         out = {
             "metric": "device-resident WS unmask GiB/s, 64 KiB masked frames, 1/2/4/8 MI355X",
             "value": round(value, 2),
