@@ -271,9 +271,36 @@ void gpu_part(feed_batch& b) {
 
 // The host half, on the loop thread: the reference's message logic and
 // onMessage callbacks, connection by connection in submission order.
+// $HVWS_REPLAY_PREFETCH (bytes, default 64 KiB; 0 = off): while connection i
+// replays, the next connections' read bytes -- just written by the device
+// across PCIe, so in DRAM, not in any cache -- are prefetched up to this far
+// ahead; the appends otherwise wait on DRAM a few cache lines at a time.
+const uint64_t g_replay_prefetch =
+    getenv("HVWS_REPLAY_PREFETCH") ? strtoull(getenv("HVWS_REPLAY_PREFETCH"), nullptr, 0) : (64u << 10);
+
 void replay_part(feed_batch& b) {
     double t0 = g_ft.on ? now_us() : 0;
+    int pf_conn = 0;          // next connection whose bytes to prefetch
+    uint64_t pf_off = 0;      // ... from this offset in its read
+    uint64_t pf_ahead = 0;    // bytes prefetched beyond the connection being replayed
     for (int i = 0; i < b.n(); ++i) {
+        if (g_replay_prefetch) {
+            if (i) pf_ahead = pf_ahead > b.len[i] ? pf_ahead - b.len[i] : 0;   // connection i is no longer ahead
+            if (pf_conn <= i) {
+                pf_conn = i + 1;
+                pf_off = 0;
+                pf_ahead = 0;
+            }
+            while (pf_conn < b.n() && pf_ahead < g_replay_prefetch) {
+                const char* p = b.data[pf_conn];
+                const uint64_t n = b.len[pf_conn];
+                for (; pf_off < n && pf_ahead < g_replay_prefetch; pf_off += 64, pf_ahead += 64) __builtin_prefetch(p + pf_off);
+                if (pf_off >= n) {
+                    ++pf_conn;
+                    pf_off = 0;
+                }
+            }
+        }
         char* dst = const_cast<char*>(b.data[i]);
         b.carry[i].data = b.parsers[i]->parser->data;
         const size_t used = replay_messages(b.parsers[i], dst, b.mapped ? 0 : b.segs[i].off, b.frames.data() + b.first[i],
