@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 #include <mutex>
 #include <shared_mutex>
@@ -65,12 +66,14 @@ struct dbuf {
 
 struct hbuf {   // grow-only pinned host allocation
     void* p = nullptr;
+    void* dev = nullptr;   // its device-mapped address, looked up once per allocation
     uint64_t cap = 0;
     unsigned flags = hipHostMallocDefault;   // hipHostMallocCoherent: device reads/writes bypass its caches
     hipError_t ensure(uint64_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
         if (p) hipHostFree(p);
         p = nullptr;
+        dev = nullptr;
         cap = 0;
         uint64_t want = std::max<uint64_t>(bytes + bytes / 2, 4096);
         hipError_t e = hipHostMalloc(&p, want, flags);
@@ -80,6 +83,7 @@ struct hbuf {   // grow-only pinned host allocation
     void release() {
         if (p) hipHostFree(p);
         p = nullptr;
+        dev = nullptr;
         cap = 0;
     }
     template <typename T>
@@ -198,6 +202,7 @@ struct hvws_ctx {
     hbuf h_small_done;             // per-segment completion words k_small writes last
     uint64_t small_seq = 0;        // value the current call's completion words carry
     int small_poll = 1;            // $HVWS_SMALL_POLL: poll those words instead of syncing the stream
+    bool small_quiet = false;      // the last small call saw all its words: its kernel no longer touches the pinned buffers
     hbuf h_feed;   // hvws_feed_many's gather buffer (reference-API thread contexts)
     dbuf d_small_in, d_small_slots;
     uint64_t small_limit = 0;   // bytes; 0 = default
@@ -327,9 +332,8 @@ int check_ctx(hvws_ctx* c) {
 // Device address of a pinned host buffer.
 template <typename T>
 T* mapped(hbuf& b) {
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, b.p, 0) != hipSuccess) return nullptr;
-    return reinterpret_cast<T*>(d);
+    if (!b.dev && b.p && hipHostGetDevicePointer(&b.dev, b.p, 0) != hipSuccess) b.dev = nullptr;
+    return reinterpret_cast<T*>(b.dev);
 }
 
 // Which per-step timing events are recorded: 2 = scan begin/end and unmask
@@ -1105,8 +1109,12 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     if (dev_base && !stage) return set_err(HVWS_EINVAL, "registered reads must be at most %llu bytes each",
                                            (unsigned long long)kStageSegment);
     const uint32_t stage_lds = stage ? (uint32_t)(((max_seg + 15) & ~15ull) + 16) : 0u;
-    // The pinned packet may still be the source of an in-flight copy.
-    HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    // The pinned packet may still be the source of an in-flight copy --
+    // unless the last small call saw every completion word: then its copy
+    // and its kernel's host accesses are over, and waiting for the stream
+    // would only wait for the kernel's end-of-pipe signal (~10 us).
+    if (!c->small_quiet) HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
+    c->small_quiet = false;
     // The packet carries the bytes only when the caller's buffer is not
     // device-mapped; the device copy exists only without zero-copy.  (With
     // dev_base, len spans all the reads' addresses, not bytes to move.)
@@ -1180,15 +1188,19 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
            HVWS_EHIP);
     if (timed) c->t_rec[c->t_cur] |= 3u;
     if (done_h) {
-        // Spin on the words; every ~64 polls ask the stream, so a kernel that
+        // Spin on the words; now and then ask the stream, so a kernel that
         // faulted (or was never dispatched) ends the wait with its error.
+        // (The stream is asked at most every ~100 us: a query takes the
+        // runtime's locks, and right after a launch one cost ~7 us.)
         uint32_t s = 0, spins = 0;
+        auto next_query = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
         while (s < nseg) {
             if (done_h[s] == seq) {
                 ++s;
                 continue;
             }
-            if ((++spins & 63u) == 0) {
+            if ((++spins & 63u) == 0 && std::chrono::steady_clock::now() >= next_query) {
+                next_query = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
                 const hipError_t q = hipStreamQuery(c->stream);
                 if (q == hipSuccess) {   // finished: every word is written
                     if (done_h[s] != seq) return set_err(HVWS_EHIP, "k_small finished without completing segment %u", s);
@@ -1202,6 +1214,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     } else {
         HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     }
+    c->small_quiet = true;
     if (!user_mapped && unmask && len) par_memcpy(h_rx, hp + o_data, len);
     // host cache in segment order
     uint64_t total = 0;
