@@ -32,6 +32,8 @@ hvws_ctx* thread_ctx();
 char* pinned_stage(uint64_t bytes);
 void ctx_copy_settings(hvws_ctx* dst, const hvws_ctx* src);
 bool is_pinned(const void* p, uint64_t len);
+bool take_frames(hvws_ctx* c, std::vector<hvws_frame>& frames, std::vector<uint64_t>& first,
+                 std::vector<uint64_t>& count);
 void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
               websocket_parser& carry_out, int& started);
 }  // namespace hvws
@@ -255,13 +257,17 @@ void gpu_part(feed_batch& b) {
         if (hvws_rx_batch(c, (uint8_t*)stage, b.total, b.segs.data(), b.carry.data(), (uint32_t)n, 1) != HVWS_OK)
             hvws::fatal("hvws_rx_batch");
     }
-    const int64_t nf = hvws_frame_count(c);
-    b.frames.resize((size_t)(nf > 0 ? nf : 0));
-    b.first.resize((size_t)n);
-    b.count.resize((size_t)n);
-    if ((nf > 0 && hvws_get_frames(c, b.frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
-        hvws_get_segment_frames(c, b.first.data(), b.count.data()) != HVWS_OK)
-        hvws::fatal("frame table read-back");
+    // small path: the records move out of the context's host cache; general
+    // path: read back
+    if (!hvws::take_frames(c, b.frames, b.first, b.count)) {
+        const int64_t nf = hvws_frame_count(c);
+        b.frames.resize((size_t)(nf > 0 ? nf : 0));
+        b.first.resize((size_t)n);
+        b.count.resize((size_t)n);
+        if ((nf > 0 && hvws_get_frames(c, b.frames.data(), 0, (uint64_t)nf) != HVWS_OK) ||
+            hvws_get_segment_frames(c, b.first.data(), b.count.data()) != HVWS_OK)
+            hvws::fatal("frame table read-back");
+    }
     lap(2);
     // Every segment leaves the (thread's, reusable) stage before any callback
     // runs: an onMessage that feeds again on this thread restages it.

@@ -1556,7 +1556,24 @@ int hvws_rx_reads(hvws_ctx* c, char* const* reads, const uint64_t* lens, websock
                                       (unsigned long long)total, (unsigned long long)limit);
     if ((rc = rx_batch_small(c, nullptr, span, segs.data(), carry ? cin.data() : nullptr, n, unmask, base)) != HVWS_OK)
         return rc;
-    // results back in caller order, offsets relative to each read
+    // results back in caller order, offsets relative to each read; reads
+    // already in address order (one arena filled in order) rebase in place
+    if (sorted) {
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint64_t rb = segs[i].off;
+            hvws_frame* r = c->hcache.data() + c->hfirst[i];
+            for (uint64_t j = 0; j < c->hcount[i]; ++j) {
+                if (r[j].hdr_off >= 0) r[j].hdr_off -= (int64_t)rb;
+                r[j].pay_off -= rb;
+            }
+            if (carry) {
+                void* keep = carry[i].data;
+                copy_parser(carry[i], cin[i]);
+                carry[i].data = keep;
+            }
+        }
+        return HVWS_OK;
+    }
     std::vector<hvws_frame> recs(c->hcache.size());
     std::vector<uint64_t> first(n), count(n);
     std::vector<dcarry> hc(n);
@@ -2173,6 +2190,21 @@ void ctx_copy_settings(hvws_ctx* dst, const hvws_ctx* src) {
     dst->small_zc = src->small_zc;
     dst->zc_batch = src->zc_batch;
     dst->vmask = src->vmask;
+}
+
+// The host record cache of the last small-path call, moved out (no copy) with
+// its per-segment first/count; the context then holds no scan (the batched
+// drop-in is the only reader of its thread context's records).
+bool take_frames(hvws_ctx* c, std::vector<hvws_frame>& frames, std::vector<uint64_t>& first,
+                 std::vector<uint64_t>& count) {
+    if (!c->have_scan || !c->hcache_valid || c->rx) return false;
+    frames.swap(c->hcache);
+    first.swap(c->hfirst);
+    count.swap(c->hcount);
+    c->hcache.clear();
+    c->hcache_valid = false;
+    c->have_scan = false;
+    return true;
 }
 
 // True when [p, p+len) lies in registered pinned memory (hvws_rx_reads can take it).
