@@ -413,6 +413,7 @@ def main():
 
     extra = {}
     sample = None
+    feed_streams = feed_pay = None
     if rank == 0:
         # STREAM-style in-place ceiling (read+write every byte) on the same buffer
         eng.sync()
@@ -464,6 +465,12 @@ def main():
             extra["stream_sweep_GBps"] = {n: round(2 * (plan.total & ~15) / float(np.median(t)) / 1e9, 1)
                                           for n, t in stimes.items()}
         extra["unmask_ms_mean"] = round(mean_unmask, 3)
+
+        # event loop, before the legs that allocate and
+        # free large buffers: host-side rates measured after them ran slower
+        if args.feed_conns > 0:
+            extra["event_loop"], feed_streams, feed_pay = event_loop_leg(eng, device, args.feed_conns,
+                                                                         args.feed_iters, plan.seed + 7)
 
         rx_plain = passes % 2 == 1   # payloads currently unmasked
         # (measured before the transmit leg: the pipeline's own allocations
@@ -545,11 +552,6 @@ def main():
 
     dp.free()
     rx.free()
-
-    feed_streams = None
-    if rank == 0 and args.feed_conns > 0:
-        extra["event_loop"], feed_streams, feed_pay = event_loop_leg(eng, device, args.feed_conns, args.feed_iters,
-                                                                     plan.seed + 7)
 
     if rank == 0:
         cpu = None
