@@ -5,6 +5,7 @@ WebSocketParser::FeedRecvData sequence produces."""
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 
 import pytest
@@ -70,7 +71,13 @@ def _loop(rng, conns, max_batch=None, dup=False, feeder=False):
     hvws_wsp_feed_many, or (feeder=True) to a pipelined hvws_feeder, whose
     rets for a submission arrive during the next submit or the final flush."""
     L = libhv_amd.lib()
-    f = L.hvws_feeder_new() if feeder else None
+    f = None
+    if feeder:
+        # "inline": every submission's device half on the loop thread (the
+        # $HVWS_FEEDER_INLINE path, read when the feeder is made)
+        os.environ["HVWS_FEEDER_INLINE"] = str(1 << 40) if feeder == "inline" else "0"
+        f = L.hvws_feeder_new()
+        os.environ.pop("HVWS_FEEDER_INLINE")
     subs = []
     pending = [c for c in conns if c.chunks]
     while pending:
@@ -117,7 +124,7 @@ def _check(conns):
         L.hvws_wsp_free(c.h)
 
 
-@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
+@pytest.mark.parametrize("feeder", [False, True, "inline"], ids=["many", "feeder", "feeder_inline"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_feed_many_matches_sequential_reference(seed, feeder):
     rng = random.Random(seed)
@@ -131,7 +138,7 @@ def test_feed_many_matches_sequential_reference(seed, feeder):
     _check(conns)
 
 
-@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
+@pytest.mark.parametrize("feeder", [False, True, "inline"], ids=["many", "feeder", "feeder_inline"])
 def test_feed_many_repeated_connection_in_batch(feeder):
     rng = random.Random(9)
     conns = []
