@@ -14,13 +14,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
-#include <unordered_map>
-#include <unordered_set>
 #include <vector>
 
 #include "hvws.h"
@@ -65,6 +64,69 @@ void stage_copy(char* stage, const hvws_segment* segs, const char* const* data, 
 }  // namespace
 
 namespace {
+// Pointer -> int index without per-element allocation (open addressing,
+// linear probing, load <= 1/2, entries of older generations read as empty):
+// a poll iteration looks every connection's parser up once or twice, and a
+// node-allocating std::unordered_set/map cost ~100 ns per parser there.
+class ptr_index {
+  public:
+    void reset(size_t n) {   // empty, room for n keys
+        size_t cap = 16;
+        while (cap < 2 * n) cap <<= 1;
+        if (cap > key_.size()) {
+            key_.assign(cap, nullptr);
+            val_.assign(cap, 0);
+            gen_.assign(cap, 0);
+            cur_ = 0;
+        }
+        if (++cur_ == 0) {   // generation counter wrapped: clear for real
+            std::fill(gen_.begin(), gen_.end(), 0u);
+            cur_ = 1;
+        }
+    }
+    // Adds p -> v; false (and no change) when p is already there.
+    bool insert(const void* p, int v) {
+        for (size_t i = slot(p);; i = (i + 1) & (key_.size() - 1)) {
+            if (gen_[i] != cur_) {
+                gen_[i] = cur_;
+                key_[i] = p;
+                val_[i] = v;
+                return true;
+            }
+            if (key_[i] == p) return false;
+        }
+    }
+    int find(const void* p) const {   // -1 when absent
+        for (size_t i = slot(p);; i = (i + 1) & (key_.size() - 1)) {
+            if (gen_[i] != cur_) return -1;
+            if (key_[i] == p) return val_[i];
+        }
+    }
+
+  private:
+    size_t slot(const void* p) const {
+        uint64_t x = (uint64_t)(uintptr_t)p;
+        x ^= x >> 33;
+        x *= 0xff51afd7ed558ccdull;
+        x ^= x >> 33;
+        return (size_t)x & (key_.size() - 1);
+    }
+    std::vector<const void*> key_;
+    std::vector<int> val_;
+    std::vector<uint32_t> gen_;
+    uint32_t cur_ = 0;
+};
+
+// End of the run of distinct parsers starting at `done` (a parser seen twice
+// starts a new run: its second chunk needs the carry its first one leaves).
+int distinct_run_end(WebSocketParser* const* parsers, int done, int n) {
+    thread_local ptr_index seen;   // used only between calls of feed_distinct / feeder_run
+    seen.reset((size_t)(n - done));
+    int end = done;
+    while (end < n && seen.insert(parsers[end], end)) ++end;
+    return end;
+}
+
 const int kMaxReserve = 1 << 24;   // MAX_PAYLOAD_LENGTH, reference WebSocketParser.cpp:6
 const size_t kMappedRead = 32 << 10;   // largest read hvws_rx_reads takes in place
 }
@@ -161,9 +223,7 @@ int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, con
     // cut the batch before any parser that already appears in it.
     int done = 0;
     while (done < n) {
-        int end = done;
-        std::unordered_set<WebSocketParser*> seen;
-        while (end < n && seen.insert(parsers[end]).second) ++end;
+        const int end = distinct_run_end(parsers, done, n);
         feed_distinct(parsers + done, data + done, len + done, end - done, rets ? rets + done : nullptr);
         done = end;
     }
@@ -351,7 +411,7 @@ struct hvws_feeder {
     bool stop = false;
     bool in_replay = false;
     uint64_t inline_bytes = 0;       // runs up to this size skip the worker ($HVWS_FEEDER_INLINE)
-    std::unordered_map<WebSocketParser*, int> pend_idx;   // parser -> index in *pending
+    ptr_index pend_idx;              // parser -> index in *pending (valid while pending is set)
 };
 
 namespace {
@@ -410,7 +470,6 @@ void feeder_replay_pending(hvws_feeder* f) {
     replay_part(*f->pending);
     f->in_replay = false;
     f->pending = nullptr;
-    f->pend_idx.clear();
 }
 
 // One run of distinct parsers: start its device half, then replay the
@@ -425,8 +484,8 @@ void feeder_run(hvws_feeder* f, WebSocketParser* const* parsers, const char* con
     // replay below), any other parser from its own state.
     feeder_wait_idle(f);
     for (int i = 0; i < n; ++i) {
-        auto it = f->pending ? f->pend_idx.find(parsers[i]) : f->pend_idx.end();
-        if (it != f->pend_idx.end()) hvws::copy_parser(b.carry[i], f->pending->carry[it->second]);
+        const int k = f->pending ? f->pend_idx.find(parsers[i]) : -1;
+        if (k >= 0) hvws::copy_parser(b.carry[i], f->pending->carry[k]);
         else hvws::copy_parser(b.carry[i], *parsers[i]->parser);
     }
     if (g_ft.on) g_ft.call();
@@ -443,7 +502,8 @@ void feeder_run(hvws_feeder* f, WebSocketParser* const* parsers, const char* con
     }
     feeder_replay_pending(f);
     f->pending = &b;
-    for (int i = 0; i < n; ++i) f->pend_idx[parsers[i]] = i;
+    f->pend_idx.reset((size_t)n);
+    for (int i = 0; i < n; ++i) f->pend_idx.insert(parsers[i], i);   // distinct within a run
 }
 }  // namespace
 
@@ -485,9 +545,7 @@ int hvws_feeder_submit(hvws_feeder* f, WebSocketParser* const* parsers, const ch
     // as hvws_feed_many: a parser seen twice starts a new run
     int done = 0;
     while (done < n) {
-        int end = done;
-        std::unordered_set<WebSocketParser*> seen;
-        while (end < n && seen.insert(parsers[end]).second) ++end;
+        const int end = distinct_run_end(parsers, done, n);
         feeder_run(f, parsers + done, data + done, len + done, end - done, rets ? rets + done : nullptr);
         done = end;
     }
