@@ -197,7 +197,7 @@ def event_loop_leg(eng, device: int, conns: int, iters: int, seed: int):
     reads side by side, so the reads go to the kernel in place (hvws_rx_reads).
     Timed: hvws_feeder_submit per iteration + the final flush (pipelined), and
     hvws_wsp_feed_many per iteration (synchronous), each over a whole pass with
-    fresh parsers after one untimed pass of each.  Returns (result dict, the masked
+    fresh parsers: the median of 3 passes each, after one untimed pass of each.  Returns (result dict, the masked
     streams for the CPU reference, their payload bytes)."""
     import libhv_amd
     from libhv_amd import synth
@@ -243,11 +243,15 @@ def event_loop_leg(eng, device: int, conns: int, iters: int, seed: int):
         return dt
 
     # each pass unmasks (or re-masks) every read in place: the same work;
-    # one untimed pass per mode first (contexts, staging, first launches)
+    # one untimed pass per mode first (contexts, staging, first launches),
+    # then the median of 3 timed passes of each, interleaved
     one_pass(True)
     one_pass(False)
-    t_pipe = one_pass(True)
-    t_sync = one_pass(False)
+    tp, ts = [], []
+    for _ in range(3):
+        tp.append(one_pass(True))
+        ts.append(one_pass(False))
+    t_pipe, t_sync = float(np.median(tp)), float(np.median(ts))
     L.hvws_feeder_free(feeder)
     L.hvws_host_free(eng.ctx, arena)
     pay = conns * iters * FEED_READ * 1024 / 1032
