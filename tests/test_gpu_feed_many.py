@@ -75,9 +75,10 @@ def _loop(rng, conns, max_batch=None, dup=False, feeder=False):
     if feeder:
         # "inline": every submission's device half on the loop thread (the
         # $HVWS_FEEDER_INLINE path, read when the feeder is made)
-        os.environ["HVWS_FEEDER_INLINE"] = str(1 << 40) if feeder == "inline" else "0"
+        if feeder == "inline":
+            os.environ["HVWS_FEEDER_INLINE"] = str(1 << 40)
         f = L.hvws_feeder_new()
-        os.environ.pop("HVWS_FEEDER_INLINE")
+        os.environ.pop("HVWS_FEEDER_INLINE", None)
     subs = []
     pending = [c for c in conns if c.chunks]
     while pending:

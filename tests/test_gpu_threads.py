@@ -1,8 +1,8 @@
 """GPU: several event-loop threads drive the drop-in at once (SURVEY.md
 sec. 8(b): "callable from multiple loop threads at once ... per-thread or
 per-device contexts and HIP streams, with no global device lock").  Each
-thread owns its connections and feeds them with hvws_wsp_feed_many or
-per-read hvws_wsp_feed while the others do the same; every connection must
+thread owns its connections and feeds them with hvws_wsp_feed_many, its own
+pipelined feeder, or per-read hvws_wsp_feed while the others do the same; every connection must
 end exactly as the reference's sequential FeedRecvData would leave it.
 ctypes releases the GIL around foreign calls, so the library calls overlap."""
 from __future__ import annotations
@@ -20,7 +20,7 @@ import libhv_amd
 pytestmark = pytest.mark.gpu
 
 
-def _worker(seed, conns_out, errors, per_read):
+def _worker(seed, conns_out, errors, per_read, feeder=False):
     try:
         rng = random.Random(seed)
         conns = []
@@ -36,18 +36,20 @@ def _worker(seed, conns_out, errors, per_read):
                     c.at += k
                 c.chunks = []
         else:
-            _loop(rng, conns)
+            _loop(rng, conns, feeder=feeder)   # a feeder of its own per loop thread
         conns_out.extend(conns)
         libhv_amd.lib().hvws_thread_release()   # loop-thread exit
     except Exception as e:  # noqa: BLE001 -- reported by the main thread
         errors.append(e)
 
 
+@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeders"])
 @pytest.mark.parametrize("nthreads", [2, 6])
-def test_concurrent_loop_threads(nthreads):
+def test_concurrent_loop_threads(nthreads, feeder):
     outs = [[] for _ in range(nthreads)]
     errors = []
-    ts = [threading.Thread(target=_worker, args=(100 + t, outs[t], errors, t % 3 == 2)) for t in range(nthreads)]
+    ts = [threading.Thread(target=_worker, args=(100 + t, outs[t], errors, t % 3 == 2, feeder))
+          for t in range(nthreads)]
     for t in ts:
         t.start()
     for t in ts:
