@@ -287,6 +287,50 @@ def cpu_event_loop(streams: np.ndarray, iters: int, pay: float):
     return {"us_per_iteration": round(dt / iters * 1e6, 1), "GiBps_payload": round(pay / dt / 2**30, 3), "cores": 1}
 
 
+def cpu_info() -> dict:
+    """CPU model and the CPUs this process may use: nproc (affinity) and the
+    cgroup's CPU quota (cpu.max), whichever is smaller."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(nproc, quota) if quota else nproc
+    return {"cpu_model": model, "nproc": nproc, "cgroup_cpus": quota, "usable_cpus": usable}
+
+
+def gather_rows(dist, row) -> np.ndarray:
+    """Every rank's `row` (floats), as a (world, len(row)) array on every rank
+    (gloo all_gather; a single row when not distributed).  Timing only -- no
+    data-path collective."""
+    r = np.asarray(row, dtype=np.float64)
+    if dist is None:
+        return r[None, :]
+    import torch
+
+    t = torch.tensor(r)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return np.stack([o.numpy() for o in out])
+
+
+def span_of(rows: np.ndarray, i_start: int = 0, i_end: int = 1) -> float:
+    """max over ranks of end - min over ranks of start (one host clock:
+    time.perf_counter is CLOCK_MONOTONIC, shared by the processes of a node)."""
+    return float(rows[:, i_end].max() - rows[:, i_start].min())
+
+
 def init_dist():
     """(rank, world, local_rank, dist-or-None).  One process per GPU; gloo
     carries only the barrier and the timing reduction (no data collectives)."""
@@ -319,20 +363,150 @@ def max_over_ranks(dist, seconds: float) -> float:
     return float(t.item())
 
 
+def host_inclusive_leg(eng, plan, dp, rx, args, dist, rank: int, world: int, device: int):
+    """Host memory in, host memory out: the first ~host_gib of
+    this rank's batch from pinned host memory through hvws_pipeline (chunked
+    H2D -> scan -> unmask -> D2H, 3-slot ring).  Every rank runs it at the
+    same time -- each call starts after a gloo barrier -- so with N GPUs the
+    links and host DRAM are shared as in a real N-GPU server (SURVEY sec. 7
+    hard part 4).  Returns (this rank's row, rank-0-only result or None,
+    the CPU sample (rank 0) or None)."""
+    import libhv_amd
+    from libhv_amd import synth
+
+    L = libhv_amd.lib()
+    sizes = synth.frame_size(plan.flags, plan.length)
+    ends = np.cumsum(sizes)
+    m = int(np.searchsorted(ends, int(args.host_gib * 2**30), side="right"))
+    m = max(1, min(m, plan.n))
+    hbytes = int(ends[m - 1])
+    pay = float(plan.length[:m].sum())
+    eng.synth(rx, plan.total, plan.seed, dp, 0)
+    pinned = L.hvws_host_alloc(eng.ctx, hbytes)
+    host = np.ctypeslib.as_array((ctypes.c_uint8 * hbytes).from_address(pinned))
+    libhv_amd._check(L.hvws_d2h(eng.ctx, pinned, rx.ptr, hbytes), "d2h")
+    eng.sync()
+    sample = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        # CPU baseline sample = the first whole frames of the same (masked) batch
+        ms = max(1, int(np.searchsorted(ends, args.cpu_sample_mib << 20, side="right")))
+        sample = np.array(host[: int(ends[ms - 1])], copy=True)
+    chunk = args.host_chunk_mib << 20
+    # one untimed call (slot allocation, the link warming up), then 3 timed
+    # calls, all ranks starting each call together; each call toggles the
+    # host bytes between masked and unmasked
+    rows = []
+    for r in range(4):
+        carry = libhv_amd.WsParser()
+        L.websocket_parser_init(ctypes.byref(carry))
+        if dist is not None:
+            dist.barrier()
+        t = time.perf_counter()
+        libhv_amd._check(L.hvws_pipeline(eng.ctx, pinned, hbytes, chunk, ctypes.byref(carry)), "pipeline")
+        t1 = time.perf_counter()
+        if r:
+            rows.append(gather_rows(dist, [t, t1, hbytes, pay]))
+    L.hvws_host_free(eng.ctx, pinned)
+    if dist is not None:
+        dist.barrier()
+    link = pcie_ceiling(device, piece=chunk)   # every rank at once, like the pipeline
+    lrows = gather_rows(dist, [link["h2d_GBps"], link["d2h_GBps"], link["concurrent_GBps_per_direction"]])
+    if rank != 0:
+        return None, sample
+    # per call: the aggregate over ranks = all bytes / (latest end - earliest start)
+    agg = [float(x[:, 2].sum()) / span_of(x) for x in rows]
+    agg_pay = [float(x[:, 3].sum()) / span_of(x) for x in rows]
+    k = int(np.argsort(agg)[len(agg) // 2])   # median call
+    per_rank = []
+    for q in range(rows[0].shape[0]):
+        dts = [float(x[q, 1] - x[q, 0]) for x in rows]
+        dt = float(np.median(dts))
+        per_rank.append({"rank": q, "GBps_wire": round(hbytes / dt / 1e9, 2),
+                         "GiBps_payload": round(pay / dt / 2**30, 2),
+                         "link_concurrent_GBps_per_direction": float(lrows[q, 2]),
+                         "frac_of_own_link": round(hbytes / dt / 1e9 / float(lrows[q, 2]), 3)})
+    link_sum = float(lrows[:, 2].sum())
+    res = {
+        "GiBps_payload": per_rank[0]["GiBps_payload"],
+        "GBps_wire": per_rank[0]["GBps_wire"],
+        "frac_of_concurrent_link": per_rank[0]["frac_of_own_link"],
+        "bytes": hbytes, "chunk": chunk,
+        "note": "pinned H2D + scan + unmask + D2H, 3-slot ring, PCIe-bound; median of 3 calls after 1 warm-up; "
+                "all ranks run each call together (gloo barrier before each)",
+        "link": link,
+        "per_rank": per_rank,
+        "aggregate": {
+            "GBps_wire": round(agg[k] / 1e9, 2),
+            "GiBps_payload": round(agg_pay[k] / 2**30, 2),
+            "ranks": world,
+            "sum_of_links_GBps_per_direction": round(link_sum, 2),
+            "frac_of_sum_of_links": round(agg[k] / 1e9 / link_sum, 3),
+            "method": "all ranks' bytes / (latest end - earliest start) per call, host CLOCK_MONOTONIC; "
+                      "median call of 3; links measured concurrently on every rank",
+        },
+    }
+    return res, sample
+
+
+def tx_leg(eng, plan, dp, rx, rx_plain: bool, segs, tpath: str) -> dict:
+    """Transmit side: rebuild every frame of the batch
+    from its plaintext payload with hvws_build_frames; the output must be the
+    masked batch byte for byte."""
+    import libhv_amd
+    from libhv_amd import synth
+
+    if not rx_plain:
+        eng.step(rx, plan.total, segs)   # leave rx holding plaintext payloads
+    hdr = synth.frame_size(plan.flags, plan.length) - plan.length
+    tx = libhv_amd.TxPlan(eng, plan.frame_off + hdr, plan.length, plan.flags, plan.mask)
+    out_buf = eng.alloc(plan.total + 64)
+    tms = []
+    for _ in range(4):
+        eng.build_frames(out_buf, plan.total + 64, rx, plan.total, tx)
+        tms.append(eng.last_kernel_ms())
+    ok = eng.synth(out_buf, plan.total, plan.seed, dp, 1) == 0
+    tx_alg = plan.payload_bytes + plan.total
+    tx_ach = tx_alg / (float(np.mean(tms[1:])) * 1e-3) / 1e9
+    bname = libhv_amd.lib().hvws_build_kernel_name().decode()
+    tx_traffic = None
+    if os.path.exists(tpath):
+        ent = json.load(open(tpath)).get(bname, {}).get(str(plan.total))
+        tx_traffic = ent["hbm_bytes"] if ent else None
+    out_buf.free()
+    tx.free()
+    if not ok:
+        raise SystemExit("transmit build differs from the masked batch")
+    return {
+        "kernel": bname, "traffic": tx_traffic,
+        "achieved": round(tx_ach, 1), "unit": "GB/s", "frac": round(tx_ach / HBM_PEAK_GBS, 4),
+        "alg_bytes_per_launch": tx_alg, "kernel_ms_mean": round(float(np.mean(tms[1:])), 3),
+        "verified": ok,
+    }
+
+
+def fixture_for(cfg: str, rank: int):
+    """(name, entry) of the committed reference digests for this rank's batch
+    (tests/golden/configs.json: c5_rank<r> = the c3-shaped batch of seed
+    1000 + r, streamed through the reference by make_golden.py --big)."""
+    path = os.path.join(ROOT, "tests", "golden", "configs.json")
+    if cfg != "c3" or not os.path.exists(path):
+        return None, None
+    name = f"c5_rank{rank}"
+    return name, json.load(open(path)).get(name)
+
+
 def main():
     args = parse()
     rank, world, local, dist = init_dist()
     if world > 1:
-        # N > 1: the replicas' timed steps only.  The CPU baseline is taken at
-        # N = 1 (rank 0), and so are the host-inclusive and transmit legs.
+        # The CPU baseline is taken at N = 1 only.  At N > 1 every rank runs
+        # the timed steps and the host-inclusive leg (together, so links and
+        # host DRAM are shared as in production); rank 0 alone runs the
+        # transmit and event-loop legs.
         args.cpu_seconds = 0
-        args.host_gib = 0
-        args.no_tx = True
-        args.feed_conns = 0
     import torch
 
     import libhv_amd
-    from libhv_amd import synth
 
     def barrier():
         eng.sync()
@@ -359,26 +533,42 @@ def main():
     P = plan.masked_payload_bytes()
     HB = plan.header_bytes
     segs = eng.prepare(plan.segments)   # ctypes tables built once, outside the timed loop
+    fx_name, fx = fixture_for(cfg, rank)
+    if fx is not None:
+        # the batch this rank built is the reference's (masked digest)
+        d = f"{eng.digest(rx, plan.total):016x}"
+        if d != fx["digest_masked"]:
+            raise SystemExit(f"rank {rank}: masked batch digest {d} != {fx_name} {fx['digest_masked']}")
 
     # The batch is resident in HBM before the timed region, so steps use
     # hvws_step_resident: each step's discovery (second stream) overlaps the
     # previous step's unmask; every step still scans and unmasks the whole
     # batch (the same buffer: headers are never modified, payloads toggle).
     step = eng.step if args.serial else eng.step_resident
+    L = libhv_amd.lib()
     if args.validate:
-        libhv_amd.lib().hvws_set_validation(eng.ctx, 0x3F)   # HVWS_V_ALL
+        L.hvws_set_validation(eng.ctx, 0x3F)   # HVWS_V_ALL
     for _ in range(args.warmup):
         step(rx, plan.total, segs)
     barrier()
     # Steps are issued back to back (each still synchronises once inside its
     # scan to size the frame table); the per-launch kernel times are read
-    # from the engine's event ring after the timed region.
+    # from the engine's event ring after the timed region.  Per device: span
+    # markers on the context's streams (hvws_span_*); across devices: the
+    # host's CLOCK_MONOTONIC (time.perf_counter), common to all ranks of the
+    # node -- value = all payload / (latest end - earliest start).
     t0 = time.perf_counter()
+    libhv_amd._check(L.hvws_span_begin(eng.ctx), "span_begin")
     for _ in range(args.steps):
         step(rx, plan.total, segs)
+    span_ms = ctypes.c_float(0)
+    libhv_amd._check(L.hvws_span_end(eng.ctx, ctypes.byref(span_ms)), "span_end")
+    eng.sync()
+    t1 = time.perf_counter()
     barrier()
-    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
-    scan_path = libhv_amd.lib().hvws_last_scan_path(eng.ctx)
+    trows = gather_rows(dist, [t0, t1, span_ms.value])
+    elapsed = span_of(trows)
+    scan_path = L.hvws_last_scan_path(eng.ctx)
     times = eng.step_times(min(args.steps, 32))
     scan_ms = [t[0] for t in times]
     unmask_ms = [t[1] for t in times]
@@ -397,17 +587,27 @@ def main():
         other_ms = (time.perf_counter() - t) / n_other * 1e3
     # Correctness after the timed region: an odd number of passes leaves the
     # payload unmasked, an even number masked again (XOR is an involution).
+    # Byte-exact against the plan (device synth VERIFY), and -- for c3-shaped
+    # batches -- the whole buffer's digest against the reference's fixture.
     passes = args.warmup + args.steps + (4 if rank == 0 else 0)
     bad = eng.synth(rx, plan.total, plan.seed, dp, 2 if passes % 2 else 1)
     if bad:
         raise SystemExit(f"rank {rank}: {bad} bytes differ from the expected batch after {passes} passes")
+    digest_ok = None
+    if fx is not None:
+        want = fx["digest_unmasked"] if passes % 2 else fx["digest_masked"]
+        d = f"{eng.digest(rx, plan.total):016x}"
+        digest_ok = d == want
+        if not digest_ok:
+            raise SystemExit(f"rank {rank}: digest {d} after {passes} passes != reference {fx_name} {want}")
+    vrows = gather_rows(dist, [rank, device, -1 if digest_ok is None else int(digest_ok)])
 
     value = world * plan.payload_bytes * args.steps / elapsed / 2**30
     mean_unmask = float(np.mean(unmask_ms))
     alg_bytes = 2 * P + HB
     achieved = alg_bytes / (mean_unmask * 1e-3) / 1e9
 
-    kname = libhv_amd.lib().hvws_unmask_kernel_name_for(plan.total).decode()
+    kname = L.hvws_unmask_kernel_name_for(plan.total).decode()
     traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
@@ -436,12 +636,28 @@ def main():
             extra["validation"] = "HVWS_V_ALL"
         extra["other_step_call_ms"] = round(other_ms, 3) if other_ms is not None else None
         extra["scan_path"] = {0: "count_emit", 1: "count_read_emit", 2: "single", 3: "speculative",
-                              4: "speculative_rejected"}.get(scan_path, scan_path)
+                              4: "speculative_rejected", 5: "slack", 6: "slack_rejected"}.get(scan_path, scan_path)
+        extra["timing"] = {
+            "method": "per device: hvws_span_begin/end markers on the context's streams (HIP events); "
+                      "across devices: latest end - earliest start on the host CLOCK_MONOTONIC after a barrier",
+            "elapsed_s": round(elapsed, 6),
+            "per_rank": [{"rank": int(r), "device_span_ms": round(float(trows[r, 2]), 3),
+                          "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3),
+                          "end_offset_ms": round(float(trows[r, 1] - trows[:, 0].min()) * 1e3, 3)}
+                         for r in range(trows.shape[0])],
+            "device_span_ms_max": round(float(trows[:, 2].max()), 3),
+        }
+        extra["verified"] = {
+            "method": "every payload byte vs its plaintext (device synth VERIFY) after the run; digest of the "
+                      "whole rx buffer vs the reference's (tests/golden/configs.json c5_rank<r>) before and after",
+            "ranks": [{"rank": int(v[0]), "device": int(v[1]),
+                       "fixture": (f"c5_rank{int(v[0])}" if v[2] >= 0 else None),
+                       "digest_match": (bool(v[2]) if v[2] >= 0 else None)} for v in vrows],
+        }
         if args.sweep_unmask:
             # every geometry, interleaved round by round in this process; an
             # even number of passes per geometry leaves the batch masked, which
             # is verified byte-for-byte afterwards
-            L = libhv_amd.lib()
             names, times = [], {}
             v = 0
             while L.hvws_set_unmask_variant(v) == 0:
@@ -476,83 +692,21 @@ def main():
             extra["event_loop"], feed_streams, feed_pay = event_loop_leg(eng, device, args.feed_conns,
                                                                          args.feed_iters, plan.seed + 7)
 
-        rx_plain = passes % 2 == 1   # payloads currently unmasked
-        # (measured before the transmit leg: the pipeline's own allocations
-        # ran measurably slower after that leg's 68.7 GB buffer came and went)
-        # host-inclusive: pinned host rx -> device -> scan+unmask -> host
-        if args.host_gib > 0:
-            sizes = synth.frame_size(plan.flags, plan.length)
-            ends = np.cumsum(sizes)
-            m = int(np.searchsorted(ends, int(args.host_gib * 2**30), side="right"))
-            m = max(1, min(m, plan.n))
-            hbytes = int(ends[m - 1])
-            eng.synth(rx, plan.total, plan.seed, dp, 0)
-            rx_plain = False
-            L = libhv_amd.lib()
-            pinned = L.hvws_host_alloc(eng.ctx, hbytes)
-            host = np.ctypeslib.as_array((ctypes.c_uint8 * hbytes).from_address(pinned))
-            libhv_amd._check(L.hvws_d2h(eng.ctx, pinned, rx.ptr, hbytes), "d2h")
-            eng.sync()
-            # CPU baseline sample = the first whole frames of the same (masked) batch
-            sample = None
-            if args.cpu_seconds > 0:
-                ms = max(1, int(np.searchsorted(ends, args.cpu_sample_mib << 20, side="right")))
-                sample = np.array(host[: int(ends[ms - 1])], copy=True)
-            chunk = args.host_chunk_mib << 20
-            # one untimed call (first-call costs: slot allocation, the link
-            # warming up), then the median of 3 timed calls; each call
-            # toggles the host bytes between masked and unmasked
-            runs = []
-            for r in range(4):
-                carry = libhv_amd.WsParser()
-                L.websocket_parser_init(ctypes.byref(carry))
-                t = time.perf_counter()
-                libhv_amd._check(L.hvws_pipeline(eng.ctx, pinned, hbytes, chunk, ctypes.byref(carry)), "pipeline")
-                if r:
-                    runs.append(time.perf_counter() - t)
-            dt = float(np.median(runs))
-            link = pcie_ceiling(device, piece=chunk)
-            extra["host_inclusive"] = {
-                "GiBps_payload": round(float(plan.length[:m].sum()) / dt / 2**30, 2),
-                "GBps_wire": round(hbytes / dt / 1e9, 2),
-                "frac_of_concurrent_link": round(hbytes / dt / 1e9 / link["concurrent_GBps_per_direction"], 3),
-                "bytes": hbytes, "chunk": chunk,
-                "note": "pinned H2D + scan + unmask + D2H, 3-slot ring, PCIe-bound; median of 3 calls after 1 warm-up",
-                "link": link,
-            }
-            L.hvws_host_free(eng.ctx, pinned)
+    rx_plain = passes % 2 == 1   # payloads currently unmasked
+    # host-inclusive: pinned host rx -> device -> scan+unmask -> host, every
+    # rank at once (measured before the transmit leg: the pipeline's own
+    # allocations ran measurably slower after that leg's 68.7 GB buffer came
+    # and went)
+    if dist is not None:
+        dist.barrier()   # rank 0's extra legs above
+    if args.host_gib > 0:
+        res, sample = host_inclusive_leg(eng, plan, dp, rx, args, dist, rank, world, device)
+        rx_plain = False
+        if rank == 0:
+            extra["host_inclusive"] = res
 
-        if not args.no_tx:
-            # transmit side: rebuild every frame of the
-            # batch from its plaintext payload with hvws_build_frames; the output
-            # must be the masked batch byte for byte
-            if not rx_plain:
-                eng.step(rx, plan.total, segs)   # leave rx holding plaintext payloads
-            hdr = synth.frame_size(plan.flags, plan.length) - plan.length
-            tx = libhv_amd.TxPlan(eng, plan.frame_off + hdr, plan.length, plan.flags, plan.mask)
-            out_buf = eng.alloc(plan.total + 64)
-            tms = []
-            for _ in range(4):
-                eng.build_frames(out_buf, plan.total + 64, rx, plan.total, tx)
-                tms.append(eng.last_kernel_ms())
-            ok = eng.synth(out_buf, plan.total, plan.seed, dp, 1) == 0
-            tx_alg = plan.payload_bytes + plan.total
-            tx_ach = tx_alg / (float(np.mean(tms[1:])) * 1e-3) / 1e9
-            bname = libhv_amd.lib().hvws_build_kernel_name().decode()
-            tx_traffic = None
-            if os.path.exists(tpath):
-                ent = json.load(open(tpath)).get(bname, {}).get(str(plan.total))
-                tx_traffic = ent["hbm_bytes"] if ent else None
-            extra["tx"] = {
-                "kernel": bname, "traffic": tx_traffic,
-                "achieved": round(tx_ach, 1), "unit": "GB/s", "frac": round(tx_ach / HBM_PEAK_GBS, 4),
-                "alg_bytes_per_launch": tx_alg, "kernel_ms_mean": round(float(np.mean(tms[1:])), 3),
-                "verified": ok,
-            }
-            out_buf.free()
-            tx.free()
-            if not ok:
-                raise SystemExit("transmit build differs from the masked batch")
+    if rank == 0 and not args.no_tx:
+        extra["tx"] = tx_leg(eng, plan, dp, rx, rx_plain, segs, tpath)
 
     dp.free()
     rx.free()
@@ -560,16 +714,20 @@ def main():
     if rank == 0:
         cpu = None
         if sample is not None:
+            ci = cpu_info()
             v1, kind, passes1, _ = cpu_baseline(sample, args.cpu_seconds, 1)
-            nthr = min(16, os.cpu_count() or 1)
+            nthr = ci["usable_cpus"]
             vn, _, _, _ = cpu_baseline(sample, args.cpu_seconds / 2, nthr)
             cpu = {
                 "value": round(v1, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+                "cpu_model": ci["cpu_model"], "nproc": ci["nproc"], "cgroup_cpus": ci["cgroup_cpus"],
                 "sample": f"{sample.nbytes} B of the same batch ({args.config} frames) x {passes1} passes, "
                           "WebSocketParser semantics (header parse + in-place unmask + message append), 8 KiB chunks",
-                "multi_thread": {"value": round(vn, 3), "threads": nthr},
+                "multi_thread": {"value": round(vn, 3), "threads": nthr,
+                                 "note": "one independent stream per thread; threads = min(nproc, cgroup CPU quota)"},
                 "decode_only": {"value": round(cpu_decode_only(sample, plan, args.cpu_seconds / 4), 3), "cores": 1,
                                 "note": "websocket_decode over the sample's masked payload spans"},
+                "note": "a reported baseline (the reference CPU path on this host), not the optimisation target",
             }
             if feed_streams is not None:
                 cpu["event_loop"] = cpu_event_loop(feed_streams, args.feed_iters, feed_pay)
@@ -610,6 +768,7 @@ def main():
         out.update(extra)
         print(json.dumps(out), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
     eng.close()
 

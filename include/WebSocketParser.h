@@ -53,7 +53,12 @@ typedef std::shared_ptr<WebSocketParser> WebSocketParserPtr;
 /* Batched FeedRecvData for an event loop: n connections' reads in one GPU
  * round trip (one segment each).  Same effects, per parser, as calling
  * parsers[i]->FeedRecvData(data[i], len[i]) in order i = 0..n-1; rets[i]
- * receives each call's return value.  New entry point (no reference twin). */
+ * receives each call's return value.  New entry point (no reference twin).
+ * Nested feeds: an onMessage replayed by this call (or by a feeder) may feed
+ * any parser whose results are final; feeding one whose state a replay still
+ * to come on this thread will write (later in the same batch, or in a
+ * feeder's run already in flight) returns -1 and changes nothing -- as does
+ * FeedRecvData on such a parser.  Returns n, or -1. */
 HV_EXPORT int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n,
                              int* rets);
 

@@ -240,6 +240,13 @@ enum {
     HVWS_PATH_SLACK_FAILED = 6      /* a segment outgrew its region, then COUNT/EMIT */
 };
 int hvws_last_scan_path(hvws_ctx* ctx);
+
+/* Device span of a timed region: hvws_span_begin records a marker on each of
+ * the context's compute streams, hvws_span_end records the end markers, waits
+ * for them and returns (latest end - earliest begin) in ms.  For benchmarks:
+ * the per-device time of a run of steps. */
+int hvws_span_begin(hvws_ctx* ctx);
+int hvws_span_end(hvws_ctx* ctx, float* ms);
 /* Batches whose record bound (rx_len / 2 + 2 * nseg + 1) is at most
  * `records` are scanned COUNT -> EMIT with the table sized by that bound
  * (default 2^24); larger ones wait for a count (or speculate).  1 makes
@@ -330,7 +337,8 @@ int hvws_host_unregister(hvws_ctx* ctx, void* p);
  * total at most the small-batch limit (64 MiB by default), and reads must not
  * overlap.  Read i is segment i: hvws_get_segment_frames / hvws_get_frames
  * report its frames with hdr_off / pay_off relative to reads[i]; carry is
- * in/out per read.  HVWS_EINVAL (nothing done) if a read is not registered. */
+ * in/out per read.  HVWS_EINVAL (nothing done) if a read is not registered,
+ * or if the context's small-batch path is off (hvws_set_small_batch_limit ~0). */
 int hvws_rx_reads(hvws_ctx* ctx, char* const* reads, const uint64_t* lens, websocket_parser* carry, uint32_t n,
                   int unmask);
 
@@ -360,9 +368,14 @@ int   hvws_wsp_feed_many(void* const* handles, const char* const* data, const si
  * submit k+1 (or flush).  The caller keeps submission k's buffers and its
  * rets array alive and untouched until then.  Submitting 0 reads = flush.
  * A parser whose feed returned short must be closed (as libhv does); its
- * results already in flight are then undefined.  Not callable from inside
- * the feeder's own callbacks (returns -1).  new() binds the calling thread's
- * device; free() flushes. */
+ * results already in flight are then undefined.  Submit and flush are not
+ * callable from inside the feeder's own callbacks (they return -1), nor may a
+ * submission hold a parser that a replay still to come will write (see
+ * hvws_feed_many; -1).  new() binds the calling thread's device; free()
+ * flushes.  free() from inside one of the feeder's own callbacks is deferred:
+ * the feeder is freed when the submit / flush that replays it returns (the
+ * rest of that run's callbacks still run; runs of that submission not yet
+ * started are dropped and its return value counts the reads taken). */
 typedef struct hvws_feeder hvws_feeder;
 hvws_feeder* hvws_feeder_new(void);
 void hvws_feeder_free(hvws_feeder* f);

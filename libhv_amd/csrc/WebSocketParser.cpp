@@ -129,6 +129,8 @@ int distinct_run_end(WebSocketParser* const* parsers, int done, int n) {
 
 const int kMaxReserve = 1 << 24;   // MAX_PAYLOAD_LENGTH, reference WebSocketParser.cpp:6
 const size_t kMappedRead = 32 << 10;   // largest read hvws_rx_reads takes in place
+
+bool any_busy(WebSocketParser* const* parsers, int n);   // below, with the replay
 }
 
 WebSocketParser::WebSocketParser() {
@@ -204,6 +206,8 @@ size_t replay_messages(WebSocketParser* wp, const char* base, uint64_t base_off,
 
 int WebSocketParser::FeedRecvData(const char* data, size_t len) {
     if (len == 0) return 0;
+    WebSocketParser* self = this;
+    if (any_busy(&self, 1)) return -1;   // a replay still to come would overwrite this feed
     std::vector<hvws_frame> frames;
     websocket_parser out;
     int started = 0;
@@ -219,6 +223,7 @@ static int feed_distinct(WebSocketParser* const* parsers, const char* const* dat
                          int* rets);
 
 int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, const size_t* len, int n, int* rets) {
+    if (n < 0 || any_busy(parsers, n)) return -1;
     // A connection's second chunk needs the carry its first chunk leaves, so
     // cut the batch before any parser that already appears in it.
     int done = 0;
@@ -344,12 +349,33 @@ void gpu_part(feed_batch& b) {
 const uint64_t g_replay_prefetch =
     getenv("HVWS_REPLAY_PREFETCH") ? strtoull(getenv("HVWS_REPLAY_PREFETCH"), nullptr, 0) : (64u << 10);
 
-void replay_part(feed_batch& b) {
+// Replays running on this thread (nested when an onMessage feeds again).
+// While one runs, the states of its parsers after the one being replayed --
+// and of every parser in a feeder's in-flight run -- are already decided by
+// carries taken before any callback: a nested feed on such a parser would be
+// overwritten when its turn comes, so it is refused (parser_busy).  The
+// indexes are built only when a nested feed actually asks.
+struct replay_scope {
+    const feed_batch* b;
+    const int* pos;                // index in b being replayed
+    const feed_batch* inflight;    // feeder: run whose device half is issued, or nullptr
+    ptr_index idx_b, idx_f;
+    bool built = false;
+};
+thread_local std::vector<replay_scope*> t_replays;
+
+void replay_part(feed_batch& b, const feed_batch* inflight = nullptr) {
     double t0 = g_ft.on ? now_us() : 0;
+    int i = 0;
+    replay_scope scope{&b, &i, inflight};
+    struct push {   // popped however the replay ends (an onMessage may throw)
+        explicit push(replay_scope* s) { t_replays.push_back(s); }
+        ~push() { t_replays.pop_back(); }
+    } pushed(&scope);
     int pf_conn = 0;          // next connection whose bytes to prefetch
     uint64_t pf_off = 0;      // ... from this offset in its read
     uint64_t pf_ahead = 0;    // bytes prefetched beyond the connection being replayed
-    for (int i = 0; i < b.n(); ++i) {
+    for (; i < b.n(); ++i) {
         if (g_replay_prefetch) {
             if (i) pf_ahead = pf_ahead > b.len[i] ? pf_ahead - b.len[i] : 0;   // connection i is no longer ahead
             if (pf_conn <= i) {
@@ -374,6 +400,32 @@ void replay_part(feed_batch& b) {
         if (b.rets) b.rets[i] = (int)used;
     }
     if (g_ft.on) g_ft.add(4, now_us() - t0);
+}
+
+// True when a feed of `p` now (from inside a replayed callback) would be
+// overwritten by a replay still to come on this thread.
+bool parser_busy(const WebSocketParser* p) {
+    for (replay_scope* s : t_replays) {
+        if (!s->built) {
+            s->idx_b.reset((size_t)s->b->n());
+            for (int k = 0; k < s->b->n(); ++k) s->idx_b.insert(s->b->parsers[k], k);
+            if (s->inflight) {
+                s->idx_f.reset((size_t)s->inflight->n());
+                for (int k = 0; k < s->inflight->n(); ++k) s->idx_f.insert(s->inflight->parsers[k], k);
+            }
+            s->built = true;
+        }
+        if (s->idx_b.find(p) > *s->pos) return true;
+        if (s->inflight && s->idx_f.find(p) >= 0) return true;
+    }
+    return false;
+}
+
+bool any_busy(WebSocketParser* const* parsers, int n) {
+    if (t_replays.empty()) return false;
+    for (int i = 0; i < n; ++i)
+        if (parser_busy(parsers[i])) return true;
+    return false;
 }
 }  // namespace
 
@@ -410,7 +462,8 @@ struct hvws_feeder {
     feed_batch* pending = nullptr;   // device half issued, callbacks not replayed yet
     bool stop = false;
     bool in_replay = false;
-    uint64_t inline_bytes = 0;       // runs up to this size skip the worker ($HVWS_FEEDER_INLINE)
+    bool free_requested = false;     // hvws_feeder_free from one of its callbacks: freed when the replay returns
+    uint64_t inline_bytes = 0;      // runs up to this size skip the worker ($HVWS_FEEDER_INLINE)
     ptr_index pend_idx;              // parser -> index in *pending (valid while pending is set)
 };
 
@@ -464,10 +517,10 @@ void feeder_wait_idle(hvws_feeder* f) {
     if (g_ft.on) g_ft.add(5, now_us() - t0);
 }
 
-void feeder_replay_pending(hvws_feeder* f) {
+void feeder_replay_pending(hvws_feeder* f, const feed_batch* inflight = nullptr) {
     if (!f->pending) return;
     f->in_replay = true;
-    replay_part(*f->pending);
+    replay_part(*f->pending, inflight);
     f->in_replay = false;
     f->pending = nullptr;
 }
@@ -500,7 +553,7 @@ void feeder_run(hvws_feeder* f, WebSocketParser* const* parsers, const char* con
         }
         f->cv.notify_all();
     }
-    feeder_replay_pending(f);
+    feeder_replay_pending(f, &b);
     f->pending = &b;
     f->pend_idx.reset((size_t)n);
     for (int i = 0; i < n; ++i) f->pend_idx.insert(parsers[i], i);   // distinct within a run
@@ -518,17 +571,10 @@ extern "C" hvws_feeder* hvws_feeder_new(void) {
     return f;
 }
 
-extern "C" int hvws_feeder_flush(hvws_feeder* f) {
-    if (!f) return -1;
-    if (f->in_replay) return -1;   // from inside one of its own callbacks
+namespace {
+void feeder_destroy(hvws_feeder* f) {
     feeder_wait_idle(f);
     feeder_replay_pending(f);
-    return 0;
-}
-
-extern "C" void hvws_feeder_free(hvws_feeder* f) {
-    if (!f) return;
-    hvws_feeder_flush(f);
     {
         std::lock_guard<std::mutex> lk(f->m);
         f->stop = true;
@@ -538,18 +584,50 @@ extern "C" void hvws_feeder_free(hvws_feeder* f) {
     delete f;
 }
 
+// Ends a top-level submit / flush: a free asked for by one of its callbacks
+// happens now that the replay has returned.  Returns rc.
+int feeder_settle(hvws_feeder* f, int rc) {
+    if (!f->free_requested) return rc;
+    feeder_destroy(f);
+    return rc;
+}
+}  // namespace
+
+extern "C" int hvws_feeder_flush(hvws_feeder* f) {
+    if (!f) return -1;
+    if (f->in_replay) return -1;   // from inside one of its own callbacks
+    feeder_wait_idle(f);
+    feeder_replay_pending(f);
+    return feeder_settle(f, 0);
+}
+
+extern "C" void hvws_feeder_free(hvws_feeder* f) {
+    if (!f) return;
+    if (f->in_replay) {
+        // From inside one of its own callbacks: the replay that called it is
+        // still iterating this feeder's run.  Freed when that submit / flush
+        // returns (after the rest of its callbacks).
+        f->free_requested = true;
+        return;
+    }
+    feeder_destroy(f);
+}
+
 int hvws_feeder_submit(hvws_feeder* f, WebSocketParser* const* parsers, const char* const* data, const size_t* len,
                        int n, int* rets) {
-    if (!f || n < 0 || f->in_replay) return -1;
+    if (!f || n < 0 || f->in_replay || f->free_requested) return -1;
     if (n == 0) return hvws_feeder_flush(f);
+    if (any_busy(parsers, n)) return -1;   // from another replay on this thread that would overwrite these
     // as hvws_feed_many: a parser seen twice starts a new run
     int done = 0;
-    while (done < n) {
+    while (done < n && !f->free_requested) {
         const int end = distinct_run_end(parsers, done, n);
         feeder_run(f, parsers + done, data + done, len + done, end - done, rets ? rets + done : nullptr);
         done = end;
     }
-    return n;
+    // freed from a callback: the runs not started yet are dropped (their
+    // rets untouched); the count says how many reads were taken
+    return feeder_settle(f, done);
 }
 
 // ---------------------------------------------------------------- C handle

@@ -234,6 +234,9 @@ struct hvws_ctx {
     uint8_t t_rec[kTimeRing] = {};      // which of the slot's 4 events were recorded (bit i)
     uint64_t t_seq = 0;   // scans recorded so far
     int t_cur = 0;        // ring slot of the last scan
+    // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
+    // on both of the context's compute streams
+    hipEvent_t span_ev[4] = {};
     int variant = 0;   // k_unmask geometry the tile index was built for
     bool nfr_known = false;   // else c->nfr is an upper bound, the count is on the device
     // table invariant check (hvws_set_table_checks)
@@ -1225,7 +1228,9 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     c->hfirst.resize(nseg);
     c->hcount.resize(nseg);
     c->hcarry.resize(nseg);
-    const bool on_host = total <= hcap;
+    // A segment whose records fit the pinned area (first + count <= hcap)
+    // wrote them there; the others left them in their device slots only.
+    bool on_host = true;
     const drec* slots_base = c->d_small_slots.as<drec>();
     uint64_t k = 0;
     for (uint32_t s = 0; s < nseg; ++s) {
@@ -1234,9 +1239,10 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
         c->hcount[s] = cnt;
         c->hcarry[s] = ho[s].st;
         if (cnt) {
-            if (on_host) {
+            if (ho[s].first + cnt <= hcap) {
                 memcpy(&c->hcache[k], hr + ho[s].first, cnt * sizeof(drec));
             } else {
+                on_host = false;
                 HIP_OR(hipMemcpyAsync(&c->hcache[k], slots_base + hb[s], cnt * sizeof(drec), hipMemcpyDeviceToHost,
                                       c->stream),
                        HVWS_EHIP);
@@ -1445,6 +1451,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
             if (ev) hipEventDestroy(ev);
     for (auto& ev : c->up_ev)
         if (ev) hipEventDestroy(ev);
+    for (auto& ev : c->span_ev)
+        if (ev) hipEventDestroy(ev);
     c->h_status.release();
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy_in) hipStreamDestroy(c->copy_in);
@@ -1523,6 +1531,9 @@ int hvws_rx_reads(hvws_ctx* c, char* const* reads, const uint64_t* lens, websock
     if (rc) return rc;
     if (n && (!reads || !lens)) return set_err(HVWS_EINVAL, "null read table");
     if (n == 0) return set_err(HVWS_EINVAL, "no reads");
+    // In-place reads exist only on the small path: with it switched off
+    // (hvws_set_small_batch_limit ~0) callers fall back to the general path.
+    if (c->small_limit == ~0ull) return set_err(HVWS_EINVAL, "small-batch path disabled on this context");
     // device address of every read; the batch goes to k_small in address order
     std::vector<uint8_t*> dev(n);
     bool sorted = true;
@@ -1551,7 +1562,7 @@ int hvws_rx_reads(hvws_ctx* c, char* const* reads, const uint64_t* lens, websock
         total += lens[i];
         if (carry) copy_parser(cin[k], carry[i]);
     }
-    const uint64_t limit = c->small_limit && c->small_limit != ~0ull ? c->small_limit : kSmallBatch;
+    const uint64_t limit = c->small_limit ? c->small_limit : kSmallBatch;
     if (total > limit) return set_err(HVWS_EINVAL, "%llu bytes of reads (at most %llu per call)",
                                       (unsigned long long)total, (unsigned long long)limit);
     if ((rc = rx_batch_small(c, nullptr, span, segs.data(), carry ? cin.data() : nullptr, n, unmask, base)) != HVWS_OK)
@@ -1792,6 +1803,39 @@ int hvws_last_times(hvws_ctx* c, float out[2]) {
     out[0] = out[1] = -1.0f;
     if (!c->have_scan || c->t_seq == 0) return set_err(HVWS_EINVAL, "no scan");
     return step_times_at(c, c->t_cur, out);
+}
+
+// Timed region on the device: markers on both compute streams (the scan
+// stream and the unmask stream of pipelined steps), so the span runs from
+// whichever stream starts first to whichever ends last.
+int hvws_span_begin(hvws_ctx* c) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    for (auto& ev : c->span_ev)
+        if (!ev) HIP_OR(hipEventCreate(&ev), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->span_ev[0], c->stream), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->span_ev[1], c->sstream ? c->sstream : c->stream), HVWS_EHIP);
+    return HVWS_OK;
+}
+
+int hvws_span_end(hvws_ctx* c, float* ms) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (!ms || !c->span_ev[0]) return set_err(HVWS_EINVAL, "no hvws_span_begin");
+    HIP_OR(hipEventRecord(c->span_ev[2], c->stream), HVWS_EHIP);
+    HIP_OR(hipEventRecord(c->span_ev[3], c->sstream ? c->sstream : c->stream), HVWS_EHIP);
+    HIP_OR(hipEventSynchronize(c->span_ev[2]), HVWS_EHIP);
+    HIP_OR(hipEventSynchronize(c->span_ev[3]), HVWS_EHIP);
+    // max over (begin, end) pairs = latest end - earliest begin
+    float best = 0.0f;
+    for (int b = 0; b < 2; ++b)
+        for (int e = 2; e < 4; ++e) {
+            float t = 0.0f;
+            HIP_OR(hipEventElapsedTime(&t, c->span_ev[b], c->span_ev[e]), HVWS_EHIP);
+            best = std::max(best, t);
+        }
+    *ms = best;
+    return HVWS_OK;
 }
 
 int hvws_step_times(hvws_ctx* c, float* out, int max_steps) {

@@ -915,10 +915,15 @@ __global__ __launch_bounds__(64) void k_small(const uint8_t* __restrict__ rx, ui
     }
 
     base = __shfl(base, 0);
+    const uint64_t nl = n < SMALL_LREC ? n : SMALL_LREC;
     if (base + n <= h_rec_cap) {
-        const uint64_t nl = n < SMALL_LREC ? n : SMALL_LREC;
         for (uint64_t i = lane; i < nl; i += 64) h_rec[base + i] = lrec[i];
         for (uint64_t i = SMALL_LREC + lane; i < n; i += 64) h_rec[base + i] = slot[i];
+    } else if (!(unmask && n > SMALL_LREC)) {
+        // Past the pinned record area: the host reads this segment from its
+        // device slot, so the slot must hold every record (the XOR path above
+        // copied the LDS ones only when it needed them).
+        for (uint64_t i = lane; i < nl; i += 64) slot[i] = lrec[i];
     }
     if (lane == 0) {
         dsmall_out o;

@@ -15,6 +15,8 @@ Every expected output below comes from that library:
     form.
 The fixtures are data (inputs + expected outputs); no reference source is
 stored.  Usage: python tests/golden/make_golden.py [--configs c1,c2,c4]
+       python tests/golden/make_golden.py --skip-streams --configs '' \\
+              --big c3,c5_rank0,c5_rank1,c5_rank2,c5_rank3,c5_rank4,c5_rank5,c5_rank6,c5_rank7
 """
 from __future__ import annotations
 
@@ -185,9 +187,57 @@ def make_configs(names):
         json.dump(out, f, indent=1)
 
 
+def big_plan(name: str):
+    """c3 (seed 1, the tests' batch) or c5_rank{r}: the c3-shaped batch bench.py
+    rank r builds (synth.config_plan('c3', seed=1000 + r))."""
+    if name == "c3":
+        return synth.config_plan("c3", seed=1)
+    if name.startswith("c5_rank"):
+        return synth.config_plan("c3", seed=1000 + int(name[len("c5_rank"):]))
+    raise KeyError(name)
+
+
+def streamed_digest(plan, threads: int):
+    return H.streamed_digest(plan, threads, "ref")
+
+
+def make_big_configs(names, threads: int):
+    """Configs too large to hold (c3: 68.7 GB; the eight config-5 rank
+    batches): reference digests streamed in bounded memory.  Checked first on
+    c2, whose whole-buffer digests (make_configs) are committed."""
+    path = os.path.join(HERE, "configs.json")
+    out = json.load(open(path))
+    d = streamed_digest(synth.config_plan("c2", seed=1), threads)
+    g = out["c2"]
+    assert (f"{d[0]:016x}", f"{d[1]:016x}", d[2], d[3], d[4]) == (
+        g["digest_masked"], g["digest_unmasked"], g["messages"], g["message_bytes"], g["message_xsum"]), \
+        "streamed digest != whole-buffer digest on c2"
+    for name in names:
+        plan = big_plan(name)
+        d = streamed_digest(plan, threads)
+        fn = "config_plan('c3', seed=1)" if name == "c3" else f"config_plan('c3', seed={plan.seed})"
+        out[name] = {
+            "plan": {"fn": f"libhv_amd.synth.{fn}", "frames": plan.n, "rx_bytes": plan.total,
+                     "payload_bytes": plan.payload_bytes},
+            "digest_masked": f"{d[0]:016x}",
+            "digest_unmasked": f"{d[1]:016x}",
+            "messages": d[2],
+            "message_bytes": d[3],
+            "message_xsum": d[4],
+            "chunk": 8192,
+            "method": "streamed: reference websocket_build_frame per frame + reference parser in 8 KiB chunks, "
+                      "digest folded per 8-byte word (tests/csrc/cfgdigest.c)",
+        }
+        print(name, plan.n, out[name]["digest_masked"], out[name]["digest_unmasked"], flush=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c1,c2")
+    ap.add_argument("--big", default="", help="streamed digests, e.g. c3,c5_rank0,...,c5_rank7")
+    ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
     ap.add_argument("--skip-streams", action="store_true")
     ap.add_argument("--only-keys", action="store_true")
     a = ap.parse_args()
@@ -200,6 +250,8 @@ def main():
         make_streams()
     if a.configs:
         make_configs([c for c in a.configs.split(",") if c])
+    if a.big:
+        make_big_configs([c for c in a.big.split(",") if c], a.threads)
 
 
 if __name__ == "__main__":

@@ -104,3 +104,54 @@ def test_no_cpu_fallback_without_gpu():
 def test_engine_errors_are_reported():
     with pytest.raises(libhv_amd.HvwsError):
         libhv_amd.Engine(0) if libhv_amd.device_count() == 0 else libhv_amd.Engine(10_000)
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "http", "WebSocketParser.h")),
+                    reason="reference headers only in the build container")
+def test_builds_against_reference_headers(tmp_path):
+    """libhv's callers compile against libhv's own headers.  tests/csrc/refabi.cpp
+    is built against the reference's http/{WebSocketParser.h, websocket_parser.h,
+    wsdef.h} (+ hexport.h) and against include/, each linked to libhvws.so with
+    no undefined symbol allowed; the same static_asserts on the layouts pass in
+    both; both programs print the same answers from the host-only entry
+    points, which equal the reference library's."""
+    src = os.path.join(ROOT, "tests", "csrc", "refabi.cpp")
+    out = {}
+    for name, inc in (("ref", [f"-I{REF}", f"-I{REF}/http"]), ("ours", [f"-I{INC}"])):
+        exe = str(tmp_path / f"refabi_{name}")
+        cmd = ["g++", "-std=c++11", "-O1", "-Wall", "-Werror", "-Wno-invalid-offsetof", *inc, src,
+               f"-L{os.path.dirname(libhv_amd.LIB_PATH)}", "-lhvws",
+               f"-Wl,-rpath,{os.path.dirname(libhv_amd.LIB_PATH)}", "-Wl,--no-undefined",
+               "-Wl,--unresolved-symbols=report-all", "-o", exe]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        out[name] = r.stdout
+    assert out["ref"] == out["ours"]
+    lines = out["ref"].splitlines()
+    assert lines[0] == "init 0 0 0 0 0 0 1" and lines[1] == "settings 1 1 1"
+    assert lines[-1] == "sizes 48 24 80"
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wsharness as H
+
+    if H.have_ref():
+        R = H.ref()
+        R.websocket_calc_frame_size.restype = ctypes.c_size_t
+        R.websocket_calc_frame_size.argtypes = [ctypes.c_int, ctypes.c_size_t]
+        R.ws_calc_frame_size.restype = ctypes.c_int
+        R.ws_calc_frame_size.argtypes = [ctypes.c_int, ctypes.c_bool]
+        n = 0
+        for ln in lines:
+            f = ln.split()
+            if f[0] == "calc":
+                assert int(f[3]) == R.websocket_calc_frame_size(int(f[2]), int(f[1])), ln
+                n += 1
+            elif f[0] == "wscalc":
+                assert (int(f[2]), int(f[3])) == (R.ws_calc_frame_size(int(f[1]), False),
+                                                  R.ws_calc_frame_size(int(f[1]), True)), ln
+                n += 1
+        assert n == 43

@@ -31,7 +31,13 @@ def _worker(rank, world, port, q):
     plan = bench.rank_plan("c1", r, 8)
     dist.barrier()
     t = bench.max_over_ranks(dist, 1.0 + r)
-    q.put((r, w, local, t, int(plan.mask[:16].astype(np.uint64).sum()), plan.total, len(plan.segments)))
+    # the per-rank timing rows bench.py gathers (start, end, device span):
+    # rank r starts at 100 + r and ends at 110 + 3 r
+    rows = bench.gather_rows(dist, [100.0 + r, 110.0 + 3 * r, 7.0 + r])
+    span = bench.span_of(rows)
+    name, fx = bench.fixture_for("c3", r)
+    q.put((r, w, local, t, int(plan.mask[:16].astype(np.uint64).sum()), plan.total, len(plan.segments),
+           rows.tolist(), span, name, fx["plan"]["frames"] if fx else None))
     dist.destroy_process_group()
 
 
@@ -51,3 +57,8 @@ def test_two_ranks_gloo():
     assert all(o[3] == 2.0 for o in out)              # max over ranks
     assert out[0][4] != out[1][4]                      # disjoint batches (distinct seeds)
     assert out[0][5] == out[1][5] and out[0][6] == 8   # same shape per rank
+    # gathered rows identical on both ranks, in rank order
+    assert out[0][7] == out[1][7] == [[100.0, 110.0, 7.0], [101.0, 113.0, 8.0]]
+    assert out[0][8] == out[1][8] == 13.0              # latest end - earliest start
+    # each rank's c3-shaped batch has its own reference fixture
+    assert [o[9] for o in out] == ["c5_rank0", "c5_rank1"] and all(o[10] == 1 << 20 for o in out)

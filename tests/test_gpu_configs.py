@@ -5,7 +5,9 @@ the reference digests in tests/golden/configs.json:
   * after one pass every payload byte equals its plaintext and every header
     byte is untouched (hvws_synth VERIFY_PLAIN, a byte-exact check);
   * a second pass restores the masked batch exactly (XOR involution);
-  * the unmasked digest equals the reference's (configs 1, 2, 4);
+  * the masked and unmasked digests equal the reference's (configs 1-4, and
+    the eight config-5 rank batches bench.py builds: tests/golden/configs.json,
+    c3 and c5_rank* streamed through the reference by make_golden.py --big);
   * one frame record per frame."""
 from __future__ import annotations
 
@@ -67,7 +69,15 @@ def test_config2_1m_x_1k(eng, nseg):
 
 @pytest.mark.parametrize("nseg", [4096, 1])
 def test_config3_1m_x_64k(eng, nseg):
-    _run(eng, synth.config_plan("c3", seed=1), nseg, GOLD.get("c3"))
+    _run(eng, synth.config_plan("c3", seed=1), nseg, GOLD["c3"])
+
+
+@pytest.mark.parametrize("rank", range(8))
+def test_config5_rank_batches(eng, rank):
+    """Config 5 (8M x 64 KiB over 8 GPUs) is eight disjoint c3-shaped batches,
+    one per rank (bench.py rank_plan: seed 1000 + rank).  Each one, on this
+    GPU, against its reference digests."""
+    _run(eng, synth.config_plan("c3", seed=1000 + rank), 4096, GOLD[f"c5_rank{rank}"])
 
 
 @pytest.mark.parametrize("nseg", [1, 1024])

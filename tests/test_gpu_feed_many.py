@@ -246,6 +246,94 @@ def test_feed_many_record_density(read):
     _check(conns)
 
 
+@pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
+def test_nested_feed_of_parser_still_to_replay_refused(feeder):
+    """An onMessage that feeds a parser whose state a replay still to come on
+    this thread will write -- later in the same run, or in a feeder's run
+    already in flight -- is refused (-1; libhv closes such a connection)
+    instead of being overwritten silently.  Feeding any other parser works,
+    and every connection still matches the reference."""
+    L = libhv_amd.lib()
+    rng = random.Random(61)
+    a, b, c = (Conn(S.rand_stream(rng, 4, max_len=300), [0]) for _ in range(3))
+    got = []
+
+    def on_a(user, op, data, n):
+        a.sink._on(user, op, data, n)
+        if got:
+            return
+        def one(conn):
+            hs = (ctypes.c_void_p * 1)(conn.h)
+            ds = (ctypes.c_void_p * 1)(ctypes.addressof(conn.buf))
+            ls = (ctypes.c_size_t * 1)(len(conn.data))
+            rets = (ctypes.c_int * 1)()
+            return L.hvws_wsp_feed_many(hs, ds, ls, 1, rets), rets[0]
+        got.append(one(b))                                                   # still to replay: refused
+        got.append(L.hvws_wsp_feed(b.h, ctypes.addressof(b.buf), len(b.data)))   # same through FeedRecvData
+        got.append(one(c))                                                   # not in flight: fed
+
+    a.cb = libhv_amd.MSG_CB(on_a)
+    L.hvws_wsp_set_sink(a.h, a.cb, None)
+
+    def sub(f, conns):
+        n = len(conns)
+        hs = (ctypes.c_void_p * n)(*[x.h for x in conns])
+        ds = (ctypes.c_void_p * n)(*[ctypes.addressof(x.buf) for x in conns])
+        ls = (ctypes.c_size_t * n)(*[len(x.data) for x in conns])
+        rets = (ctypes.c_int * n)()
+        if f:
+            assert L.hvws_wsp_feeder_submit(f, hs, ds, ls, n, rets) == n
+        else:
+            assert L.hvws_wsp_feed_many(hs, ds, ls, n, rets) == n
+        return rets
+
+    if feeder:
+        f = L.hvws_feeder_new()
+        ra = sub(f, [a])
+        rb = sub(f, [b])     # a's callbacks replay here, with b's run in flight
+        assert L.hvws_feeder_flush(f) == 0
+        L.hvws_feeder_free(f)
+        rets = [ra[0], rb[0]]
+    else:
+        r = sub(None, [a, b])
+        rets = [r[0], r[1]]
+    assert got[0][0] == -1 and got[1] == -1 and got[2] == (1, len(c.data)), got
+    for conn, r in zip((a, b, c), rets + [got[2][1]]):
+        conn.fed, conn.rets = [len(conn.data)], [r]
+    _check([a, b, c])
+
+
+def test_feeder_free_from_callback():
+    """hvws_feeder_free from inside one of the feeder's own callbacks is
+    deferred until the flush that replays it returns: the rest of that run's
+    callbacks still run, and nothing is used after the free."""
+    L = libhv_amd.lib()
+    rng = random.Random(71)
+    conns = [Conn(S.rand_stream(rng, 5, max_len=400), [0]) for _ in range(6)]
+    f = L.hvws_feeder_new()
+    freed = []
+
+    def on0(user, op, data, n):
+        conns[0].sink._on(user, op, data, n)
+        if not freed:
+            freed.append(1)
+            L.hvws_feeder_free(f)
+
+    conns[0].cb = libhv_amd.MSG_CB(on0)
+    L.hvws_wsp_set_sink(conns[0].h, conns[0].cb, None)
+    n = len(conns)
+    hs = (ctypes.c_void_p * n)(*[c.h for c in conns])
+    ds = (ctypes.c_void_p * n)(*[ctypes.addressof(c.buf) for c in conns])
+    ls = (ctypes.c_size_t * n)(*[len(c.data) for c in conns])
+    rets = (ctypes.c_int * n)()
+    assert L.hvws_wsp_feeder_submit(f, hs, ds, ls, n, rets) == n
+    assert L.hvws_feeder_flush(f) == 0   # replays; the callback frees f, which happens on return
+    assert freed
+    for i, c in enumerate(conns):
+        c.fed, c.rets = [len(c.data)], [rets[i]]
+    _check(conns)
+
+
 def test_feeder_callbacks_one_submission_late():
     """A feeder replays submission k's callbacks during submit k+1 (or flush):
     nothing is delivered by the first submit, everything by the flush; a

@@ -300,6 +300,31 @@ def test_rx_batch_host_roundtrip(eng):
     assert np.array_equal(buf, exp)
 
 
+@pytest.mark.parametrize("payload,unmask", [(10, True), (10, False), (0, True), (0, False)],
+                         ids=["512rec_unmask", "512rec_raw", "1365rec_unmask", "1365rec_raw"])
+def test_rx_batch_small_path_over_host_record_area(eng, payload, unmask):
+    """A small-path batch (k_small) with more records than the pinned record
+    area holds (2^20): segments past it hand their records back through their
+    device slots, which must be complete -- also for segments of <= 512
+    records (kept in LDS) and without the unmask.  8 KiB segments of 16-byte
+    frames (512 records each) or 6-byte empty frames (1365 each)."""
+    n_seg = 4096 if payload else 1024
+    per = 8192 // (payload + 6)
+    plan = synth.uniform_plan(n_seg * per, payload, 23)
+    plan.segments = [(s * per * (payload + 6), per * (payload + 6)) for s in range(n_seg)]
+    host = H.synth_cpu(plan)
+    exp_recs, exp_carry, _, exp = _oracle_batch(host, plan.segments, None)
+    assert len(exp_recs) > 1 << 20
+    libhv_amd.lib().hvws_set_small_batch_limit(eng.ctx, 0)   # default: batches <= 64 MiB take k_small
+    buf = host.copy()
+    eng.rx_batch(buf, plan.segments, None, unmask)
+    assert np.array_equal(buf, exp if unmask else host)
+    frames = eng.frames()
+    assert len(frames) == len(exp_recs)
+    for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
+        assert np.array_equal(frames[f], exp_recs[f]), f
+
+
 def test_pipeline_host_inclusive(eng):
     """Chunked H2D -> scan -> unmask -> D2H with the carry chained across chunk
     boundaries (frames straddle chunks)."""

@@ -157,9 +157,36 @@ class PinnedConn(Conn):
         ctypes.memmove(addr, data, len(data))
 
 
+def test_rx_reads_refused_with_small_path_off(eng):
+    """hvws_set_small_batch_limit(ctx, ~0) turns the small path off; reads in
+    place exist only there, so hvws_rx_reads refuses and the batched drop-in
+    falls back to the general path (test_feed_from_pinned_buffers[general])."""
+    L = libhv_amd.lib()
+    base = _arena(eng, 4096)
+    try:
+        r = (ctypes.c_void_p * 1)(base)
+        ln = (ctypes.c_uint64 * 1)(100)
+        old = L.hvws_set_small_batch_limit(eng.ctx, (1 << 64) - 1)
+        assert L.hvws_rx_reads(eng.ctx, r, ln, None, 1, 1) == EINVAL
+        L.hvws_set_small_batch_limit(eng.ctx, old)
+        assert L.hvws_rx_reads(eng.ctx, r, ln, None, 1, 1) == 0, L.hvws_last_error()
+    finally:
+        L.hvws_host_free(eng.ctx, base)
+
+
+@pytest.mark.parametrize("path", ["small", "general"])
 @pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_feed_from_pinned_buffers(eng, seed, feeder):
+def test_feed_from_pinned_buffers(eng, seed, feeder, path):
+    L = libhv_amd.lib()
+    L.hvws_set_small_batch_limit(None, 0 if path == "small" else (1 << 64) - 1)
+    try:
+        _feed_from_pinned(eng, seed, feeder)
+    finally:
+        L.hvws_set_small_batch_limit(None, 0)
+
+
+def _feed_from_pinned(eng, seed, feeder):
     rng = random.Random(100 + seed)
     streams = []
     for _ in range(rng.randint(20, 120)):

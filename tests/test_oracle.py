@@ -134,3 +134,32 @@ def test_config_digests(name):
     assert (int(stats[0]), int(stats[1]), int(stats[2])) == (g["messages"], g["message_bytes"], g["message_xsum"])
     if name == "c1":
         assert hashlib.sha256(buf.tobytes()).hexdigest() == g["sha256_unmasked"]
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_streamed_digest_method(name, threads):
+    """The streamed digest (tests/csrc/cfgdigest.c) behind the c3 / config-5
+    fixtures -- frames built window by window, byte ranges per thread, the
+    frame a range starts inside rebuilt and refed -- gives the whole-buffer
+    digests and message statistics of the committed configs (here with the
+    oracle's builder and parser; make_golden.py runs it with the reference's)."""
+    g = json.load(open(os.path.join(GOLD, "configs.json")))[name]
+    d = H.streamed_digest(synth.config_plan(name, seed=1), threads, "oracle")
+    assert (f"{d[0]:016x}", f"{d[1]:016x}", d[2], d[3], d[4]) == (
+        g["digest_masked"], g["digest_unmasked"], g["messages"], g["message_bytes"], g["message_xsum"])
+
+
+def test_config5_fixtures_match_bench_plans():
+    """The eight config-5 fixtures (and c3) describe the batches bench.py and
+    the GPU tests build: same frame count, rx and payload bytes; all digests
+    distinct (distinct seeds)."""
+    G = json.load(open(os.path.join(GOLD, "configs.json")))
+    names = ["c3"] + [f"c5_rank{r}" for r in range(8)]
+    for nm in names:
+        plan = synth.config_plan("c3", seed=1 if nm == "c3" else 1000 + int(nm[-1]))
+        g = G[nm]
+        assert (plan.n, plan.total, plan.payload_bytes) == (g["plan"]["frames"], g["plan"]["rx_bytes"],
+                                                            g["plan"]["payload_bytes"])
+        assert g["messages"] == plan.n and g["message_bytes"] == plan.payload_bytes
+    assert len({G[nm]["digest_unmasked"] for nm in names}) == len(names)

@@ -278,3 +278,39 @@ def digest_np(buf: np.ndarray) -> int:
     w = b.view("<u8")
     k = np.arange(len(w), dtype=np.uint64) * np.uint64(0xD1B54A32D192ED03)
     return int(mix64(w ^ k).sum(dtype=np.uint64))
+
+
+class _CfgFns(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in ("build", "mnew", "msink", "mfeed", "mfree", "synth")]
+
+
+CFGDIGEST_SO = os.path.join(ROOT, "tests", "_build", "libcfgdigest.so")
+
+
+def streamed_digest(plan, threads: int, impl: str = "ref"):
+    """[digest_masked, digest_unmasked, messages, message_bytes, message_xsum]
+    of a plan's batch without holding it (tests/csrc/cfgdigest.c): frames built
+    window by window by `impl`'s websocket_build_frame ("ref": the reference's,
+    oracle/_ref; "oracle": the restatement), unmasked by its parser + message
+    layer in 8 KiB chunks.  Plans with fragments run as one range."""
+    L, O = (ref() if impl == "ref" else oracle()), oracle()
+    D = _load(CFGDIGEST_SO, "cfgdigest")
+    fin_only = bool(np.all((plan.flags & 0x10) != 0) and np.all((plan.flags & 0x0F) != 0))
+    if not fin_only:
+        threads = 1   # fragments carry message state across frames: one range
+    build = "websocket_build_frame" if impl == "ref" else "ows_build_frame"
+    fns = _CfgFns(_addr(L, build), _addr(L, "msgp_new"), _addr(L, "msgp_set_sink"), _addr(L, "msgp_feed"),
+                  _addr(L, "msgp_free"), _addr(O, "ows_synth_plain"))
+    off = np.ascontiguousarray(plan.frame_off, np.uint64)
+    fl = np.ascontiguousarray(plan.flags, np.uint8)
+    mk = np.ascontiguousarray(plan.mask, np.uint32)
+    ln = np.ascontiguousarray(plan.length, np.uint64)
+    tx = np.ascontiguousarray(plan.text, np.uint8) if plan.text is not None else None
+    out = (ctypes.c_uint64 * 5)()
+    D.cfgd_run.restype = ctypes.c_int
+    D.cfgd_run.argtypes = [ctypes.POINTER(_CfgFns), ctypes.c_uint64, ctypes.c_uint64] + [ctypes.c_void_p] * 5 + \
+        [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    rc = D.cfgd_run(ctypes.byref(fns), plan.seed, plan.n, off.ctypes.data, fl.ctypes.data, mk.ctypes.data,
+                    ln.ctypes.data, tx.ctypes.data if tx is not None else None, plan.total, threads, out)
+    assert rc == 0, "cfgd_run failed"
+    return [int(x) for x in out]
