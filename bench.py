@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--feed-conns", type=int, default=1024,
                     help="event-loop leg: connections per poll iteration (0: skip)")
     ap.add_argument("--feed-iters", type=int, default=20, help="event-loop leg: poll iterations (8 KiB reads each)")
+    ap.add_argument("--dropin-reads", type=int, default=2000,
+                    help="drop-in leg: FeedRecvData calls per pass, one 8 KiB read each (0: skip)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
     return ap.parse_args()
@@ -264,6 +266,90 @@ def event_loop_leg(eng, device: int, conns: int, iters: int, seed: int):
         "api": "hvws_feeder_submit (pipelined) / hvws_feed_many over hvws_host_alloc read buffers (hvws_rx_reads)",
     }
     return res, streams, pay
+
+
+def dropin_leg(eng, device: int, seed: int, reads: int = 2000, builds: int = 4000, passes: int = 3) -> dict:
+    """The literal drop-in's per-call latency (SURVEY 8(f) row 1 as libhv calls
+    it unchanged): WebSocketParser::FeedRecvData once per 8 KiB read
+    (http/server/HttpHandler.cpp:757-763) on one connection, and a masked
+    125-byte websocket_build_frame per message (http/WebSocketChannel.cpp:66-79
+    via ws_build_frame).  Timed in C (tests/csrc/callbench.c), no interpreter
+    in the loop; the resident worker (hvws_set_door) on and off, interleaved,
+    median of `passes`; the reference on one core beside it."""
+    import libhv_amd
+    from libhv_amd import synth
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wsharness as H
+
+    L = libhv_amd.lib()
+    L.hvws_set_thread_device(device)
+    CB = ctypes.CDLL(os.path.join(ROOT, "tests", "_build", "libcallbench.so"))
+    CB.cb_feed.restype = ctypes.c_double
+    CB.cb_feed.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_size_t] * 2
+    CB.cb_build.restype = ctypes.c_double
+    CB.cb_build.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_size_t, ctypes.c_int]
+    total = FEED_READ * reads
+    fp = synth.uniform_plan(total // 1032 + 2, 1024, seed)
+    dpf = libhv_amd.DevicePlan(eng, fp)
+    buf = eng.alloc(fp.total + 64)
+    eng.synth(buf, fp.total, fp.seed, dpf, 0)
+    masked = buf.download(fp.total)[:total].copy()
+    buf.free()
+    dpf.free()
+    work = np.empty_like(masked)
+    R = H.ref() if H.have_ref() else H.oracle()
+    addr = lambda lib, f: ctypes.cast(getattr(lib, f), ctypes.c_void_p).value  # noqa: E731
+
+    def feed_once(impl: str) -> float:
+        work[:] = masked
+        if impl == "ref":
+            h = R.msgp_new()
+            dt = CB.cb_feed(addr(R, "msgp_feed"), h, work.ctypes.data, total, FEED_READ)
+            R.msgp_free(h)
+        else:
+            L.hvws_set_door(None, 1 if impl == "door" else 0)
+            h = L.hvws_wsp_new()
+            dt = CB.cb_feed(addr(L, "hvws_wsp_feed"), h, work.ctypes.data, total, FEED_READ)
+            L.hvws_wsp_free(h)
+        assert dt > 0, f"drop-in leg: a read was not consumed ({impl})"
+        return dt / reads * 1e6
+
+    payload = np.frombuffer(np.random.default_rng(seed).bytes(125), np.uint8).copy()
+    key = ctypes.create_string_buffer(b"\x12\x34\x56\x78", 4)
+    out = ctypes.create_string_buffer(256)
+
+    def build_once(impl: str) -> float:
+        if impl == "ref":
+            fn = addr(R, "websocket_build_frame" if H.have_ref() else "ows_build_frame")
+        else:
+            L.hvws_set_door(None, 1 if impl == "door" else 0)
+            fn = addr(L, "websocket_build_frame")
+        dt = CB.cb_build(fn, out, 0x2 | 0x10 | 0x20, key, payload.ctypes.data, 125, builds)
+        assert dt > 0, f"drop-in leg: build_frame size mismatch ({impl})"
+        return dt / builds * 1e6
+
+    for impl in ("door", "launch", "ref"):   # warm: worker resident, contexts and buffers made
+        feed_once(impl)
+        build_once(impl)
+    res = {k: [] for k in ("feed_door", "feed_launch", "feed_ref", "build_door", "build_launch", "build_ref")}
+    for _ in range(passes):
+        for impl in ("door", "launch", "ref"):
+            res["feed_" + impl].append(feed_once(impl))
+            res["build_" + impl].append(build_once(impl))
+    L.hvws_set_door(None, -1)
+    med = {k: round(float(np.median(v)), 2) for k, v in res.items()}
+    return {
+        "feed_8KiB_read_us": {"resident_worker": med["feed_door"], "launch_per_call": med["feed_launch"],
+                              "reference_1core": med["feed_ref"]},
+        "build_frame_125B_masked_us": {"resident_worker": med["build_door"], "launch_per_call": med["build_launch"],
+                                       "reference_1core": med["build_ref"]},
+        "reads": reads, "builds": builds,
+        "note": "WebSocketParser::FeedRecvData per 8 KiB read of 1 KiB masked frames (pageable buffer, one "
+                "connection) and masked websocket_build_frame of 125 B, per call, timed in C; median of "
+                f"{passes} interleaved passes",
+    }
 
 
 def cpu_event_loop(streams: np.ndarray, iters: int, pay: float):
@@ -691,6 +777,8 @@ def main():
         if args.feed_conns > 0:
             extra["event_loop"], feed_streams, feed_pay = event_loop_leg(eng, device, args.feed_conns,
                                                                          args.feed_iters, plan.seed + 7)
+        if args.dropin_reads > 0:
+            extra["drop_in"] = dropin_leg(eng, device, plan.seed + 11, args.dropin_reads)
 
     rx_plain = passes % 2 == 1   # payloads currently unmasked
     # host-inclusive: pinned host rx -> device -> scan+unmask -> host, every

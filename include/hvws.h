@@ -317,6 +317,26 @@ uint32_t hvws_set_validation(hvws_ctx* ctx, uint32_t classes);
  * either way; only latency differs. */
 uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
 
+/* Resident small-path worker.  The reference API's single calls -- FeedRecvData
+ * and websocket_parser_execute on a read of <= 32 KiB, websocket_decode,
+ * websocket_parser_decode and a masked websocket_build_frame of <= 32 KiB --
+ * are served by one workgroup (k_door) that stays on the device between
+ * calls and takes requests from a mailbox in pinned host memory: no kernel
+ * launch per call.  It runs on a stream of its own (its own hardware queue)
+ * and parks itself after $HVWS_DOOR_IDLE_US (default 20000) without a
+ * request; the next call relaunches it.  Context teardown, thread exit and
+ * process exit park it too.  on = 1 / 0 (off: each call launches k_small, or
+ * the XOR kernel, as before), -1 = default ($HVWS_DOOR, on).  ctx NULL = the
+ * calling thread's context.  Returns the previous setting.  Results are
+ * identical either way; only latency differs. */
+int hvws_set_door(hvws_ctx* ctx, int on);
+/* out = {worker launches, requests posted, requests the current worker
+ * served, worker resident now} (tests, benchmarks). */
+int hvws_door_stats(hvws_ctx* ctx, uint64_t out[4]);
+/* Idle time after which workers launched from now on park (microseconds;
+ * 0 = the default, 20000).  Returns the previous value. */
+uint64_t hvws_set_door_idle_us(uint64_t us);
+
 /* Small batches whose segments are all <= 32 KiB (total <= 1 MiB; an event
  * loop's reads) are read by the device straight from pinned host memory, each
  * segment staged in LDS, with no H2D copy ahead of the launch (on = 1, the

@@ -181,6 +181,9 @@ _SIGS = {
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_span_begin": (ctypes.c_int, [ctypes.c_void_p]),
     "hvws_span_end": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "hvws_set_door": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hvws_door_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_set_door_idle_us": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_set_small_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),

@@ -1,6 +1,7 @@
 // hvws_engine.cpp -- host side of the MI355X WebSocket receive engine:
 // per-(thread, device) contexts, frame-table management, kernel sequencing,
 // and the C ABI declared in include/hvws.h and include/hvws_synth.h.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -94,6 +95,7 @@ struct hbuf {   // grow-only pinned host allocation
 
 namespace hvws {
 hvws_ctx* thread_ctx();
+[[noreturn]] void fatal(const char* what);
 }
 
 static_assert(sizeof(drec) == sizeof(hvws_frame), "drec mirrors hvws_frame");
@@ -234,6 +236,17 @@ struct hvws_ctx {
     uint8_t t_rec[kTimeRing] = {};      // which of the slot's 4 events were recorded (bit i)
     uint64_t t_seq = 0;   // scans recorded so far
     int t_cur = 0;        // ring slot of the last scan
+    // resident small-path worker (k_door): its own stream (a dedicated
+    // hardware queue, so the resident kernel never holds up other work), the
+    // mailbox, the data and record areas (fine-grained pinned) and a device
+    // slot for records past the worker's LDS area
+    hipStream_t door_stream = nullptr;
+    hbuf h_door, h_door_data, h_door_rec;
+    dbuf d_door_slot;
+    bool door_live = false;     // launched and not yet seen to have ended
+    uint64_t door_seq = 0;      // last request number posted
+    int door_mode = -1;         // hvws_set_door: -1 default ($HVWS_DOOR, on), 0 off, 1 on
+    uint64_t door_launches = 0, door_calls = 0;
     // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
     // on both of the context's compute streams
     hipEvent_t span_ev[4] = {};
@@ -1268,6 +1281,178 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     return HVWS_OK;
 }
 
+// ------------------------------------------------- resident small-path worker
+// k_door (hvws_kernels.hip, ddoor in hvws_internal.h) serves the reference
+// API's single calls -- FeedRecvData / websocket_parser_execute on one read,
+// websocket_decode, websocket_parser_decode, a masked websocket_build_frame --
+// from a mailbox in fine-grained pinned memory: no launch, no dispatch and no
+// end-of-kernel signal per call.
+
+// Idle time after which a worker parks ($HVWS_DOOR_IDLE_US, default 20 ms),
+// in ticks of the 100 MHz realtime clock.
+std::atomic<uint64_t> g_door_idle_us{0};   // 0: not yet read from the environment
+
+uint64_t door_idle_us() {
+    uint64_t us = g_door_idle_us.load(std::memory_order_relaxed);
+    if (!us) {
+        const char* e = getenv("HVWS_DOOR_IDLE_US");
+        us = e && strtoull(e, nullptr, 0) ? strtoull(e, nullptr, 0) : 20000;
+        g_door_idle_us.store(us, std::memory_order_relaxed);
+    }
+    return us;
+}
+
+uint64_t door_idle_ticks() { return door_idle_us() * 100; }
+
+bool door_on(hvws_ctx* c) {
+    if (c->door_mode >= 0) return c->door_mode != 0;
+    static const int env = getenv("HVWS_DOOR") ? atoi(getenv("HVWS_DOOR")) : 1;
+    return env != 0;
+}
+
+std::mutex g_door_m;
+std::vector<hvws_ctx*> g_doors;   // contexts with a worker stream (parked at exit)
+void door_park(hvws_ctx* c);
+
+void door_atexit() {
+    std::lock_guard<std::mutex> lk(g_door_m);
+    for (hvws_ctx* c : g_doors) {
+        hipSetDevice(c->device);
+        door_park(c);
+    }
+}
+
+int door_ensure(hvws_ctx* c) {
+    if (c->door_stream) return HVWS_OK;
+    hipDeviceProp_t prop;
+    HIP_OR(hipGetDeviceProperties(&prop, c->device), HVWS_EHIP);
+    // A CU-masked stream gets a hardware queue of its own instead of sharing
+    // one round-robin with other streams, so the resident kernel holds up no
+    // other work.  The mask names every CU.
+    std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0u);
+    for (int i = 0; i < prop.multiProcessorCount; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+    HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
+    c->h_door.flags = c->h_door_data.flags = c->h_door_rec.flags = hipHostMallocCoherent;
+    HIP_OR(c->h_door.ensure(sizeof(ddoor)), HVWS_ENOMEM);
+    HIP_OR(c->h_door_data.ensure(kDoorMax + 256), HVWS_ENOMEM);
+    HIP_OR(c->h_door_rec.ensure(kDoorRecords * sizeof(drec)), HVWS_ENOMEM);
+    HIP_OR(c->d_door_slot.ensure(kDoorRecords * sizeof(drec)), HVWS_ENOMEM);
+    memset(c->h_door.p, 0, sizeof(ddoor));
+    if (!mapped<ddoor>(c->h_door) || !mapped<uint8_t>(c->h_door_data) || !mapped<drec>(c->h_door_rec))
+        return set_err(HVWS_EHIP, "worker mailbox not device-mapped");
+    std::lock_guard<std::mutex> lk(g_door_m);
+    // registered after the HIP runtime's own exit handlers, so it runs before them
+    static const bool reg = (atexit(door_atexit), true);
+    (void)reg;
+    g_doors.push_back(c);
+    return HVWS_OK;
+}
+
+// Post the request already written into the mailbox and wait for it.  The
+// worker is (re)launched when none is resident; one that parked just before
+// the request arrived is seen to have ended (stream idle, `done` behind) and
+// relaunched.  Kernel faults surface through the stream.
+int door_call(hvws_ctx* c) {
+    ddoor* b = c->h_door.as<ddoor>();
+    const uint64_t seq = ++c->door_seq;
+    __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+    ++c->door_calls;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto next_query = t0 + std::chrono::microseconds(100);
+    uint32_t spins = 0, launches = 0;
+    for (;;) {
+        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+        if (!c->door_live) {
+            if (launches++ >= 4) return set_err(HVWS_EHIP, "k_door: the worker takes no requests");
+            __atomic_store_n(&b->alive, 1ull, __ATOMIC_RELAXED);
+            HIP_OR(launch_door(mapped<ddoor>(c->h_door), mapped<uint8_t>(c->h_door_data), mapped<drec>(c->h_door_rec),
+                               c->d_door_slot.as<drec>(), door_idle_ticks(), __atomic_load_n(&b->done, __ATOMIC_ACQUIRE),
+                               c->door_stream),
+                   HVWS_EHIP);
+            c->door_live = true;
+            ++c->door_launches;
+            continue;
+        }
+        const bool parked = __atomic_load_n(&b->alive, __ATOMIC_RELAXED) == 0;
+        if (parked || ((++spins & 63u) == 0 && std::chrono::steady_clock::now() >= next_query)) {
+            const auto now = std::chrono::steady_clock::now();
+            next_query = now + std::chrono::microseconds(100);
+            const hipError_t q = hipStreamQuery(c->door_stream);
+            if (q == hipSuccess) {   // the worker has ended
+                if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+                c->door_live = false;
+                continue;
+            }
+            if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "k_door: %s", hipGetErrorString(q));
+            if (now - t0 > std::chrono::seconds(10)) return set_err(HVWS_EHIP, "k_door: no answer in 10 s");
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// Send the resident worker home (context teardown, thread and process exit).
+void door_park(hvws_ctx* c) {
+    if (!c->door_stream || !c->door_live) return;
+    c->h_door.as<ddoor>()->op = DOOR_EXIT;
+    if (door_call(c) != HVWS_OK) (void)hipGetLastError();
+    hipStreamSynchronize(c->door_stream);
+    c->door_live = false;
+}
+
+void door_release(hvws_ctx* c) {
+    if (!c->door_stream) return;
+    door_park(c);
+    {
+        std::lock_guard<std::mutex> lk(g_door_m);
+        g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
+    }
+    hipStreamDestroy(c->door_stream);
+    c->door_stream = nullptr;
+    c->h_door.release();
+    c->h_door_data.release();
+    c->h_door_rec.release();
+    c->d_door_slot.release();
+}
+
+// One read through the worker (gpu_feed's fast path): false when the worker
+// does not take it (off, or longer than kDoorMax).
+bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry, bool unmask,
+               std::vector<hvws_frame>& frames, websocket_parser& carry_out, int& started) {
+    if (!door_on(c) || len > kDoorMax || door_ensure(c) != HVWS_OK) return false;
+    ddoor* b = c->h_door.as<ddoor>();
+    uint8_t* data = c->h_door_data.as<uint8_t>();
+    memcpy(data, buf, len);
+    b->op = DOOR_FEED;
+    b->unmask = unmask ? 1u : 0u;
+    b->len = len;
+    b->vmask = c->vmask;
+    to_dcarry(carry, b->carry);
+    if (door_call(c) != HVWS_OK) hvws::fatal("k_door");
+    const uint64_t n = b->count;
+    frames.resize((size_t)n);
+    if (n) memcpy(frames.data(), c->h_door_rec.p, (size_t)n * sizeof(drec));
+    if (unmask) memcpy(buf, data, len);
+    copy_parser(carry_out, carry);
+    const dcarry out = b->out;
+    from_dcarry(out, carry_out);
+    started = (int)out.started;
+    return true;
+}
+
+bool door_xor(hvws_ctx* c, char* dst, const char* src, size_t n, uint32_t key, uint32_t phase) {
+    if (!door_on(c) || n > kDoorMax || door_ensure(c) != HVWS_OK) return false;
+    ddoor* b = c->h_door.as<ddoor>();
+    uint8_t* data = c->h_door_data.as<uint8_t>();
+    memcpy(data, src, n);
+    b->op = DOOR_XOR;
+    b->len = n;
+    b->key = key;
+    b->phase = phase;
+    if (door_call(c) != HVWS_OK) hvws::fatal("k_door");
+    memcpy(dst, data, n);
+    return true;
+}
+
 // ------------------------------------------- registered pinned host memory
 // Ranges the device can read and write in place (hvws_host_alloc,
 // hvws_host_register).  hvws_rx_reads looks every read up here; a
@@ -1414,6 +1599,7 @@ hvws_ctx* hvws_ctx_create(int device) {
 void hvws_ctx_destroy(hvws_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
+    door_release(c);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->sstream) hipStreamSynchronize(c->sstream);
     for (tset& t : c->ts) {
@@ -2106,6 +2292,33 @@ uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {
     return old;
 }
 
+int hvws_set_door(hvws_ctx* c, int on) {
+    if (!c) c = hvws::thread_ctx();
+    const int old = door_on(c) ? 1 : 0;
+    if (on == 0 && c->door_live) {
+        hipSetDevice(c->device);
+        door_park(c);
+    }
+    c->door_mode = on < 0 ? -1 : (on ? 1 : 0);
+    return old;
+}
+
+uint64_t hvws_set_door_idle_us(uint64_t us) {
+    const uint64_t old = door_idle_us();
+    g_door_idle_us.store(us ? us : 20000, std::memory_order_relaxed);
+    return old;
+}
+
+int hvws_door_stats(hvws_ctx* c, uint64_t out[4]) {
+    if (!c) c = hvws::thread_ctx();
+    if (!out) return set_err(HVWS_EINVAL, "null output");
+    out[0] = c->door_launches;
+    out[1] = c->door_calls;
+    out[2] = c->h_door.p ? __atomic_load_n(&c->h_door.as<ddoor>()->served, __ATOMIC_ACQUIRE) : 0;
+    out[3] = c->door_live ? 1 : 0;
+    return HVWS_OK;
+}
+
 uint64_t hvws_set_small_batch_limit(hvws_ctx* c, uint64_t bytes) {
     if (!c) c = hvws::thread_ctx();   // the calling thread's reference-API context
     const uint64_t old = c->small_limit ? c->small_limit : kSmallBatch;
@@ -2215,8 +2428,21 @@ namespace hvws {
     abort();
 }
 
+// Parks the thread context's resident worker when the thread exits (the
+// context itself lives on until hvws_thread_release, as before).
+struct thread_door_guard {
+    ~thread_door_guard() {
+        if (t_ctx && t_ctx->door_live) {
+            hipSetDevice(t_ctx->device);
+            door_park(t_ctx);
+        }
+    }
+};
+thread_local thread_door_guard t_door_guard;
+
 hvws_ctx* thread_ctx() {
     if (t_ctx) return t_ctx;
+    (void)&t_door_guard;
     int dev = t_device;
     if (dev < 0) {
         const char* e = getenv("HVWS_DEVICE");
@@ -2267,6 +2493,7 @@ void gpu_xor_host(char* dst, const char* src, size_t n, uint32_t key, uint32_t p
     if (n == 0) return;
     hvws_ctx* c = thread_ctx();
     if (hipSetDevice(c->device) != hipSuccess) fatal("hipSetDevice");
+    if (door_xor(c, dst, src, n, key, phase)) return;
     if (c->xor_stage.ensure(n + 64) != hipSuccess) fatal("device staging allocation");
     uint8_t* d = c->xor_stage.as<uint8_t>();
     if (hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
@@ -2283,6 +2510,8 @@ void gpu_xor_host(char* dst, const char* src, size_t n, uint32_t key, uint32_t p
 void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
               websocket_parser& carry_out, int& started) {
     hvws_ctx* c = thread_ctx();
+    if (hipSetDevice(c->device) != hipSuccess) fatal("hipSetDevice");
+    if (door_feed(c, buf, len, carry, unmask, frames, carry_out, started)) return;
     hvws_segment seg = {0, (uint64_t)len};
     websocket_parser cin;
     copy_parser(cin, carry);

@@ -277,6 +277,48 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
                         drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
                         uint32_t stage_lds, uint64_t* h_done, uint64_t seq, hipStream_t st,
                         hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// Resident small-path worker ("door", k_door): one workgroup that stays on
+// the device between calls and takes one request at a time from a mailbox in
+// fine-grained pinned host memory, so a reference-API call (FeedRecvData,
+// websocket_parser_execute, websocket_decode, a masked websocket_build_frame)
+// pays neither a launch nor a dispatch.  The host writes the request fields,
+// then `seq` (release); the worker serves it and publishes `done = seq`
+// (system-scope release) after its results.  A worker idle for idle_ticks of
+// the 100 MHz realtime clock parks itself (alive = 0, after one last look at
+// seq) and the next request relaunches it.
+enum : uint32_t { DOOR_FEED = 1u, DOOR_XOR = 2u, DOOR_EXIT = 3u };
+constexpr uint32_t kDoorThreads = 256;              // 4 waves: staging and XOR in parallel, walk on wave 0
+constexpr uint64_t kDoorMax = 32ull << 10;          // largest request (bytes)
+constexpr uint64_t kDoorRecords = kDoorMax / 2 + 3; // records a kDoorMax segment can hold
+struct ddoor {
+    // host -> device (written before seq)
+    uint64_t seq;
+    uint32_t op;
+    uint32_t unmask;
+    uint64_t len;
+    uint32_t vmask;
+    uint32_t key;       // DOOR_XOR: mask word (mask[0] in bits 0-7)
+    uint32_t phase;     // DOOR_XOR: mask_offset of the first byte
+    uint32_t pad0;
+    dcarry   carry;     // DOOR_FEED: carry in
+    uint64_t pad1[5];
+    // device -> host (own cache lines; `done` written last)
+    uint64_t done;      // seq of the last request served
+    uint64_t alive;     // 1 while a worker runs (0 once it parked)
+    uint64_t count;     // DOOR_FEED: records written
+    uint64_t served;    // requests served by this worker (diagnostic)
+    dcarry   out;       // DOOR_FEED: carry out
+    uint64_t pad2[2];
+};
+static_assert(sizeof(dcarry) == 48, "dcarry layout");
+static_assert(offsetof(ddoor, done) == 128, "ddoor: device fields on their own lines");
+static_assert(offsetof(ddoor, carry) == 40 && offsetof(ddoor, len) == 16 && offsetof(ddoor, vmask) == 24,
+              "k_door reads the request as words 1-10");
+// data: kDoorMax + 64 bytes (pinned, 256-aligned); h_rec: kDoorRecords records
+// (pinned); d_slot: kDoorRecords records (device) for records past the LDS area.
+hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uint64_t idle_ticks, uint64_t first_seq,
+                       hipStream_t st);
+
 // Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
 // copy_width() threads (the caller included; serial when another caller
 // holds the pool); par_memcpy splits copies of >= kParCopyMin bytes.

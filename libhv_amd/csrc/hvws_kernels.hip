@@ -967,6 +967,212 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ k_door
+//
+// The resident small-path worker (ddoor, hvws_internal.h): one workgroup of
+// kDoorThreads threads that stays on the device between reference-API calls.
+// Thread 0 polls the mailbox in fine-grained host memory (one relaxed
+// system-scope load, then s_sleep -- no fence per poll); on a new request
+// every wave stages the request's bytes into LDS (all loads in flight at once
+// across PCIe), wave 0 runs the carried-in frame, the walk and the tail (the
+// k_small device code), then every wave XORs its chunks chunk-major (each
+// chunk's mask from the records that overlap it, so no two threads write one
+// chunk) and stores the changed ones straight back into the mailbox's data
+// area; records, count and carry follow, each thread releases its stores at
+// system scope, and thread 0 publishes `done`.  A request costs no launch, no
+// dispatch and no end-of-kernel signal, and the segment's work is spread
+// over four waves instead of one.  Parking: idle for idle_ticks of the
+// 100 MHz realtime clock, the worker clears `alive`, takes one last look at
+// `seq` (serving a request that arrived meanwhile) and exits; the host
+// relaunches it on the next request once the stream shows it has ended.
+__global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, uint8_t* __restrict__ data,
+                                                       drec* __restrict__ h_rec, drec* __restrict__ d_slot,
+                                                       uint64_t idle_ticks, uint64_t first_seq) {
+    extern __shared__ u32x4 lds_door[];
+    __shared__ drec lrec[SMALL_LREC];
+    __shared__ uint64_t s_seq, s_len, s_n;
+    __shared__ uint32_t s_op, s_unmask, s_vmask, s_key, s_phase, s_exit;
+    __shared__ dcarry s_carry;
+    const uint32_t tid = threadIdx.x;
+    uint8_t* lds = reinterpret_cast<uint8_t*>(lds_door);
+    uint64_t last = first_seq;
+    uint64_t served = 0;
+    for (;;) {
+        if (tid == 0) {
+            uint64_t t0 = wall_clock64();
+            uint64_t s;
+            uint32_t ex = 0;
+            for (;;) {
+                s = __hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (s != last) break;
+                if (wall_clock64() - t0 > idle_ticks) {
+                    __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __threadfence_system();
+                    s = __hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (s != last) {   // arrived while parking: serve it
+                        __hip_atomic_store(&box->alive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                    ex = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_exit = ex;
+            s_seq = s;
+            if (!ex) {
+                // The request fields were written before seq.  Read with
+                // system-scope loads (vector memory, no cache can hold a
+                // previous request's values); the acquire also invalidates
+                // this CU's L1 and the L2 for the data the waves load next.
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                const uint64_t* w = reinterpret_cast<const uint64_t*>(box);
+                uint64_t q[11];
+#pragma unroll
+                for (int i = 0; i < 11; ++i) q[i] = __hip_atomic_load(w + 1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s_op = (uint32_t)q[0];
+                s_unmask = (uint32_t)(q[0] >> 32);
+                s_len = q[1] < kDoorMax ? q[1] : kDoorMax;
+                s_vmask = (uint32_t)q[2];
+                s_key = (uint32_t)(q[2] >> 32);
+                s_phase = (uint32_t)q[3];
+                dcarry cin;
+                memcpy(&cin, &q[4], sizeof(dcarry));
+                s_carry = cin;
+            }
+        }
+        __syncthreads();
+        if (s_exit) return;
+        const uint64_t seq = s_seq;
+        const uint32_t op = s_op;
+        if (op == DOOR_EXIT) {
+            if (tid == 0) {
+                __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+                __hip_atomic_store(&box->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
+        const uint64_t L = s_len;
+        const uint64_t nch = (L + 15u) / 16u;   // the data area has slack past L: whole chunks throughout
+        if (op == DOOR_XOR) {
+            // websocket_decode over the data area (16-byte aligned): byte i
+            // uses mask[(i + phase) & 3]
+            const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
+            const u32x4 k4 = u32x4{kw, kw, kw, kw};
+            constexpr int XB = (int)(kDoorMax / 16u / kDoorThreads);
+            u32x4 v[XB];
+#pragma unroll
+            for (int u = 0; u < XB; ++u) {
+                const uint64_t c = (uint64_t)u * kDoorThreads + tid;
+                if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
+            }
+#pragma unroll
+            for (int u = 0; u < XB; ++u) {
+                const uint64_t c = (uint64_t)u * kDoorThreads + tid;
+                if (c < nch) *reinterpret_cast<u32x4*>(data + c * 16u) = v[u] ^ k4;
+            }
+        } else {
+            // stage the segment in LDS: every chunk's load in flight at once
+            {
+                constexpr int SB = (int)(kDoorMax / 16u / kDoorThreads);
+                u32x4 v[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const uint64_t c = (uint64_t)u * kDoorThreads + tid;
+                    if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const uint64_t c = (uint64_t)u * kDoorThreads + tid;
+                    if (c < nch) *reinterpret_cast<u32x4*>(lds + c * 16u) = v[u];
+                }
+            }
+            __syncthreads();
+            if (tid < 64) {   // wave 0: carried-in frame, walk, tail (k_small's code)
+                dcarry st = s_carry;
+                st.started = 0;
+                uint64_t pos = 0, n = 0;
+                const uint32_t vmask = s_vmask;
+                auto emit = [&](uint64_t idx, const frec& v) {
+                    drec o;
+                    o.hdr_off = v.hdr_off;
+                    o.pay_off = v.pay_off;
+                    o.pay_len = v.pay_len;
+                    o.length = v.length;
+                    o.key = v.key;
+                    o.info = v.info;
+                    if (idx < SMALL_LREC) lrec[idx] = o;
+                    else d_slot[idx] = o;
+                };
+                if (st.state != S_START) {
+                    frec r;
+                    if (scalar_frame(lds, L, st, pos, r, vmask)) {
+                        if (tid == 0) emit(0, r);
+                        n = 1;
+                    }
+                }
+                walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
+                if (tid == 0) {
+                    s_n = n;
+                    s_carry = st;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            const uint64_t n = s_n;
+            auto rec = [&](uint64_t i) -> drec { return i < SMALL_LREC ? lrec[i] : d_slot[i]; };
+            if (s_unmask && n) {
+                for (uint64_t c = (uint64_t)tid * 16u; c < L; c += (uint64_t)kDoorThreads * 16u) {
+                    uint64_t k = 0, k_end = n;   // first record whose payload ends after c
+                    while (k < k_end) {
+                        const uint64_t mid = (k + k_end) >> 1;
+                        const drec m = rec(mid);
+                        if (m.pay_off + m.pay_len > c) k_end = mid;
+                        else k = mid + 1;
+                    }
+                    uint64_t mlo = 0, mhi = 0;
+                    for (; k < n; ++k) {
+                        const drec f = rec(k);
+                        if (f.pay_off >= c + 16) break;
+                        if (!(f.info & F_MASK) || f.pay_len == 0) continue;
+                        const uint32_t phase = (f.info >> 8) & 3u;
+                        const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + c - f.pay_off) & 3u));
+                        const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                        const int64_t a = (int64_t)(f.pay_off > c ? f.pay_off - c : 0);
+                        const uint64_t pe = f.pay_off + f.pay_len;
+                        const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
+                        mlo |= kk & byte_range(a, e);
+                        mhi |= kk & byte_range(a - 8, e - 8);
+                        if (e == 16) break;   // this payload runs past the chunk
+                    }
+                    if (!(mlo | mhi)) continue;   // no masked byte here: the data area already holds it
+                    const u32x4 m4 = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+                    *reinterpret_cast<u32x4*>(data + c) = *reinterpret_cast<const u32x4*>(lds + c) ^ m4;
+                }
+            }
+            for (uint64_t i = tid; i < n; i += kDoorThreads) h_rec[i] = rec(i);
+            if (tid == 0) {
+                box->count = n;
+                box->out = s_carry;
+                box->served = ++served;
+            }
+        }
+        // every thread's stores reach host memory before `done` says so
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(&box->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = seq;
+    }
+}
+
+hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uint64_t idle_ticks, uint64_t first_seq,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 16, st, box, data, h_rec, d_slot, idle_ticks,
+                       first_seq);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------- k_offsets
 // Exclusive scan of counts[0..nseg) into bases[], total into *total.  One
 // block of 1024 threads; each thread owns a contiguous run.
