@@ -1,6 +1,6 @@
-"""Which operation on a c3-sized rx buffer keeps hipFree from returning its
-memory?  For each operation: allocate, build the batch, run it, free with
-hipFree directly (its return code printed) and read hipMemGetInfo."""
+"""Does hvws_dev_free return a c3-sized rx buffer after each kind of
+operation?  (Before the empty-launch fix, hipFree after hvws_digest or
+hvws_step left the 68.7 GB allocated.)"""
 import ctypes
 import os
 import sys
@@ -38,10 +38,8 @@ for name, op in ops.items():
     eng.synth(rx, plan.total, plan.seed, dp, 0)
     op(rx)
     eng.sync()
-    hip.hipDeviceSynchronize()
-    rc = hip.hipFree(ctypes.c_void_p(rx.ptr))
-    rx.ptr = None
-    print(name, "hipFree", rc, hip.hipGetErrorString(rc).decode(), free_gb(), flush=True)
+    rx.free()   # hvws_dev_free
+    print(name, "freed", free_gb(), flush=True)
     if free_gb() < 150:
         print("stopping: memory held", flush=True)
         break
