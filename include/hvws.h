@@ -323,7 +323,7 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
  * are served by one workgroup (k_door) that stays on the device between
  * calls and takes requests from a mailbox in pinned host memory: no kernel
  * launch per call.  It runs on a stream of its own (its own hardware queue)
- * and parks itself after $HVWS_DOOR_IDLE_US (default 20000) without a
+ * and parks itself after $HVWS_DOOR_IDLE_US (default 5000) without a
  * request; the next call relaunches it.  Context teardown, thread exit and
  * process exit park it too.  on = 1 / 0 (off: each call launches k_small, or
  * the XOR kernel, as before), -1 = default ($HVWS_DOOR, on).  ctx NULL = the
@@ -334,8 +334,14 @@ int hvws_set_door(hvws_ctx* ctx, int on);
  * served, worker resident now} (tests, benchmarks). */
 int hvws_door_stats(hvws_ctx* ctx, uint64_t out[4]);
 /* Idle time after which workers launched from now on park (microseconds;
- * 0 = the default, 20000).  Returns the previous value. */
+ * 0 = the default, 5000).  Returns the previous value.  The runtime's frees
+ * (hipFree, hipHostFree) wait for every stream, a resident worker's too: the
+ * library parks the calling thread's own worker before each of its frees; a
+ * worker of another thread holds such a free up to its idle time. */
 uint64_t hvws_set_door_idle_us(uint64_t us);
+/* Diagnostics: 100 MHz device-clock stamps of the worker's last read request
+ * -- seen, staged, walked, XORed, records written (before the release). */
+int hvws_door_stamps(hvws_ctx* ctx, uint64_t out[8]);
 
 /* Small batches whose segments are all <= 32 KiB (total <= 1 MiB; an event
  * loop's reads) are read by the device straight from pinned host memory, each

@@ -42,13 +42,21 @@ int set_err(int code, const char* fmt, ...) {
                            __LINE__);                                                   \
     } while (0)
 
+// The runtime's frees (hipFree, hipHostFree) wait for every stream of the
+// device -- a resident k_door worker's too, until it parks.  Every free here
+// first parks the calling thread's own worker (defined with the worker).
+void door_park_self();
+
 // Grow-only device allocation.
 struct dbuf {
     void* p = nullptr;
     uint64_t cap = 0;
     hipError_t ensure(uint64_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
-        if (p) hipFree(p);
+        if (p) {
+            door_park_self();
+            hipFree(p);
+        }
         p = nullptr;
         cap = 0;
         uint64_t want = std::max<uint64_t>(bytes + bytes / 2, 4096);
@@ -57,7 +65,10 @@ struct dbuf {
         return e;
     }
     void release() {
-        if (p) hipFree(p);
+        if (p) {
+            door_park_self();
+            hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -72,7 +83,10 @@ struct hbuf {   // grow-only pinned host allocation
     unsigned flags = hipHostMallocDefault;   // hipHostMallocCoherent: device reads/writes bypass its caches
     hipError_t ensure(uint64_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
-        if (p) hipHostFree(p);
+        if (p) {
+            door_park_self();
+            hipHostFree(p);
+        }
         p = nullptr;
         dev = nullptr;
         cap = 0;
@@ -82,7 +96,10 @@ struct hbuf {   // grow-only pinned host allocation
         return e;
     }
     void release() {
-        if (p) hipHostFree(p);
+        if (p) {
+            door_park_self();
+            hipHostFree(p);
+        }
         p = nullptr;
         dev = nullptr;
         cap = 0;
@@ -1288,7 +1305,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
 // from a mailbox in fine-grained pinned memory: no launch, no dispatch and no
 // end-of-kernel signal per call.
 
-// Idle time after which a worker parks ($HVWS_DOOR_IDLE_US, default 20 ms),
+// Idle time after which a worker parks ($HVWS_DOOR_IDLE_US, default 5 ms),
 // in ticks of the 100 MHz realtime clock.
 std::atomic<uint64_t> g_door_idle_us{0};   // 0: not yet read from the environment
 
@@ -1296,7 +1313,7 @@ uint64_t door_idle_us() {
     uint64_t us = g_door_idle_us.load(std::memory_order_relaxed);
     if (!us) {
         const char* e = getenv("HVWS_DOOR_IDLE_US");
-        us = e && strtoull(e, nullptr, 0) ? strtoull(e, nullptr, 0) : 20000;
+        us = e && strtoull(e, nullptr, 0) ? strtoull(e, nullptr, 0) : 5000;
         g_door_idle_us.store(us, std::memory_order_relaxed);
     }
     return us;
@@ -1397,6 +1414,18 @@ void door_park(hvws_ctx* c) {
     if (door_call(c) != HVWS_OK) (void)hipGetLastError();
     hipStreamSynchronize(c->door_stream);
     c->door_live = false;
+}
+
+// The calling thread's context for the reference-API entry points.
+thread_local int t_device = -1;
+thread_local hvws_ctx* t_ctx = nullptr;
+
+void door_park_self() {
+    hvws_ctx* c = t_ctx;
+    if (c && c->door_live) {
+        hipSetDevice(c->device);
+        door_park(c);
+    }
 }
 
 void door_release(hvws_ctx* c) {
@@ -1517,9 +1546,6 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     HIP_OR(issue_unmask(c, d_rx, rx_len), HVWS_EHIP);
     return HVWS_OK;
 }
-
-thread_local int t_device = -1;
-thread_local hvws_ctx* t_ctx = nullptr;
 
 void stall_fn(void* usec) { usleep((useconds_t)(uintptr_t)usec); }
 
@@ -1664,8 +1690,15 @@ void* hvws_dev_alloc(hvws_ctx* c, uint64_t bytes) {
 
 void hvws_dev_free(hvws_ctx* c, void* p) {
     if (!c || !p) return;
+    door_park_self();
     hipSetDevice(c->device);
+    // The runtime holds the buffers of the last kernel dispatched on a stream
+    // until the next dispatch there: without an empty launch on each of the
+    // context's compute streams, a freed 68.7 GB batch stayed allocated.
+    for (hipStream_t s : {c->stream, c->sstream})
+        if (s && launch_noop(s) != hipSuccess) (void)hipGetLastError();
     hipStreamSynchronize(c->stream);
+    if (c->sstream) hipStreamSynchronize(c->sstream);
     hipFree(p);
 }
 
@@ -1683,6 +1716,7 @@ void* hvws_host_alloc(hvws_ctx* c, uint64_t bytes) {
 
 void hvws_host_free(hvws_ctx* c, void* p) {
     if (!c || !p) return;
+    door_park_self();
     hipSetDevice(c->device);
     pin_remove(p);
     hipHostFree(p);
@@ -1707,6 +1741,7 @@ int hvws_host_unregister(hvws_ctx* c, void* p) {
     if (rc) return rc;
     const pinned_range r = pin_remove(p);
     if (!r.lo || !r.registered) return set_err(HVWS_EINVAL, "not a range from hvws_host_register");
+    door_park_self();
     HIP_OR(hipHostUnregister(p), HVWS_EHIP);
     return HVWS_OK;
 }
@@ -2303,9 +2338,17 @@ int hvws_set_door(hvws_ctx* c, int on) {
     return old;
 }
 
+int hvws_door_stamps(hvws_ctx* c, uint64_t out[8]) {
+    if (!c) c = hvws::thread_ctx();
+    if (!out) return set_err(HVWS_EINVAL, "null output");
+    memset(out, 0, 8 * sizeof(uint64_t));
+    if (c->h_door.p) memcpy(out, c->h_door.as<ddoor>()->stamp, 8 * sizeof(uint64_t));
+    return HVWS_OK;
+}
+
 uint64_t hvws_set_door_idle_us(uint64_t us) {
     const uint64_t old = door_idle_us();
-    g_door_idle_us.store(us ? us : 20000, std::memory_order_relaxed);
+    g_door_idle_us.store(us ? us : 5000, std::memory_order_relaxed);
     return old;
 }
 

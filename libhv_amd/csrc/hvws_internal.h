@@ -309,6 +309,10 @@ struct ddoor {
     uint64_t served;    // requests served by this worker (diagnostic)
     dcarry   out;       // DOOR_FEED: carry out
     uint64_t pad2[2];
+    // realtime-clock stamps of the last request (100 MHz): seen, staged,
+    // walked, xored, stored (before the release), and the sum of ticks spent
+    // polling; read by hvws_door_stats' diagnostics
+    uint64_t stamp[8];
 };
 static_assert(sizeof(dcarry) == 48, "dcarry layout");
 static_assert(offsetof(ddoor, done) == 128, "ddoor: device fields on their own lines");
@@ -352,6 +356,7 @@ hipError_t launch_unmask_tiles(const uint64_t* off, const uint64_t* len, const u
                                uint64_t tile, uint64_t rx_len, hipStream_t st);
 hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st);
 hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st);
+hipError_t launch_noop(hipStream_t st);   // see hvws_dev_free
 
 // Synthetic data (hvws_synth.hip).
 hipError_t launch_synth(uint8_t* buf, uint64_t buf_len, uint64_t seed, uint64_t nframes,

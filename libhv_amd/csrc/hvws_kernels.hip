@@ -997,6 +997,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
     uint8_t* lds = reinterpret_cast<uint8_t*>(lds_door);
     uint64_t last = first_seq;
     uint64_t served = 0;
+    __shared__ uint64_t s_t[6];
     for (;;) {
         if (tid == 0) {
             uint64_t t0 = wall_clock64();
@@ -1020,6 +1021,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             }
             s_exit = ex;
             s_seq = s;
+            s_t[0] = wall_clock64();
             if (!ex) {
                 // The request fields were written before seq.  Read with
                 // system-scope loads (vector memory, no cache can hold a
@@ -1089,6 +1091,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                 }
             }
             __syncthreads();
+            if (tid == 0) s_t[1] = wall_clock64();
             if (tid < 64) {   // wave 0: carried-in frame, walk, tail (k_small's code)
                 dcarry st = s_carry;
                 st.started = 0;
@@ -1120,6 +1123,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             }
             __threadfence_block();
             __syncthreads();
+            if (tid == 0) s_t[2] = wall_clock64();
             const uint64_t n = s_n;
             auto rec = [&](uint64_t i) -> drec { return i < SMALL_LREC ? lrec[i] : d_slot[i]; };
             if (s_unmask && n) {
@@ -1151,11 +1155,17 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                     *reinterpret_cast<u32x4*>(data + c) = *reinterpret_cast<const u32x4*>(lds + c) ^ m4;
                 }
             }
+            if (tid == 0) s_t[3] = wall_clock64();
             for (uint64_t i = tid; i < n; i += kDoorThreads) h_rec[i] = rec(i);
             if (tid == 0) {
                 box->count = n;
                 box->out = s_carry;
                 box->served = ++served;
+                box->stamp[0] = s_t[0];
+                box->stamp[1] = s_t[1];
+                box->stamp[2] = s_t[2];
+                box->stamp[3] = s_t[3];
+                box->stamp[4] = wall_clock64();
             }
         }
         // every thread's stores reach host memory before `done` says so
@@ -2206,6 +2216,18 @@ hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t patte
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// An empty launch: the HIP runtime keeps the buffers named by the last kernel
+// dispatched on a stream referenced until another kernel is dispatched there,
+// so hipFree of such a buffer does not return its memory (profiles/r3c_raw:
+// 68.7 GB held after hvws_digest / hvws_step).  hvws_dev_free issues one on
+// each of the context's streams first.
+__global__ void k_noop() {}
+
+hipError_t launch_noop(hipStream_t st) {
+    hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, st);
+    return hipGetLastError();
 }
 
 hipError_t launch_xor_span(uint8_t* d, uint64_t n, uint32_t key, uint32_t phase, hipStream_t st) {

@@ -1,0 +1,47 @@
+"""Where a FeedRecvData read spends its time on the resident worker: device
+stamps (100 MHz realtime clock) of each 8 KiB read -- request seen -> staged
+-> walked -> XORed -> records written -- against the host's wall time per
+call.  Medians over n reads."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import libhv_amd  # noqa: E402
+from libhv_amd import synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+L = libhv_amd.lib()
+with libhv_amd.Engine(0) as eng:
+    fp = synth.uniform_plan(n * 8 + 16, 1024, 5)
+    dp = libhv_amd.DevicePlan(eng, fp)
+    b = eng.alloc(fp.total + 64)
+    eng.synth(b, fp.total, fp.seed, dp, 0)
+    data = b.download(fp.total)
+    b.free()
+    dp.free()
+buf = ctypes.create_string_buffer(data.tobytes(), len(data))
+L.hvws_set_door(None, 1)
+h = L.hvws_wsp_new()
+st = (ctypes.c_uint64 * 8)()
+rows, wall = [], []
+for i in range(n):
+    t = time.perf_counter()
+    r = L.hvws_wsp_feed(h, ctypes.addressof(buf) + i * 8192, 8192)
+    wall.append(time.perf_counter() - t)
+    assert r == 8192
+    L.hvws_door_stamps(None, st)
+    rows.append(list(st[:5]))
+rows = np.array(rows[n // 10:], dtype=np.float64)
+d = np.diff(rows, axis=1) * 10.0 / 1000.0   # ticks of 10 ns -> us
+out = {"reads": n, "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
+       "device_us_median": {k: round(float(np.median(d[:, i])), 2)
+                            for i, k in enumerate(["stage", "walk", "xor_and_stores", "records"])},
+       "device_us_total_median": round(float(np.median((rows[:, 4] - rows[:, 0]) * 0.01)), 2)}
+print(json.dumps(out))
+L.hvws_wsp_free(h)

@@ -27,6 +27,27 @@ pytestmark = pytest.mark.gpu
 GOLD = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs.json")))
 
 
+_RX = {}
+
+
+def _rx(eng, nbytes):
+    """One device buffer per size, reused by every test of this module: the
+    driver clears freed VRAM in the background, so freeing and reallocating a
+    68.7 GB batch per test ran out of memory by the third c3-sized test."""
+    b = _RX.get(nbytes)
+    if b is None or b.eng is not eng:
+        b = _RX[nbytes] = eng.alloc(nbytes)
+    return b
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _free_buffers():
+    yield
+    for b in _RX.values():
+        b.free()
+    _RX.clear()
+
+
 def _run(eng, plan, nseg, golden=None, sieve=None, path2=None):
     """sieve: assert the frame sieve's chain covered every frame (one segment);
     path2: the HVWS_PATH_* the second step must take."""
@@ -35,7 +56,7 @@ def _run(eng, plan, nseg, golden=None, sieve=None, path2=None):
         L.hvws_set_sieve_min(0)   # default threshold; contexts forget "uniform, skip the sieve"
     plan.split(nseg)
     dp = libhv_amd.DevicePlan(eng, plan)
-    rx = eng.alloc(plan.total + 64)
+    rx = _rx(eng, plan.total + 64)
     try:
         eng.synth(rx, plan.total, plan.seed, dp, 0)
         if golden:
@@ -59,7 +80,6 @@ def _run(eng, plan, nseg, golden=None, sieve=None, path2=None):
             assert L.hvws_last_scan_path(eng.ctx) == path2
     finally:
         dp.free()
-        rx.free()
 
 
 @pytest.mark.parametrize("nseg", [1, 4096])
