@@ -237,9 +237,27 @@ enum {
     HVWS_PATH_SPEC = 3,             /* speculative table checked exact on the device */
     HVWS_PATH_SPEC_FAILED = 4,      /* speculation rejected by the check, then COUNT/EMIT */
     HVWS_PATH_SLACK = 5,            /* mixed sizes: one EMIT walk into per-segment regions, compacted on the device */
-    HVWS_PATH_SLACK_FAILED = 6      /* a segment outgrew its region, then COUNT/EMIT */
+    HVWS_PATH_SLACK_FAILED = 6,     /* a segment outgrew its region, then COUNT/EMIT */
+    HVWS_PATH_FUSED = 7             /* uniform segments discovered inside the unmask pass (hvws_set_fused) */
 };
 int hvws_last_scan_path(hvws_ctx* ctx);
+
+/* FUSED steps (hvws_step / hvws_step_resident): once the last exact scan of
+ * a multi-segment batch found every segment uniform (the SPEC estimates held)
+ * and frames average <= 16 KiB, discovery runs inside the unmask pass: each
+ * segment's first whole frame sets the size every later frame is checked
+ * against while its payload is unmasked.  The verdict comes when that pass
+ * ends; hvws_step_resident reads it during the next call (or any other call
+ * on the context -- every entry point settles a pending batch first), so its
+ * frames, carries and bytes are as the contract says whenever they can be
+ * observed.  A batch whose frames did not all have that size is undone (the
+ * pass again, XOR being its own inverse) and re-run on the exact path; so is
+ * a batch queued behind it.  mode: 2 when the last scan says uniform (the
+ * default), 0 off, 1 try on every step (tests), -1 back to $HVWS_FUSED (or 2).
+ * Returns the previous mode. */
+int hvws_set_fused(hvws_ctx* ctx, int mode);
+/* out = {fused steps issued, batches re-run on the exact path}. */
+int hvws_fused_stats(hvws_ctx* ctx, uint64_t out[2]);
 
 /* Device span of a timed region: hvws_span_begin records a marker on each of
  * the context's compute streams, hvws_span_end records the end markers, waits

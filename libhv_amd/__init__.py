@@ -185,6 +185,8 @@ _SIGS = {
     "hvws_door_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_door_idle_us": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_door_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_set_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hvws_fused_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_set_small_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),

@@ -126,6 +126,7 @@ struct tset {
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first, tile_key, tile_kind;
     dbuf pbar;   // grid-barrier words of the one-launch scan (k_pscan)
+    dbuf f_fmid, f_done, f_ctl, f_wgseg, f_segs, f_carry;   // FUSED path (k_fprep / k_fused)
     uint64_t frame_cap = 0;
     hipEvent_t free_ev = nullptr;   // recorded after the last kernel reading the set (pipelined steps)
     hipEvent_t free_wait = nullptr; // what the next scan into the set waits for: free_ev, or the stop
@@ -134,7 +135,8 @@ struct tset {
     void release() {
         for (dbuf* b : {&carry_out, &counts, &bases, &total, &sc_mid, &sc_npred, &sc_pbase, &sc_fail, &sc_masked,
                         &sc_total, &sc_est, &f_hdr, &f_off, &f_len, &f_length, &f_key, &f_keyrot, &f_info,
-                        &tile_first, &tile_key, &tile_kind, &pbar})
+                        &tile_first, &tile_key, &tile_kind, &pbar, &f_fmid, &f_done, &f_ctl, &f_wgseg, &f_segs,
+                        &f_carry})
             b->release();
         frame_cap = 0;
     }
@@ -264,6 +266,26 @@ struct hvws_ctx {
     uint64_t door_seq = 0;      // last request number posted
     int door_mode = -1;         // hvws_set_door: -1 default ($HVWS_DOOR, on), 0 off, 1 on
     uint64_t door_launches = 0, door_calls = 0;
+    // FUSED path: the batch issued into each table set and not yet settled
+    // (its verdict read; fixed on the exact path if it failed), the verdict
+    // slots (one per set: a later batch must not overwrite an unread one) and
+    // the gate word the next k_fused reads
+    struct fused_pend {
+        bool active = false;
+        uint64_t seq = 0, nwg = 0;
+        uint8_t* rx = nullptr;
+        uint64_t rx_len = 0;
+        bool piped = false;
+        std::vector<hvws_segment> segs;
+        std::vector<websocket_parser> carry;
+        bool has_carry = false;
+    } fz[2];
+    hbuf h_fstatus;
+    dbuf fz_gate;
+    int fused_mode = -1;        // hvws_set_fused: -1 default ($HVWS_FUSED, on), 0 off, 1 always try
+    bool fz_busy = false;       // inside a fused issue or settle (no nested settling)
+    uint64_t fused_steps = 0, fused_fixes = 0;
+    uint64_t fz_nfr = 0;        // records of the last batch whose count is known (sizes the next table)
     // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
     // on both of the context's compute streams
     hipEvent_t span_ev[4] = {};
@@ -356,9 +378,14 @@ void from_dcarry(const dcarry& d, websocket_parser& p) {
     reinterpret_cast<uint8_t*>(&p)[kViolByte] = (uint8_t)d.viol;
 }
 
-int check_ctx(hvws_ctx* c) {
+int fused_settle_all(hvws_ctx* c);
+
+// Every entry point: a fused batch still pending is settled first (its bytes,
+// frames and carries are final afterwards).
+int check_ctx(hvws_ctx* c, bool settle = true) {
     if (!c) return set_err(HVWS_EINVAL, "null context");
     HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
+    if (settle && !c->fz_busy && (c->fz[0].active || c->fz[1].active)) return fused_settle_all(c);
     return HVWS_OK;
 }
 
@@ -1349,7 +1376,12 @@ int door_ensure(hvws_ctx* c) {
     std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0u);
     for (int i = 0; i < prop.multiProcessorCount; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
     HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
-    c->h_door.flags = c->h_door_data.flags = c->h_door_rec.flags = hipHostMallocCoherent;
+    // The mailbox is fine-grained (polled, uncached); the data and record
+    // areas are ordinary pinned memory: the worker's system-scope acquire on
+    // each request invalidates its caches before it stages the bytes, and its
+    // release writes its results back.  (Fine-grained data made the staging
+    // loads of an 8 KiB read take 6.2 us, profiles/r3f_raw.)
+    c->h_door.flags = hipHostMallocCoherent;
     HIP_OR(c->h_door.ensure(sizeof(ddoor)), HVWS_ENOMEM);
     HIP_OR(c->h_door_data.ensure(kDoorMax + 256), HVWS_ENOMEM);
     HIP_OR(c->h_door_rec.ensure(kDoorRecords * sizeof(drec)), HVWS_ENOMEM);
@@ -1547,6 +1579,273 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     return HVWS_OK;
 }
 
+// ------------------------------------------------------------- FUSED path
+// (k_fprep / k_fwgseg / k_fused, hvws_kernels.hip.)  Batches of uniform
+// segments of small frames, once the last exact scan found the estimates
+// holding: discovery happens inside the unmask pass.  The verdict arrives
+// when that pass ends, so it is read lazily: a pipelined step settles the
+// previous batch (its pass ends while this batch's prep runs beside it); every
+// other entry point settles whatever is pending first (check_ctx).  A failed
+// batch is undone by the same kernel in undo mode and re-run on the exact
+// path; a batch issued behind it saw the gate and did nothing, and is re-run
+// exactly too.
+constexpr int HVWS_PATH_FUSED_INTERNAL = 7;
+
+// 0 off, 1 on every step, 2 when the last scan says uniform ($HVWS_FUSED for -1; default 2)
+int fused_mode(hvws_ctx* c) {
+    if (c->fused_mode >= 0) return c->fused_mode;
+    static const int env = getenv("HVWS_FUSED") ? atoi(getenv("HVWS_FUSED")) : 2;
+    return env < 0 ? 2 : (env > 2 ? 2 : env);
+}
+
+bool fused_eligible(hvws_ctx* c, uint64_t rx_len, uint32_t nseg) {
+    const int mode = fused_mode(c);
+    if (mode == 0 || nseg == 0 || c->vmask) return false;
+    if (c->nfr_known) c->fz_nfr = c->nfr;   // the last exact count (a pending fused batch has none yet)
+    if (mode == 1) return true;   // tests: whatever the last scan said
+    if (nseg < 2 || !c->spec_ok || c->fz_nfr == 0) return false;
+    // small frames only: at 64 KiB frames the separate scan is 0.6 % of a
+    // step and k_unmask's tile geometry is at the in-place ceiling
+    return rx_len / c->fz_nfr <= (16u << 10);
+}
+
+int fused_wait(hvws_ctx* c, int set, uint64_t seq, dspec_status& out) {
+    const dspec_status* st = c->h_fstatus.as<dspec_status>() + set;
+    for (uint64_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) {
+            out = *st;
+            return HVWS_OK;
+        }
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) {
+                    out = *st;
+                    return HVWS_OK;
+                }
+                return set_err(HVWS_EHIP, "fused pass did not publish (seq %llu)", (unsigned long long)seq);
+            }
+            if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "stream error: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint64_t seq, bool undo) {
+    tset& T = c->ts[set];
+    fused_args a;
+    a.rx = d_rx;
+    a.rx_len = rx_len;
+    a.segs = T.f_segs.as<dseg>();
+    a.fmid = T.f_fmid.as<dfmid>();
+    a.est = T.sc_est.as<uint64_t>();
+    a.bases = T.bases.as<uint64_t>();
+    a.total = T.total.as<uint64_t>();
+    a.first_fail = T.sc_fail.as<uint64_t>();
+    a.done_cnt = T.f_done.as<uint64_t>();
+    a.ctl = T.f_ctl.as<dfctl>();
+    a.wg_seg = T.f_wgseg.as<uint32_t>();
+    a.fr.hdr_off = T.f_hdr.as<int64_t>();
+    a.fr.pay_off = T.f_off.as<uint64_t>();
+    a.fr.pay_len = T.f_len.as<uint64_t>();
+    a.fr.length = T.f_length.as<uint64_t>();
+    a.fr.key = T.f_key.as<uint32_t>();
+    a.fr.keyrot = T.f_keyrot.as<uint32_t>();
+    a.fr.info = T.f_info.as<uint32_t>();
+    a.fr.cap = T.frame_cap;
+    a.carry_out = T.carry_out.as<dcarry>();
+    a.counts = T.counts.as<uint64_t>();
+    a.gate = c->fz_gate.as<uint64_t>();
+    a.status = mapped<dspec_status>(c->h_fstatus) + set;
+    a.seq = seq;
+    a.nseg = nseg;
+    a.vmask = c->vmask;
+    a.undo = undo ? 1u : 0u;
+    return a;
+}
+
+// The exact path for a batch (its own segment table and carries again).
+int exact_rerun(hvws_ctx* c, hvws_ctx::fused_pend& p) {
+    const uint32_t nseg = (uint32_t)p.segs.size();
+    int rc = upload_segments(c, p.segs.data(), p.has_carry ? p.carry.data() : nullptr, nseg, p.rx_len);
+    if (rc != HVWS_OK) return rc;
+    c->cs = c->stream;
+    bool unmasked = false;
+    if ((rc = scan_device_carry(c, p.rx, p.rx_len, nseg, p.rx, &unmasked)) != HVWS_OK) return rc;
+    return unmasked ? HVWS_OK : unmask_impl(c, p.rx, p.rx_len);
+}
+
+// Read the verdict of the batch pending in `set`; fix it (and the newer
+// batch, gated behind it) on the exact path if it failed.
+int fused_settle(hvws_ctx* c, int set) {
+    hvws_ctx::fused_pend& p = c->fz[set];
+    if (!p.active) return HVWS_OK;
+    const bool prev_busy = c->fz_busy;
+    c->fz_busy = true;
+    dspec_status v;
+    int rc = fused_wait(c, set, p.seq, v);
+    p.active = false;
+    if (rc == HVWS_OK && (v.flags & SPEC_OK) && !(v.flags & FUSED_GATED)) {
+        if (set == c->cur) {
+            c->nfr = v.total;
+            c->nfr_known = true;
+        }
+        c->fz_nfr = v.total;
+        c->fz_busy = prev_busy;
+        return HVWS_OK;
+    }
+    if (rc != HVWS_OK) {
+        c->fz_busy = prev_busy;
+        return rc;
+    }
+    // failed (or gated): undo what the pass XORed, clear the gate, re-run exactly
+    ++c->fused_fixes;
+    c->spec_ok = false;
+    hvws_ctx::fused_pend newer;
+    const int other = set ^ 1;
+    const bool has_newer = c->fz[other].active && set != c->cur;   // issued behind it, gated
+    if (has_newer) {
+        newer = c->fz[other];
+        c->fz[other].active = false;
+    }
+    if (!(v.flags & FUSED_UNTOUCHED)) {
+        const fused_args a = fused_args_of(c, set, p.rx, p.rx_len, (uint32_t)p.segs.size(), p.seq, true);
+        HIP_OR(launch_fused(a, p.nwg, c->stream), HVWS_EHIP);
+    }
+    HIP_OR(hipMemsetAsync(c->fz_gate.p, 0, 8, c->stream), HVWS_EHIP);
+    c->cur = set ^ 1;   // the exact scan takes the set after this one's (it flips)
+    rc = exact_rerun(c, p);
+    if (rc == HVWS_OK && has_newer) rc = exact_rerun(c, newer);
+    c->piped = false;   // the next pipelined step re-arms both sets' free events
+    c->fz_busy = prev_busy;
+    return rc;
+}
+
+int fused_settle_all(hvws_ctx* c) {
+    if (c->fz_busy) return HVWS_OK;
+    int rc = HVWS_OK;
+    // older first: the set that is not current
+    if (c->fz[c->cur ^ 1].active && (rc = fused_settle(c, c->cur ^ 1)) != HVWS_OK) return rc;
+    if (c->fz[c->cur].active && (rc = fused_settle(c, c->cur)) != HVWS_OK) return rc;
+    return HVWS_OK;
+}
+
+// Issue one batch on the FUSED path.  piped: its prep runs on the scan
+// stream beside the previous batch's pass, and the previous batch is settled
+// after this one is queued; else everything runs on the context stream and
+// the batch is settled before returning.
+int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+                const websocket_parser* carry_in, uint32_t nseg, bool piped) {
+    int rc;
+    c->fz_busy = true;
+    struct unbusy {
+        hvws_ctx* c;
+        ~unbusy() { c->fz_busy = false; }
+    } ub{c};
+    const int set = c->cur ^ 1;
+    if (c->fz[set].active && (rc = fused_settle(c, set)) != HVWS_OK) return rc;   // two batches ago (normally settled)
+    if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
+    c->prev_path = c->scan_path;
+    c->cur ^= 1;
+    tset& T = c->T();
+    hipStream_t ps = piped ? c->sstream : c->stream;
+    if (piped && T.free_pending) {
+        HIP_OR(hipStreamWaitEvent(ps, T.free_wait, 0), HVWS_EHIP);
+        T.free_pending = false;
+    }
+    // tables: the frame table holds the last count with room (the estimate
+    // must fit it, else the pass declines and the exact path runs)
+    const uint64_t want = std::max<uint64_t>({c->fz_nfr + c->fz_nfr / 8 + 64, c->ts[c->cur ^ 1].frame_cap, 1024});
+    HIP_OR(ensure_frames(c, want), HVWS_ENOMEM);
+    const uint64_t nwg = T.frame_cap / kFusedRecords + 1;
+    HIP_OR(T.counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(T.bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(T.total.ensure(8), HVWS_ENOMEM);
+    HIP_OR(T.carry_out.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    HIP_OR(T.sc_est.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(T.sc_fail.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(T.f_fmid.ensure((uint64_t)nseg * sizeof(dfmid) + 64), HVWS_ENOMEM);
+    HIP_OR(T.f_done.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
+    HIP_OR(T.f_ctl.ensure(sizeof(dfctl)), HVWS_ENOMEM);
+    HIP_OR(T.f_wgseg.ensure(nwg * 4 + 64), HVWS_ENOMEM);
+    HIP_OR(T.f_segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
+    HIP_OR(T.f_carry.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
+    c->h_fstatus.flags = hipHostMallocCoherent;
+    if (!c->h_fstatus.p) {
+        HIP_OR(c->h_fstatus.ensure(2 * sizeof(dspec_status)), HVWS_ENOMEM);
+        memset(c->h_fstatus.p, 0, 2 * sizeof(dspec_status));
+    }
+    if (!c->fz_gate.p) {
+        HIP_OR(c->fz_gate.ensure(64), HVWS_ENOMEM);
+        HIP_OR(hipMemsetAsync(c->fz_gate.p, 0, 64, c->stream), HVWS_EHIP);
+    }
+    if (!mapped<dspec_status>(c->h_fstatus)) return set_err(HVWS_EHIP, "fused status not device-mapped");
+    HIP_OR(begin_timed_scan(c, false), HVWS_EHIP);
+    HIP_OR(hipMemsetAsync(T.f_ctl.p, 0, sizeof(dfctl), ps), HVWS_EHIP);
+    HIP_OR(launch_fprep(d_rx, rx_len, c->up_src_segs, c->up_src_carry, T.f_segs.as<dseg>(), T.f_carry.as<dcarry>(),
+                        nseg, T.f_fmid.as<dfmid>(), T.sc_est.as<uint64_t>(), T.sc_fail.as<uint64_t>(),
+                        T.f_done.as<uint64_t>(), T.carry_out.as<dcarry>(), T.counts.as<uint64_t>(), T.f_ctl.as<dfctl>(),
+                        c->vmask, ps),
+           HVWS_EHIP);
+    if (c->up_slot >= 0) {   // the pinned upload slot is free once k_fprep has run
+        HIP_OR(hipEventRecord(c->up_ev[c->up_slot], ps), HVWS_EHIP);
+        c->up_pending[c->up_slot] = true;
+        c->up_slot = -1;
+    }
+    c->up_src_segs = nullptr;
+    c->up_src_carry = nullptr;
+    HIP_OR(launch_offsets(T.sc_est.as<uint64_t>(), T.bases.as<uint64_t>(), nseg, T.total.as<uint64_t>(), ps), HVWS_EHIP);
+    HIP_OR(launch_fwgseg(T.bases.as<uint64_t>(), T.sc_est.as<uint64_t>(), nseg, T.f_wgseg.as<uint32_t>(), nwg, ps),
+           HVWS_EHIP);
+    if (piped) {
+        HIP_OR(hipEventRecord(c->scan_done, ps), HVWS_EHIP);
+        HIP_OR(hipStreamWaitEvent(c->stream, c->scan_done, 0), HVWS_EHIP);
+    }
+    const uint64_t seq = ++c->scan_seq;
+    const fused_args a = fused_args_of(c, c->cur, d_rx, rx_len, nseg, seq, false);
+    const bool timed = step_events(c) >= 1;
+    HIP_OR(launch_fused(a, nwg, c->stream, timed ? c->tev[c->t_cur][2] : nullptr, timed ? c->tev[c->t_cur][3] : nullptr),
+           HVWS_EHIP);
+    if (timed) c->t_rec[c->t_cur] |= (uint8_t)(4u | 8u);
+    c->t_unmask[c->t_cur] = true;
+    if (piped) {   // the next prep into this set waits for this pass
+        if (timed) {
+            T.free_wait = c->tev[c->t_cur][3];
+        } else {
+            HIP_OR(hipEventRecord(T.free_ev, c->stream), HVWS_EHIP);
+            T.free_wait = T.free_ev;
+        }
+        T.free_pending = true;
+    }
+    hvws_ctx::fused_pend& p = c->fz[c->cur];
+    p.active = true;
+    p.seq = seq;
+    p.nwg = nwg;
+    p.rx = d_rx;
+    p.rx_len = rx_len;
+    p.piped = piped;
+    p.segs.assign(segs, segs + nseg);
+    p.has_carry = carry_in != nullptr;
+    if (carry_in) p.carry.assign(carry_in, carry_in + nseg);
+    else p.carry.clear();
+    ++c->fused_steps;
+    c->scan_path = HVWS_PATH_FUSED_INTERNAL;
+    c->nseg = nseg;
+    c->nfr_known = false;
+    c->rx = d_rx;
+    c->rx_len = rx_len;
+    c->have_scan = true;
+    c->hcache_valid = false;
+    // settle the previous batch (its pass ends while this batch's prep runs),
+    // or, serial, this one
+    if (piped) {
+        if (c->fz[c->cur ^ 1].active && (rc = fused_settle(c, c->cur ^ 1)) != HVWS_OK) return rc;
+    } else if ((rc = fused_settle(c, c->cur)) != HVWS_OK) {
+        return rc;
+    }
+    return HVWS_OK;
+}
+
 void stall_fn(void* usec) { usleep((useconds_t)(uintptr_t)usec); }
 
 }  // namespace
@@ -1626,6 +1925,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     door_release(c);
+    if (fused_settle_all(c) != HVWS_OK) (void)hipGetLastError();   // pending fused batches: bytes final first
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->sstream) hipStreamSynchronize(c->sstream);
     for (tset& t : c->ts) {
@@ -1666,6 +1966,8 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     for (auto& ev : c->span_ev)
         if (ev) hipEventDestroy(ev);
     c->h_status.release();
+    c->h_fstatus.release();
+    c->fz_gate.release();
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy_in) hipStreamDestroy(c->copy_in);
     if (c->copy_out) hipStreamDestroy(c->copy_out);
@@ -1895,10 +2197,22 @@ int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) { return unmask_imp
 
 int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
                        const websocket_parser* carry_in, uint32_t nseg) {
-    int rc = check_ctx(c);
+    int rc = check_ctx(c, false);
     if (rc) return rc;
     if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
+    if (fused_eligible(c, rx_len, nseg)) {
+        if (!c->piped) {
+            for (tset& t : c->ts) {
+                HIP_OR(hipEventRecord(t.free_ev, c->stream), HVWS_EHIP);
+                t.free_wait = t.free_ev;
+                t.free_pending = true;
+            }
+            c->piped = true;
+        }
+        return fused_issue(c, d_rx, rx_len, segs, carry_in, nseg, true);
+    }
+    if ((rc = fused_settle_all(c)) != HVWS_OK) return rc;
     if (!c->piped) {
         // Entering pipelined mode: both table sets may still be read by work
         // queued on the context stream.
@@ -1924,6 +2238,11 @@ int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* s
     if (rc) return rc;
     if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
+    if (fused_eligible(c, rx_len, nseg)) {
+        c->cs = c->stream;
+        c->piped = false;
+        return fused_issue(c, d_rx, rx_len, segs, carry_in, nseg, false);
+    }
     if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
     bool unmasked = false;
     if ((rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked)) != HVWS_OK) return rc;
@@ -2325,6 +2644,20 @@ uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {
     const uint32_t old = c->vmask;
     c->vmask = classes & V_ALL;
     return old;
+}
+
+int hvws_set_fused(hvws_ctx* c, int mode) {
+    if (!c) return -1;
+    const int old = c->fused_mode;
+    c->fused_mode = mode < 0 ? -1 : (mode > 2 ? 2 : mode);
+    return old;
+}
+
+int hvws_fused_stats(hvws_ctx* c, uint64_t out[2]) {
+    if (!c || !out) return set_err(HVWS_EINVAL, "null argument");
+    out[0] = c->fused_steps;
+    out[1] = c->fused_fixes;
+    return HVWS_OK;
 }
 
 int hvws_set_door(hvws_ctx* c, int on) {

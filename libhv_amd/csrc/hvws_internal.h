@@ -277,6 +277,66 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
                         drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
                         uint32_t stage_lds, uint64_t* h_done, uint64_t seq, hipStream_t st,
                         hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// FUSED scan path (hvws_kernels.hip, k_fprep / k_fwgseg / k_fused): uniform
+// segments discovered inside the unmask pass itself.  Per segment, k_fprep
+// runs the carried-in frame exactly and takes the first whole frame's size as
+// the stride hypothesis; k_fused then checks every hypothesised header while
+// it unmasks the payloads it implies, writes the records, finishes each
+// segment's tail exactly and publishes a verdict.  A batch whose hypothesis
+// failed anywhere is undone by the same kernel in undo mode (it XORs exactly
+// the same bytes with the same masks: the hypothesised header bytes it reads
+// are never among the bytes it XORs) and re-run on the exact path.
+struct dfmid {
+    dcarry   st;        // parser state at pos (after the carried-in frame)
+    uint64_t pos;       // segment offset of the first hypothesised whole frame
+    uint64_t stride;    // its size (0: none)
+    uint64_t nwhole;    // hypothesised whole frames
+    uint32_t n_a;       // 1: the carried-in frame has a record (ra)
+    uint32_t tail;      // 1: the tail's header completes (a record is predicted)
+    int64_t  ra_hdr;    // the carried-in frame's record, segment-relative
+    uint64_t ra_off, ra_len, ra_length;
+    uint32_t ra_key, ra_info;
+};
+struct dfctl {          // per table set, zeroed before k_fprep
+    uint64_t segs_done; // segments finished (k_fprep: no records; k_fused: the rest)
+    uint64_t fail;      // a segment's hypothesis or count failed
+    uint64_t pad[6];
+};
+constexpr uint32_t kFusedRecords = 16;    // records per k_fused workgroup
+constexpr uint32_t kFusedThreads = 256;
+constexpr uint32_t FUSED_GATED = 8u;      // status flag: not run (the previous fused batch failed)
+constexpr uint32_t FUSED_UNTOUCHED = 16u; // status flag: failed before any byte was XORed
+struct fused_args {
+    uint8_t*        rx;
+    uint64_t        rx_len;
+    const dseg*     segs;
+    const dfmid*    fmid;
+    const uint64_t* est;
+    const uint64_t* bases;
+    const uint64_t* total;
+    uint64_t*       first_fail;
+    uint64_t*       done_cnt;
+    dfctl*          ctl;
+    const uint32_t* wg_seg;
+    dframes         fr;
+    dcarry*         carry_out;
+    uint64_t*       counts;
+    uint64_t*       gate;       // context word: 1 while a fused batch has failed and is not yet settled
+    dspec_status*   status;     // device-mapped pinned host
+    uint64_t        seq;
+    uint32_t        nseg;
+    uint32_t        vmask;
+    uint32_t        undo;
+};
+hipError_t launch_fprep(const uint8_t* rx, uint64_t rx_len, const dseg* src_segs, const dcarry* src_carry, dseg* segs_w,
+                        dcarry* carry_w, uint32_t nseg, dfmid* fmid, uint64_t* est, uint64_t* first_fail,
+                        uint64_t* done_cnt, dcarry* carry_out, uint64_t* counts, dfctl* ctl, uint32_t vmask,
+                        hipStream_t st);
+hipError_t launch_fwgseg(const uint64_t* bases, const uint64_t* est, uint32_t nseg, uint32_t* wg_seg, uint64_t nwg,
+                         hipStream_t st);
+hipError_t launch_fused(const fused_args& a, uint64_t nwg, hipStream_t st, hipEvent_t ev_start = nullptr,
+                        hipEvent_t ev_stop = nullptr);
+
 // Resident small-path worker ("door", k_door): one workgroup that stays on
 // the device between calls and takes one request at a time from a mailbox in
 // fine-grained pinned host memory, so a reference-API call (FeedRecvData,

@@ -997,7 +997,8 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
     uint8_t* lds = reinterpret_cast<uint8_t*>(lds_door);
     uint64_t last = first_seq;
     uint64_t served = 0;
-    __shared__ uint64_t s_t[6];
+    __shared__ uint64_t s_t[6], s_m[2];
+    __shared__ uint64_t s_req[16];
     for (;;) {
         if (tid == 0) {
             uint64_t t0 = wall_clock64();
@@ -1022,29 +1023,32 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             s_exit = ex;
             s_seq = s;
             s_t[0] = wall_clock64();
-            if (!ex) {
-                // The request fields were written before seq.  Read with
-                // system-scope loads (vector memory, no cache can hold a
-                // previous request's values); the acquire also invalidates
-                // this CU's L1 and the L2 for the data the waves load next.
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                const uint64_t* w = reinterpret_cast<const uint64_t*>(box);
-                uint64_t q[11];
-#pragma unroll
-                for (int i = 0; i < 11; ++i) q[i] = __hip_atomic_load(w + 1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_op = (uint32_t)q[0];
-                s_unmask = (uint32_t)(q[0] >> 32);
-                s_len = q[1] < kDoorMax ? q[1] : kDoorMax;
-                s_vmask = (uint32_t)q[2];
-                s_key = (uint32_t)(q[2] >> 32);
-                s_phase = (uint32_t)q[3];
-                dcarry cin;
-                memcpy(&cin, &q[4], sizeof(dcarry));
-                s_carry = cin;
-            }
+            // The request fields were written before seq; the acquire also
+            // invalidates this CU's L1 and the L2 for the data loaded next.
+            if (!ex) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         __syncthreads();
         if (s_exit) return;
+        if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
+            const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(box) + tid);
+            reinterpret_cast<u32x4*>(s_req)[tid] = piece;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const uint64_t* q = s_req + 1;   // word 0 is seq
+            s_op = (uint32_t)q[0];
+            s_unmask = (uint32_t)(q[0] >> 32);
+            s_len = q[1] < kDoorMax ? q[1] : kDoorMax;
+            s_vmask = (uint32_t)q[2];
+            s_key = (uint32_t)(q[2] >> 32);
+            s_phase = (uint32_t)q[3];
+            dcarry cin;
+            memcpy(&cin, &q[4], sizeof(dcarry));
+            s_carry = cin;
+            s_t[5] = wall_clock64();
+            s_m[0] = __builtin_amdgcn_s_memtime();
+        }
+        __syncthreads();
         const uint64_t seq = s_seq;
         const uint32_t op = s_op;
         if (op == DOOR_EXIT) {
@@ -1123,7 +1127,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             }
             __threadfence_block();
             __syncthreads();
-            if (tid == 0) s_t[2] = wall_clock64();
+            if (tid == 0) {
+                s_t[2] = wall_clock64();
+                s_m[1] = __builtin_amdgcn_s_memtime();
+            }
             const uint64_t n = s_n;
             auto rec = [&](uint64_t i) -> drec { return i < SMALL_LREC ? lrec[i] : d_slot[i]; };
             if (s_unmask && n) {
@@ -1166,6 +1173,8 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                 box->stamp[2] = s_t[2];
                 box->stamp[3] = s_t[3];
                 box->stamp[4] = wall_clock64();
+                box->stamp[5] = s_t[5];
+                box->stamp[6] = s_m[1] - s_m[0];   // shader clocks from the request read to the walk's end
             }
         }
         // every thread's stores reach host memory before `done` says so
@@ -1180,6 +1189,492 @@ hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uin
                        hipStream_t st) {
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 16, st, box, data, h_rec, d_slot, idle_ticks,
                        first_seq);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ FUSED
+//
+// Uniform segments discovered inside the unmask pass (dfmid, hvws_internal.h).
+// The separate discovery walk of the SPEC path reads one 128-byte line per
+// 8-byte header beside the previous batch's unmask (134 MB of line traffic
+// per 1M frames at config 2, which slowed that unmask by ~15 %); here the
+// headers are read with the payload lines around them, by the pass that XORs
+// them.
+//
+// k_fprep   one thread per segment: the carried-in frame (exact state
+//           machine), the first whole frame's size = the stride hypothesis,
+//           the number of whole frames it implies, whether the tail's header
+//           completes, hence the record estimate est[s].  A segment with no
+//           record is finished here (its carry-out by the state machine).
+// k_fwgseg  workgroup -> first segment map for k_fused (kFusedRecords records
+//           per workgroup, records numbered by the exclusive scan of est).
+// k_fused   per workgroup: its records' headers checked against the
+//           hypothesis (a header whose size differs marks the segment's first
+//           failure), records written, and the payloads XORed chunk by chunk;
+//           a chunk wholly inside the workgroup's contiguous frames is a
+//           plain read-modify-write, one shared with another workgroup's
+//           frames is XORed dword by dword with atomics.  The last workgroup
+//           to finish a segment's frames runs its tail exactly (record, XOR,
+//           carry-out) if every hypothesised header held; the last segment
+//           publishes the verdict (dspec_status) and the context's gate.
+// Undo mode (a failed batch): the same XOR, same bytes, same masks -- the
+// masks come from hypothesised header bytes, which the pass never XORs (they
+// are disjoint from the hypothesised payloads), so they read the same both
+// times -- and the same tails (run only where every header held, i.e. where
+// the headers are true headers).
+constexpr uint64_t FUSED_NONE = ~0ull;
+
+__global__ __launch_bounds__(256) void k_fprep(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                               const dseg* __restrict__ src_segs, const dcarry* __restrict__ src_carry,
+                                               dseg* __restrict__ segs_w, dcarry* __restrict__ carry_w, uint32_t nseg,
+                                               dfmid* __restrict__ fmid, uint64_t* __restrict__ est,
+                                               uint64_t* __restrict__ first_fail, uint64_t* __restrict__ done_cnt,
+                                               dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
+                                               dfctl* __restrict__ ctl, uint32_t vmask) {
+    const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+    if (s >= nseg) return;
+    dseg sg;
+    dcarry st;
+    if (src_segs) {   // zero-copy upload: read the pinned slot, keep device copies
+        sg = src_segs[s];
+        st = src_carry[s];
+        segs_w[s] = sg;
+        carry_w[s] = st;
+    } else {
+        sg = segs_w[s];
+        st = carry_w[s];
+    }
+    st.started = 0;
+    const uint64_t L = sg.len;
+    const uint8_t* seg = rx + sg.off;
+    uint64_t pos = 0;
+    dfmid m;
+    m.n_a = 0;
+    m.tail = 0;
+    m.stride = 0;
+    m.nwhole = 0;
+    m.ra_hdr = -1;
+    m.ra_off = m.ra_len = m.ra_length = 0;
+    m.ra_key = m.ra_info = 0;
+    if (st.state != S_START) {
+        frec r;
+        if (scalar_frame(seg, L, st, pos, r, vmask)) {
+            m.n_a = 1;
+            m.ra_hdr = r.hdr_off;
+            m.ra_off = r.pay_off;
+            m.ra_len = r.pay_len;
+            m.ra_length = r.length;
+            m.ra_key = r.key;
+            m.ra_info = r.info;
+        }
+    }
+    m.st = st;
+    m.pos = pos;
+    if (st.state == S_START && pos < L) {
+        hdr h;
+        if (parse_at(rx, rx_len, sg.off, L, pos, h)) {
+            m.stride = (uint64_t)h.hlen + h.length;
+            m.nwhole = (L - pos) / m.stride;
+        }
+        const uint64_t pt = pos + m.nwhole * m.stride;
+        if (pt < L && L - pt >= 2) {   // the tail's header completes iff its size byte says it fits
+            const uint32_t b1 = seg[pt + 1];
+            const uint32_t len7 = b1 & 0x7Fu;
+            const uint64_t hlen = 2u + (len7 == 126 ? 2u : (len7 == 127 ? 8u : 0u)) + ((b1 & 0x80u) ? 4u : 0u);
+            m.tail = hlen <= L - pt ? 1u : 0u;
+        }
+    }
+    const uint64_t e = m.n_a + m.nwhole + m.tail;
+    fmid[s] = m;
+    est[s] = e;
+    first_fail[s] = FUSED_NONE;
+    done_cnt[s] = 0;
+    if (e == 0) {
+        // no record: what follows pos is at most a partial header
+        if (st.state == S_START && pos < L) {
+            frec r;
+            if (scalar_frame(seg, L, st, pos, r, vmask)) atomicOr((unsigned long long*)&ctl->fail, 1ull);
+        }
+        carry_out[s] = st;
+        counts[s] = 0;
+        __threadfence();
+        atomicAdd((unsigned long long*)&ctl->segs_done, 1ull);
+    }
+}
+
+hipError_t launch_fprep(const uint8_t* rx, uint64_t rx_len, const dseg* src_segs, const dcarry* src_carry, dseg* segs_w,
+                        dcarry* carry_w, uint32_t nseg, dfmid* fmid, uint64_t* est, uint64_t* first_fail,
+                        uint64_t* done_cnt, dcarry* carry_out, uint64_t* counts, dfctl* ctl, uint32_t vmask,
+                        hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fprep, dim3((nseg + 255u) / 256u), dim3(256), 0, st, rx, rx_len, src_segs, src_carry, segs_w,
+                       carry_w, nseg, fmid, est, first_fail, done_cnt, carry_out, counts, ctl, vmask);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_fwgseg(const uint64_t* __restrict__ bases, const uint64_t* __restrict__ est,
+                                                uint32_t nseg, uint32_t* __restrict__ wg_seg, uint64_t nwg) {
+    const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+    if (s >= nseg) return;
+    const uint64_t e = est[s];
+    if (!e) return;
+    const uint64_t b = bases[s];
+    // workgroups whose first record w * F lies in [b, b + e) -- only those
+    // k_fused launches (an estimate past the table makes it decline anyway)
+    for (uint64_t w = (b + kFusedRecords - 1) / kFusedRecords; w * kFusedRecords < b + e && w < nwg; ++w) wg_seg[w] = s;
+}
+
+hipError_t launch_fwgseg(const uint64_t* bases, const uint64_t* est, uint32_t nseg, uint32_t* wg_seg, uint64_t nwg,
+                         hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fwgseg, dim3((nseg + 255u) / 256u), dim3(256), 0, st, bases, est, nseg, wg_seg, nwg);
+    return hipGetLastError();
+}
+
+// XOR key bytes into the 16-byte chunk at c: plain read-modify-write when the
+// workgroup owns the whole chunk, else dword atomics (another workgroup may
+// XOR other bytes of it at the same time).
+__device__ __forceinline__ void fused_apply(uint8_t* rx, uint64_t c, uint64_t mlo, uint64_t mhi, bool own) {
+    if (!(mlo | mhi)) return;
+    const u32x4 m4 = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+    u32x4* p = reinterpret_cast<u32x4*>(rx + c);
+    if (own) {
+        *p = *p ^ m4;
+        return;
+    }
+    uint32_t* d = reinterpret_cast<uint32_t*>(rx + c);
+    if (m4.x) atomicXor(d + 0, m4.x);
+    if (m4.y) atomicXor(d + 1, m4.y);
+    if (m4.z) atomicXor(d + 2, m4.z);
+    if (m4.w) atomicXor(d + 3, m4.w);
+}
+
+// Mask bytes [po, pe) of a payload whose 4-byte aligned key word is kw, cut to
+// the chunk at c.
+__device__ __forceinline__ void fused_mask(uint64_t c, uint64_t po, uint64_t pe, uint32_t kw, uint64_t& mlo,
+                                           uint64_t& mhi) {
+    if (pe <= c || po >= c + 16 || pe <= po) return;
+    const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+    const int64_t a = (int64_t)(po > c ? po - c : 0);
+    const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
+    mlo |= kk & byte_range(a, e);
+    mhi |= kk & byte_range(a - 8, e - 8);
+}
+
+// Segment s's frames are all processed: finish it.  Thread 0 only.  Returns
+// the tail's XOR span (po == pe: none) and its frame's extent.
+__device__ void fused_finish(const fused_args& a, uint32_t s, bool undo, uint64_t& t_po, uint64_t& t_pe,
+                             uint32_t& t_kw, uint64_t& t_lo, uint64_t& t_hi) {
+    t_po = t_pe = t_lo = t_hi = 0;
+    t_kw = 0;
+    const dfmid m = a.fmid[s];
+    const dseg sg = a.segs[s];
+    const uint64_t L = sg.len;
+    const uint64_t ff = __hip_atomic_load(&a.first_fail[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool fail = ff != FUSED_NONE;
+    if (!fail) {
+        dcarry st = m.st;
+        uint64_t pos = m.pos;
+        if (m.nwhole) {   // the state the whole frames leave (Q14: the last frame's fields persist)
+            uint64_t lo, hi;
+            const uint64_t ql = m.pos + (m.nwhole - 1) * m.stride;
+            ld16(a.rx, a.rx_len, sg.off + ql, lo, hi);
+            const hdr hl = parse_hdr(lo, hi);
+            st.state = S_START;
+            st.flags = hl.flags;
+            st.length = hl.length;
+            st.require = 0;
+            st.offset = 0;
+            st.mask_offset = (hl.flags & F_MASK) ? (uint32_t)(hl.length & 3u) : 0u;
+            st.started = 0;
+            if (hl.flags & F_MASK) {
+                st.mask = hl.key;
+            } else {   // the key of the last masked frame, if any
+                for (uint64_t k = m.nwhole - 1; k-- > 0;) {
+                    ld16(a.rx, a.rx_len, sg.off + m.pos + k * m.stride, lo, hi);
+                    const hdr hk = parse_hdr(lo, hi);
+                    if (hk.flags & F_MASK) {
+                        st.mask = hk.key;
+                        break;
+                    }
+                }
+            }
+            pos = m.pos + m.nwhole * m.stride;
+        }
+        bool has_t = false;
+        frec rt;
+        const uint64_t pt = pos;
+        if (st.state == S_START && pos < L) has_t = scalar_frame(a.rx + sg.off, L, st, pos, rt, a.vmask);
+        // A tail frame that completed here is a whole frame to the exact walk
+        // (which leaves `started` clear); a frame after it means more records
+        // than estimated.
+        const bool more = st.state == S_START && pos < L;
+        if (st.state == S_START) st.started = 0;
+        const uint64_t actual = m.n_a + m.nwhole + (has_t ? 1u : 0u) + (more ? 1u : 0u);
+        if (has_t && (rt.info & I_BODY) && (rt.info & F_MASK) && rt.pay_len) {
+            t_po = sg.off + rt.pay_off;
+            t_pe = t_po + rt.pay_len;
+            t_kw = key_for_aligned(rt.key, t_po, (rt.info >> 8) & 3u);
+            t_lo = sg.off + pt;
+            t_hi = sg.off + L;
+        }
+        if (!undo) {
+            if (actual != a.est[s]) fail = true;
+            else if (has_t) store_frame(a.fr, a.bases[s] + m.n_a + m.nwhole, sg.off, rt);
+            a.carry_out[s] = st;
+            a.counts[s] = actual;
+        }
+    }
+    if (!undo && fail) atomicOr((unsigned long long*)&a.ctl->fail, 1ull);
+}
+
+__device__ void fused_publish(const fused_args& a, uint32_t extra_flags) {
+    __threadfence();
+    const uint64_t fail = __hip_atomic_load(&a.ctl->fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool bad = fail || (extra_flags & (FUSED_GATED | FUSED_UNTOUCHED));
+    a.status->total = *a.total;
+    a.status->flags = (bad ? 0u : (SPEC_OK | SPEC_MATCH)) | extra_flags;
+    a.status->pad2[0] = 0;
+    a.status->pad2[1] = 0;
+    if (!(extra_flags & FUSED_GATED)) *a.gate = bad ? 1ull : 0ull;
+    __threadfence_system();
+    __hip_atomic_store(&a.status->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
+    constexpr uint32_t F = kFusedRecords;
+    __shared__ uint64_t p_fs[F], p_fe[F], p_po[F], p_pe[F];
+    __shared__ uint32_t p_kw[F], p_seg[F];
+    __shared__ uint32_t r_type[F], r_seg[F];
+    __shared__ uint64_t run_lo[F], run_hi[F];
+    __shared__ uint32_t run_p0[F], run_p1[F], run_c0[F + 1];
+    __shared__ uint32_t s_go, s_nrun, s_ncomp;
+    __shared__ uint32_t comp_seg[F];
+    __shared__ uint64_t t_span[5];
+    __shared__ uint32_t t_kwv;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t w = blockIdx.x;
+    uint64_t total = 0;
+    if (tid == 0) {
+        uint32_t go = 1;
+        total = *a.total;
+        if (!a.undo && *a.gate) {   // the previous fused batch failed: this one is re-run after the fix
+            go = 0;
+            if (w == 0) fused_publish(a, FUSED_GATED | FUSED_UNTOUCHED);
+        } else if (total > a.fr.cap) {   // the table cannot hold the estimate: nothing done, exact path
+            go = 0;
+            if (w == 0 && !a.undo) fused_publish(a, FUSED_UNTOUCHED);
+        } else if (w * F >= total) {
+            go = 0;
+            if (w == 0 && !a.undo && __hip_atomic_load(&a.ctl->segs_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                                         a.nseg)
+                fused_publish(a, 0u);   // no records anywhere: k_fprep finished every segment
+        }
+        s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) return;
+    total = *a.total;
+
+    // 1. the workgroup's records
+    if (tid < F) {
+        const uint64_t r = w * F + tid;
+        uint32_t type = 0, s = 0;
+        uint64_t fs = 0, fe = 0, po = 0, pe = 0;
+        uint32_t kw = 0;
+        if (r < total) {
+            s = a.wg_seg[w];
+            while (r >= a.bases[s] + a.est[s]) ++s;
+            const dfmid m = a.fmid[s];
+            const dseg sg = a.segs[s];
+            const uint64_t j = r - a.bases[s];
+            if (j < m.n_a) {
+                type = 1;
+                fs = sg.off;
+                fe = sg.off + m.pos;
+                if (!a.undo) {
+                    frec v;
+                    v.hdr_off = m.ra_hdr;
+                    v.pay_off = m.ra_off;
+                    v.pay_len = m.ra_len;
+                    v.length = m.ra_length;
+                    v.key = m.ra_key;
+                    v.info = m.ra_info;
+                    store_frame(a.fr, r, sg.off, v);
+                }
+                if ((m.ra_info & I_BODY) && (m.ra_info & F_MASK) && m.ra_len) {
+                    po = sg.off + m.ra_off;
+                    pe = po + m.ra_len;
+                    kw = key_for_aligned(m.ra_key, po, (m.ra_info >> 8) & 3u);
+                }
+            } else if (j - m.n_a < m.nwhole) {
+                type = 2;
+                const uint64_t jw = j - m.n_a;
+                const uint64_t q = m.pos + jw * m.stride;
+                fs = sg.off + q;
+                fe = fs + m.stride;
+                uint64_t lo, hi;
+                ld16(a.rx, a.rx_len, fs, lo, hi);
+                const hdr h = parse_hdr(lo, hi);
+                if ((uint64_t)h.hlen + h.length == m.stride) {
+                    if (!a.undo) {
+                        frec v;
+                        whole_frame_rec(v, q, h, a.vmask);
+                        store_frame(a.fr, r, sg.off, v);
+                    }
+                    if ((h.flags & F_MASK) && h.length) {
+                        po = fs + h.hlen;
+                        pe = fe;
+                        kw = key_for_aligned(h.key, po, 0u);
+                    }
+                } else if (!a.undo) {
+                    atomicMin((unsigned long long*)&a.first_fail[s], (unsigned long long)jw);
+                }
+            } else {
+                type = 3;   // the tail: run exactly when the segment is finished
+            }
+        }
+        if (po == pe) po = pe = fe;   // empty span at the frame end: pe stays non-decreasing
+        r_type[tid] = type;
+        r_seg[tid] = s;
+        p_fs[tid] = fs;
+        p_fe[tid] = fe;
+        p_po[tid] = po;
+        p_pe[tid] = pe;
+        p_kw[tid] = kw;
+        p_seg[tid] = s;
+    }
+    __syncthreads();
+    // runs: consecutive frames (carried-in / whole) that touch end to end
+    if (tid == 0) {
+        uint32_t np = 0, nrun = 0, nc = 0;
+        for (uint32_t t = 0; t < F; ++t) {
+            if (r_type[t] != 1 && r_type[t] != 2) continue;
+            if (np != t) {   // compact
+                p_fs[np] = p_fs[t];
+                p_fe[np] = p_fe[t];
+                p_po[np] = p_po[t];
+                p_pe[np] = p_pe[t];
+                p_kw[np] = p_kw[t];
+                p_seg[np] = p_seg[t];
+            }
+            if (nrun && run_hi[nrun - 1] == p_fs[np]) {
+                run_hi[nrun - 1] = p_fe[np];
+                run_p1[nrun - 1] = np + 1;
+            } else {
+                run_lo[nrun] = p_fs[np];
+                run_hi[nrun] = p_fe[np];
+                run_p0[nrun] = np;
+                run_p1[nrun] = np + 1;
+                ++nrun;
+            }
+            ++np;
+        }
+        for (uint32_t k = 0; k < nrun; ++k) {
+            run_c0[k] = nc;
+            if (run_hi[k] > run_lo[k]) nc += (uint32_t)(((run_hi[k] - 1) >> 4) - (run_lo[k] >> 4) + 1);
+        }
+        run_c0[nrun] = nc;
+        s_nrun = nrun;
+    }
+    __syncthreads();
+
+    // 2. XOR, chunk by chunk over the runs
+    const uint32_t nrun = s_nrun, nc = run_c0[nrun];
+    for (uint32_t f = tid; f < nc; f += kFusedThreads) {
+        uint32_t k = 0;
+        while (run_c0[k + 1] <= f) ++k;
+        const uint64_t c = (run_lo[k] & ~15ull) + (uint64_t)(f - run_c0[k]) * 16u;
+        uint32_t lo = run_p0[k], hi = run_p1[k];   // first piece whose payload span ends after c
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (p_pe[mid] > c) hi = mid;
+            else lo = mid + 1;
+        }
+        uint64_t mlo = 0, mhi = 0;
+        for (uint32_t i = lo; i < run_p1[k] && p_po[i] < c + 16; ++i) fused_mask(c, p_po[i], p_pe[i], p_kw[i], mlo, mhi);
+        fused_apply(a.rx, c, mlo, mhi, c >= run_lo[k] && c + 16 <= run_hi[k]);
+    }
+
+    // 3. segments whose frames are now all processed: tails, carry-outs, verdict
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t nc2 = 0;
+        if (!a.undo) {
+            uint32_t t = 0;
+            while (t < F) {
+                const uint32_t s = r_seg[t];
+                uint64_t units = 0;
+                bool tail_only = false;
+                uint32_t t2 = t;
+                for (; t2 < F && r_seg[t2] == s && r_type[t2] != 0; ++t2) {
+                    if (r_type[t2] == 1 || r_type[t2] == 2) ++units;
+                    if (r_type[t2] == 3) {
+                        const dfmid m = a.fmid[s];
+                        if (m.n_a + m.nwhole == 0) tail_only = true;
+                    }
+                }
+                if (t2 == t) break;   // past the last record
+                if (units) {
+                    const dfmid m = a.fmid[s];
+                    const uint64_t old = atomicAdd((unsigned long long*)&a.done_cnt[s], (unsigned long long)units);
+                    if (old + units == m.n_a + m.nwhole) comp_seg[nc2++] = s;
+                } else if (tail_only) {
+                    comp_seg[nc2++] = s;
+                }
+                t = t2;
+            }
+        } else {
+            // undo: the tail of every segment whose last record is here
+            for (uint32_t t = 0; t < F; ++t) {
+                if (r_type[t] == 0) break;
+                const uint32_t s = r_seg[t];
+                if (w * F + t == a.bases[s] + a.est[s] - 1) comp_seg[nc2++] = s;
+            }
+        }
+        s_ncomp = nc2;
+        __threadfence();
+    }
+    __syncthreads();
+    const uint32_t ncomp = s_ncomp;
+    for (uint32_t i = 0; i < ncomp; ++i) {
+        if (tid == 0) {
+            uint64_t po, pe, lo, hi;
+            uint32_t kw;
+            fused_finish(a, comp_seg[i], a.undo != 0, po, pe, kw, lo, hi);
+            t_span[0] = po;
+            t_span[1] = pe;
+            t_span[2] = lo;
+            t_span[3] = hi;
+            t_kwv = kw;
+        }
+        __syncthreads();
+        const uint64_t po = t_span[0], pe = t_span[1], lo = t_span[2], hi = t_span[3];
+        if (pe > po) {
+            const uint64_t c0 = po & ~15ull;
+            for (uint64_t c = c0 + (uint64_t)tid * 16u; c < pe; c += (uint64_t)kFusedThreads * 16u) {
+                uint64_t mlo = 0, mhi = 0;
+                fused_mask(c, po, pe, t_kwv, mlo, mhi);
+                fused_apply(a.rx, c, mlo, mhi, c >= lo && c + 16 <= hi);
+            }
+        }
+        __threadfence();
+        __syncthreads();
+        if (tid == 0 && !a.undo) {
+            const uint64_t old = atomicAdd((unsigned long long*)&a.ctl->segs_done, 1ull);
+            if (old + 1 == a.nseg) fused_publish(a, 0u);
+        }
+    }
+}
+
+hipError_t launch_fused(const fused_args& a, uint64_t nwg, hipStream_t st, hipEvent_t ev_start, hipEvent_t ev_stop) {
+    if (nwg == 0) nwg = 1;
+    if (nwg > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(k_fused, dim3((uint32_t)nwg), dim3(kFusedThreads), 0, st, ev_start, ev_stop, 0u, a);
+    else
+        hipLaunchKernelGGL(k_fused, dim3((uint32_t)nwg), dim3(kFusedThreads), 0, st, a);
     return hipGetLastError();
 }
 

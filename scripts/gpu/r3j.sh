@@ -1,0 +1,20 @@
+# round 3: worker with ordinary pinned data areas + serial walk prefix (k_door, k_small)
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r3j
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 120 python -u scripts/probe/door_phases.py 2000 > gpurun_out/r3j/door_phases.json 2>&1 || { echo "phases failed"; tail -20 gpurun_out/r3j/door_phases.json; exit 1; }
+cat gpurun_out/r3j/door_phases.json
+timeout -k 10 200 python -u scripts/bench_dropin.py > gpurun_out/r3j/dropin.json 2> gpurun_out/r3j/dropin.err || { echo "dropin failed"; tail -20 gpurun_out/r3j/dropin.err; exit 1; }
+cat gpurun_out/r3j/dropin.json
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  -k "door or feed_many or feeder or rx_reads or threads or messages or execute or decode or small or batch_configs or over_host_record_area" \
+  > gpurun_out/r3j/pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r3j/pytest.log; exit 1; }
+tail -3 gpurun_out/r3j/pytest.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
+  -k "fused or batch_segments_with_carry or batch_every_cut or batch_empty or batch_configs_small or dense_tiny or speculative_table or pipelined_steps" \
+  > gpurun_out/r3j/pytest.log 2>&1 || { echo "pytest failed"; grep -E "PASS|FAIL" gpurun_out/r3j/pytest.log | tail -5; tail -60 gpurun_out/r3j/pytest.log; exit 1; }
+tail -3 gpurun_out/r3j/pytest.log
+for f in 2 0; do
+  HVWS_FUSED=$f timeout -k 10 200 python -u bench.py --config c2 --steps 200 --warmup 5 --no-tx --host-gib 0 --cpu-seconds 0 --feed-conns 0 --dropin-reads 0 > gpurun_out/r3j/c2_fused$f.json 2> gpurun_out/r3j/c2_fused$f.err || { echo "bench c2 failed"; tail -20 gpurun_out/r3j/c2_fused$f.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/r3j/c2_fused$f.json')); print('fused=$f', d['value'], d['ms_per_step'], d['scan_path'], d['unmask_ms_mean'], d['roofline']['frac'])"
+done
