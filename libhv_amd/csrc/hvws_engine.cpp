@@ -179,6 +179,7 @@ struct hvws_ctx {
     // estimates hold (then the next batch speculates).
     hbuf h_status;
     uint64_t scan_seq = 0;
+    uint64_t match_seq = 0;   // a COUNT_EMIT scan's published SPEC_MATCH, not read yet (0 = none)
     bool spec_ok = false;
     // The last check saw a segment with >= spec_min predicted frames: the
     // next one-walk pass keeps the grid-wide k_verify pair (else head + walk).
@@ -304,6 +305,7 @@ struct hvws_ctx {
 
 namespace {
 constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
+int fused_mode(hvws_ctx* c);
 constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
 constexpr uint64_t kSingleMin = 1ull << 20;   // records: smallest one-stream table before its count is known
 constexpr uint64_t kSlackMaxRecords = 1ull << 26;   // SLACK scratch table at most (48 B each: 3.2 GB)
@@ -735,6 +737,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     uint64_t nfr = bound;
     c->nfr_known = false;
     c->pscan_ran = false;
+    c->match_seq = 0;
     bool tiles_done = false;
     if (nseg == 1) {
         c->scan_path = HVWS_PATH_SINGLE;
@@ -820,7 +823,15 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         sc.sieve = nullptr;
     } else if (bound <= (c->fast_bound ? c->fast_bound : kFastFrameBound)) {
         c->scan_path = HVWS_PATH_COUNT_EMIT;
+        if (fused_mode(c) != 0 && nseg >= 2) {
+            // publish whether the uniform estimates held (read lazily by the
+            // next fused_eligible): no host wait here
+            sc.status = status_d;
+            sc.seq = ++c->scan_seq;
+            c->match_seq = sc.seq;
+        }
         HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
+        sc.status = nullptr;
         HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
         HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
     } else {
@@ -1602,6 +1613,15 @@ bool fused_eligible(hvws_ctx* c, uint64_t rx_len, uint32_t nseg) {
     const int mode = fused_mode(c);
     if (mode == 0 || nseg == 0 || c->vmask) return false;
     if (c->nfr_known) c->fz_nfr = c->nfr;   // the last exact count (a pending fused batch has none yet)
+    if (c->match_seq) {   // a COUNT_EMIT scan's verdict, once the device has published it
+        const dspec_status* st = c->h_status.as<dspec_status>();
+        if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == c->match_seq) {
+            c->spec_ok = (st->flags & SPEC_MATCH) != 0;
+            c->match_seq = 0;
+        } else if (mode == 2) {
+            return false;   // not known yet: this batch scans exactly
+        }
+    }
     if (mode == 1) return true;   // tests: whatever the last scan said
     if (nseg < 2 || !c->spec_ok || c->fz_nfr == 0) return false;
     // small frames only: at 64 KiB frames the separate scan is 0.6 % of a

@@ -1579,21 +1579,47 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
     }
     __syncthreads();
 
-    // 2. XOR, chunk by chunk over the runs
+    // 2. XOR, chunk by chunk over the runs: a round's loads of the chunks
+    // this workgroup owns are all issued before any mask is applied
     const uint32_t nrun = s_nrun, nc = run_c0[nrun];
-    for (uint32_t f = tid; f < nc; f += kFusedThreads) {
-        uint32_t k = 0;
-        while (run_c0[k + 1] <= f) ++k;
-        const uint64_t c = (run_lo[k] & ~15ull) + (uint64_t)(f - run_c0[k]) * 16u;
-        uint32_t lo = run_p0[k], hi = run_p1[k];   // first piece whose payload span ends after c
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (p_pe[mid] > c) hi = mid;
-            else lo = mid + 1;
+    constexpr uint32_t U = 8;
+    for (uint32_t base = 0; base < nc; base += kFusedThreads * U) {
+        u32x4 v[U];
+        uint32_t rk[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t f = base + u * kFusedThreads + tid;
+            rk[u] = 0;
+            if (f >= nc) continue;
+            uint32_t k = 0;
+            while (run_c0[k + 1] <= f) ++k;
+            rk[u] = k;
+            const uint64_t c = (run_lo[k] & ~15ull) + (uint64_t)(f - run_c0[k]) * 16u;
+            if (c >= run_lo[k] && c + 16 <= run_hi[k]) v[u] = *reinterpret_cast<const u32x4*>(a.rx + c);
         }
-        uint64_t mlo = 0, mhi = 0;
-        for (uint32_t i = lo; i < run_p1[k] && p_po[i] < c + 16; ++i) fused_mask(c, p_po[i], p_pe[i], p_kw[i], mlo, mhi);
-        fused_apply(a.rx, c, mlo, mhi, c >= run_lo[k] && c + 16 <= run_hi[k]);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t f = base + u * kFusedThreads + tid;
+            if (f >= nc) continue;
+            const uint32_t k = rk[u];
+            const uint64_t c = (run_lo[k] & ~15ull) + (uint64_t)(f - run_c0[k]) * 16u;
+            uint32_t lo = run_p0[k], hi = run_p1[k];   // first piece whose payload span ends after c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (p_pe[mid] > c) hi = mid;
+                else lo = mid + 1;
+            }
+            uint64_t mlo = 0, mhi = 0;
+            for (uint32_t i = lo; i < run_p1[k] && p_po[i] < c + 16; ++i)
+                fused_mask(c, p_po[i], p_pe[i], p_kw[i], mlo, mhi);
+            if (!(mlo | mhi)) continue;
+            if (c >= run_lo[k] && c + 16 <= run_hi[k]) {
+                *reinterpret_cast<u32x4*>(a.rx + c) =
+                    v[u] ^ u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+            } else {
+                fused_apply(a.rx, c, mlo, mhi, false);
+            }
+        }
     }
 
     // 3. segments whose frames are now all processed: tails, carry-outs, verdict
