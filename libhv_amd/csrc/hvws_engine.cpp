@@ -179,7 +179,7 @@ struct hvws_ctx {
     // estimates hold (then the next batch speculates).
     hbuf h_status;
     uint64_t scan_seq = 0;
-    uint64_t match_seq = 0;   // a COUNT_EMIT scan's published SPEC_MATCH, not read yet (0 = none)
+    uint64_t status_read = 0;   // newest published scan status fused_eligible has looked at
     bool spec_ok = false;
     // The last check saw a segment with >= spec_min predicted frames: the
     // next one-walk pass keeps the grid-wide k_verify pair (else head + walk).
@@ -287,6 +287,7 @@ struct hvws_ctx {
     bool fz_busy = false;       // inside a fused issue or settle (no nested settling)
     uint64_t fused_steps = 0, fused_fixes = 0;
     uint64_t fz_nfr = 0;        // records of the last batch whose count is known (sizes the next table)
+    uint32_t fz_skip = 0;       // auto mode: batches left to scan exactly after a failed fused pass
     // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
     // on both of the context's compute streams
     hipEvent_t span_ev[4] = {};
@@ -306,6 +307,7 @@ struct hvws_ctx {
 namespace {
 constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
 int fused_mode(hvws_ctx* c);
+constexpr uint32_t kFusedBackoff = 16;   // exact batches after a failed fused pass (auto mode)
 constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
 constexpr uint64_t kSingleMin = 1ull << 20;   // records: smallest one-stream table before its count is known
 constexpr uint64_t kSlackMaxRecords = 1ull << 26;   // SLACK scratch table at most (48 B each: 3.2 GB)
@@ -698,6 +700,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                                                     (unsigned long long)status_h->seq, (unsigned long long)sc.seq);
         n = status_h->total;
         flags = status_h->flags;
+        c->status_read = sc.seq;   // read here: fused_eligible looks only at newer verdicts
         if (flags & SPEC_ERR) return set_err(HVWS_EHIP, "one-launch scan: a grid barrier timed out (seq %llu)",
                                              (unsigned long long)sc.seq);
         if (n >= 0xFFFFFFF0ull)
@@ -737,7 +740,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     uint64_t nfr = bound;
     c->nfr_known = false;
     c->pscan_ran = false;
-    c->match_seq = 0;
     bool tiles_done = false;
     if (nseg == 1) {
         c->scan_path = HVWS_PATH_SINGLE;
@@ -824,11 +826,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     } else if (bound <= (c->fast_bound ? c->fast_bound : kFastFrameBound)) {
         c->scan_path = HVWS_PATH_COUNT_EMIT;
         if (fused_mode(c) != 0 && nseg >= 2) {
-            // publish whether the uniform estimates held (read lazily by the
-            // next fused_eligible): no host wait here
+            // publish whether the uniform estimates held (read lazily by a
+            // later fused_eligible): no host wait here
             sc.status = status_d;
             sc.seq = ++c->scan_seq;
-            c->match_seq = sc.seq;
         }
         HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
         sc.status = nullptr;
@@ -1613,16 +1614,29 @@ bool fused_eligible(hvws_ctx* c, uint64_t rx_len, uint32_t nseg) {
     const int mode = fused_mode(c);
     if (mode == 0 || nseg == 0 || c->vmask) return false;
     if (c->nfr_known) c->fz_nfr = c->nfr;   // the last exact count (a pending fused batch has none yet)
-    if (c->match_seq) {   // a COUNT_EMIT scan's verdict, once the device has published it
+    if (c->h_status.p) {
+        // Exact scans publish their verdict and count (COUNT_EMIT with no
+        // host wait); take the newest one the device has published since the
+        // last look (pipelined, the last scan's may still be running).  A
+        // stale verdict is only a hint: the fused pass checks every header
+        // it assumes.
         const dspec_status* st = c->h_status.as<dspec_status>();
-        if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == c->match_seq) {
-            c->spec_ok = (st->flags & SPEC_MATCH) != 0;
-            c->match_seq = 0;
-        } else if (mode == 2) {
-            return false;   // not known yet: this batch scans exactly
+        const uint64_t s = __atomic_load_n(&st->seq, __ATOMIC_ACQUIRE);
+        if (s > c->status_read) {
+            c->status_read = s;
+            const uint64_t tot = st->total;
+            const uint32_t fl = st->flags;
+            if (!(fl & SPEC_ERR) && tot < 0xFFFFFFF0ull) {
+                c->spec_ok = (fl & SPEC_MATCH) != 0;
+                if (tot) c->fz_nfr = tot;
+            }
         }
     }
     if (mode == 1) return true;   // tests: whatever the last scan said
+    if (c->fz_skip) {   // a fused pass failed recently
+        --c->fz_skip;
+        return false;
+    }
     if (nseg < 2 || !c->spec_ok || c->fz_nfr == 0) return false;
     // small frames only: at 64 KiB frames the separate scan is 0.6 % of a
     // step and k_unmask's tile geometry is at the in-place ceiling
@@ -1721,6 +1735,7 @@ int fused_settle(hvws_ctx* c, int set) {
     // failed (or gated): undo what the pass XORed, clear the gate, re-run exactly
     ++c->fused_fixes;
     c->spec_ok = false;
+    if (!(v.flags & FUSED_GATED)) c->fz_skip = kFusedBackoff;   // auto mode: exact scans for a while
     hvws_ctx::fused_pend newer;
     const int other = set ^ 1;
     const bool has_newer = c->fz[other].active && set != c->cur;   // issued behind it, gated
@@ -2670,6 +2685,7 @@ int hvws_set_fused(hvws_ctx* c, int mode) {
     if (!c) return -1;
     const int old = c->fused_mode;
     c->fused_mode = mode < 0 ? -1 : (mode > 2 ? 2 : mode);
+    c->fz_skip = 0;
     return old;
 }
 
