@@ -1665,7 +1665,8 @@ int fused_wait(hvws_ctx* c, int set, uint64_t seq, dspec_status& out) {
     }
 }
 
-fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint64_t seq, bool undo) {
+fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint64_t seq, bool undo,
+                         uint64_t nwg) {
     tset& T = c->ts[set];
     fused_args a;
     a.rx = d_rx;
@@ -1686,7 +1687,8 @@ fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, u
     a.fr.key = T.f_key.as<uint32_t>();
     a.fr.keyrot = T.f_keyrot.as<uint32_t>();
     a.fr.info = T.f_info.as<uint32_t>();
-    a.fr.cap = T.frame_cap;
+    // records the launch covers: an estimate past them declines the pass
+    a.fr.cap = std::min<uint64_t>(T.frame_cap, nwg * kFusedRecords);
     a.carry_out = T.carry_out.as<dcarry>();
     a.counts = T.counts.as<uint64_t>();
     a.gate = c->fz_gate.as<uint64_t>();
@@ -1735,7 +1737,9 @@ int fused_settle(hvws_ctx* c, int set) {
     // failed (or gated): undo what the pass XORed, clear the gate, re-run exactly
     ++c->fused_fixes;
     c->spec_ok = false;
-    if (!(v.flags & FUSED_GATED)) c->fz_skip = kFusedBackoff;   // auto mode: exact scans for a while
+    // a real misprediction (not a batch larger than the launch, not one gated
+    // behind a failure): auto mode scans exactly for a while
+    if (!(v.flags & (FUSED_GATED | FUSED_UNTOUCHED))) c->fz_skip = kFusedBackoff;
     hvws_ctx::fused_pend newer;
     const int other = set ^ 1;
     const bool has_newer = c->fz[other].active && set != c->cur;   // issued behind it, gated
@@ -1744,7 +1748,7 @@ int fused_settle(hvws_ctx* c, int set) {
         c->fz[other].active = false;
     }
     if (!(v.flags & FUSED_UNTOUCHED)) {
-        const fused_args a = fused_args_of(c, set, p.rx, p.rx_len, (uint32_t)p.segs.size(), p.seq, true);
+        const fused_args a = fused_args_of(c, set, p.rx, p.rx_len, (uint32_t)p.segs.size(), p.seq, true, p.nwg);
         HIP_OR(launch_fused(a, p.nwg, c->stream), HVWS_EHIP);
     }
     HIP_OR(hipMemsetAsync(c->fz_gate.p, 0, 8, c->stream), HVWS_EHIP);
@@ -1789,10 +1793,13 @@ int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
         T.free_pending = false;
     }
     // tables: the frame table holds the last count with room (the estimate
-    // must fit it, else the pass declines and the exact path runs)
-    const uint64_t want = std::max<uint64_t>({c->fz_nfr + c->fz_nfr / 8 + 64, c->ts[c->cur ^ 1].frame_cap, 1024});
-    HIP_OR(ensure_frames(c, want), HVWS_ENOMEM);
-    const uint64_t nwg = T.frame_cap / kFusedRecords + 1;
+    // must fit it, else the pass declines and the exact path runs).  Exact
+    // size: with growth room on top, the two sets would ratchet each other up.
+    const uint64_t want = std::max<uint64_t>(c->fz_nfr + c->fz_nfr / 8 + 64, 1024);
+    HIP_OR(ensure_frames(c, want, /*exact=*/true), HVWS_ENOMEM);
+    // workgroups for the expected records only (a table sized for a larger
+    // batch would launch idle workgroups by the million)
+    const uint64_t nwg = std::min<uint64_t>(T.frame_cap, want) / kFusedRecords + 1;
     HIP_OR(T.counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(T.bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(T.total.ensure(8), HVWS_ENOMEM);
@@ -1837,7 +1844,7 @@ int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
         HIP_OR(hipStreamWaitEvent(c->stream, c->scan_done, 0), HVWS_EHIP);
     }
     const uint64_t seq = ++c->scan_seq;
-    const fused_args a = fused_args_of(c, c->cur, d_rx, rx_len, nseg, seq, false);
+    const fused_args a = fused_args_of(c, c->cur, d_rx, rx_len, nseg, seq, false, nwg);
     const bool timed = step_events(c) >= 1;
     HIP_OR(launch_fused(a, nwg, c->stream, timed ? c->tev[c->t_cur][2] : nullptr, timed ? c->tev[c->t_cur][3] : nullptr),
            HVWS_EHIP);

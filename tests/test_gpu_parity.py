@@ -1070,6 +1070,34 @@ def test_fused_pipelined_failure_between_batches(eng):
         assert np.array_equal(frames[f], exp_recs[f]), f
 
 
+def test_fused_grown_batch_declines(eng):
+    """A batch with many more records than the last one: the fused launch
+    covers the expected records only, so the pass declines untouched and the
+    batch runs exactly; the next one of that size takes the FUSED path."""
+    L = libhv_amd.lib()
+    rng = random.Random(515)
+    small = _cut_uniform(rng, 150, 1024, 6)
+    big = _cut_uniform(rng, 3000, 1024, 6)
+    old = L.hvws_set_fused(eng.ctx, 1)
+    try:
+        L.hvws_set_fused(eng.ctx, 0)
+        _check_step(eng, *small, False)
+        L.hvws_set_fused(eng.ctx, 1)
+        for piped in (False, True):
+            b0 = _fused_stats(eng)
+            _check_step(eng, *big, piped)
+            b1 = _fused_stats(eng)
+            assert b1[0] == b0[0] + 1 and b1[1] == b0[1] + 1, (b0, b1)   # declined, then exact
+            path = _check_step(eng, *big, piped)
+            b2 = _fused_stats(eng)
+            assert path == 7 and b2[0] == b1[0] + 1 and b2[1] == b1[1], (b1, b2)
+            L.hvws_set_fused(eng.ctx, 0)
+            _check_step(eng, *small, False)
+            L.hvws_set_fused(eng.ctx, 1)
+    finally:
+        L.hvws_set_fused(eng.ctx, old)
+
+
 def test_fused_same_buffer_repeated(eng):
     """The bench's shape: one resident uniform batch stepped 9 times,
     pipelined, FUSED (auto): every pass unmasks or re-masks it in place
