@@ -302,7 +302,7 @@ struct dfctl {          // per table set, zeroed before k_fprep
     uint64_t fail;      // a segment's hypothesis or count failed
     uint64_t pad[6];
 };
-constexpr uint32_t kFusedRecords = 16;    // records per k_fused workgroup
+constexpr uint32_t kFusedRecords = 64;    // records per k_fused workgroup (one per lane of wave 0)
 constexpr uint32_t kFusedThreads = 256;
 constexpr uint32_t FUSED_GATED = 8u;      // status flag: not run (the previous fused batch failed)
 constexpr uint32_t FUSED_UNTOUCHED = 16u; // status flag: failed before any byte was XORed

@@ -1370,7 +1370,9 @@ __device__ void fused_finish(const fused_args& a, uint32_t s, bool undo, uint64_
     const dfmid m = a.fmid[s];
     const dseg sg = a.segs[s];
     const uint64_t L = sg.len;
-    const uint64_t ff = __hip_atomic_load(&a.first_fail[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // an atomic read-modify-write reads at the coherence point every
+    // workgroup's atomicMin reached (no workgroup fences its L2 for it)
+    const uint64_t ff = atomicMin((unsigned long long*)&a.first_fail[s], (unsigned long long)FUSED_NONE);
     bool fail = ff != FUSED_NONE;
     if (!fail) {
         dcarry st = m.st;
@@ -1429,8 +1431,7 @@ __device__ void fused_finish(const fused_args& a, uint32_t s, bool undo, uint64_
 }
 
 __device__ void fused_publish(const fused_args& a, uint32_t extra_flags) {
-    __threadfence();
-    const uint64_t fail = __hip_atomic_load(&a.ctl->fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t fail = atomicOr((unsigned long long*)&a.ctl->fail, 0ull);
     const bool bad = fail || (extra_flags & (FUSED_GATED | FUSED_UNTOUCHED));
     a.status->total = *a.total;
     a.status->flags = (bad ? 0u : (SPEC_OK | SPEC_MATCH)) | extra_flags;
@@ -1441,11 +1442,17 @@ __device__ void fused_publish(const fused_args& a, uint32_t extra_flags) {
     __hip_atomic_store(&a.status->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+    return (uint64_t)hi << 32 | lo;
+}
+
 __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
     constexpr uint32_t F = kFusedRecords;
+    static_assert(F == 64, "one record per lane of wave 0");
     __shared__ uint64_t p_fs[F], p_fe[F], p_po[F], p_pe[F];
-    __shared__ uint32_t p_kw[F], p_seg[F];
-    __shared__ uint32_t r_type[F], r_seg[F];
+    __shared__ uint32_t p_kw[F];
     __shared__ uint64_t run_lo[F], run_hi[F];
     __shared__ uint32_t run_p0[F], run_p1[F], run_c0[F + 1];
     __shared__ uint32_t s_go, s_nrun, s_ncomp;
@@ -1461,7 +1468,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
         if (!a.undo && *a.gate) {   // the previous fused batch failed: this one is re-run after the fix
             go = 0;
             if (w == 0) fused_publish(a, FUSED_GATED | FUSED_UNTOUCHED);
-        } else if (total > a.fr.cap) {   // the table cannot hold the estimate: nothing done, exact path
+        } else if (total > a.fr.cap) {   // the launch cannot hold the estimate: nothing done, exact path
             go = 0;
             if (w == 0 && !a.undo) fused_publish(a, FUSED_UNTOUCHED);
         } else if (w * F >= total) {
@@ -1476,10 +1483,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
     if (!s_go) return;
     total = *a.total;
 
-    // 1. the workgroup's records
+    // 1. the workgroup's records, one per lane of wave 0; then its runs of
+    // frames that touch end to end, found with ballots (no serial pass)
+    uint32_t type = 0, s = 0;
+    uint64_t n_units = 0;   // the lane's segment: carried-in + whole frames
     if (tid < F) {
         const uint64_t r = w * F + tid;
-        uint32_t type = 0, s = 0;
         uint64_t fs = 0, fe = 0, po = 0, pe = 0;
         uint32_t kw = 0;
         if (r < total) {
@@ -1487,6 +1496,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
             while (r >= a.bases[s] + a.est[s]) ++s;
             const dfmid m = a.fmid[s];
             const dseg sg = a.segs[s];
+            n_units = m.n_a + m.nwhole;
             const uint64_t j = r - a.bases[s];
             if (j < m.n_a) {
                 type = 1;
@@ -1535,47 +1545,48 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
             }
         }
         if (po == pe) po = pe = fe;   // empty span at the frame end: pe stays non-decreasing
-        r_type[tid] = type;
-        r_seg[tid] = s;
-        p_fs[tid] = fs;
-        p_fe[tid] = fe;
-        p_po[tid] = po;
-        p_pe[tid] = pe;
-        p_kw[tid] = kw;
-        p_seg[tid] = s;
-    }
-    __syncthreads();
-    // runs: consecutive frames (carried-in / whole) that touch end to end
-    if (tid == 0) {
-        uint32_t np = 0, nrun = 0, nc = 0;
-        for (uint32_t t = 0; t < F; ++t) {
-            if (r_type[t] != 1 && r_type[t] != 2) continue;
-            if (np != t) {   // compact
-                p_fs[np] = p_fs[t];
-                p_fe[np] = p_fe[t];
-                p_po[np] = p_po[t];
-                p_pe[np] = p_pe[t];
-                p_kw[np] = p_kw[t];
-                p_seg[np] = p_seg[t];
+        const bool keep = type == 1 || type == 2;
+        const uint64_t km = __ballot(keep);
+        const uint64_t prev_fe = shfl_up64(fe, 1);
+        const bool prev_keep = tid > 0 && ((km >> (tid - 1)) & 1ull);
+        const bool start = keep && !(prev_keep && prev_fe == fs);
+        const uint64_t sm = __ballot(start);
+        const uint64_t lt = tid ? (~0ull >> (64 - tid)) : 0ull;
+        const uint32_t np = (uint32_t)__popcll(km & lt);   // index among the kept records
+        const bool next_keep = tid + 1 < F && ((km >> (tid + 1)) & 1ull);
+        const bool next_start = tid + 1 < F && ((sm >> (tid + 1)) & 1ull);
+        const uint32_t run = (uint32_t)__popcll(sm & (lt | (1ull << tid))) - 1u;
+        if (keep) {
+            p_fs[np] = fs;
+            p_fe[np] = fe;
+            p_po[np] = po;
+            p_pe[np] = pe;
+            p_kw[np] = kw;
+            if (start) {
+                run_lo[run] = fs;
+                run_p0[run] = np;
             }
-            if (nrun && run_hi[nrun - 1] == p_fs[np]) {
-                run_hi[nrun - 1] = p_fe[np];
-                run_p1[nrun - 1] = np + 1;
-            } else {
-                run_lo[nrun] = p_fs[np];
-                run_hi[nrun] = p_fe[np];
-                run_p0[nrun] = np;
-                run_p1[nrun] = np + 1;
-                ++nrun;
+            if (!next_keep || next_start) {   // the run's last frame: its end and chunk count
+                run_hi[run] = fe;
+                run_p1[run] = np + 1;
             }
-            ++np;
         }
-        for (uint32_t k = 0; k < nrun; ++k) {
-            run_c0[k] = nc;
-            if (run_hi[k] > run_lo[k]) nc += (uint32_t)(((run_hi[k] - 1) >> 4) - (run_lo[k] >> 4) + 1);
+        // chunks per run (lane k holds run k's), exclusive scan across the wave
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nrun = (uint32_t)__popcll(sm);
+        uint32_t cnt = 0;
+        if (tid < nrun && run_hi[tid] > run_lo[tid])
+            cnt = (uint32_t)(((run_hi[tid] - 1) >> 4) - (run_lo[tid] >> 4) + 1);
+        uint32_t inc = cnt;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (tid >= d) inc += o;
         }
-        run_c0[nrun] = nc;
-        s_nrun = nrun;
+        if (tid <= nrun) run_c0[tid] = inc - cnt;   // lane nrun: the total
+        if (tid == F - 1 && nrun == F) run_c0[F] = inc;
+        if (tid == 0) s_nrun = nrun;
     }
     __syncthreads();
 
@@ -1622,45 +1633,49 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
         }
     }
 
-    // 3. segments whose frames are now all processed: tails, carry-outs, verdict
-    __threadfence();
+    // 3. segments whose frames are now all processed: tails, carry-outs, verdict.
+    // What the finishing workgroup needs from the others travels by atomics
+    // only (first_fail, done_cnt, ctl): hypothesised header bytes are never
+    // XORed, and the XORed payloads, records and carries are read by later
+    // launches (stream order).  So no agent-scope fence here -- on gfx950 one
+    // writes back the whole XCD L2 (buffer_wbl2), per workgroup -- only this
+    // workgroup's own memory operations completed (atomicMin performed)
+    // before its done_cnt increment.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
-    if (tid == 0) {
-        uint32_t nc2 = 0;
-        if (!a.undo) {
-            uint32_t t = 0;
-            while (t < F) {
-                const uint32_t s = r_seg[t];
-                uint64_t units = 0;
-                bool tail_only = false;
-                uint32_t t2 = t;
-                for (; t2 < F && r_seg[t2] == s && r_type[t2] != 0; ++t2) {
-                    if (r_type[t2] == 1 || r_type[t2] == 2) ++units;
-                    if (r_type[t2] == 3) {
-                        const dfmid m = a.fmid[s];
-                        if (m.n_a + m.nwhole == 0) tail_only = true;
-                    }
-                }
-                if (t2 == t) break;   // past the last record
-                if (units) {
-                    const dfmid m = a.fmid[s];
-                    const uint64_t old = atomicAdd((unsigned long long*)&a.done_cnt[s], (unsigned long long)units);
-                    if (old + units == m.n_a + m.nwhole) comp_seg[nc2++] = s;
-                } else if (tail_only) {
-                    comp_seg[nc2++] = s;
-                }
-                t = t2;
-            }
-        } else {
-            // undo: the tail of every segment whose last record is here
-            for (uint32_t t = 0; t < F; ++t) {
-                if (r_type[t] == 0) break;
-                const uint32_t s = r_seg[t];
-                if (w * F + t == a.bases[s] + a.est[s] - 1) comp_seg[nc2++] = s;
+    if (tid < F) {
+        // segments finished here: per segment group of lanes (same segment,
+        // a record), its leader adds the group's carried-in + whole frames to
+        // done_cnt; the one completing the count finishes the segment.  A
+        // segment whose only record is its tail is finished by that lane.
+        // Undo: the tail of every segment whose last record is here.
+        const bool valid = type != 0;
+        const uint64_t lt = tid ? (~0ull >> (64 - tid)) : 0ull;
+        const uint32_t prev_s = (uint32_t)__shfl_up((int)s, 1, 64);
+        const uint64_t vm = __ballot(valid);
+        const bool prev_valid = tid > 0 && ((vm >> (tid - 1)) & 1ull);
+        const bool lead = valid && !(prev_valid && prev_s == s);
+        const uint64_t lm = __ballot(lead);
+        const uint64_t um = __ballot(type == 1 || type == 2);
+        bool comp = false;
+        if (a.undo) {
+            comp = valid && w * F + tid == a.bases[s] + a.est[s] - 1;
+        } else if (lead) {
+            // the group: lanes [tid, next leader or first lane without a record)
+            const uint64_t after = tid + 1 < F ? (~0ull << (tid + 1)) : 0ull;
+            const uint64_t stop = (lm | ~vm) & after;
+            const uint64_t grp = (stop ? ((stop & (0ull - stop)) - 1ull) : ~0ull) & ~lt;
+            const uint64_t units = (uint64_t)__popcll(um & grp);
+            if (units) {
+                const uint64_t old = atomicAdd((unsigned long long*)&a.done_cnt[s], (unsigned long long)units);
+                comp = old + units == n_units;
+            } else {
+                comp = n_units == 0;   // the tail alone
             }
         }
-        s_ncomp = nc2;
-        __threadfence();
+        const uint64_t cm = __ballot(comp);
+        if (comp) comp_seg[__popcll(cm & lt)] = s;
+        if (tid == 0) s_ncomp = (uint32_t)__popcll(cm);
     }
     __syncthreads();
     const uint32_t ncomp = s_ncomp;
@@ -1685,7 +1700,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(fused_args a) {
                 fused_apply(a.rx, c, mlo, mhi, c >= lo && c + 16 <= hi);
             }
         }
-        __threadfence();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         if (tid == 0 && !a.undo) {
             const uint64_t old = atomicAdd((unsigned long long*)&a.ctl->segs_done, 1ull);
