@@ -252,11 +252,14 @@ int hvws_last_scan_path(hvws_ctx* ctx);
  * frames, carries and bytes are as the contract says whenever they can be
  * observed.  A batch whose frames did not all have that size is undone (the
  * pass again, XOR being its own inverse) and re-run on the exact path; so is
- * a batch queued behind it.  mode: 2 when the last scan says uniform (the
- * default; a COUNT_EMIT scan's verdict is read once the device has published
- * it, without a wait, and after a failed pass the next 16 batches scan
- * exactly), 0 off, 1 try on every step (tests), -1 back to $HVWS_FUSED (or
- * 2).  Returns the previous mode. */
+ * a batch queued behind it.  mode: 2 when the last scan says uniform (a
+ * COUNT_EMIT scan's verdict is read once the device has published it,
+ * without a wait; after a failed or declined pass the next 16 batches scan
+ * exactly; frames must average 64 B - 16 KiB and segments be sorted and
+ * disjoint), 0 off (the default: the pass measures slower than SPEC's
+ * overlapped discovery + k_unmask at config 2), 1 try on
+ * every step (tests), -1 back to $HVWS_FUSED (or 0).  Returns the previous
+ * mode. */
 int hvws_set_fused(hvws_ctx* ctx, int mode);
 /* out = {fused steps issued, batches re-run on the exact path}. */
 int hvws_fused_stats(hvws_ctx* ctx, uint64_t out[2]);

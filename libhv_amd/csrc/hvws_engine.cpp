@@ -273,7 +273,7 @@ struct hvws_ctx {
     // the gate word the next k_fused reads
     struct fused_pend {
         bool active = false;
-        uint64_t seq = 0, nwg = 0;
+        uint64_t seq = 0;
         uint8_t* rx = nullptr;
         uint64_t rx_len = 0;
         bool piped = false;
@@ -1603,14 +1603,22 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
 // exactly too.
 constexpr int HVWS_PATH_FUSED_INTERNAL = 7;
 
-// 0 off, 1 on every step, 2 when the last scan says uniform ($HVWS_FUSED for -1; default 2)
+// 0 off, 1 on every step, 2 when the last scan says uniform ($HVWS_FUSED for
+// -1; default 0: measured slower than SPEC + k_unmask at config 2)
 int fused_mode(hvws_ctx* c) {
     if (c->fused_mode >= 0) return c->fused_mode;
-    static const int env = getenv("HVWS_FUSED") ? atoi(getenv("HVWS_FUSED")) : 2;
-    return env < 0 ? 2 : (env > 2 ? 2 : env);
+    static const int env = getenv("HVWS_FUSED") ? atoi(getenv("HVWS_FUSED")) : 0;
+    return env < 0 ? 0 : (env > 2 ? 2 : env);
 }
 
-bool fused_eligible(hvws_ctx* c, uint64_t rx_len, uint32_t nseg) {
+// k_ftile finds a tile's segments by offset: they must be sorted and disjoint
+bool segments_sorted(const hvws_segment* segs, uint32_t nseg) {
+    for (uint32_t i = 1; i < nseg; ++i)
+        if (segs[i].off < segs[i - 1].off + segs[i - 1].len) return false;
+    return true;
+}
+
+bool fused_eligible(hvws_ctx* c, uint64_t rx_len, const hvws_segment* segs, uint32_t nseg) {
     const int mode = fused_mode(c);
     if (mode == 0 || nseg == 0 || c->vmask) return false;
     if (c->nfr_known) c->fz_nfr = c->nfr;   // the last exact count (a pending fused batch has none yet)
@@ -1632,7 +1640,7 @@ bool fused_eligible(hvws_ctx* c, uint64_t rx_len, uint32_t nseg) {
             }
         }
     }
-    if (mode == 1) return true;   // tests: whatever the last scan said
+    if (mode == 1) return segments_sorted(segs, nseg);   // tests: whatever the last scan said
     if (c->fz_skip) {   // a fused pass failed recently
         --c->fz_skip;
         return false;
@@ -1640,7 +1648,8 @@ bool fused_eligible(hvws_ctx* c, uint64_t rx_len, uint32_t nseg) {
     if (nseg < 2 || !c->spec_ok || c->fz_nfr == 0) return false;
     // small frames only: at 64 KiB frames the separate scan is 0.6 % of a
     // step and k_unmask's tile geometry is at the in-place ceiling
-    return rx_len / c->fz_nfr <= (16u << 10);
+    const uint64_t avg = rx_len / c->fz_nfr;
+    return avg <= (16u << 10) && avg >= kFusedTile / kFusedMaxSpans && segments_sorted(segs, nseg);
 }
 
 int fused_wait(hvws_ctx* c, int set, uint64_t seq, dspec_status& out) {
@@ -1665,8 +1674,7 @@ int fused_wait(hvws_ctx* c, int set, uint64_t seq, dspec_status& out) {
     }
 }
 
-fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint64_t seq, bool undo,
-                         uint64_t nwg) {
+fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint64_t seq, bool undo) {
     tset& T = c->ts[set];
     fused_args a;
     a.rx = d_rx;
@@ -1679,7 +1687,8 @@ fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, u
     a.first_fail = T.sc_fail.as<uint64_t>();
     a.done_cnt = T.f_done.as<uint64_t>();
     a.ctl = T.f_ctl.as<dfctl>();
-    a.wg_seg = T.f_wgseg.as<uint32_t>();
+    a.tiles = T.f_wgseg.as<dftile>();
+    a.ntiles = (rx_len + kFusedTile - 1) / kFusedTile;
     a.fr.hdr_off = T.f_hdr.as<int64_t>();
     a.fr.pay_off = T.f_off.as<uint64_t>();
     a.fr.pay_len = T.f_len.as<uint64_t>();
@@ -1687,8 +1696,7 @@ fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, u
     a.fr.key = T.f_key.as<uint32_t>();
     a.fr.keyrot = T.f_keyrot.as<uint32_t>();
     a.fr.info = T.f_info.as<uint32_t>();
-    // records the launch covers: an estimate past them declines the pass
-    a.fr.cap = std::min<uint64_t>(T.frame_cap, nwg * kFusedRecords);
+    a.fr.cap = T.frame_cap;   // an estimate past the table declines the pass
     a.carry_out = T.carry_out.as<dcarry>();
     a.counts = T.counts.as<uint64_t>();
     a.gate = c->fz_gate.as<uint64_t>();
@@ -1697,6 +1705,8 @@ fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, u
     a.nseg = nseg;
     a.vmask = c->vmask;
     a.undo = undo ? 1u : 0u;
+    static const uint32_t dbg = getenv("HVWS_FUSED_DBG") ? (uint32_t)atoi(getenv("HVWS_FUSED_DBG")) : 0u;
+    a.dbg = dbg;
     return a;
 }
 
@@ -1737,9 +1747,10 @@ int fused_settle(hvws_ctx* c, int set) {
     // failed (or gated): undo what the pass XORed, clear the gate, re-run exactly
     ++c->fused_fixes;
     c->spec_ok = false;
-    // a real misprediction (not a batch larger than the launch, not one gated
-    // behind a failure): auto mode scans exactly for a while
-    if (!(v.flags & (FUSED_GATED | FUSED_UNTOUCHED))) c->fz_skip = kFusedBackoff;
+    // a real misprediction or frames too small for the tiles (not a batch
+    // larger than the table, not one gated behind a failure): auto mode scans
+    // exactly for a while
+    if (!(v.flags & (FUSED_GATED | FUSED_UNTOUCHED)) || (v.flags & FUSED_DECLINED)) c->fz_skip = kFusedBackoff;
     hvws_ctx::fused_pend newer;
     const int other = set ^ 1;
     const bool has_newer = c->fz[other].active && set != c->cur;   // issued behind it, gated
@@ -1748,8 +1759,8 @@ int fused_settle(hvws_ctx* c, int set) {
         c->fz[other].active = false;
     }
     if (!(v.flags & FUSED_UNTOUCHED)) {
-        const fused_args a = fused_args_of(c, set, p.rx, p.rx_len, (uint32_t)p.segs.size(), p.seq, true, p.nwg);
-        HIP_OR(launch_fused(a, p.nwg, c->stream), HVWS_EHIP);
+        const fused_args a = fused_args_of(c, set, p.rx, p.rx_len, (uint32_t)p.segs.size(), p.seq, true);
+        HIP_OR(launch_fused(a, c->stream), HVWS_EHIP);
     }
     HIP_OR(hipMemsetAsync(c->fz_gate.p, 0, 8, c->stream), HVWS_EHIP);
     c->cur = set ^ 1;   // the exact scan takes the set after this one's (it flips)
@@ -1797,9 +1808,7 @@ int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
     // size: with growth room on top, the two sets would ratchet each other up.
     const uint64_t want = std::max<uint64_t>(c->fz_nfr + c->fz_nfr / 8 + 64, 1024);
     HIP_OR(ensure_frames(c, want, /*exact=*/true), HVWS_ENOMEM);
-    // workgroups for the expected records only (a table sized for a larger
-    // batch would launch idle workgroups by the million)
-    const uint64_t nwg = std::min<uint64_t>(T.frame_cap, want) / kFusedRecords + 1;
+    const uint64_t ntiles = (rx_len + kFusedTile - 1) / kFusedTile;
     HIP_OR(T.counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(T.bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(T.total.ensure(8), HVWS_ENOMEM);
@@ -1809,7 +1818,7 @@ int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
     HIP_OR(T.f_fmid.ensure((uint64_t)nseg * sizeof(dfmid) + 64), HVWS_ENOMEM);
     HIP_OR(T.f_done.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
     HIP_OR(T.f_ctl.ensure(sizeof(dfctl)), HVWS_ENOMEM);
-    HIP_OR(T.f_wgseg.ensure(nwg * 4 + 64), HVWS_ENOMEM);
+    HIP_OR(T.f_wgseg.ensure(ntiles * sizeof(dftile) + 64), HVWS_ENOMEM);
     HIP_OR(T.f_segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
     HIP_OR(T.f_carry.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
     c->h_fstatus.flags = hipHostMallocCoherent;
@@ -1837,16 +1846,17 @@ int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
     c->up_src_segs = nullptr;
     c->up_src_carry = nullptr;
     HIP_OR(launch_offsets(T.sc_est.as<uint64_t>(), T.bases.as<uint64_t>(), nseg, T.total.as<uint64_t>(), ps), HVWS_EHIP);
-    HIP_OR(launch_fwgseg(T.bases.as<uint64_t>(), T.sc_est.as<uint64_t>(), nseg, T.f_wgseg.as<uint32_t>(), nwg, ps),
+    HIP_OR(launch_ftile(d_rx, T.f_segs.as<dseg>(), T.f_fmid.as<dfmid>(), T.sc_est.as<uint64_t>(),
+                        T.bases.as<uint64_t>(), nseg, rx_len, T.f_wgseg.as<dftile>(), T.f_ctl.as<dfctl>(), ps),
            HVWS_EHIP);
     if (piped) {
         HIP_OR(hipEventRecord(c->scan_done, ps), HVWS_EHIP);
         HIP_OR(hipStreamWaitEvent(c->stream, c->scan_done, 0), HVWS_EHIP);
     }
     const uint64_t seq = ++c->scan_seq;
-    const fused_args a = fused_args_of(c, c->cur, d_rx, rx_len, nseg, seq, false, nwg);
+    const fused_args a = fused_args_of(c, c->cur, d_rx, rx_len, nseg, seq, false);
     const bool timed = step_events(c) >= 1;
-    HIP_OR(launch_fused(a, nwg, c->stream, timed ? c->tev[c->t_cur][2] : nullptr, timed ? c->tev[c->t_cur][3] : nullptr),
+    HIP_OR(launch_fused(a, c->stream, timed ? c->tev[c->t_cur][2] : nullptr, timed ? c->tev[c->t_cur][3] : nullptr),
            HVWS_EHIP);
     if (timed) c->t_rec[c->t_cur] |= (uint8_t)(4u | 8u);
     c->t_unmask[c->t_cur] = true;
@@ -1862,7 +1872,6 @@ int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
     hvws_ctx::fused_pend& p = c->fz[c->cur];
     p.active = true;
     p.seq = seq;
-    p.nwg = nwg;
     p.rx = d_rx;
     p.rx_len = rx_len;
     p.piped = piped;
@@ -2243,7 +2252,7 @@ int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_s
     if (rc) return rc;
     if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
-    if (fused_eligible(c, rx_len, nseg)) {
+    if (fused_eligible(c, rx_len, segs, nseg)) {
         if (!c->piped) {
             for (tset& t : c->ts) {
                 HIP_OR(hipEventRecord(t.free_ev, c->stream), HVWS_EHIP);
@@ -2280,7 +2289,7 @@ int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* s
     if (rc) return rc;
     if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
-    if (fused_eligible(c, rx_len, nseg)) {
+    if (fused_eligible(c, rx_len, segs, nseg)) {
         c->cs = c->stream;
         c->piped = false;
         return fused_issue(c, d_rx, rx_len, segs, carry_in, nseg, false);

@@ -296,16 +296,34 @@ struct dfmid {
     int64_t  ra_hdr;    // the carried-in frame's record, segment-relative
     uint64_t ra_off, ra_len, ra_length;
     uint32_t ra_key, ra_info;
+    uint64_t a_po, a_pe; // the carried-in frame's masked payload span (rx offsets; empty: none)
+    uint64_t t_po, t_pe; // the tail frame's masked payload bytes in the segment
+    uint32_t a_kw, t_kw; // their 4-byte-aligned key words
 };
 struct dfctl {          // per table set, zeroed before k_fprep
-    uint64_t segs_done; // segments finished (k_fprep: no records; k_fused: the rest)
+    uint64_t segs_done; // k_ffinish workgroups done (the last publishes)
     uint64_t fail;      // a segment's hypothesis or count failed
-    uint64_t pad[6];
+    uint64_t decline;   // k_ftile: a tile's segments or spans exceed its LDS (the batch runs exactly)
+    uint64_t pad[5];
 };
-constexpr uint32_t kFusedRecords = 64;    // records per k_fused workgroup (one per lane of wave 0)
-constexpr uint32_t kFusedThreads = 256;
+constexpr uint32_t kFusedT = 512, kFusedU = 2;   // k_fused tile geometry (k_unmask<512,2>)
+constexpr uint64_t kFusedTile = (uint64_t)kFusedT * kFusedU * 16u;
+constexpr uint32_t kFusedMaxSegs = 64;    // segments per tile
+constexpr uint32_t kFusedMaxSpans = 256;  // payload spans per tile (frames >= 64 B on average)
+constexpr uint32_t FUSED_NOSEG = 0xFFFFFFFFu;
+struct dftile {            // per k_fused tile (k_ftile): its first segment's frames here
+    uint64_t j_lo, nj;     // whole frames overlapping the tile
+    uint64_t w0, stride, nwhole, rec0, off;   // the segment's hypothesis, record of whole frame 0, its offset
+    uint64_t a_po, a_pe, t_po, t_pe;          // its carried-in / tail payload spans (fmid)
+    uint64_t sp_po, sp_pe; // the masked payload span of the whole frame the tile starts inside (empty: none)
+    uint32_t a_kw, t_kw, sp_kw;
+    uint32_t s0;           // the first segment ending after the tile's start; FUSED_NOSEG: no segment bytes
+    uint32_t nin;          // segments with bytes in the tile
+    uint32_t fl;           // 1: carried-in span here, 2: tail span here, 4: s0 starts here, 8: s0 has records
+};
 constexpr uint32_t FUSED_GATED = 8u;      // status flag: not run (the previous fused batch failed)
 constexpr uint32_t FUSED_UNTOUCHED = 16u; // status flag: failed before any byte was XORed
+constexpr uint32_t FUSED_DECLINED = 32u;  // status flag (with UNTOUCHED): a tile's frames do not fit its LDS
 struct fused_args {
     uint8_t*        rx;
     uint64_t        rx_len;
@@ -317,7 +335,8 @@ struct fused_args {
     uint64_t*       first_fail;
     uint64_t*       done_cnt;
     dfctl*          ctl;
-    const uint32_t* wg_seg;
+    const dftile*   tiles;      // k_ftile: per tile, its first segment and the span it starts inside
+    uint64_t        ntiles;
     dframes         fr;
     dcarry*         carry_out;
     uint64_t*       counts;
@@ -327,14 +346,16 @@ struct fused_args {
     uint32_t        nseg;
     uint32_t        vmask;
     uint32_t        undo;
+    uint32_t        dbg;        // $HVWS_FUSED_DBG (probes): 2 no header parse, 4 no record stores, 8 loads only, 64 no data stores, 128 no header windows
 };
 hipError_t launch_fprep(const uint8_t* rx, uint64_t rx_len, const dseg* src_segs, const dcarry* src_carry, dseg* segs_w,
                         dcarry* carry_w, uint32_t nseg, dfmid* fmid, uint64_t* est, uint64_t* first_fail,
                         uint64_t* done_cnt, dcarry* carry_out, uint64_t* counts, dfctl* ctl, uint32_t vmask,
                         hipStream_t st);
-hipError_t launch_fwgseg(const uint64_t* bases, const uint64_t* est, uint32_t nseg, uint32_t* wg_seg, uint64_t nwg,
-                         hipStream_t st);
-hipError_t launch_fused(const fused_args& a, uint64_t nwg, hipStream_t st, hipEvent_t ev_start = nullptr,
+hipError_t launch_ftile(const uint8_t* rx, const dseg* segs, const dfmid* fmid, const uint64_t* est,
+                        const uint64_t* bases, uint32_t nseg, uint64_t rx_len, dftile* tiles, dfctl* ctl,
+                        hipStream_t st);
+hipError_t launch_fused(const fused_args& a, hipStream_t st, hipEvent_t ev_start = nullptr,
                         hipEvent_t ev_stop = nullptr);
 
 // Resident small-path worker ("door", k_door): one workgroup that stays on

@@ -963,14 +963,28 @@ def test_fused_uniform_batches(eng, piped):
     try:
         rng = random.Random(909)
         for size, nframes, nseg in ((1024, 900, 13), (100, 3000, 64), (0, 500, 5), (125, 700, 70), (3000, 300, 4),
-                                    (7, 2000, 9)):
+                                    (7, 2000, 9), (30, 2000, 9), (15000, 40, 3)):
             buf, segs, carries = _cut_uniform(rng, nframes, size, nseg)
             exp = _oracle_batch(buf, segs, carries)
             _check_step(eng, buf, segs, carries, False, exp)      # exact: learns that the estimates hold
             before = _fused_stats(eng)
             path = _check_step(eng, buf, segs, carries, piped, exp)
             after = _fused_stats(eng)
-            assert path == 7 and after[0] == before[0] + 1 and after[1] == before[1], (size, path, before, after)
+            if size + 6 < 64:
+                # frames this small are not tried (auto); forced, where a
+                # 16 KiB tile holds more of them than its LDS span list, the
+                # pass declines untouched and the batch runs exactly
+                assert path != 7 and after == before, (size, path)
+                L.hvws_set_fused(eng.ctx, 1)
+                path = _check_step(eng, buf, segs, carries, piped, exp)
+                L.hvws_set_fused(eng.ctx, 2)
+                after2 = _fused_stats(eng)
+                if min(nframes, 16384 // (size + 6)) > 256:   # a tile's frames overflow its LDS list
+                    assert path != 7 and after2[0] == after[0] + 1 and after2[1] == after[1] + 1, (size, path)
+                else:
+                    assert path == 7 and after2[0] == after[0] + 1 and after2[1] == after[1], (size, path)
+            else:
+                assert path == 7 and after[0] == before[0] + 1 and after[1] == before[1], (size, path, before, after)
     finally:
         L.hvws_set_fused(eng.ctx, old)
 
@@ -1070,30 +1084,29 @@ def test_fused_pipelined_failure_between_batches(eng):
         assert np.array_equal(frames[f], exp_recs[f]), f
 
 
-def test_fused_grown_batch_declines(eng):
-    """A batch with many more records than the last one: the fused launch
-    covers the expected records only, so the pass declines untouched and the
-    batch runs exactly; the next one of that size takes the FUSED path."""
+def test_fused_grown_batch(eng):
+    """A batch with many more records than the last one: the frame table is
+    sized from the last count, so the pass declines untouched (and the batch
+    runs exactly) when the table cannot hold its estimate, and runs fused when
+    it can; either way the results are exact, and the next batch of that size
+    takes the FUSED path with no re-run."""
     L = libhv_amd.lib()
     rng = random.Random(515)
     small = _cut_uniform(rng, 150, 1024, 6)
     big = _cut_uniform(rng, 3000, 1024, 6)
     old = L.hvws_set_fused(eng.ctx, 1)
     try:
-        L.hvws_set_fused(eng.ctx, 0)
-        _check_step(eng, *small, False)
-        L.hvws_set_fused(eng.ctx, 1)
         for piped in (False, True):
-            b0 = _fused_stats(eng)
-            _check_step(eng, *big, piped)
-            b1 = _fused_stats(eng)
-            assert b1[0] == b0[0] + 1 and b1[1] == b0[1] + 1, (b0, b1)   # declined, then exact
-            path = _check_step(eng, *big, piped)
-            b2 = _fused_stats(eng)
-            assert path == 7 and b2[0] == b1[0] + 1 and b2[1] == b1[1], (b1, b2)
             L.hvws_set_fused(eng.ctx, 0)
             _check_step(eng, *small, False)
             L.hvws_set_fused(eng.ctx, 1)
+            b0 = _fused_stats(eng)
+            _check_step(eng, *big, piped)
+            b1 = _fused_stats(eng)
+            assert b1[0] == b0[0] + 1 and b1[1] - b0[1] in (0, 1), (b0, b1)
+            path = _check_step(eng, *big, piped)
+            b2 = _fused_stats(eng)
+            assert path == 7 and b2[0] == b1[0] + 1 and b2[1] == b1[1], (b1, b2)
     finally:
         L.hvws_set_fused(eng.ctx, old)
 
