@@ -564,7 +564,7 @@ def tx_leg(eng, plan, dp, rx, rx_plain: bool, segs, tpath: str) -> dict:
     ok = eng.synth(out_buf, plan.total, plan.seed, dp, 1) == 0
     tx_alg = plan.payload_bytes + plan.total
     tx_ach = tx_alg / (float(np.mean(tms[1:])) * 1e-3) / 1e9
-    bname = libhv_amd.lib().hvws_build_kernel_name().decode()
+    bname = libhv_amd.lib().hvws_last_build_kernel(eng.ctx).decode()
     tx_traffic = None
     if os.path.exists(tpath):
         ent = json.load(open(tpath)).get(bname, {}).get(str(plan.total))

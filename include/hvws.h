@@ -302,6 +302,13 @@ int hvws_build_frames(hvws_ctx* ctx, uint8_t* d_out, uint64_t out_cap, const uin
  * hvws_build_frames or hvws_encode_keys kernel; the build kernel's name. */
 int hvws_last_kernel_ms(hvws_ctx* ctx, float* ms);
 const char* hvws_build_kernel_name(void);
+/* The kernel the last hvws_build_frames on ctx ran: the general k_build, or
+ * k_build_id when every frame's payload sat at its output offset in the
+ * payload buffer (pay_off[i] == out_off[i] + header length, e.g. a relay
+ * re-framing the batch it received): then the source bytes of every output
+ * chunk are known before its frames, as in the unmask.
+ * Results never depend on it. */
+const char* hvws_last_build_kernel(hvws_ctx* ctx);
 
 /* ---- handshake, device resident --------------------------------------- */
 /* Sec-WebSocket-Accept for n upgrade requests: accept + 32*i receives the 28

@@ -163,3 +163,71 @@ def test_build_roundtrip_batch(eng, name, plan):
             b.free()
         dp.free()
         tx.free()
+
+
+def _gpu_build_same_offset(eng, frames, rng, move=None):
+    """Payloads placed where the output puts them (k_build_id's layout), the
+    bytes between them (the headers' places) random junk the build must not
+    copy; `move` = a frame index whose payload is moved one byte instead."""
+    L = libhv_amd.lib()
+    flags = [f for f, _, _ in frames]
+    mask = [int.from_bytes(k, "little") if k else 0 for _, _, k in frames]
+    lens = [len(p) for _, p, _ in frames]
+    sizes = synth.frame_size(np.array(flags, dtype=np.uint8), np.array(lens, dtype=np.uint64))
+    total = int(sizes.sum())
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    hdr = sizes - np.array(lens, dtype=np.uint64)
+    offs = (starts + hdr.astype(np.int64)).tolist()
+    pay = bytearray(rng.integers(0, 256, total + 32, dtype=np.uint8).tobytes())
+    for i, (_, p, _k) in enumerate(frames):
+        o = offs[i] + (1 if move == i else 0)
+        pay[o:o + len(p)] = p
+        offs[i] = o
+    payload = eng.to_device(np.frombuffer(bytes(pay), dtype=np.uint8))
+    tx = libhv_amd.TxPlan(eng, offs, lens, flags, mask)
+    out = eng.alloc(total + 64)
+    try:
+        n = eng.build_frames(out, total + 64, payload, len(pay), tx)
+        assert n == total
+        got = bytes(out.download(n))
+        kern = L.hvws_last_build_kernel(eng.ctx).decode()
+    finally:
+        for b in (payload, out):
+            b.free()
+        tx.free()
+    return got, kern
+
+
+@pytest.mark.parametrize("kind", ["random", "small", "edges", "tiny", "large", "unmasked"])
+def test_build_same_offset_layout(eng, kind):
+    """Every payload already at its output offset: k_build_id (the source
+    bytes of each output chunk loaded before its frames are known), frame by
+    frame against the reference -- headers written over the junk between
+    payloads, keys at every phase, tiles with more frames than LDS holds
+    (tiny) taking its chunk-by-chunk fallback."""
+    rng = np.random.default_rng(hash(kind) & 0xFFFF)
+    if kind == "random":
+        frames = _frames(rng, 400)
+    elif kind == "small":
+        lens = np.concatenate([rng.integers(0, 20, 300), rng.integers(120, 130, 100), rng.integers(1000, 2019, 300)])
+        rng.shuffle(lens)
+        frames = _frames(rng, len(lens), lens=lens)
+    elif kind == "edges":
+        frames = _frames(rng, len(EDGE_LENS), lens=EDGE_LENS, p_mask=0.5)
+    elif kind == "tiny":
+        frames = _frames(rng, 20000, lens=rng.integers(0, 3, 20000))
+    elif kind == "large":
+        frames = _frames(rng, 12, lens=[1 << 20] * 4 + [(1 << 20) + 3] * 4 + [200003] * 4, p_mask=0.7)
+    else:
+        frames = _frames(rng, 300, p_mask=0.0)
+    got, kern = _gpu_build_same_offset(eng, frames, rng)
+    assert got == H.build_frames_ref(frames)
+    assert kern.startswith("k_build_id"), kern
+
+
+def test_build_one_moved_payload_takes_general_kernel(eng):
+    rng = np.random.default_rng(99)
+    frames = _frames(rng, 200, lens=rng.integers(1, 3000, 200))
+    got, kern = _gpu_build_same_offset(eng, frames, rng, move=137)
+    assert got == H.build_frames_ref(frames)
+    assert not kern.startswith("k_build_id"), kern
