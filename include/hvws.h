@@ -191,6 +191,20 @@ uint64_t hvws_set_sieve_min(uint64_t bytes);
  * chain; out[3] = segment offset where the exact walk resumed. */
 int hvws_last_sieve(hvws_ctx* ctx, uint64_t out[4]);
 
+/* Frame-sieve windows.  A long stream of large frames is sieved only over the
+ * first `window_bytes` of every region of about `hops` mean-sized frames (the
+ * mean from the context's last exact count of a one-segment scan); the chain's
+ * link walks cross the rest of each region frame by frame, so the sieve reads
+ * window / region of the bytes instead of all of them.  hops = 0 sieves every
+ * position (the round-2 behaviour).  Process-wide tuning (default 64 and
+ * 1 MiB + 16 KiB; $HVWS_SIEVE_HOPS, $HVWS_SIEVE_WINDOW; window 0 = default);
+ * results never depend on it.  prev (may be NULL) receives the old values. */
+void hvws_set_sieve_windows(uint64_t hops, uint64_t window_bytes, uint64_t prev[2]);
+
+/* Window geometry of the last sieved scan on ctx, in 8 KiB tiles: out[0] =
+ * region, out[1] = window (equal: every tile sieved; 0, 0: no sieve ran). */
+int hvws_last_sieve_windows(hvws_ctx* ctx, uint64_t out[2]);
+
 /* Verify after every scan that frame ends (pay_off + pay_len) never
  * decrease over the table -- the invariant the unmask tile index is built on
  * -- and fail the scan with HVWS_EINVAL otherwise.  Costs one device sync

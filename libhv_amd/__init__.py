@@ -178,6 +178,8 @@ _SIGS = {
     "hvws_set_sieve_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_table_checks": (ctypes.c_int, [ctypes.c_int]),
     "hvws_last_sieve": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_set_sieve_windows": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_last_sieve_windows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_last_build_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     "hvws_span_begin": (ctypes.c_int, [ctypes.c_void_p]),

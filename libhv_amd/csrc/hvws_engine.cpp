@@ -203,7 +203,7 @@ struct hvws_ctx {
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
     // after each sieved scan (read as hints by the next one).
-    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_rank, sv_cnt, sv_tmp;
+    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_hops, sv_rank, sv_cnt, sv_tmp;
     uint64_t sv_cap = 0, sv_capc = 0;
     uint64_t sv_hint_pre = 0, sv_hint_surv = 0;   // counts of the latest sieved scan read back
     hbuf h_sv;
@@ -211,6 +211,9 @@ struct hvws_ctx {
     bool sv_ran = false;       // the last scan launched the sieve
     hipEvent_t sv_ev = nullptr;   // h_sv holds the last sieved scan's state once this has completed
     uint64_t sv_gen = 0;       // sieve_generation() the history below belongs to
+    uint64_t sv_win_len = 0;   // segment length of the last sieved scan if it sieved windows only, else 0
+    uint32_t sv_full_left = 0; // scans left that sieve every tile (a windowed chain fell short)
+    uint32_t sv_rt = 0, sv_wt = 0;   // window geometry of the last sieved scan (tiles)
     // hvws_pipeline: its three device slots and their events, kept across
     // calls (a per-call hipMalloc/hipFree pair cost the first call ~2x)
     dbuf pipe_slot[3], pipe_segs;
@@ -489,6 +492,11 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
         const bool counted = surv <= pre && pre <= c->sv_cap;   // else it overflowed and never counted survivors
         c->sv_hint_pre = pre;
         c->sv_hint_surv = counted ? surv : 0;
+        // A windowed chain that stopped well before the end (a walk hit its
+        // frame cap, or traffic changed): the next 15 scans sieve every tile.
+        const dsieve* d = c->h_sv.as<dsieve>();
+        if (c->sv_win_len && d->active && (!d->use || d->pend + (4ull << 20) < c->sv_win_len)) c->sv_full_left = 15;
+        c->sv_win_len = 0;
     }
     const uint64_t seen = c->sv_hint_pre, seen_s = c->sv_hint_surv;
     // Capacity from the last sieved scan's entry count when there is one (the
@@ -518,6 +526,7 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     HIP_OR(c->sv_J0.ensure(capc * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_J1.ensure(capc * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_mark.ensure(capc * 8), HVWS_ENOMEM);
+    HIP_OR(c->sv_hops.ensure(capc * 4), HVWS_ENOMEM);
     HIP_OR(c->sv_rank.ensure(capc * 8), HVWS_ENOMEM);
     HIP_OR(c->sv_cnt.ensure(32), HVWS_ENOMEM);
     HIP_OR(c->sv_tmp.ensure((4 * ((nmax + 1023) / 1024) + 64) * 8), HVWS_ENOMEM);
@@ -533,6 +542,7 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     b.J0 = c->sv_J0.as<uint32_t>();
     b.J1 = c->sv_J1.as<uint32_t>();
     b.mark = c->sv_mark.as<uint64_t>();
+    b.hops = c->sv_hops.as<uint32_t>();
     b.rank = c->sv_rank.as<uint64_t>();
     b.m_total = c->sv_cnt.as<uint64_t>();
     b.npath = c->sv_cnt.as<uint64_t>() + 1;
@@ -541,6 +551,15 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     b.capC = capc;
     b.keep = c->sv_keep.as<uint64_t>();
     b.kbase = c->sv_kbase.as<uint64_t>();
+    if (c->sv_full_left) {
+        --c->sv_full_left;
+        b.rt = b.wt = 1;
+    } else {
+        sieve_geometry(rx_len, c->single_hint, b.rt, b.wt);
+    }
+    c->sv_win_len = b.rt != b.wt ? rx_len : 0;
+    c->sv_rt = b.rt;
+    c->sv_wt = b.wt;
     return HVWS_OK;
 }
 
@@ -763,6 +782,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             c->sv_skip = 0;
             c->sv_ran = false;
             c->sv_hint_pre = c->sv_hint_surv = 0;
+            c->sv_win_len = 0;
+            c->sv_full_left = 0;
         }
         if (rx_len >= sieve_min()) {
             if (sieve_state_ready(c) && c->h_sv.as<dsieve>()->active == 0 && c->sv_skip == 0) c->sv_skip = 15;
@@ -779,7 +800,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                     (void)hipGetLastError();
                     for (dbuf* b : {&c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
                                     &c->sv_Spre, &c->sv_S,
-                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_rank, &c->sv_tmp})
+                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_tmp})
                         b->release();
                     c->sv_ran = false;
                 }
@@ -1988,7 +2009,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         b->release();
     for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
                     &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
-                    &c->sv_mark, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
+                    &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
         b->release();
     c->h_sv.release();
     if (c->sv_ev) hipEventDestroy(c->sv_ev);
@@ -2805,6 +2826,18 @@ int hvws_last_sieve(hvws_ctx* c, uint64_t out[4]) {
     out[1] = d->active ? n[0] : 0;
     out[2] = d->use ? d->npath : 0;
     out[3] = d->use ? d->pend : 0;
+    return HVWS_OK;
+}
+
+void hvws_set_sieve_windows(uint64_t hops, uint64_t window_bytes, uint64_t prev[2]) {
+    set_sieve_windows(hops, window_bytes, prev);
+}
+
+int hvws_last_sieve_windows(hvws_ctx* c, uint64_t out[2]) {
+    if (!c) c = thread_ctx();
+    if (!c || !out) return set_err(HVWS_EINVAL, "hvws_last_sieve_windows: NULL argument");
+    out[0] = c->sv_ran ? c->sv_rt : 0;
+    out[1] = c->sv_ran ? c->sv_wt : 0;
     return HVWS_OK;
 }
 

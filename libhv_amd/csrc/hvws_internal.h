@@ -187,8 +187,8 @@ struct dsieve {
     uint64_t active;        // this scan's one segment is sieved
     uint64_t use;           // k_walk resumes at pend with npath chain frames recorded
     uint64_t pend;          // segment offset where the exact walk resumes
-    uint64_t last;          // 1 + S index of the chain's last frame
-    uint64_t last_masked;   // 1 + S index of the chain's last masked frame
+    uint64_t last;          // 1 + segment offset of the chain's last frame
+    uint64_t last_masked;   // 1 + segment offset of the chain's last masked frame
     uint64_t npath;         // frames on the chain
     uint64_t pad[2];
 };
@@ -209,18 +209,24 @@ struct sieve_bufs {
     uint32_t* J0;        // successor / doubling tables       (capC each)
     uint32_t* J1;
     uint64_t* mark;      // 1 = on the chain                  (capC)
-    uint64_t* rank;      // exclusive scan of mark            (capC)
+    uint32_t* hops;      // whole frames from a node to its successor (capC)
+    uint64_t* rank;      // exclusive scan of mark * hops     (capC)
     uint64_t* m_total;   // survivors
     uint64_t* npath;     // chain frames
     uint64_t* tmp;       // scan scratch (>= 4 * ceil(max(capS, tiles) / 1024) + 64 words)
     uint64_t  capS;      // entries before verification, < 2^32
     uint64_t  capC;      // survivors / chain nodes, <= capS
+    uint32_t  rt, wt;    // windows: the first wt of every rt tiles are sieved (rt == wt: every tile)
 };
 uint64_t sieve_tiles_max(uint64_t rx_len);
 uint64_t sieve_slot_words(uint64_t rx_len);
 uint64_t sieve_min();                  // bytes after the first whole frame from which a mixed stream is sieved
 uint64_t set_sieve_min(uint64_t v);    // 0 = default; returns the previous value
 uint64_t sieve_generation();           // bumped by set_sieve_min (contexts forget their sieve history)
+// Window geometry for a one-segment scan of rx_len bytes whose last exact
+// count was nframes (0: unknown -> every tile): rt, wt in tiles.
+void sieve_geometry(uint64_t rx_len, uint64_t nframes, uint32_t& rt, uint32_t& wt);
+void set_sieve_windows(uint64_t hops, uint64_t window, uint64_t prev[2]);   // bumps sieve_generation()
 hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid, const uint64_t* npred,
                         const sieve_bufs& b, hipStream_t st);
 hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid,

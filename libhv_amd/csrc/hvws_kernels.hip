@@ -639,7 +639,7 @@ __device__ __forceinline__ void walk_body(const uint8_t* __restrict__ rx, uint64
         if (sv && s == 0 && sv->use) {
             const uint64_t np = sv->pend;
             hdr h;
-            parse_at(rx, rx_len, sb, L, sv_S[sv->last - 1], h);
+            parse_at(rx, rx_len, sb, L, sv->last - 1, h);
             n += sv->npath;
             pos = np;
             st.flags = h.flags;
@@ -650,7 +650,7 @@ __device__ __forceinline__ void walk_body(const uint8_t* __restrict__ rx, uint64
             st.started = 0;
             if (sv->last_masked) {
                 hdr hm;
-                parse_at(rx, rx_len, sb, L, sv_S[sv->last_masked - 1], hm);
+                parse_at(rx, rx_len, sb, L, sv->last_masked - 1, hm);
                 st.mask = hm.key;
             }
         }

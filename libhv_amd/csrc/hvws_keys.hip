@@ -16,9 +16,14 @@ namespace hvws {
 
 namespace {
 
-// "258EAFA5-E914-47DA-95CA-C5AB0DC85B11" as big-endian words (RFC 6455 sec. 1.3)
-__constant__ uint32_t kGuidW[9] = {0x32353845u, 0x41464135u, 0x2D453931u, 0x342D3437u, 0x44412D39u,
-                                   0x3543412Du, 0x43354142u, 0x30444338u, 0x35423131u};
+// "258EAFA5-E914-47DA-95CA-C5AB0DC85B11" as big-endian words (RFC 6455 sec. 1.3).
+// Compile-time literals (not __constant__ memory), so the 24-character path's
+// first-block schedule folds every GUID-only term: W6..W15 are known, and
+// e.g. W16 = rol(W13 ^ W8 ^ W2 ^ W0) keeps one XOR with a constant.
+__device__ __forceinline__ constexpr uint32_t guid_w(int t) {
+    return t == 0 ? 0x32353845u : t == 1 ? 0x41464135u : t == 2 ? 0x2D453931u : t == 3 ? 0x342D3437u
+         : t == 4 ? 0x44412D39u : t == 5 ? 0x3543412Du : t == 6 ? 0x43354142u : t == 7 ? 0x30444338u : 0x35423131u;
+}
 
 __device__ __forceinline__ uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 
@@ -92,7 +97,7 @@ __device__ __forceinline__ uint8_t msg_byte(const uint8_t* key, uint64_t kl, uin
     if (i < kl) return key[i];
     if (i < kl + 36) {
         const uint64_t g = i - kl;
-        return (uint8_t)(kGuidW[g >> 2] >> (24 - 8 * (g & 3)));
+        return (uint8_t)(guid_w((int)(g >> 2)) >> (24 - 8 * (g & 3)));
     }
     if (i == kl + 36) return 0x80;
     const uint64_t bits = (kl + 36) * 8;
@@ -114,7 +119,7 @@ __device__ __forceinline__ void key24_words(const uint8_t* key, uint32_t* w) {
                    key[4 * t + 3];
     }
 #pragma unroll
-    for (int t = 0; t < 9; ++t) w[6 + t] = kGuidW[t];
+    for (int t = 0; t < 9; ++t) w[6 + t] = guid_w(t);
     w[15] = 0x80000000u;
 }
 

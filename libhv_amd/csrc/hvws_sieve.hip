@@ -23,13 +23,23 @@
 //                    tile is flagged, and
 //   k_sieve_verify   finishes those from HBM, one thread each;
 //   scan, compact    -> sorted survivor array S.
-//   k_sieve_link     succ(j) = index of S[j] + size(S[j]) in S (binary
-//                    search), or none.
+//   k_sieve_link     succ(j): walk the exact frames from S[j] until one
+//                    starts at a survivor (looked up in the S entries of its
+//                    tile), hops(j) = frames walked; or none.
+//
+// Windows.  A long stream of large frames need not be sieved everywhere: only
+// the first wt tiles of every rt ("windows", sized past the largest frame the
+// traffic holds) are, and the link walks cross the gaps frame by frame -- one
+// dependent header load per frame, ~rt * 8 KiB / mean frame size of them per
+// region, all regions in parallel.  The host picks rt from the last exact
+// count of the context's one-segment scans (sieve_geometry); rt == wt sieves
+// every tile (hops(j) is then mostly 1).
 //   k_sieve_jump     pointer doubling from the stream's first whole frame
 //                    (known exactly from k_head): after round r the first
 //                    2^(r+1) frames of the true chain are marked.
-//   scan             marks -> record ranks.
-//   k_sieve_emit     frame records of the marked chain.
+//   scan             marks * hops -> record ranks.
+//   k_sieve_emit     frame records of the marked chain (each node re-walks
+//                    its hops).
 //
 // Exactness: the chain is followed from a true header through exact
 // successor positions, so every marked node is a true frame and they come in
@@ -50,6 +60,18 @@ constexpr uint32_t SV_SLOT = 16;                       // survivors kept per til
 constexpr int SV_DEPTH = 3;                            // hops a survivor's chain must stay plausible
 constexpr uint32_t SV_TERM = 0xFFFFFFFFu;
 constexpr uint32_t SV_GRID = 4096;
+constexpr uint32_t SV_HOP_CAP = 4096;                  // frames one link walk may cross
+
+// Tiles of the segment that are sieved (the first wt of every rt of the NT
+// tiles from A0), and the stream tile of sieved tile t.
+__device__ __forceinline__ uint64_t sv_ntiles(uint64_t NT, uint32_t rt, uint32_t wt) {
+    if (!NT) return 0;
+    const uint64_t nreg = (NT + rt - 1) / rt, last = NT - (nreg - 1) * rt;
+    return (nreg - 1) * wt + (last < wt ? last : wt);
+}
+__device__ __forceinline__ uint64_t sv_tile(uint64_t t, uint32_t rt, uint32_t wt) {
+    return rt == wt ? t : (t / wt) * rt + t % wt;
+}
 
 // The sieve runs on segment 0 when k_head found its first whole frame at
 // pos, sizes that vary (probe) and no verified uniform prefix.
@@ -350,7 +372,8 @@ __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                                                             const uint64_t* __restrict__ npred, uint64_t sieve_min,
                                                             uint64_t* __restrict__ tcount, uint32_t* __restrict__ slot,
                                                             uint32_t* __restrict__ pool, unsigned long long* __restrict__ pool_n,
-                                                            uint64_t pool_cap, uint64_t ntiles_max, dsieve* __restrict__ sv) {
+                                                            uint64_t pool_cap, uint64_t ntiles_max, dsieve* __restrict__ sv,
+                                                            uint32_t rt, uint32_t wt) {
     __shared__ sieve_lds sh;
     uint64_t sb, L, pos;
     const bool want = sieve_wanted(segs, mid, npred, sieve_min, sb, L, pos);
@@ -362,22 +385,23 @@ __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     if (!want) return;
     if (threadIdx.x < 8) sh.l[(SV_TILE + SV_HALO) / 4 + threadIdx.x] = 0;   // read past the last halo chunk
     const uint64_t A0 = (sb + pos) & ~15ull;
-    const uint64_t ntiles = (sb + L - A0 + SV_TILE - 1) / SV_TILE;
+    const uint64_t ntiles = sv_ntiles((sb + L - A0 + SV_TILE - 1) / SV_TILE, rt, wt);
     for (uint64_t t = ntiles + blockIdx.x; t < ntiles_max; t += gridDim.x)
         if (threadIdx.x == 0) tcount[t] = 0;
     tile_regs r;
     uint64_t t = blockIdx.x;
-    if (t < ntiles) load_tile(rx, rx_len, A0 + t * SV_TILE, r);
+    if (t < ntiles) load_tile(rx, rx_len, A0 + sv_tile(t, rt, wt) * SV_TILE, r);
     int par = 0;
     for (; t < ntiles; t += gridDim.x, par ^= 1) {
         const uint64_t tn = t + gridDim.x;
+        const uint64_t T0 = A0 + sv_tile(t, rt, wt) * SV_TILE, Tn = A0 + sv_tile(tn, rt, wt) * SV_TILE;
         if (MODE == 3) {   // timing experiment: the loads alone
-            if (tn < ntiles) load_tile(rx, rx_len, A0 + tn * SV_TILE, r);
+            if (tn < ntiles) load_tile(rx, rx_len, Tn, r);
             if (threadIdx.x == 0) tcount[t] = r.v[0].x == 0x12345678u && r.v[1].y == 7u ? 1u : 0u;
             continue;
         }
-        if (MODE == 4 && t != blockIdx.x) load_tile(rx, rx_len, A0 + t * SV_TILE, r);
-        sieve_tile<MODE>(rx, rx_len, sh, r, par, A0 + t * SV_TILE, tn < ntiles, A0 + tn * SV_TILE, sb, L, pos);
+        if (MODE == 4 && t != blockIdx.x) load_tile(rx, rx_len, T0, r);
+        sieve_tile<MODE>(rx, rx_len, sh, r, par, T0, tn < ntiles, Tn, sb, L, pos);
         // wave 0 records while the other waves stage the next tile (the
         // bitmaps alternate by parity; the next barrier orders the rest)
         if (threadIdx.x < 64) record_tile(sh, par, t, tcount, slot, pool, pool_n, pool_cap);
@@ -391,15 +415,15 @@ __global__ __launch_bounds__(256) void k_sieve_fill(const dseg* __restrict__ seg
                                                     const uint64_t* __restrict__ tbase, const uint32_t* __restrict__ slot,
                                                     const uint32_t* __restrict__ pool, uint64_t* __restrict__ S,
                                                     const uint64_t* __restrict__ m_total, uint64_t capS,
-                                                    const dsieve* __restrict__ sv) {
+                                                    const dsieve* __restrict__ sv, uint32_t rt, uint32_t wt) {
     if (!sv->active || *m_total > capS) return;
     const uint64_t sb = segs[0].off, L = segs[0].len, pos = mid[0].pos;
     const uint64_t A0 = (sb + pos) & ~15ull;
-    const uint64_t ntiles = (sb + L - A0 + SV_TILE - 1) / SV_TILE;
+    const uint64_t ntiles = sv_ntiles((sb + L - A0 + SV_TILE - 1) / SV_TILE, rt, wt);
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t n = tcount[t], b = tbase[t];
         if (n == 0) continue;
-        const uint64_t T0 = A0 + t * SV_TILE - sb;
+        const uint64_t T0 = A0 + sv_tile(t, rt, wt) * SV_TILE - sb;
         const uint32_t* src = n <= SV_SLOT ? slot + t * SV_SLOT : pool + slot[t * SV_SLOT];
         for (uint64_t k = 0; k < n; ++k) {
             const uint32_t e = src[k];
@@ -448,39 +472,80 @@ __device__ __forceinline__ bool sieve_on(const dsieve* sv, const uint64_t* m_tot
     return sv->active && *m_total <= capS;
 }
 
-// J[j] = index of the survivor at S[j] + size(S[j]), or SV_TERM; mark[j] = 1
-// for the stream's first whole frame; mark[j] = 0 for j in [m, capS).
+// Index of the survivor at segment offset x, or SV_TERM: x must lie in a
+// sieved tile; that tile's survivors are S[kb(tbase[ct]) .. kb(tbase[ct+1]))
+// (kb maps a pre-verification index to the first survivor at or after it).
+__device__ __forceinline__ uint32_t sv_lookup(const uint64_t* __restrict__ S, uint64_t m,
+                                              const uint64_t* __restrict__ tbase, const uint64_t* __restrict__ kbase,
+                                              uint64_t capS, uint64_t A0, uint64_t sb, uint64_t ntiles, uint32_t rt,
+                                              uint32_t wt, uint64_t x) {
+    const uint64_t rel = sb + x - A0, rb = (uint64_t)rt * SV_TILE;
+    const uint64_t r = rel / rb, off = rel - r * rb;
+    if (off >= (uint64_t)wt * SV_TILE) return SV_TERM;
+    const uint64_t ct = r * wt + off / SV_TILE;
+    if (ct >= ntiles) return SV_TERM;
+    const uint64_t b0 = tbase[ct], b1 = tbase[ct + 1];
+    if (b0 >= b1) return SV_TERM;
+    uint64_t lo = b0 < capS ? kbase[b0] : m, hi = b1 < capS ? kbase[b1] : m;
+    if (hi > m) hi = m;
+    while (lo < hi) {
+        const uint64_t md = (lo + hi) >> 1;
+        if (S[md] < x) lo = md + 1;
+        else hi = md;
+    }
+    return lo < m && S[lo] == x ? (uint32_t)lo : SV_TERM;
+}
+
+// J[j] = index of the next survivor the exact walk from S[j] reaches (every
+// frame on the way whole and plausible, at most SV_HOP_CAP of them), or
+// SV_TERM; hops[j] = whole frames from S[j] up to that survivor (or up to
+// where the walk stopped); mark[j] = 1 for the stream's first whole frame,
+// mark[j] = 0 for j in [m, capC).
 __global__ __launch_bounds__(256) void k_sieve_link(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                     const dseg* __restrict__ segs, const dmid* __restrict__ mid,
                                                     const uint64_t* __restrict__ S, const uint64_t* __restrict__ m_total,
-                                                    uint64_t capS, uint32_t* __restrict__ J, uint64_t* __restrict__ mark,
-                                                    const dsieve* __restrict__ sv) {
-    if (!sieve_on(sv, m_total, capS)) return;
+                                                    uint64_t capC, uint32_t* __restrict__ J, uint32_t* __restrict__ hops,
+                                                    uint64_t* __restrict__ mark, const dsieve* __restrict__ sv,
+                                                    const uint64_t* __restrict__ tbase, const uint64_t* __restrict__ kbase,
+                                                    const uint64_t* __restrict__ m_pre, uint64_t capS, uint32_t rt,
+                                                    uint32_t wt) {
+    if (!sieve_on(sv, m_total, capC) || *m_pre > capS) return;
     const uint64_t m = *m_total, sb = segs[0].off, L = segs[0].len, pos = mid[0].pos;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < capS; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t A0 = (sb + pos) & ~15ull;
+    const uint64_t ntiles = sv_ntiles((sb + L - A0 + SV_TILE - 1) / SV_TILE, rt, wt);
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < capC; j += (uint64_t)gridDim.x * blockDim.x) {
         if (j >= m) {
             mark[j] = 0;
             continue;
         }
-        // Only whole frames are chain nodes: a node's successor is the first
-        // entry equal to its exact end, if a whole frame starts there.
         const uint64_t q = S[j];
         hdr h;
-        uint32_t nx = SV_TERM;
+        uint32_t nx = SV_TERM, k = 0;
         if (parse_at(rx, rx_len, sb, L, q, h)) {
-            const uint64_t x = q + h.hlen + h.length;
-            uint64_t lo = j + 1, hi = m;
-            while (lo < hi) {
-                const uint64_t md = (lo + hi) >> 1;
-                if (S[md] < x) lo = md + 1;
-                else hi = md;
+            uint64_t x = q;
+#pragma unroll 1
+            for (;;) {
+                x += h.hlen + h.length;
+                ++k;
+                if (!parse_at(rx, rx_len, sb, L, x, h)) break;   // the segment ends (or cuts the frame) at x
+                nx = sv_lookup(S, m, tbase, kbase, capS, A0, sb, ntiles, rt, wt, x);
+                if (nx != SV_TERM || !plausible(h) || k >= SV_HOP_CAP) break;
             }
-            hdr hx;
-            if (lo < m && S[lo] == x && parse_at(rx, rx_len, sb, L, x, hx)) nx = (uint32_t)lo;
         }
         J[j] = nx;
+        hops[j] = k;
         mark[j] = q == pos && (j == 0 || S[j - 1] != pos) ? 1u : 0u;
     }
+}
+
+// Record ranks are weighted by the frames each marked node stands for.
+__global__ __launch_bounds__(256) void k_sieve_weight(const uint64_t* __restrict__ mark, const uint32_t* __restrict__ hops,
+                                                      uint64_t* __restrict__ w, const uint64_t* __restrict__ m_total,
+                                                      uint64_t capC, const dsieve* __restrict__ sv) {
+    if (!sieve_on(sv, m_total, capC)) return;
+    const uint64_t m = *m_total;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < capC; j += (uint64_t)gridDim.x * blockDim.x)
+        w[j] = j < m && mark[j] ? hops[j] : 0;
 }
 
 // Pointer doubling, round r (jump 2^r): a marked node marks the node 2^r
@@ -502,30 +567,39 @@ __global__ __launch_bounds__(256) void k_sieve_jump(const uint32_t* __restrict__
     }
 }
 
-// Records of the marked chain: record n_a + rank[j] for node j.  The last
-// node hands k_walk the resume position; the last masked one its key (Q14).
+// Records of the marked chain: node j's hops[j] frames are records
+// n_a + rank[j] ...  The node that ends the chain hands k_walk the resume
+// position and its last frame; the last masked frame's offset is the max
+// over nodes (Q14: its key stays in the parser).
 __global__ __launch_bounds__(256) void k_sieve_emit(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                     const dseg* __restrict__ segs, const dmid* __restrict__ mid,
                                                     const uint64_t* __restrict__ S, const uint64_t* __restrict__ m_total,
                                                     uint64_t capS, const uint64_t* __restrict__ mark,
-                                                    const uint64_t* __restrict__ rank,
+                                                    const uint32_t* __restrict__ hops, const uint64_t* __restrict__ rank,
                                                     const uint64_t* __restrict__ npath_p, dframes fr, uint32_t vmask,
                                                     dsieve* __restrict__ sv) {
     if (!sieve_on(sv, m_total, capS)) return;
     const uint64_t m = *m_total, npath = *npath_p, sb = segs[0].off, L = segs[0].len, n_a = mid[0].n_a;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
         if (!mark[j]) continue;
-        const uint64_t q = S[j];
-        hdr h;
-        parse_at(rx, rx_len, sb, L, q, h);
-        frec v;
-        whole_frame_rec(v, q, h, vmask);
-        const uint64_t k = rank[j];
-        store_frame(fr, n_a + k, sb, v);
-        if (h.flags & F_MASK) atomicMax((unsigned long long*)&sv->last_masked, (unsigned long long)(j + 1));
-        if (k + 1 == npath) {
-            sv->pend = q + h.hlen + h.length;
-            sv->last = j + 1;
+        const uint64_t k0 = rank[j];
+        const uint32_t n = hops[j];
+        uint64_t x = S[j], prev = x, lm = 0;
+#pragma unroll 1
+        for (uint32_t i = 0; i < n; ++i) {
+            hdr h;
+            parse_at(rx, rx_len, sb, L, x, h);
+            frec v;
+            whole_frame_rec(v, x, h, vmask);
+            store_frame(fr, n_a + k0 + i, sb, v);
+            if (h.flags & F_MASK) lm = x + 1;
+            prev = x;
+            x += h.hlen + h.length;
+        }
+        if (lm) atomicMax((unsigned long long*)&sv->last_masked, (unsigned long long)lm);
+        if (n && k0 + n == npath) {
+            sv->pend = x;
+            sv->last = prev + 1;
             sv->npath = npath;
             sv->use = 1;
         }
@@ -560,6 +634,48 @@ uint64_t set_sieve_min(uint64_t v) {
 
 uint64_t sieve_generation() { return g_sieve_gen; }
 
+// Windows: regions of about $HVWS_SIEVE_HOPS (default 64) mean-sized frames,
+// each sieved over its first $HVWS_SIEVE_WINDOW bytes (default 1 MiB + 16 KiB:
+// past the largest frame of config 4, so a walk entering a region almost
+// always lands on a survivor of its window).  Regions shorter than two
+// windows, or no count yet: every tile.  Results never depend on it.
+constexpr uint64_t SIEVE_HOPS_DEFAULT = 64, SIEVE_WINDOW_DEFAULT = (1 << 20) + (16 << 10);
+static uint64_t g_sv_hops = ~0ull, g_sv_win = 0;   // ~0 / 0: not yet read from the environment
+
+static void sieve_windows_init() {
+    if (g_sv_hops == ~0ull) {
+        const char* e = getenv("HVWS_SIEVE_HOPS");
+        g_sv_hops = e ? (uint64_t)atoll(e) : SIEVE_HOPS_DEFAULT;
+    }
+    if (!g_sv_win) {
+        const char* e = getenv("HVWS_SIEVE_WINDOW");
+        const long long x = e ? atoll(e) : 0;
+        g_sv_win = x > 0 ? (uint64_t)x : SIEVE_WINDOW_DEFAULT;
+    }
+}
+
+void set_sieve_windows(uint64_t hops, uint64_t window, uint64_t prev[2]) {
+    sieve_windows_init();
+    if (prev) {
+        prev[0] = g_sv_hops;
+        prev[1] = g_sv_win;
+    }
+    g_sv_hops = hops;
+    g_sv_win = window ? window : SIEVE_WINDOW_DEFAULT;
+    ++g_sieve_gen;
+}
+
+void sieve_geometry(uint64_t rx_len, uint64_t nframes, uint32_t& rt, uint32_t& wt) {
+    sieve_windows_init();
+    rt = wt = 1;
+    if (!nframes || !g_sv_hops || g_sv_hops > (1ull << 20)) return;
+    const uint64_t rb = rx_len / nframes * g_sv_hops;
+    const uint64_t wtiles = (g_sv_win + SV_TILE - 1) / SV_TILE, rtiles = rb / SV_TILE;
+    if (rtiles < 2 * wtiles || rtiles > 0xFFFFFFFFull) return;
+    rt = (uint32_t)rtiles;
+    wt = (uint32_t)wtiles;
+}
+
 // Survivor-array capacity rounds: log2 of the capacity bounds the chain.
 static uint32_t jump_rounds(uint64_t capS) {
     uint32_t r = 0;
@@ -582,7 +698,7 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 #define HVWS_SIEVE_COUNT(M)                                                                                     \
     hipLaunchKernelGGL(k_sieve_count<M>, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,    \
                        sieve_min(), b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), \
-                       b.capS, ntm, sv)
+                       b.capS, ntm, sv, b.rt, b.wt)
     switch (mode) {
         case 1: HVWS_SIEVE_COUNT(1); break;
         case 2: HVWS_SIEVE_COUNT(2); break;
@@ -594,7 +710,7 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     if ((e = launch_exclusive_scan(b.tcount, b.tbase, ntm, b.tmp, b.m_pre, st)) != hipSuccess) return e;
     const uint64_t fb = (ntm + 255) / 256;
     hipLaunchKernelGGL(k_sieve_fill, dim3((uint32_t)(fb < 8192 ? fb : 8192)), dim3(256), 0, st, segs, mid, b.tcount,
-                       b.tbase, b.slot, b.pool, b.Spre, b.m_pre, b.capS, sv);
+                       b.tbase, b.slot, b.pool, b.Spre, b.m_pre, b.capS, sv, b.rt, b.wt);
     // Pre-verification entries use capacity capS; the survivors and the chain
     // arrays capC (about the survivor count: the doubling rounds and the mark
     // scan run over it).  More survivors than capC: the sieve stands down.
@@ -605,7 +721,7 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     hipLaunchKernelGGL(k_sieve_compact, dim3(lg), dim3(256), 0, st, b.Spre, b.m_pre, b.capS, b.keep, b.kbase, b.S, b.capC,
                        sv);
     hipLaunchKernelGGL(k_sieve_link, dim3(lc), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capC, b.J0,
-                       b.mark, sv);
+                       b.hops, b.mark, sv, b.tbase, b.kbase, b.m_pre, b.capS, b.rt, b.wt);
     uint32_t* Jin = b.J0;
     uint32_t* Jout = b.J1;
     const uint32_t rounds = jump_rounds(b.capC);
@@ -616,7 +732,9 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
         Jin = Jout;
         Jout = t;
     }
-    e = launch_exclusive_scan(b.mark, b.rank, b.capC, b.tmp, b.npath, st);
+    // weights into keep (free once the link has read kbase)
+    hipLaunchKernelGGL(k_sieve_weight, dim3(lc), dim3(256), 0, st, b.mark, b.hops, b.keep, b.m_total, b.capC, sv);
+    e = launch_exclusive_scan(b.keep, b.rank, b.capC, b.tmp, b.npath, st);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
@@ -625,7 +743,7 @@ hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* seg
                              const sieve_bufs& b, dframes fr, uint32_t vmask, hipStream_t st) {
     const uint32_t lc = (uint32_t)((b.capC + 255) / 256 < 8192 ? (b.capC + 255) / 256 : 8192);
     hipLaunchKernelGGL(k_sieve_emit, dim3(lc), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capC,
-                       b.mark, b.rank, b.npath, fr, vmask, reinterpret_cast<dsieve*>(b.state));
+                       b.mark, b.hops, b.rank, b.npath, fr, vmask, reinterpret_cast<dsieve*>(b.state));
     return hipGetLastError();
 }
 

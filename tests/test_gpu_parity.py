@@ -747,7 +747,73 @@ def test_sieve_mixed_stream(eng, sieve_low, target, lo, hi, seed):
     assert set(paths.values()) == {2}, paths   # HVWS_PATH_SINGLE
     active, surv, npath, pend = _last_sieve(eng)
     assert active == 1 and npath == plan.n and pend == plan.total, (active, surv, npath, pend, plan.n)
-    assert surv >= plan.n
+    rt, wt = _last_windows(eng)
+    # every tile sieved: every frame is a survivor; windows: only theirs
+    assert surv >= plan.n if rt == wt else 0 < surv, (surv, plan.n, rt, wt)
+
+
+@pytest.fixture
+def sieve_windows():
+    """Set the sieve's window geometry for one test (hops, window bytes)."""
+    L = libhv_amd.lib()
+    prev = (ctypes.c_uint64 * 2)()
+    L.hvws_set_sieve_windows(64, 0, prev)
+    yield lambda hops, win: L.hvws_set_sieve_windows(hops, win, None)
+    L.hvws_set_sieve_windows(prev[0], prev[1], None)
+
+
+def _last_windows(eng):
+    out = (ctypes.c_uint64 * 2)()
+    assert libhv_amd.lib().hvws_last_sieve_windows(eng.ctx, out) == 0
+    return list(out)
+
+
+@pytest.mark.parametrize("target,lo,hi,seed,hops,win", [
+    (24 << 20, 128, 1 << 20, 151, 64, (1 << 20) + (16 << 10)),   # config-4 shape, default geometry
+    (24 << 20, 128, 1 << 20, 152, 8, 64 << 10),                  # windows shorter than frames: walks cross them
+    (6 << 20, 1, 4096, 153, 256, 32 << 10),                      # small frames, long walks
+    (12 << 20, 100, 70000, 154, 32, 16 << 10)])
+def test_sieve_windows(eng, sieve_low, sieve_windows, target, lo, hi, seed, hops, win):
+    """Windowed sieve: only the first `win` bytes of every region of ~hops
+    frames are sieved, link walks cross the rest.  The first scan has no count
+    (every tile); later ones are windowed.  Records and bytes bit-exact in
+    every scan path, the chain covers every frame."""
+    sieve_windows(hops, win)
+    plan = synth.mixed_plan(target, seed, lo=lo, hi=hi)
+    host = H.synth_cpu(plan)
+    for _ in range(2):
+        paths = _compare_batch(eng, host, [(0, plan.total)])
+        assert set(paths.values()) == {2}, paths   # HVWS_PATH_SINGLE
+    rt, wt = _last_windows(eng)
+    assert wt > 0 and rt >= 2 * wt, (rt, wt)
+    active, surv, npath, pend = _last_sieve(eng)
+    assert active == 1 and npath == plan.n and pend == plan.total, (active, surv, npath, pend, plan.n)
+
+
+def test_sieve_windows_walk_cap(eng, sieve_low, sieve_windows):
+    """A region the link walks cannot cross within their frame cap (a run of
+    tiny frames between large ones, one region for the whole stream): the
+    chain stops, the exact walk finishes the segment (results exact), and the
+    context sieves every tile for the next scans."""
+    sieve_windows(1 << 20, 64 << 10)
+    parts = [synth.mixed_plan(6 << 20, 161, lo=256 << 10, hi=1 << 20),
+             synth.mixed_plan(1 << 20, 162, lo=1, hi=4),
+             synth.mixed_plan(6 << 20, 163, lo=256 << 10, hi=1 << 20)]
+    host = np.concatenate([H.synth_cpu(p) for p in parts])
+    n = sum(p.n for p in parts)
+    exp_recs, _, _, _ = _oracle_batch(host, [(0, len(host))], None)
+    assert len(exp_recs) == n
+    L = libhv_amd.lib()
+    saw_short = saw_full = False
+    for _ in range(3):
+        paths = _compare_batch(eng, host, [(0, len(host))])
+        assert set(paths.values()) == {2}, paths
+        rt, wt = _last_windows(eng)
+        active, _, npath, pend = _last_sieve(eng)
+        if rt != wt and active == 1:
+            saw_short |= pend < len(host)
+        saw_full |= rt == wt == 1
+    assert saw_short and saw_full
 
 
 def test_sieve_cut_and_carried(eng, sieve_low):
