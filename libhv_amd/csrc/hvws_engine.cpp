@@ -214,6 +214,7 @@ struct hvws_ctx {
     uint64_t sv_win_len = 0;   // segment length of the last sieved scan if it sieved windows only, else 0
     uint32_t sv_full_left = 0; // scans left that sieve every tile (a windowed chain fell short)
     uint32_t sv_rt = 0, sv_wt = 0;   // window geometry of the last sieved scan (tiles)
+    bool sv_hint_win = false;  // sv_hint_* come from a windowed scan
     // hvws_pipeline: its three device slots and their events, kept across
     // calls (a per-call hipMalloc/hipFree pair cost the first call ~2x)
     dbuf pipe_slot[3], pipe_segs;
@@ -496,9 +497,18 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
         // frame cap, or traffic changed): the next 15 scans sieve every tile.
         const dsieve* d = c->h_sv.as<dsieve>();
         if (c->sv_win_len && d->active && (!d->use || d->pend + (4ull << 20) < c->sv_win_len)) c->sv_full_left = 15;
+        c->sv_hint_win = c->sv_win_len != 0;
         c->sv_win_len = 0;
     }
-    const uint64_t seen = c->sv_hint_pre, seen_s = c->sv_hint_surv;
+    if (c->sv_full_left) {
+        --c->sv_full_left;
+        b.rt = b.wt = 1;
+    } else {
+        sieve_geometry(rx_len, c->single_hint, b.rt, b.wt);
+    }
+    // Counts of a windowed scan say nothing about a scan of every tile.
+    const bool stale = b.rt == b.wt && c->sv_hint_win;
+    const uint64_t seen = stale ? 0 : c->sv_hint_pre, seen_s = stale ? 0 : c->sv_hint_surv;
     // Capacity from the last sieved scan's entry count when there is one (the
     // chain steps and their scans run over the whole capacity), else one
     // entry per KiB of the batch.
@@ -551,12 +561,6 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     b.capC = capc;
     b.keep = c->sv_keep.as<uint64_t>();
     b.kbase = c->sv_kbase.as<uint64_t>();
-    if (c->sv_full_left) {
-        --c->sv_full_left;
-        b.rt = b.wt = 1;
-    } else {
-        sieve_geometry(rx_len, c->single_hint, b.rt, b.wt);
-    }
     c->sv_win_len = b.rt != b.wt ? rx_len : 0;
     c->sv_rt = b.rt;
     c->sv_wt = b.wt;
@@ -784,6 +788,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             c->sv_hint_pre = c->sv_hint_surv = 0;
             c->sv_win_len = 0;
             c->sv_full_left = 0;
+            c->sv_hint_win = false;
         }
         if (rx_len >= sieve_min()) {
             if (sieve_state_ready(c) && c->h_sv.as<dsieve>()->active == 0 && c->sv_skip == 0) c->sv_skip = 15;

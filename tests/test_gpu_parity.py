@@ -801,19 +801,22 @@ def test_sieve_windows_walk_cap(eng, sieve_low, sieve_windows):
              synth.mixed_plan(6 << 20, 163, lo=256 << 10, hi=1 << 20)]
     host = np.concatenate([H.synth_cpu(p) for p in parts])
     n = sum(p.n for p in parts)
-    exp_recs, _, _, _ = _oracle_batch(host, [(0, len(host))], None)
+    segs = [(0, len(host))]
+    exp_recs, exp_carry, exp_started, exp = _oracle_batch(host, segs, None)
     assert len(exp_recs) == n
-    L = libhv_amd.lib()
-    saw_short = saw_full = False
-    for _ in range(3):
-        paths = _compare_batch(eng, host, [(0, len(host))])
-        assert set(paths.values()) == {2}, paths
+    kinds = []   # per scan: "full", "short" (windowed, chain stopped early) or "long"
+    for i in range(20):
+        mode = SCAN_MODES[i % 3]
+        assert _step_checked(eng, host, segs, None, exp_recs, exp_carry, exp_started, exp, mode) == 2
         rt, wt = _last_windows(eng)
         active, _, npath, pend = _last_sieve(eng)
-        if rt != wt and active == 1:
-            saw_short |= pend < len(host)
-        saw_full |= rt == wt == 1
-    assert saw_short and saw_full
+        assert active == 1
+        kinds.append("full" if rt == wt else "short" if pend < len(host) else "long")
+    # a windowed scan stops at the tiny frames; the scans after it sieve
+    # every tile again
+    assert "short" in kinds, kinds
+    k = kinds.index("short")
+    assert k + 1 < len(kinds) and kinds[k + 1] == "full", kinds
 
 
 def test_sieve_cut_and_carried(eng, sieve_low):
