@@ -203,7 +203,7 @@ struct hvws_ctx {
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
     // after each sieved scan (read as hints by the next one).
-    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_hops, sv_rank, sv_cnt, sv_tmp;
+    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_hops, sv_rank, sv_cnt, sv_tmp, sv_scr;
     uint64_t sv_cap = 0, sv_capc = 0;
     uint64_t sv_hint_pre = 0, sv_hint_surv = 0;   // counts of the latest sieved scan read back
     hbuf h_sv;
@@ -519,8 +519,25 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     // chain arrays: from the last survivor count (the chain steps scale with it)
     // (no usable count -- none yet, or the last scan overflowed its entries and
     // never counted survivors -- means the full capacity)
-    const uint64_t capc = seen_s ? std::min<uint64_t>(cap, std::max<uint64_t>(1ull << 16, seen_s + seen_s / 4 + 1024))
-                                 : cap;
+    uint64_t capc = seen_s ? std::min<uint64_t>(cap, std::max<uint64_t>(1ull << 16, seen_s + seen_s / 4 + 1024))
+                           : cap;
+    b.scr = nullptr;
+    b.lgP = 0;
+    if (b.rt != b.wt && seen_s) {
+        // Windowed: survivors lie in the windows only (a count from a scan of
+        // every tile scales by their share).  A small capacity keeps the
+        // doubling rounds in one LDS-resident launch and the walks' offset
+        // scratch (2^lgP per node, about twice the frames a region holds) small.
+        const uint64_t est = c->sv_hint_win ? seen_s : seen_s * b.wt / b.rt * 2;
+        capc = std::min<uint64_t>(cap, std::max<uint64_t>(4096, est + est / 2 + 2048));
+        uint32_t lgP = 4;
+        while (lgP < 12 && (1ull << lgP) < 2 * sieve_hops()) ++lgP;
+        if ((capc << lgP) <= (1ull << 25)) {
+            HIP_OR(c->sv_scr.ensure((capc << lgP) * 8), HVWS_ENOMEM);
+            b.scr = c->sv_scr.as<uint64_t>();
+            b.lgP = lgP;
+        }
+    }
     c->sv_capc = capc;
     const uint64_t ntm = sieve_tiles_max(rx_len);
     const uint64_t nmax = std::max(cap, ntm);
@@ -805,7 +822,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                     (void)hipGetLastError();
                     for (dbuf* b : {&c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
                                     &c->sv_Spre, &c->sv_S,
-                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_tmp})
+                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_tmp, &c->sv_scr})
                         b->release();
                     c->sv_ran = false;
                 }
@@ -2014,7 +2031,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         b->release();
     for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
                     &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
-                    &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp})
+                    &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp, &c->sv_scr})
         b->release();
     c->h_sv.release();
     if (c->sv_ev) hipEventDestroy(c->sv_ev);

@@ -217,6 +217,8 @@ struct sieve_bufs {
     uint64_t  capS;      // entries before verification, < 2^32
     uint64_t  capC;      // survivors / chain nodes, <= capS
     uint32_t  rt, wt;    // windows: the first wt of every rt tiles are sieved (rt == wt: every tile)
+    uint64_t* scr;       // windowed: each node's first 2^lgP frame offsets (capC << lgP), or nullptr
+    uint32_t  lgP;
 };
 uint64_t sieve_tiles_max(uint64_t rx_len);
 uint64_t sieve_slot_words(uint64_t rx_len);
@@ -227,6 +229,7 @@ uint64_t sieve_generation();           // bumped by set_sieve_min (contexts forg
 // count was nframes (0: unknown -> every tile): rt, wt in tiles.
 void sieve_geometry(uint64_t rx_len, uint64_t nframes, uint32_t& rt, uint32_t& wt);
 void set_sieve_windows(uint64_t hops, uint64_t window, uint64_t prev[2]);   // bumps sieve_generation()
+uint64_t sieve_hops();                 // frames per region the window geometry aims at (0: windows off)
 hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid, const uint64_t* npred,
                         const sieve_bufs& b, hipStream_t st);
 hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid,

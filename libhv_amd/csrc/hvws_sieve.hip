@@ -500,7 +500,8 @@ __device__ __forceinline__ uint32_t sv_lookup(const uint64_t* __restrict__ S, ui
 // frame on the way whole and plausible, at most SV_HOP_CAP of them), or
 // SV_TERM; hops[j] = whole frames from S[j] up to that survivor (or up to
 // where the walk stopped); mark[j] = 1 for the stream's first whole frame,
-// mark[j] = 0 for j in [m, capC).
+// mark[j] = 0 for j in [m, capC).  With P > 0 the first P frame offsets of
+// each walk go to scr[j * P ...], so the records need no second walk.
 __global__ __launch_bounds__(256) void k_sieve_link(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                     const dseg* __restrict__ segs, const dmid* __restrict__ mid,
                                                     const uint64_t* __restrict__ S, const uint64_t* __restrict__ m_total,
@@ -508,7 +509,7 @@ __global__ __launch_bounds__(256) void k_sieve_link(const uint8_t* __restrict__ 
                                                     uint64_t* __restrict__ mark, const dsieve* __restrict__ sv,
                                                     const uint64_t* __restrict__ tbase, const uint64_t* __restrict__ kbase,
                                                     const uint64_t* __restrict__ m_pre, uint64_t capS, uint32_t rt,
-                                                    uint32_t wt) {
+                                                    uint32_t wt, uint64_t* __restrict__ scr, uint32_t P) {
     if (!sieve_on(sv, m_total, capC) || *m_pre > capS) return;
     const uint64_t m = *m_total, sb = segs[0].off, L = segs[0].len, pos = mid[0].pos;
     const uint64_t A0 = (sb + pos) & ~15ull;
@@ -523,12 +524,22 @@ __global__ __launch_bounds__(256) void k_sieve_link(const uint8_t* __restrict__ 
         uint32_t nx = SV_TERM, k = 0;
         if (parse_at(rx, rx_len, sb, L, q, h)) {
             uint64_t x = q;
+            // the window the walk is in or heads for: [wlo, whi) absolute
+            const uint64_t rb = (uint64_t)rt * SV_TILE, wb = (uint64_t)wt * SV_TILE;
+            uint64_t wlo = A0 + (sb + q - A0) / rb * rb, whi = wlo + wb;
+            uint64_t* sp = P ? scr + j * P : nullptr;
 #pragma unroll 1
             for (;;) {
+                if (k < P) sp[k] = x;   // frame k of this node (k_sieve_emit_pos reads them back)
                 x += h.hlen + h.length;
                 ++k;
                 if (!parse_at(rx, rx_len, sb, L, x, h)) break;   // the segment ends (or cuts the frame) at x
-                nx = sv_lookup(S, m, tbase, kbase, capS, A0, sb, ntiles, rt, wt, x);
+                const uint64_t ax = sb + x;
+                if (ax >= wlo + rb) {   // a later region (division only when the walk crosses one)
+                    wlo = A0 + (ax - A0) / rb * rb;
+                    whi = wlo + wb;
+                }
+                nx = ax < whi ? sv_lookup(S, m, tbase, kbase, capS, A0, sb, ntiles, rt, wt, x) : SV_TERM;
                 if (nx != SV_TERM || !plausible(h) || k >= SV_HOP_CAP) break;
             }
         }
@@ -536,6 +547,39 @@ __global__ __launch_bounds__(256) void k_sieve_link(const uint8_t* __restrict__ 
         hops[j] = k;
         mark[j] = q == pos && (j == 0 || S[j - 1] != pos) ? 1u : 0u;
     }
+}
+
+// All doubling rounds in one workgroup when the chain arrays fit in LDS
+// (windowed scans: a few thousand survivors) -- one launch instead of
+// ceil(log2 capC), each of which costs a dispatch beside the unmask.
+constexpr uint32_t SV_JLDS = 8192;
+
+__global__ __launch_bounds__(256) void k_sieve_jump_lds(const uint32_t* __restrict__ J, uint64_t* __restrict__ mark,
+                                                         const uint64_t* __restrict__ m_total, uint64_t capC,
+                                                         const dsieve* __restrict__ sv) {
+    __shared__ uint32_t jj[2][SV_JLDS];
+    __shared__ uint8_t mk[SV_JLDS];
+    if (!sieve_on(sv, m_total, capC)) return;
+    const uint32_t m = (uint32_t)*m_total;   // <= capC <= SV_JLDS (host)
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+        jj[0][j] = J[j];
+        mk[j] = mark[j] ? 1 : 0;
+    }
+    __syncthreads();
+    uint32_t c = 0;
+    for (uint32_t r = 0; (1u << r) < m; ++r, c ^= 1) {
+        for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+            const uint32_t n = jj[c][j];
+            if (n == SV_TERM) {
+                jj[c ^ 1][j] = SV_TERM;
+                continue;
+            }
+            if (mk[j]) mk[n] = 1;   // only ever set: racing writers agree
+            jj[c ^ 1][j] = jj[c][n];
+        }
+        __syncthreads();
+    }
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) mark[j] = mk[j];
 }
 
 // Record ranks are weighted by the frames each marked node stands for.
@@ -606,6 +650,78 @@ __global__ __launch_bounds__(256) void k_sieve_emit(const uint8_t* __restrict__ 
     }
 }
 
+// The same records from the walks' stored offsets (P > 0): one wave per
+// marked node, its lanes take the node's frames 64 at a time (every header
+// load independent); frames past a walk's first P are walked by lane 0 from
+// its P-th (rare: the host sizes P at about twice a region's frames).
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_sieve_emit_pos(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                        const dseg* __restrict__ segs, const dmid* __restrict__ mid,
+                                                        const uint64_t* __restrict__ m_total, uint64_t capC,
+                                                        const uint64_t* __restrict__ mark,
+                                                        const uint32_t* __restrict__ hops,
+                                                        const uint64_t* __restrict__ rank,
+                                                        const uint64_t* __restrict__ npath_p,
+                                                        const uint64_t* __restrict__ scr, uint32_t lgP, dframes fr,
+                                                        uint32_t vmask, dsieve* __restrict__ sv) {
+    if (!sieve_on(sv, m_total, capC)) return;
+    const uint64_t m = *m_total, npath = *npath_p, sb = segs[0].off, L = segs[0].len, n_a = mid[0].n_a;
+    const uint32_t P = 1u << lgP, lane = threadIdx.x & 63u;
+    const uint64_t wv = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t j = wv; j < m; j += nw) {   // wave-uniform
+        if (!mark[j]) continue;
+        const uint32_t n = hops[j];
+        const uint64_t k0 = rank[j];
+        const uint32_t ns = n < P ? n : P;
+        uint64_t lm = 0;
+        for (uint32_t i = lane; i < ns; i += 64) {
+            const uint64_t x = scr[(j << lgP) + i];
+            hdr h;
+            parse_at(rx, rx_len, sb, L, x, h);
+            frec v;
+            whole_frame_rec(v, x, h, vmask);
+            store_frame(fr, n_a + k0 + i, sb, v);
+            if (h.flags & F_MASK) lm = x + 1;
+            if (i + 1 == n && k0 + n == npath) {   // the chain's last frame
+                sv->pend = x + h.hlen + h.length;
+                sv->last = x + 1;
+                sv->npath = npath;
+                sv->use = 1;
+            }
+        }
+        if (n > P && lane == 0) {   // the rest of a long walk
+            uint64_t x = scr[(j << lgP) + P - 1];
+            hdr h;
+            parse_at(rx, rx_len, sb, L, x, h);
+#pragma unroll 1
+            for (uint32_t t = P; t < n; ++t) {
+                x += h.hlen + h.length;
+                parse_at(rx, rx_len, sb, L, x, h);
+                frec v;
+                whole_frame_rec(v, x, h, vmask);
+                store_frame(fr, n_a + k0 + t, sb, v);
+                if (h.flags & F_MASK) lm = x + 1;
+            }
+            if (k0 + n == npath) {
+                sv->pend = x + h.hlen + h.length;
+                sv->last = x + 1;
+                sv->npath = npath;
+                sv->use = 1;
+            }
+        }
+        lm = wave_max64(lm);
+        if (lane == 0 && lm) atomicMax((unsigned long long*)&sv->last_masked, (unsigned long long)lm);
+    }
+}
+
 // ---------------------------------------------------------------- launcher
 
 uint64_t sieve_tiles_max(uint64_t rx_len) { return rx_len / SV_TILE + 2; }
@@ -634,12 +750,12 @@ uint64_t set_sieve_min(uint64_t v) {
 
 uint64_t sieve_generation() { return g_sieve_gen; }
 
-// Windows: regions of about $HVWS_SIEVE_HOPS (default 64) mean-sized frames,
+// Windows: regions of about $HVWS_SIEVE_HOPS (default 256) mean-sized frames,
 // each sieved over its first $HVWS_SIEVE_WINDOW bytes (default 1 MiB + 16 KiB:
 // past the largest frame of config 4, so a walk entering a region almost
 // always lands on a survivor of its window).  Regions shorter than two
 // windows, or no count yet: every tile.  Results never depend on it.
-constexpr uint64_t SIEVE_HOPS_DEFAULT = 64, SIEVE_WINDOW_DEFAULT = (1 << 20) + (16 << 10);
+constexpr uint64_t SIEVE_HOPS_DEFAULT = 256, SIEVE_WINDOW_DEFAULT = (1 << 20) + (16 << 10);
 static uint64_t g_sv_hops = ~0ull, g_sv_win = 0;   // ~0 / 0: not yet read from the environment
 
 static void sieve_windows_init() {
@@ -663,6 +779,11 @@ void set_sieve_windows(uint64_t hops, uint64_t window, uint64_t prev[2]) {
     g_sv_hops = hops;
     g_sv_win = window ? window : SIEVE_WINDOW_DEFAULT;
     ++g_sieve_gen;
+}
+
+uint64_t sieve_hops() {
+    sieve_windows_init();
+    return g_sv_hops;
 }
 
 void sieve_geometry(uint64_t rx_len, uint64_t nframes, uint32_t& rt, uint32_t& wt) {
@@ -721,16 +842,23 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     hipLaunchKernelGGL(k_sieve_compact, dim3(lg), dim3(256), 0, st, b.Spre, b.m_pre, b.capS, b.keep, b.kbase, b.S, b.capC,
                        sv);
     hipLaunchKernelGGL(k_sieve_link, dim3(lc), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capC, b.J0,
-                       b.hops, b.mark, sv, b.tbase, b.kbase, b.m_pre, b.capS, b.rt, b.wt);
-    uint32_t* Jin = b.J0;
-    uint32_t* Jout = b.J1;
-    const uint32_t rounds = jump_rounds(b.capC);
-    for (uint32_t r = 0; r < rounds; ++r) {
-        hipLaunchKernelGGL(k_sieve_jump, dim3(lc < 1024 ? lc : 1024), dim3(256), 0, st, Jin, Jout, b.mark, b.m_total,
-                           b.capC, sv, r);
-        uint32_t* t = Jin;
-        Jin = Jout;
-        Jout = t;
+                       b.hops, b.mark, sv, b.tbase, b.kbase, b.m_pre, b.capS, b.rt, b.wt, b.scr,
+                       b.scr ? 1u << b.lgP : 0u);
+    if (b.capC <= SV_JLDS) {
+        // 256 threads: a 16-wave workgroup waits for a CU with 16 free slots
+        // beside the unmask grid
+        hipLaunchKernelGGL(k_sieve_jump_lds, dim3(1), dim3(256), 0, st, b.J0, b.mark, b.m_total, b.capC, sv);
+    } else {
+        uint32_t* Jin = b.J0;
+        uint32_t* Jout = b.J1;
+        const uint32_t rounds = jump_rounds(b.capC);
+        for (uint32_t r = 0; r < rounds; ++r) {
+            hipLaunchKernelGGL(k_sieve_jump, dim3(lc < 1024 ? lc : 1024), dim3(256), 0, st, Jin, Jout, b.mark,
+                               b.m_total, b.capC, sv, r);
+            uint32_t* t = Jin;
+            Jin = Jout;
+            Jout = t;
+        }
     }
     // weights into keep (free once the link has read kbase)
     hipLaunchKernelGGL(k_sieve_weight, dim3(lc), dim3(256), 0, st, b.mark, b.hops, b.keep, b.m_total, b.capC, sv);
@@ -741,6 +869,13 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 
 hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid,
                              const sieve_bufs& b, dframes fr, uint32_t vmask, hipStream_t st) {
+    if (b.scr) {
+        const uint64_t g = (b.capC + 3) / 4;   // a wave per node
+        hipLaunchKernelGGL(k_sieve_emit_pos, dim3((uint32_t)(g < 8192 ? g : 8192)), dim3(256), 0, st, rx, rx_len,
+                           segs, mid, b.m_total, b.capC, b.mark, b.hops, b.rank, b.npath, b.scr, b.lgP, fr, vmask,
+                           reinterpret_cast<dsieve*>(b.state));
+        return hipGetLastError();
+    }
     const uint32_t lc = (uint32_t)((b.capC + 255) / 256 < 8192 ? (b.capC + 255) / 256 : 8192);
     hipLaunchKernelGGL(k_sieve_emit, dim3(lc), dim3(256), 0, st, rx, rx_len, segs, mid, b.S, b.m_total, b.capC,
                        b.mark, b.hops, b.rank, b.npath, fr, vmask, reinterpret_cast<dsieve*>(b.state));

@@ -757,7 +757,7 @@ def sieve_windows():
     """Set the sieve's window geometry for one test (hops, window bytes)."""
     L = libhv_amd.lib()
     prev = (ctypes.c_uint64 * 2)()
-    L.hvws_set_sieve_windows(64, 0, prev)
+    L.hvws_set_sieve_windows(256, 0, prev)
     yield lambda hops, win: L.hvws_set_sieve_windows(hops, win, None)
     L.hvws_set_sieve_windows(prev[0], prev[1], None)
 
@@ -769,7 +769,7 @@ def _last_windows(eng):
 
 
 @pytest.mark.parametrize("target,lo,hi,seed,hops,win", [
-    (24 << 20, 128, 1 << 20, 151, 64, (1 << 20) + (16 << 10)),   # config-4 shape, default geometry
+    (24 << 20, 128, 1 << 20, 151, 64, (1 << 20) + (16 << 10)),   # config-4 shape, default window
     (24 << 20, 128, 1 << 20, 152, 8, 64 << 10),                  # windows shorter than frames: walks cross them
     (6 << 20, 1, 4096, 153, 256, 32 << 10),                      # small frames, long walks
     (12 << 20, 100, 70000, 154, 32, 16 << 10)])
