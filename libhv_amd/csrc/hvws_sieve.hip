@@ -550,9 +550,9 @@ __global__ __launch_bounds__(256) void k_sieve_link(const uint8_t* __restrict__ 
 }
 
 // All doubling rounds in one workgroup when the chain arrays fit in LDS
-// (windowed scans: a few thousand survivors) -- one launch instead of
+// (windowed scans: up to ~10 000 survivors) -- one launch instead of
 // ceil(log2 capC), each of which costs a dispatch beside the unmask.
-constexpr uint32_t SV_JLDS = 8192;
+constexpr uint32_t SV_JLDS = 16384;   // 2 x 64 KiB of successors + 16 KiB of marks
 
 __global__ __launch_bounds__(256) void k_sieve_jump_lds(const uint32_t* __restrict__ J, uint64_t* __restrict__ mark,
                                                          const uint64_t* __restrict__ m_total, uint64_t capC,
