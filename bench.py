@@ -338,6 +338,7 @@ def dropin_leg(eng, device: int, seed: int, reads: int = 2000, builds: int = 400
         for impl in ("door", "launch", "ref"):
             res["feed_" + impl].append(feed_once(impl))
             res["build_" + impl].append(build_once(impl))
+    L.hvws_set_door(None, 0)    # park the worker now (not from an exit handler)
     L.hvws_set_door(None, -1)
     med = {k: round(float(np.median(v)), 2) for k, v in res.items()}
     return {

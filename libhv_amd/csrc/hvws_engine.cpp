@@ -215,6 +215,7 @@ struct hvws_ctx {
     uint32_t sv_full_left = 0; // scans left that sieve every tile (a windowed chain fell short)
     uint32_t sv_rt = 0, sv_wt = 0;   // window geometry of the last sieved scan (tiles)
     bool sv_hint_win = false;  // sv_hint_* come from a windowed scan
+    uint64_t sv_mean = 0;      // bytes per frame along the last sieved chain (0: none yet)
     // hvws_pipeline: its three device slots and their events, kept across
     // calls (a per-call hipMalloc/hipFree pair cost the first call ~2x)
     dbuf pipe_slot[3], pipe_segs;
@@ -499,12 +500,16 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
         if (c->sv_win_len && d->active && (!d->use || d->pend + (4ull << 20) < c->sv_win_len)) c->sv_full_left = 15;
         c->sv_hint_win = c->sv_win_len != 0;
         c->sv_win_len = 0;
+        // bytes per frame along the last chain: the window geometry's mean
+        // (single_hint is read only when the frame table had to be sized by
+        // an estimate, so it can belong to an older stream)
+        if (d->active && d->use && d->npath) c->sv_mean = std::max<uint64_t>(1, d->pend / d->npath);
     }
     if (c->sv_full_left) {
         --c->sv_full_left;
         b.rt = b.wt = 1;
     } else {
-        sieve_geometry(rx_len, c->single_hint, b.rt, b.wt);
+        sieve_geometry(rx_len, c->sv_mean ? rx_len / c->sv_mean : c->single_hint, b.rt, b.wt);
     }
     // Counts of a windowed scan say nothing about a scan of every tile.
     const bool stale = b.rt == b.wt && c->sv_hint_win;
@@ -806,6 +811,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             c->sv_win_len = 0;
             c->sv_full_left = 0;
             c->sv_hint_win = false;
+            c->sv_mean = 0;
         }
         if (rx_len >= sieve_min()) {
             if (sieve_state_ready(c) && c->h_sv.as<dsieve>()->active == 0 && c->sv_skip == 0) c->sv_skip = 15;
@@ -1417,6 +1423,7 @@ void door_park(hvws_ctx* c);
 void door_atexit() {
     std::lock_guard<std::mutex> lk(g_door_m);
     for (hvws_ctx* c : g_doors) {
+        if (!c->door_stream || !c->door_live) continue;   // no HIP call at exit unless a worker may still run
         hipSetDevice(c->device);
         door_park(c);
     }
@@ -1498,6 +1505,12 @@ int door_call(hvws_ctx* c) {
 // Send the resident worker home (context teardown, thread and process exit).
 void door_park(hvws_ctx* c) {
     if (!c->door_stream || !c->door_live) return;
+    // already parked by itself (idle): nothing to ask, no relaunch just to exit
+    if (__atomic_load_n(&c->h_door.as<ddoor>()->alive, __ATOMIC_ACQUIRE) == 0 &&
+        hipStreamQuery(c->door_stream) == hipSuccess) {
+        c->door_live = false;
+        return;
+    }
     c->h_door.as<ddoor>()->op = DOOR_EXIT;
     if (door_call(c) != HVWS_OK) (void)hipGetLastError();
     hipStreamSynchronize(c->door_stream);
