@@ -595,6 +595,10 @@ def fixture_for(cfg: str, rank: int):
 
 def main():
     args = parse()
+    wd = float(os.environ.get("HVWS_BENCH_WATCHDOG", "0") or 0)
+    if wd > 0:   # debugging aid: every thread's Python stack to stderr after wd seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(wd, repeat=True)
     rank, world, local, dist = init_dist()
     if world > 1:
         # The CPU baseline is taken at N = 1 only.  At N > 1 every rank runs
