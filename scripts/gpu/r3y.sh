@@ -7,6 +7,10 @@ S=scripts/gpu_step.sh
 TAG=${1:-r3y}
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 rm -f gpurun_out/.stop
+# the worker now loads a request's first chunks beside the request itself
+$S pytest_door_$TAG 300 python -u -m pytest tests/test_gpu_door.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "door or execute or message or decode or build_frame"
+grep -q " passed" gpurun_out/pytest_door_$TAG.log && ! grep -q "failed" gpurun_out/pytest_door_$TAG.log || { echo "door tests not green"; exit 1; }
+$S door_phases_$TAG 120 python3 scripts/probe/door_phases.py 2000
 B4="python3 bench.py --config c4 --segments 1 --steps 30 --warmup 3 --cpu-seconds 0 --host-gib 0 --no-tx --feed-conns 0 --dropin-reads 0"
 $S c4s1_$TAG 200 $B4
 $S pmcF_c4s1_$TAG 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF_c4s1_$TAG -o p -- $B4

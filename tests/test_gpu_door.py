@@ -64,6 +64,26 @@ def test_door_messages_match_oracle(door, seed):
     assert _stats()[1] == st[1]   # worker off: no request posted
 
 
+def test_door_staging_guess(door):
+    """The worker loads the first chunks of a request beside the request
+    itself, guessing its length from the previous one: reads that grow past,
+    shrink below and match the guess (1 B .. 32 KiB) all equal the oracle's."""
+    rng = random.Random(17)
+    data = S.rand_stream(rng, 120, max_len=3000)
+    sizes = [100, 32768, 5, 20000, 8192, 1, 32768, 32767, 16, 8192, 8192, 9000, 3]
+    chunks, tot = [], 0
+    for c in sizes * 4:
+        if tot >= len(data):
+            break
+        chunks.append(min(c, len(data) - tot))
+        tot += chunks[-1]
+    if tot < len(data):
+        chunks.append(len(data) - tot)
+    before = _stats()
+    assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks)
+    assert _stats()[1] > before[1], "no request reached the worker"
+
+
 def test_door_execute_callbacks_and_early_return(door):
     """websocket_parser_execute through the worker: callback logs (with and
     without the user's in-callback decode) and early returns equal the oracle's."""
