@@ -595,8 +595,8 @@ def fixture_for(cfg: str, rank: int):
 
 def main():
     args = parse()
-    wd = float(os.environ.get("HVWS_BENCH_WATCHDOG", "0") or 0)
-    if wd > 0:   # debugging aid: every thread's Python stack to stderr after wd seconds
+    wd = float(os.environ.get("HVWS_BENCH_WATCHDOG", "150") or 0)
+    if wd > 0:   # a stuck run leaves every thread's Python stack on stderr (0: off)
         import faulthandler
         faulthandler.dump_traceback_later(wd, repeat=True)
     rank, world, local, dist = init_dist()
