@@ -1420,13 +1420,20 @@ std::mutex g_door_m;
 std::vector<hvws_ctx*> g_doors;   // contexts with a worker stream (parked at exit)
 void door_park(hvws_ctx* c);
 
+// At exit every worker is parked and its CU-masked stream destroyed here,
+// while the runtime is still up (this library is finalized before the HIP
+// runtime it links), instead of leaving the runtime's own teardown -- or a
+// profiler's -- to meet a queue that still holds a resident kernel.
 void door_atexit() {
     std::lock_guard<std::mutex> lk(g_door_m);
     for (hvws_ctx* c : g_doors) {
-        if (!c->door_stream || !c->door_live) continue;   // no HIP call at exit unless a worker may still run
+        if (!c->door_stream) continue;
         hipSetDevice(c->device);
         door_park(c);
+        hipStreamDestroy(c->door_stream);
+        c->door_stream = nullptr;
     }
+    g_doors.clear();
 }
 
 int door_ensure(hvws_ctx* c) {

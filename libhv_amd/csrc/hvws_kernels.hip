@@ -1002,8 +1002,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
     uint64_t served = 0;
     __shared__ uint64_t s_t[6], s_m[2];
     __shared__ uint64_t s_req[16];
-    __shared__ uint64_t s_spec;   // chunks staged before the request is read: the last request's
-    if (tid == 0) s_spec = 8192 / 16;
     for (;;) {
         if (tid == 0) {
             uint64_t t0 = wall_clock64();
@@ -1034,17 +1032,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
         }
         __syncthreads();
         if (s_exit) return;
-        // The data area's first chunks load in the same round trip as the
-        // request (a guess at its length: the last request's); the data was
-        // written before seq, and these loads come after the acquire.
-        constexpr int SB = (int)(kDoorMax / 16u / kDoorThreads);
-        const uint64_t nspec = s_spec;
-        u32x4 v[SB];
-#pragma unroll
-        for (int u = 0; u < SB; ++u) {
-            const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-            if (c < nspec) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
-        }
         if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
             const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(box) + tid);
             reinterpret_cast<u32x4*>(s_req)[tid] = piece;
@@ -1063,8 +1050,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             s_carry = cin;
             s_t[5] = wall_clock64();
             s_m[0] = __builtin_amdgcn_s_memtime();
-            const uint64_t nc = (s_len + 15u) / 16u;
-            s_spec = nc ? nc : 1;
         }
         __syncthreads();
         const uint64_t seq = s_seq;
@@ -1079,25 +1064,33 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
         }
         const uint64_t L = s_len;
         const uint64_t nch = (L + 15u) / 16u;   // the data area has slack past L: whole chunks throughout
-        // chunks past the guess: a second round trip
-#pragma unroll
-        for (int u = 0; u < SB; ++u) {
-            const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-            if (c >= nspec && c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
-        }
         if (op == DOOR_XOR) {
             // websocket_decode over the data area (16-byte aligned): byte i
             // uses mask[(i + phase) & 3]
             const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
             const u32x4 k4 = u32x4{kw, kw, kw, kw};
+            constexpr int XB = (int)(kDoorMax / 16u / kDoorThreads);
+            u32x4 v[XB];
 #pragma unroll
-            for (int u = 0; u < SB; ++u) {
+            for (int u = 0; u < XB; ++u) {
+                const uint64_t c = (uint64_t)u * kDoorThreads + tid;
+                if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
+            }
+#pragma unroll
+            for (int u = 0; u < XB; ++u) {
                 const uint64_t c = (uint64_t)u * kDoorThreads + tid;
                 if (c < nch) *reinterpret_cast<u32x4*>(data + c * 16u) = v[u] ^ k4;
             }
         } else {
-            // stage the segment in LDS
+            // stage the segment in LDS: every chunk's load in flight at once
             {
+                constexpr int SB = (int)(kDoorMax / 16u / kDoorThreads);
+                u32x4 v[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const uint64_t c = (uint64_t)u * kDoorThreads + tid;
+                    if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
+                }
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
                     const uint64_t c = (uint64_t)u * kDoorThreads + tid;
