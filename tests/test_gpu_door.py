@@ -64,10 +64,9 @@ def test_door_messages_match_oracle(door, seed):
     assert _stats()[1] == st[1]   # worker off: no request posted
 
 
-def test_door_staging_guess(door):
-    """The worker loads the first chunks of a request beside the request
-    itself, guessing its length from the previous one: reads that grow past,
-    shrink below and match the guess (1 B .. 32 KiB) all equal the oracle's."""
+def test_door_varying_read_sizes(door):
+    """Consecutive reads through one worker that grow, shrink and repeat
+    (1 B .. 32 KiB, the worker's largest request) all equal the oracle's."""
     rng = random.Random(17)
     data = S.rand_stream(rng, 120, max_len=3000)
     sizes = [100, 32768, 5, 20000, 8192, 1, 32768, 32767, 16, 8192, 8192, 9000, 3]
