@@ -1420,20 +1420,16 @@ std::mutex g_door_m;
 std::vector<hvws_ctx*> g_doors;   // contexts with a worker stream (parked at exit)
 void door_park(hvws_ctx* c);
 
-// At exit every worker is parked and its CU-masked stream destroyed here,
-// while the runtime is still up (this library is finalized before the HIP
-// runtime it links), instead of leaving the runtime's own teardown -- or a
-// profiler's -- to meet a queue that still holds a resident kernel.
+// At exit a worker still running is parked (no other HIP call here: an
+// exit handler that also destroyed the CU-masked streams hung a test
+// process's exit, profiles/r3ab_raw).
 void door_atexit() {
     std::lock_guard<std::mutex> lk(g_door_m);
     for (hvws_ctx* c : g_doors) {
-        if (!c->door_stream) continue;
+        if (!c->door_stream || !c->door_live) continue;
         hipSetDevice(c->device);
         door_park(c);
-        hipStreamDestroy(c->door_stream);
-        c->door_stream = nullptr;
     }
-    g_doors.clear();
 }
 
 int door_ensure(hvws_ctx* c) {
@@ -2795,9 +2791,17 @@ int hvws_fused_stats(hvws_ctx* c, uint64_t out[2]) {
 int hvws_set_door(hvws_ctx* c, int on) {
     if (!c) c = hvws::thread_ctx();
     const int old = door_on(c) ? 1 : 0;
-    if (on == 0 && c->door_live) {
+    if (on == 0 && c->door_stream) {
+        // off: park the worker and give its CU-masked stream back now (the
+        // next call that wants a worker makes a new one).  A process whose
+        // profiler meets such a stream at exit crashed in its exit-time
+        // destructors (profiles/r3x_rocprof_c3.md).
         hipSetDevice(c->device);
         door_park(c);
+        hipStreamDestroy(c->door_stream);
+        c->door_stream = nullptr;
+        std::lock_guard<std::mutex> lk(g_door_m);
+        g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
     }
     c->door_mode = on < 0 ? -1 : (on ? 1 : 0);
     return old;
