@@ -338,8 +338,11 @@ def dropin_leg(eng, device: int, seed: int, reads: int = 2000, builds: int = 400
         for impl in ("door", "launch", "ref"):
             res["feed_" + impl].append(feed_once(impl))
             res["build_" + impl].append(build_once(impl))
-    L.hvws_set_door(None, 0)    # park the worker now (not from an exit handler)
     L.hvws_set_door(None, -1)
+    # the leg's thread context goes now, worker and its CU-masked stream with
+    # it (a process under rocprofv3 that still held such a stream at exit
+    # crashed in its exit-time destructors, profiles/r3x_rocprof_c3.md)
+    L.hvws_thread_release()
     med = {k: round(float(np.median(v)), 2) for k, v in res.items()}
     return {
         "feed_8KiB_read_us": {"resident_worker": med["feed_door"], "launch_per_call": med["feed_launch"],

@@ -2791,17 +2791,9 @@ int hvws_fused_stats(hvws_ctx* c, uint64_t out[2]) {
 int hvws_set_door(hvws_ctx* c, int on) {
     if (!c) c = hvws::thread_ctx();
     const int old = door_on(c) ? 1 : 0;
-    if (on == 0 && c->door_stream) {
-        // off: park the worker and give its CU-masked stream back now (the
-        // next call that wants a worker makes a new one).  A process whose
-        // profiler meets such a stream at exit crashed in its exit-time
-        // destructors (profiles/r3x_rocprof_c3.md).
+    if (on == 0 && c->door_live) {
         hipSetDevice(c->device);
         door_park(c);
-        hipStreamDestroy(c->door_stream);
-        c->door_stream = nullptr;
-        std::lock_guard<std::mutex> lk(g_door_m);
-        g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
     }
     c->door_mode = on < 0 ? -1 : (on ? 1 : 0);
     return old;
