@@ -581,38 +581,6 @@ __device__ __forceinline__ void walk_frames(const uint8_t* __restrict__ rx, uint
     }
 }
 
-// The first whole frames of a short segment in LDS, one header per step:
-// every lane of the wave walks the same headers (broadcast LDS reads, so the
-// state stays wave-uniform without shuffles) and lane 0 writes the records.
-// One LDS round trip per frame instead of walk_frames' speculation rounds,
-// which cost more than they save for the handful of frames one event-loop read
-// holds (k_door).  Leaves st / pos / n exactly as walk_frames would; stops at
-// a frame the segment cuts, or after maxf frames (walk_frames goes on).
-template <typename Emit>
-__device__ __forceinline__ void serial_frames(const uint8_t* __restrict__ s, uint64_t L, dcarry& st, uint64_t& pos,
-                                              uint64_t& n, uint32_t vmask, uint32_t maxf, Emit&& emit) {
-    const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll 1
-    for (uint32_t k = 0; k < maxf && st.state == S_START && pos < L; ++k) {
-        hdr h;
-        if (!parse_at(s, L, 0, L, pos, h)) break;   // cut by the segment end: the tail
-        if (lane == 0) {
-            frec v;
-            whole_frame_rec(v, pos, h, vmask);
-            emit(n, v);
-        }
-        st.flags = h.flags;   // Q14: the last frame's fields persist
-        st.length = h.length;
-        st.require = 0;
-        st.offset = 0;
-        st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
-        st.started = 0;
-        if (h.flags & F_MASK) st.mask = h.key;
-        ++n;
-        pos += (uint64_t)h.hlen + h.length;
-    }
-}
-
 // ----------------------------------------------------------------- k_walk
 // carry_rec (EMIT, one-launch scan): also write the record of the frame
 // carried in from the previous batch (k_head<true>'s job in the kernel
@@ -1154,7 +1122,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                         n = 1;
                     }
                 }
-                serial_frames(lds, L, st, pos, n, vmask, 32, emit);
                 walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
                 if (tid == 0) {
                     s_n = n;
