@@ -60,8 +60,9 @@ def parse():
     ap.add_argument("--feed-conns", type=int, default=1024,
                     help="event-loop leg: connections per poll iteration (0: skip)")
     ap.add_argument("--feed-iters", type=int, default=20, help="event-loop leg: poll iterations (8 KiB reads each)")
-    ap.add_argument("--dropin-reads", type=int, default=2000,
-                    help="drop-in leg: FeedRecvData calls per pass, one 8 KiB read each (0: skip)")
+    ap.add_argument("--dropin-reads", type=int, default=0,
+                    help="drop-in leg: FeedRecvData calls per pass, one 8 KiB read each (0: skip; "
+                         "scripts/bench_dropin.py runs it alone)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
     return ap.parse_args()

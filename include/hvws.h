@@ -370,7 +370,7 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
  * and parks itself after $HVWS_DOOR_IDLE_US (default 5000) without a
  * request; the next call relaunches it.  Context teardown, thread exit and
  * process exit park it too.  on = 1 / 0 (off: each call launches k_small, or
- * the XOR kernel, as before), -1 = default ($HVWS_DOOR, on).  ctx NULL = the
+ * the XOR kernel, as before), -1 = default ($HVWS_DOOR, off).  ctx NULL = the
  * calling thread's context.  Returns the previous setting.  Results are
  * identical either way; only latency differs. */
 int hvws_set_door(hvws_ctx* ctx, int on);
