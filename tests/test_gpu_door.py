@@ -186,6 +186,7 @@ def test_door_per_thread_workers():
 
     def loop(cases):
         try:
+            libhv_amd.lib().hvws_set_door(None, 1)   # this thread's context (the worker is opt-in)
             for data, chunks in cases:
                 if H.run_messages("gpu", data, chunks) != H.run_messages("oracle", data, chunks):
                     errs.append("mismatch")
