@@ -1510,6 +1510,15 @@ int door_call(hvws_ctx* c) {
 // Send the resident worker home (context teardown, thread and process exit).
 void door_park(hvws_ctx* c) {
     if (!c->door_stream || !c->door_live) return;
+    // $HVWS_DOOR_PARK_FAST=1 (diagnostic only): take a worker that looks
+    // parked (alive == 0, stream idle) as parked without an exit request --
+    // the variant in use when the bench hung
+    static const bool fast = getenv("HVWS_DOOR_PARK_FAST") && atoi(getenv("HVWS_DOOR_PARK_FAST"));
+    if (fast && __atomic_load_n(&c->h_door.as<ddoor>()->alive, __ATOMIC_ACQUIRE) == 0 &&
+        hipStreamQuery(c->door_stream) == hipSuccess) {
+        c->door_live = false;
+        return;
+    }
     c->h_door.as<ddoor>()->op = DOOR_EXIT;
     if (door_call(c) != HVWS_OK) (void)hipGetLastError();
     hipStreamSynchronize(c->door_stream);
