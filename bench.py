@@ -65,7 +65,102 @@ def parse():
                          "scripts/bench_dropin.py runs it alone)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the rank launcher and the timing reductions: no GPU call, "
+                         "no measurement (tests/test_distributed.py)")
     return ap.parse_args()
+
+
+def visible_devices() -> int:
+    """GPUs this process could use, counted without initialising any of them
+    (the launcher parent makes no GPU call): HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES when set, else the KFD topology's GPU nodes."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip()])
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(base):
+            try:
+                props = open(os.path.join(base, node, "properties")).read().split("\n")
+            except OSError:
+                continue
+            simd = [ln.split()[1] for ln in props if ln.startswith("simd_count ")]
+            if simd and int(simd[0]) > 0:
+                n += 1
+    except OSError:
+        pass
+    return n
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: one child
+    process per GPU, as libhv runs one event loop per worker thread
+    (http/server/HttpServer.cpp:216-233) and as `torch.distributed.run` would
+    start them -- RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in each child's
+    environment, rendezvous on 127.0.0.1.  This process makes no GPU call.
+    Rank 0's JSON line is relayed to stdout; the exit status is non-zero when
+    any rank fails (the others are then stopped).  Fewer visible GPUs than N
+    is an error, except under HVWS_BENCH_DEVICE (every rank on one card, a
+    rehearsal) or --dry-run."""
+    import signal
+    import socket
+    import subprocess
+
+    n = args.gpus
+    rehearsal = "HVWS_BENCH_DEVICE" in os.environ or args.dry_run
+    if not rehearsal:
+        have = visible_devices()
+        if have < n:
+            print(f"bench.py: --gpus {n} but {have} GPU(s) visible; refusing to run fewer ranks "
+                  "(HVWS_BENCH_DEVICE=<d> rehearses N ranks on one card)", file=sys.stderr, flush=True)
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True))
+    chunks = []   # rank 0's stdout, read beside the polling loop (a failed rank must not wait on it)
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read().decode()), daemon=True)
+    reader.start()
+    rcs = [None] * n
+    failed = False
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0):
+                    failed = True
+        if failed:
+            break
+        time.sleep(0.05)
+    if failed:
+        for r, p in enumerate(procs):
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGTERM)
+        for r, p in enumerate(procs):
+            try:
+                rcs[r] = p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                rcs[r] = p.wait()
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr, flush=True)
+        return 1
+    reader.join(timeout=30)
+    line = [ln for ln in "".join(chunks).splitlines() if ln.startswith("{")]
+    if not line:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr, flush=True)
+        return 1
+    print(line[-1], flush=True)
+    return 0
 
 
 def log(rank, *a):
@@ -597,13 +692,50 @@ def fixture_for(cfg: str, rank: int):
     return name, json.load(open(path)).get(name)
 
 
+def dry_run(args, rank: int, world: int, local: int, dist) -> None:
+    """--dry-run: the rank plumbing of a real run with the GPU legs stubbed --
+    every rank builds its disjoint batch plan (CPU), the timing rows and the
+    digest-fixture mapping go through the same gloo reductions, rank 0 prints
+    the same keys.  No GPU call, no measurement."""
+    plan = rank_plan("c1", rank, 8)
+    if os.environ.get("HVWS_BENCH_DRYRUN_FAIL_RANK") == str(rank):
+        raise SystemExit(f"rank {rank}: failing on request (HVWS_BENCH_DRYRUN_FAIL_RANK)")
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    t1 = time.perf_counter()
+    trows = gather_rows(dist, [t0, t1, 0.0])
+    fx_name, fx = fixture_for("c3", rank)
+    vrows = gather_rows(dist, [rank, local, int(plan.seed), -1 if fx is None else 1])
+    if rank == 0:
+        print(json.dumps({
+            "metric": "device-resident WS unmask GiB/s, 64 KiB masked frames, 1/2/4/8 MI355X",
+            "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": True,
+            "timing": {"elapsed_s": span_of(trows),
+                       "per_rank": [{"rank": int(r), "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3)}
+                                    for r in range(trows.shape[0])]},
+            "verified": {"ranks": [{"rank": int(v[0]), "local_rank": int(v[1]), "seed": int(v[2]),
+                                    "fixture": f"c5_rank{int(v[0])}" if v[3] >= 0 else None} for v in vrows]},
+        }), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     wd = float(os.environ.get("HVWS_BENCH_WATCHDOG", "150") or 0)
     if wd > 0:   # a stuck run leaves every thread's Python stack on stderr (0: off)
         import faulthandler
         faulthandler.dump_traceback_later(wd, repeat=True)
     rank, world, local, dist = init_dist()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dry_run(args, rank, world, local, dist)
+        return
     if world > 1:
         # The CPU baseline is taken at N = 1 only.  At N > 1 every rank runs
         # the timed steps and the host-inclusive leg (together, so links and

@@ -62,3 +62,49 @@ def test_two_ranks_gloo():
     assert out[0][8] == out[1][8] == 13.0              # latest end - earliest start
     # each rank's c3-shaped batch has its own reference fixture
     assert [o[9] for o in out] == ["c5_rank0", "c5_rank1"] and all(o[10] == 1 << 20 for o in out)
+
+
+def _bench(argv, env_extra=None, timeout=180):
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "HVWS_BENCH_DEVICE"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + argv, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_launcher_two_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts two rank
+    processes itself (RANK / WORLD_SIZE / MASTER_* in their environment, gloo
+    rendezvous on 127.0.0.1) and relays rank 0's one JSON line; --dry-run
+    stubs the GPU legs, so the plumbing runs here on CPU."""
+    import json
+
+    p = _bench(["--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dry_run"] is True
+    assert [r["rank"] for r in out["timing"]["per_rank"]] == [0, 1]
+    v = out["verified"]["ranks"]
+    assert [r["fixture"] for r in v] == ["c5_rank0", "c5_rank1"]
+    assert [r["local_rank"] for r in v] == [0, 1] and v[0]["seed"] != v[1]["seed"]
+
+
+def test_bench_launcher_fails_with_a_rank():
+    """A rank that fails makes the launcher exit non-zero (the other rank is
+    stopped, no result line is printed)."""
+    p = _bench(["--gpus", "2", "--dry-run"], {"HVWS_BENCH_DRYRUN_FAIL_RANK": "1"})
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_launcher_refuses_too_few_gpus():
+    """Fewer visible GPUs than --gpus is an error, never a silent N = 1 run
+    (the parent exits before any rank or GPU call)."""
+    p = _bench(["--gpus", "4"], {"HIP_VISIBLE_DEVICES": "0"}, timeout=60)
+    assert p.returncode == 2 and "refusing" in p.stderr
+    assert not p.stdout.strip()
