@@ -227,15 +227,6 @@ int hvws_set_table_checks(int on);
  * calling thread's context.  Returns the previous mode. */
 int hvws_set_speculation(hvws_ctx* ctx, int mode);
 
-/* SPEC scans as one persistent launch (k_pscan: discovery, the device check
- * and the unmask tile index, phases separated by grid barriers) instead of a
- * chain of ~10 kernels, so a pipelined step's discovery runs beside the
- * previous unmask.  mode 1 = on ($HVWS_PSCAN=1), 0 = the chain (default:
- * measured slower).  Results never depend on it.  Returns the previous mode, or the
- * number of workgroups the last scan launched when mode is -1 (query; 0 =
- * that scan used the chain). */
-int hvws_set_one_launch_scan(hvws_ctx* ctx, int mode);
-
 /* One-walk passes (SPEC, SLACK): mode -1 = adaptive (default: the grid-wide
  * k_verify pair and k_head<true> run only when the last check saw a segment
  * with >= spec_min predicted frames; otherwise k_head<false>, the offsets and
@@ -251,32 +242,9 @@ enum {
     HVWS_PATH_SPEC = 3,             /* speculative table checked exact on the device */
     HVWS_PATH_SPEC_FAILED = 4,      /* speculation rejected by the check, then COUNT/EMIT */
     HVWS_PATH_SLACK = 5,            /* mixed sizes: one EMIT walk into per-segment regions, compacted on the device */
-    HVWS_PATH_SLACK_FAILED = 6,     /* a segment outgrew its region, then COUNT/EMIT */
-    HVWS_PATH_FUSED = 7             /* uniform segments discovered inside the unmask pass (hvws_set_fused) */
+    HVWS_PATH_SLACK_FAILED = 6      /* a segment outgrew its region, then COUNT/EMIT */
 };
 int hvws_last_scan_path(hvws_ctx* ctx);
-
-/* FUSED steps (hvws_step / hvws_step_resident): once the last exact scan of
- * a multi-segment batch found every segment uniform (the SPEC estimates held)
- * and frames average <= 16 KiB, discovery runs inside the unmask pass: each
- * segment's first whole frame sets the size every later frame is checked
- * against while its payload is unmasked.  The verdict comes when that pass
- * ends; hvws_step_resident reads it during the next call (or any other call
- * on the context -- every entry point settles a pending batch first), so its
- * frames, carries and bytes are as the contract says whenever they can be
- * observed.  A batch whose frames did not all have that size is undone (the
- * pass again, XOR being its own inverse) and re-run on the exact path; so is
- * a batch queued behind it.  mode: 2 when the last scan says uniform (a
- * COUNT_EMIT scan's verdict is read once the device has published it,
- * without a wait; after a failed or declined pass the next 16 batches scan
- * exactly; frames must average 64 B - 16 KiB and segments be sorted and
- * disjoint), 0 off (the default: the pass measures slower than SPEC's
- * overlapped discovery + k_unmask at config 2), 1 try on
- * every step (tests), -1 back to $HVWS_FUSED (or 0).  Returns the previous
- * mode. */
-int hvws_set_fused(hvws_ctx* ctx, int mode);
-/* out = {fused steps issued, batches re-run on the exact path}. */
-int hvws_fused_stats(hvws_ctx* ctx, uint64_t out[2]);
 
 /* Device span of a timed region: hvws_span_begin records a marker on each of
  * the context's compute streams, hvws_span_end records the end markers, waits

@@ -114,7 +114,6 @@ _SIGS = {
     "hvws_last_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "hvws_step_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "hvws_set_speculation": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "hvws_set_one_launch_scan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_set_walk_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_last_scan_path": (ctypes.c_int, [ctypes.c_void_p]),
     "hvws_set_fast_bound": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -188,8 +187,6 @@ _SIGS = {
     "hvws_door_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_door_idle_us": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_door_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
-    "hvws_set_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "hvws_fused_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_set_small_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_set_validation": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),

@@ -125,8 +125,6 @@ struct tset {
     dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total, sc_est;
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first, tile_key, tile_kind;
-    dbuf pbar;   // grid-barrier words of the one-launch scan (k_pscan)
-    dbuf f_fmid, f_done, f_ctl, f_wgseg, f_segs, f_carry;   // FUSED path (k_fprep / k_fused)
     uint64_t frame_cap = 0;
     hipEvent_t free_ev = nullptr;   // recorded after the last kernel reading the set (pipelined steps)
     hipEvent_t free_wait = nullptr; // what the next scan into the set waits for: free_ev, or the stop
@@ -135,8 +133,7 @@ struct tset {
     void release() {
         for (dbuf* b : {&carry_out, &counts, &bases, &total, &sc_mid, &sc_npred, &sc_pbase, &sc_fail, &sc_masked,
                         &sc_total, &sc_est, &f_hdr, &f_off, &f_len, &f_length, &f_key, &f_keyrot, &f_info,
-                        &tile_first, &tile_key, &tile_kind, &pbar, &f_fmid, &f_done, &f_ctl, &f_wgseg, &f_segs,
-                        &f_carry})
+                        &tile_first, &tile_key, &tile_kind})
             b->release();
         frame_cap = 0;
     }
@@ -179,18 +176,12 @@ struct hvws_ctx {
     // estimates hold (then the next batch speculates).
     hbuf h_status;
     uint64_t scan_seq = 0;
-    uint64_t status_read = 0;   // newest published scan status fused_eligible has looked at
     bool spec_ok = false;
     // The last check saw a segment with >= spec_min predicted frames: the
     // next one-walk pass keeps the grid-wide k_verify pair (else head + walk).
     bool verify_hint = true;
     int verify_mode = -1;   // hvws_set_walk_verify: -1 adaptive (the hint), 0 never, 1 always
     int spec_mode = -1;   // -1 auto, 0 never, 1 SPEC first, 2 SLACK first ($HVWS_SPEC / hvws_set_speculation)
-    // SPEC as one persistent launch (k_pscan) of pscan_blocks workgroups;
-    // 0 = the kernel chain ($HVWS_PSCAN=0 / hvws_set_one_launch_scan)
-    uint32_t pscan_blocks = 0;
-    int pscan_mode = -1;   // -1 not yet decided
-    bool pscan_ran = false;   // the last scan used it (hvws_last_scan_path reports SPEC either way)
     // SLACK (mixed sizes, several segments): scratch table, exact bases, and
     // the per-segment region cap from the last exact scan's largest segment
     dbuf sl_hdr, sl_off, sl_len, sl_length, sl_key, sl_keyrot, sl_info, sl_bx;
@@ -273,27 +264,6 @@ struct hvws_ctx {
     uint64_t door_seq = 0;      // last request number posted
     int door_mode = -1;         // hvws_set_door: -1 default ($HVWS_DOOR, off), 0 off, 1 on
     uint64_t door_launches = 0, door_calls = 0;
-    // FUSED path: the batch issued into each table set and not yet settled
-    // (its verdict read; fixed on the exact path if it failed), the verdict
-    // slots (one per set: a later batch must not overwrite an unread one) and
-    // the gate word the next k_fused reads
-    struct fused_pend {
-        bool active = false;
-        uint64_t seq = 0;
-        uint8_t* rx = nullptr;
-        uint64_t rx_len = 0;
-        bool piped = false;
-        std::vector<hvws_segment> segs;
-        std::vector<websocket_parser> carry;
-        bool has_carry = false;
-    } fz[2];
-    hbuf h_fstatus;
-    dbuf fz_gate;
-    int fused_mode = -1;        // hvws_set_fused: -1 default ($HVWS_FUSED, on), 0 off, 1 always try
-    bool fz_busy = false;       // inside a fused issue or settle (no nested settling)
-    uint64_t fused_steps = 0, fused_fixes = 0;
-    uint64_t fz_nfr = 0;        // records of the last batch whose count is known (sizes the next table)
-    uint32_t fz_skip = 0;       // auto mode: batches left to scan exactly after a failed fused pass
     // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
     // on both of the context's compute streams
     hipEvent_t span_ev[4] = {};
@@ -312,8 +282,6 @@ struct hvws_ctx {
 
 namespace {
 constexpr uint64_t kFastFrameBound = 1ull << 24;   // records: table sized by the bound, no count sync
-int fused_mode(hvws_ctx* c);
-constexpr uint32_t kFusedBackoff = 16;   // exact batches after a failed fused pass (auto mode)
 constexpr uint64_t kReadbackPrefix = 1ull << 16;   // records read back speculatively with the rest
 constexpr uint64_t kSingleMin = 1ull << 20;   // records: smallest one-stream table before its count is known
 constexpr uint64_t kSlackMaxRecords = 1ull << 26;   // SLACK scratch table at most (48 B each: 3.2 GB)
@@ -388,14 +356,9 @@ void from_dcarry(const dcarry& d, websocket_parser& p) {
     reinterpret_cast<uint8_t*>(&p)[kViolByte] = (uint8_t)d.viol;
 }
 
-int fused_settle_all(hvws_ctx* c);
-
-// Every entry point: a fused batch still pending is settled first (its bytes,
-// frames and carries are final afterwards).
-int check_ctx(hvws_ctx* c, bool settle = true) {
+int check_ctx(hvws_ctx* c) {
     if (!c) return set_err(HVWS_EINVAL, "null context");
     HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
-    if (settle && !c->fz_busy && (c->fz[0].active || c->fz[1].active)) return fused_settle_all(c);
     return HVWS_OK;
 }
 
@@ -589,31 +552,6 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     return HVWS_OK;
 }
 
-// Workgroups of the one-launch SPEC scan: 2 per CU (all resident at once
-// even beside an unmask grid that holds every other slot), or the kernel
-// chain (0) when disabled or when the occupancy query cannot vouch for it.
-uint32_t pscan_blocks(hvws_ctx* c) {
-    if (c->pscan_mode < 0) {
-        const char* e = getenv("HVWS_PSCAN");
-        c->pscan_mode = e ? (atoi(e) != 0) : 0;
-    }
-    if (!c->pscan_mode) return 0;
-    if (!c->pscan_blocks) {
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
-            return 0;
-        const int per = pscan_blocks_per_cu();   // advisory; over-reports by one on ROCm 7.2 (cdna guide sec. 1)
-        if (per < 3) return 0;
-        uint32_t want = 2u * (uint32_t)ncu;
-        if (const char* b = getenv("HVWS_PSCAN_BLOCKS")) {
-            const long v = atol(b);
-            if (v > 0 && v <= 2L * ncu) want = (uint32_t)v;
-        }
-        c->pscan_blocks = want;
-    }
-    return c->pscan_blocks;
-}
-
 // Unmask kernel launch with its timing events (no argument checks).  The
 // events ride on the unmask's own dispatch (launch_unmask).
 hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
@@ -746,8 +684,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                                                     (unsigned long long)status_h->seq, (unsigned long long)sc.seq);
         n = status_h->total;
         flags = status_h->flags;
-        c->status_read = sc.seq;   // read here: fused_eligible looks only at newer verdicts
-        if (flags & SPEC_ERR) return set_err(HVWS_EHIP, "one-launch scan: a grid barrier timed out (seq %llu)",
+        if (flags & SPEC_ERR) return set_err(HVWS_EHIP, "scan check reported an error (seq %llu)",
                                              (unsigned long long)sc.seq);
         if (n >= 0xFFFFFFF0ull)
             return set_err(HVWS_EINVAL, "batch holds %llu frames (max 2^32-16)", (unsigned long long)n);
@@ -785,7 +722,6 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     const uint64_t bound = rx_len / 2 + 2 * (uint64_t)nseg + 1;
     uint64_t nfr = bound;
     c->nfr_known = false;
-    c->pscan_ran = false;
     bool tiles_done = false;
     if (nseg == 1) {
         c->scan_path = HVWS_PATH_SINGLE;
@@ -875,14 +811,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         sc.sieve = nullptr;
     } else if (bound <= (c->fast_bound ? c->fast_bound : kFastFrameBound)) {
         c->scan_path = HVWS_PATH_COUNT_EMIT;
-        if (fused_mode(c) != 0 && nseg >= 2) {
-            // publish whether the uniform estimates held (read lazily by a
-            // later fused_eligible): no host wait here
-            sc.status = status_d;
-            sc.seq = ++c->scan_seq;
-        }
         HIP_OR(pass(SCAN_COUNT), HVWS_EHIP);
-        sc.status = nullptr;
         HIP_OR(ensure_frames(c, bound), HVWS_ENOMEM);
         HIP_OR(pass(SCAN_EMIT), HVWS_EHIP);
     } else {
@@ -904,38 +833,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 HIP_OR(ensure_frames(c, c->ts[c->cur ^ 1].frame_cap, /*exact=*/true), HVWS_ENOMEM);
             sc.seq = ++c->scan_seq;
             sc.no_verify = (c->verify_mode < 0 ? c->verify_hint : c->verify_mode != 0) ? 0u : 1u;
-            if (const uint32_t pb = pscan_blocks(c)) {
-                // one launch: SPEC pass + tile index + classes (k_pscan)
-                HIP_OR(c->T().pbar.ensure(sizeof(dpbar)), HVWS_ENOMEM);
-                pscan_args a;
-                a.rx = d_rx;
-                a.rx_len = rx_len;
-                a.segs = segs;
-                a.carry_in = cin;
-                a.carry_out = c->T().carry_out.as<dcarry>();
-                a.counts = c->T().counts.as<uint64_t>();
-                a.bases = c->T().bases.as<uint64_t>();
-                a.total = c->T().total.as<uint64_t>();
-                a.sc = sc;
-                a.fr = frames_of(c);
-                a.spec_min = spec_min();
-                a.tile_first = c->T().tile_first.as<uint32_t>();
-                a.tile_key = c->T().tile_key.as<uint32_t>();
-                a.tile_kind = c->T().tile_kind.as<uint8_t>();
-                a.ntiles = ntiles;
-                a.tile = tile;
-                a.bar = c->T().pbar.as<dpbar>();
-                a.nseg = nseg;
-                a.vmask = c->vmask;
-                HIP_OR(launch_pscan(a, pb, c->cs), HVWS_EHIP);
-                HIP_OR(release_slot(), HVWS_EHIP);
-                sc.src_segs = nullptr;
-                sc.src_carry = nullptr;
-                c->pscan_ran = true;
-            } else {
-                HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
-                if ((rc = tiles()) != HVWS_OK) return rc;
-            }
+            HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
+            if ((rc = tiles()) != HVWS_OK) return rc;
             if (unmask_into) {
                 HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len), HVWS_EHIP);
@@ -1656,312 +1555,6 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     return HVWS_OK;
 }
 
-// ------------------------------------------------------------- FUSED path
-// (k_fprep / k_fwgseg / k_fused, hvws_kernels.hip.)  Batches of uniform
-// segments of small frames, once the last exact scan found the estimates
-// holding: discovery happens inside the unmask pass.  The verdict arrives
-// when that pass ends, so it is read lazily: a pipelined step settles the
-// previous batch (its pass ends while this batch's prep runs beside it); every
-// other entry point settles whatever is pending first (check_ctx).  A failed
-// batch is undone by the same kernel in undo mode and re-run on the exact
-// path; a batch issued behind it saw the gate and did nothing, and is re-run
-// exactly too.
-constexpr int HVWS_PATH_FUSED_INTERNAL = 7;
-
-// 0 off, 1 on every step, 2 when the last scan says uniform ($HVWS_FUSED for
-// -1; default 0: measured slower than SPEC + k_unmask at config 2)
-int fused_mode(hvws_ctx* c) {
-    if (c->fused_mode >= 0) return c->fused_mode;
-    static const int env = getenv("HVWS_FUSED") ? atoi(getenv("HVWS_FUSED")) : 0;
-    return env < 0 ? 0 : (env > 2 ? 2 : env);
-}
-
-// k_ftile finds a tile's segments by offset: they must be sorted and disjoint
-bool segments_sorted(const hvws_segment* segs, uint32_t nseg) {
-    for (uint32_t i = 1; i < nseg; ++i)
-        if (segs[i].off < segs[i - 1].off + segs[i - 1].len) return false;
-    return true;
-}
-
-bool fused_eligible(hvws_ctx* c, uint64_t rx_len, const hvws_segment* segs, uint32_t nseg) {
-    const int mode = fused_mode(c);
-    if (mode == 0 || nseg == 0 || c->vmask) return false;
-    if (c->nfr_known) c->fz_nfr = c->nfr;   // the last exact count (a pending fused batch has none yet)
-    if (c->h_status.p) {
-        // Exact scans publish their verdict and count (COUNT_EMIT with no
-        // host wait); take the newest one the device has published since the
-        // last look (pipelined, the last scan's may still be running).  A
-        // stale verdict is only a hint: the fused pass checks every header
-        // it assumes.
-        const dspec_status* st = c->h_status.as<dspec_status>();
-        const uint64_t s = __atomic_load_n(&st->seq, __ATOMIC_ACQUIRE);
-        if (s > c->status_read) {
-            c->status_read = s;
-            const uint64_t tot = st->total;
-            const uint32_t fl = st->flags;
-            if (!(fl & SPEC_ERR) && tot < 0xFFFFFFF0ull) {
-                c->spec_ok = (fl & SPEC_MATCH) != 0;
-                if (tot) c->fz_nfr = tot;
-            }
-        }
-    }
-    if (mode == 1) return segments_sorted(segs, nseg);   // tests: whatever the last scan said
-    if (c->fz_skip) {   // a fused pass failed recently
-        --c->fz_skip;
-        return false;
-    }
-    if (nseg < 2 || !c->spec_ok || c->fz_nfr == 0) return false;
-    // small frames only: at 64 KiB frames the separate scan is 0.6 % of a
-    // step and k_unmask's tile geometry is at the in-place ceiling
-    const uint64_t avg = rx_len / c->fz_nfr;
-    return avg <= (16u << 10) && avg >= kFusedTile / kFusedMaxSpans && segments_sorted(segs, nseg);
-}
-
-int fused_wait(hvws_ctx* c, int set, uint64_t seq, dspec_status& out) {
-    const dspec_status* st = c->h_fstatus.as<dspec_status>() + set;
-    for (uint64_t spin = 0;; ++spin) {
-        if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) {
-            out = *st;
-            return HVWS_OK;
-        }
-        if ((spin & 1023) == 1023) {
-            const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess) {
-                if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) {
-                    out = *st;
-                    return HVWS_OK;
-                }
-                return set_err(HVWS_EHIP, "fused pass did not publish (seq %llu)", (unsigned long long)seq);
-            }
-            if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "stream error: %s", hipGetErrorString(q));
-        }
-        __builtin_ia32_pause();
-    }
-}
-
-fused_args fused_args_of(hvws_ctx* c, int set, uint8_t* d_rx, uint64_t rx_len, uint32_t nseg, uint64_t seq, bool undo) {
-    tset& T = c->ts[set];
-    fused_args a;
-    a.rx = d_rx;
-    a.rx_len = rx_len;
-    a.segs = T.f_segs.as<dseg>();
-    a.fmid = T.f_fmid.as<dfmid>();
-    a.est = T.sc_est.as<uint64_t>();
-    a.bases = T.bases.as<uint64_t>();
-    a.total = T.total.as<uint64_t>();
-    a.first_fail = T.sc_fail.as<uint64_t>();
-    a.done_cnt = T.f_done.as<uint64_t>();
-    a.ctl = T.f_ctl.as<dfctl>();
-    a.tiles = T.f_wgseg.as<dftile>();
-    a.ntiles = (rx_len + kFusedTile - 1) / kFusedTile;
-    a.fr.hdr_off = T.f_hdr.as<int64_t>();
-    a.fr.pay_off = T.f_off.as<uint64_t>();
-    a.fr.pay_len = T.f_len.as<uint64_t>();
-    a.fr.length = T.f_length.as<uint64_t>();
-    a.fr.key = T.f_key.as<uint32_t>();
-    a.fr.keyrot = T.f_keyrot.as<uint32_t>();
-    a.fr.info = T.f_info.as<uint32_t>();
-    a.fr.cap = T.frame_cap;   // an estimate past the table declines the pass
-    a.carry_out = T.carry_out.as<dcarry>();
-    a.counts = T.counts.as<uint64_t>();
-    a.gate = c->fz_gate.as<uint64_t>();
-    a.status = mapped<dspec_status>(c->h_fstatus) + set;
-    a.seq = seq;
-    a.nseg = nseg;
-    a.vmask = c->vmask;
-    a.undo = undo ? 1u : 0u;
-    static const uint32_t dbg = getenv("HVWS_FUSED_DBG") ? (uint32_t)atoi(getenv("HVWS_FUSED_DBG")) : 0u;
-    a.dbg = dbg;
-    return a;
-}
-
-// The exact path for a batch (its own segment table and carries again).
-int exact_rerun(hvws_ctx* c, hvws_ctx::fused_pend& p) {
-    const uint32_t nseg = (uint32_t)p.segs.size();
-    int rc = upload_segments(c, p.segs.data(), p.has_carry ? p.carry.data() : nullptr, nseg, p.rx_len);
-    if (rc != HVWS_OK) return rc;
-    c->cs = c->stream;
-    bool unmasked = false;
-    if ((rc = scan_device_carry(c, p.rx, p.rx_len, nseg, p.rx, &unmasked)) != HVWS_OK) return rc;
-    return unmasked ? HVWS_OK : unmask_impl(c, p.rx, p.rx_len);
-}
-
-// Read the verdict of the batch pending in `set`; fix it (and the newer
-// batch, gated behind it) on the exact path if it failed.
-int fused_settle(hvws_ctx* c, int set) {
-    hvws_ctx::fused_pend& p = c->fz[set];
-    if (!p.active) return HVWS_OK;
-    const bool prev_busy = c->fz_busy;
-    c->fz_busy = true;
-    dspec_status v;
-    int rc = fused_wait(c, set, p.seq, v);
-    p.active = false;
-    if (rc == HVWS_OK && (v.flags & SPEC_OK) && !(v.flags & FUSED_GATED)) {
-        if (set == c->cur) {
-            c->nfr = v.total;
-            c->nfr_known = true;
-        }
-        c->fz_nfr = v.total;
-        c->fz_busy = prev_busy;
-        return HVWS_OK;
-    }
-    if (rc != HVWS_OK) {
-        c->fz_busy = prev_busy;
-        return rc;
-    }
-    // failed (or gated): undo what the pass XORed, clear the gate, re-run exactly
-    ++c->fused_fixes;
-    c->spec_ok = false;
-    // a real misprediction or frames too small for the tiles (not a batch
-    // larger than the table, not one gated behind a failure): auto mode scans
-    // exactly for a while
-    if (!(v.flags & (FUSED_GATED | FUSED_UNTOUCHED)) || (v.flags & FUSED_DECLINED)) c->fz_skip = kFusedBackoff;
-    hvws_ctx::fused_pend newer;
-    const int other = set ^ 1;
-    const bool has_newer = c->fz[other].active && set != c->cur;   // issued behind it, gated
-    if (has_newer) {
-        newer = c->fz[other];
-        c->fz[other].active = false;
-    }
-    if (!(v.flags & FUSED_UNTOUCHED)) {
-        const fused_args a = fused_args_of(c, set, p.rx, p.rx_len, (uint32_t)p.segs.size(), p.seq, true);
-        HIP_OR(launch_fused(a, c->stream), HVWS_EHIP);
-    }
-    HIP_OR(hipMemsetAsync(c->fz_gate.p, 0, 8, c->stream), HVWS_EHIP);
-    c->cur = set ^ 1;   // the exact scan takes the set after this one's (it flips)
-    rc = exact_rerun(c, p);
-    if (rc == HVWS_OK && has_newer) rc = exact_rerun(c, newer);
-    c->piped = false;   // the next pipelined step re-arms both sets' free events
-    c->fz_busy = prev_busy;
-    return rc;
-}
-
-int fused_settle_all(hvws_ctx* c) {
-    if (c->fz_busy) return HVWS_OK;
-    int rc = HVWS_OK;
-    // older first: the set that is not current
-    if (c->fz[c->cur ^ 1].active && (rc = fused_settle(c, c->cur ^ 1)) != HVWS_OK) return rc;
-    if (c->fz[c->cur].active && (rc = fused_settle(c, c->cur)) != HVWS_OK) return rc;
-    return HVWS_OK;
-}
-
-// Issue one batch on the FUSED path.  piped: its prep runs on the scan
-// stream beside the previous batch's pass, and the previous batch is settled
-// after this one is queued; else everything runs on the context stream and
-// the batch is settled before returning.
-int fused_issue(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
-                const websocket_parser* carry_in, uint32_t nseg, bool piped) {
-    int rc;
-    c->fz_busy = true;
-    struct unbusy {
-        hvws_ctx* c;
-        ~unbusy() { c->fz_busy = false; }
-    } ub{c};
-    const int set = c->cur ^ 1;
-    if (c->fz[set].active && (rc = fused_settle(c, set)) != HVWS_OK) return rc;   // two batches ago (normally settled)
-    if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
-    c->prev_path = c->scan_path;
-    c->cur ^= 1;
-    tset& T = c->T();
-    hipStream_t ps = piped ? c->sstream : c->stream;
-    if (piped && T.free_pending) {
-        HIP_OR(hipStreamWaitEvent(ps, T.free_wait, 0), HVWS_EHIP);
-        T.free_pending = false;
-    }
-    // tables: the frame table holds the last count with room (the estimate
-    // must fit it, else the pass declines and the exact path runs).  Exact
-    // size: with growth room on top, the two sets would ratchet each other up.
-    const uint64_t want = std::max<uint64_t>(c->fz_nfr + c->fz_nfr / 8 + 64, 1024);
-    HIP_OR(ensure_frames(c, want, /*exact=*/true), HVWS_ENOMEM);
-    const uint64_t ntiles = (rx_len + kFusedTile - 1) / kFusedTile;
-    HIP_OR(T.counts.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(T.bases.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(T.total.ensure(8), HVWS_ENOMEM);
-    HIP_OR(T.carry_out.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
-    HIP_OR(T.sc_est.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(T.sc_fail.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(T.f_fmid.ensure((uint64_t)nseg * sizeof(dfmid) + 64), HVWS_ENOMEM);
-    HIP_OR(T.f_done.ensure((uint64_t)nseg * 8 + 8), HVWS_ENOMEM);
-    HIP_OR(T.f_ctl.ensure(sizeof(dfctl)), HVWS_ENOMEM);
-    HIP_OR(T.f_wgseg.ensure(ntiles * sizeof(dftile) + 64), HVWS_ENOMEM);
-    HIP_OR(T.f_segs.ensure((uint64_t)nseg * sizeof(dseg) + 64), HVWS_ENOMEM);
-    HIP_OR(T.f_carry.ensure((uint64_t)nseg * sizeof(dcarry) + 64), HVWS_ENOMEM);
-    c->h_fstatus.flags = hipHostMallocCoherent;
-    if (!c->h_fstatus.p) {
-        HIP_OR(c->h_fstatus.ensure(2 * sizeof(dspec_status)), HVWS_ENOMEM);
-        memset(c->h_fstatus.p, 0, 2 * sizeof(dspec_status));
-    }
-    if (!c->fz_gate.p) {
-        HIP_OR(c->fz_gate.ensure(64), HVWS_ENOMEM);
-        HIP_OR(hipMemsetAsync(c->fz_gate.p, 0, 64, c->stream), HVWS_EHIP);
-    }
-    if (!mapped<dspec_status>(c->h_fstatus)) return set_err(HVWS_EHIP, "fused status not device-mapped");
-    HIP_OR(begin_timed_scan(c, false), HVWS_EHIP);
-    HIP_OR(hipMemsetAsync(T.f_ctl.p, 0, sizeof(dfctl), ps), HVWS_EHIP);
-    HIP_OR(launch_fprep(d_rx, rx_len, c->up_src_segs, c->up_src_carry, T.f_segs.as<dseg>(), T.f_carry.as<dcarry>(),
-                        nseg, T.f_fmid.as<dfmid>(), T.sc_est.as<uint64_t>(), T.sc_fail.as<uint64_t>(),
-                        T.f_done.as<uint64_t>(), T.carry_out.as<dcarry>(), T.counts.as<uint64_t>(), T.f_ctl.as<dfctl>(),
-                        c->vmask, ps),
-           HVWS_EHIP);
-    if (c->up_slot >= 0) {   // the pinned upload slot is free once k_fprep has run
-        HIP_OR(hipEventRecord(c->up_ev[c->up_slot], ps), HVWS_EHIP);
-        c->up_pending[c->up_slot] = true;
-        c->up_slot = -1;
-    }
-    c->up_src_segs = nullptr;
-    c->up_src_carry = nullptr;
-    HIP_OR(launch_offsets(T.sc_est.as<uint64_t>(), T.bases.as<uint64_t>(), nseg, T.total.as<uint64_t>(), ps), HVWS_EHIP);
-    HIP_OR(launch_ftile(d_rx, T.f_segs.as<dseg>(), T.f_fmid.as<dfmid>(), T.sc_est.as<uint64_t>(),
-                        T.bases.as<uint64_t>(), nseg, rx_len, T.f_wgseg.as<dftile>(), T.f_ctl.as<dfctl>(), ps),
-           HVWS_EHIP);
-    if (piped) {
-        HIP_OR(hipEventRecord(c->scan_done, ps), HVWS_EHIP);
-        HIP_OR(hipStreamWaitEvent(c->stream, c->scan_done, 0), HVWS_EHIP);
-    }
-    const uint64_t seq = ++c->scan_seq;
-    const fused_args a = fused_args_of(c, c->cur, d_rx, rx_len, nseg, seq, false);
-    const bool timed = step_events(c) >= 1;
-    HIP_OR(launch_fused(a, c->stream, timed ? c->tev[c->t_cur][2] : nullptr, timed ? c->tev[c->t_cur][3] : nullptr),
-           HVWS_EHIP);
-    if (timed) c->t_rec[c->t_cur] |= (uint8_t)(4u | 8u);
-    c->t_unmask[c->t_cur] = true;
-    if (piped) {   // the next prep into this set waits for this pass
-        if (timed) {
-            T.free_wait = c->tev[c->t_cur][3];
-        } else {
-            HIP_OR(hipEventRecord(T.free_ev, c->stream), HVWS_EHIP);
-            T.free_wait = T.free_ev;
-        }
-        T.free_pending = true;
-    }
-    hvws_ctx::fused_pend& p = c->fz[c->cur];
-    p.active = true;
-    p.seq = seq;
-    p.rx = d_rx;
-    p.rx_len = rx_len;
-    p.piped = piped;
-    p.segs.assign(segs, segs + nseg);
-    p.has_carry = carry_in != nullptr;
-    if (carry_in) p.carry.assign(carry_in, carry_in + nseg);
-    else p.carry.clear();
-    ++c->fused_steps;
-    c->scan_path = HVWS_PATH_FUSED_INTERNAL;
-    c->nseg = nseg;
-    c->nfr_known = false;
-    c->rx = d_rx;
-    c->rx_len = rx_len;
-    c->have_scan = true;
-    c->hcache_valid = false;
-    // settle the previous batch (its pass ends while this batch's prep runs),
-    // or, serial, this one
-    if (piped) {
-        if (c->fz[c->cur ^ 1].active && (rc = fused_settle(c, c->cur ^ 1)) != HVWS_OK) return rc;
-    } else if ((rc = fused_settle(c, c->cur)) != HVWS_OK) {
-        return rc;
-    }
-    return HVWS_OK;
-}
-
 void stall_fn(void* usec) { usleep((useconds_t)(uintptr_t)usec); }
 
 }  // namespace
@@ -2041,7 +1634,6 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     door_release(c);
-    if (fused_settle_all(c) != HVWS_OK) (void)hipGetLastError();   // pending fused batches: bytes final first
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->sstream) hipStreamSynchronize(c->sstream);
     for (tset& t : c->ts) {
@@ -2082,8 +1674,6 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     for (auto& ev : c->span_ev)
         if (ev) hipEventDestroy(ev);
     c->h_status.release();
-    c->h_fstatus.release();
-    c->fz_gate.release();
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy_in) hipStreamDestroy(c->copy_in);
     if (c->copy_out) hipStreamDestroy(c->copy_out);
@@ -2313,22 +1903,10 @@ int hvws_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) { return unmask_imp
 
 int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
                        const websocket_parser* carry_in, uint32_t nseg) {
-    int rc = check_ctx(c, false);
+    int rc = check_ctx(c);
     if (rc) return rc;
     if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
-    if (fused_eligible(c, rx_len, segs, nseg)) {
-        if (!c->piped) {
-            for (tset& t : c->ts) {
-                HIP_OR(hipEventRecord(t.free_ev, c->stream), HVWS_EHIP);
-                t.free_wait = t.free_ev;
-                t.free_pending = true;
-            }
-            c->piped = true;
-        }
-        return fused_issue(c, d_rx, rx_len, segs, carry_in, nseg, true);
-    }
-    if ((rc = fused_settle_all(c)) != HVWS_OK) return rc;
     if (!c->piped) {
         // Entering pipelined mode: both table sets may still be read by work
         // queued on the context stream.
@@ -2354,11 +1932,6 @@ int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* s
     if (rc) return rc;
     if (!segs && nseg) return set_err(HVWS_EINVAL, "null segment table");
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
-    if (fused_eligible(c, rx_len, segs, nseg)) {
-        c->cs = c->stream;
-        c->piped = false;
-        return fused_issue(c, d_rx, rx_len, segs, carry_in, nseg, false);
-    }
     if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
     bool unmasked = false;
     if ((rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked)) != HVWS_OK) return rc;
@@ -2778,21 +2351,6 @@ uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {
     return old;
 }
 
-int hvws_set_fused(hvws_ctx* c, int mode) {
-    if (!c) return -1;
-    const int old = c->fused_mode;
-    c->fused_mode = mode < 0 ? -1 : (mode > 2 ? 2 : mode);
-    c->fz_skip = 0;
-    return old;
-}
-
-int hvws_fused_stats(hvws_ctx* c, uint64_t out[2]) {
-    if (!c || !out) return set_err(HVWS_EINVAL, "null argument");
-    out[0] = c->fused_steps;
-    out[1] = c->fused_fixes;
-    return HVWS_OK;
-}
-
 int hvws_set_door(hvws_ctx* c, int on) {
     if (!c) c = hvws::thread_ctx();
     const int old = door_on(c) ? 1 : 0;
@@ -2890,15 +2448,6 @@ uint64_t hvws_set_fast_bound(hvws_ctx* c, uint64_t records) {
     if (!c) return 0;
     const uint64_t old = c->fast_bound ? c->fast_bound : kFastFrameBound;
     c->fast_bound = records;
-    return old;
-}
-
-int hvws_set_one_launch_scan(hvws_ctx* c, int mode) {
-    if (!c) c = thread_ctx();
-    if (!c) return -1;
-    if (mode < 0) return c->pscan_ran ? (int)c->pscan_blocks : 0;
-    const int old = c->pscan_mode < 0 ? (getenv("HVWS_PSCAN") ? atoi(getenv("HVWS_PSCAN")) != 0 : 0) : c->pscan_mode;
-    c->pscan_mode = mode ? 1 : 0;
     return old;
 }
 

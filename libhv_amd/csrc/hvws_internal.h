@@ -143,36 +143,6 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint32_t  no_verify;     // SPEC/SLACK: head + walk only (no k_verify pair, no k_head<true>)
 };
 
-// Grid-barrier words of the one-launch scan (k_pscan), zeroed before each launch.
-struct dpbar {
-    uint32_t count;   // arrivals: barrier k completes at k x workgroups
-    uint32_t err;     // a barrier timed out
-    uint32_t pad[14];
-};
-
-// Everything the one-launch SPEC scan reads and writes (kernel argument).
-struct pscan_args {
-    const uint8_t* rx;
-    uint64_t       rx_len;
-    const dseg*    segs;
-    const dcarry*  carry_in;
-    dcarry*        carry_out;
-    uint64_t*      counts;
-    uint64_t*      bases;
-    uint64_t*      total;
-    scan_scratch   sc;
-    dframes        fr;
-    uint64_t       spec_min;
-    uint32_t*      tile_first;
-    uint32_t*      tile_key;
-    uint8_t*       tile_kind;
-    uint64_t       ntiles;
-    uint64_t       tile;
-    dpbar*         bar;
-    uint32_t       nseg;
-    uint32_t       vmask;
-};
-
 // Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
 // b+16, ... to one XCD; map them to adjacent tiles so each XCD's L2 and
 // memory channels see one contiguous range.
@@ -259,12 +229,6 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
-// The SPEC pass + tile index/classes as one persistent launch (k_pscan) of
-// `blocks` workgroups, all of which must be resident at once (<= 2 per CU);
-// zeroes a.bar first.  The check verdict is published like k_spec_check's.
-hipError_t launch_pscan(const pscan_args& a, uint32_t blocks, hipStream_t st);
-int pscan_blocks_per_cu();
-uint32_t pscan_threads();
 // *total > cap: *total = 0; publishes the count to status (SPEC_OK if within cap).
 hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st);
 hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uint64_t* nfr_dev,
@@ -286,87 +250,6 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
                         drec* h_rec, uint64_t h_rec_cap, dsmall_out* h_out, uint8_t* h_rx, int unmask, uint32_t vmask,
                         uint32_t stage_lds, uint64_t* h_done, uint64_t seq, hipStream_t st,
                         hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-// FUSED scan path (hvws_kernels.hip, k_fprep / k_fwgseg / k_fused): uniform
-// segments discovered inside the unmask pass itself.  Per segment, k_fprep
-// runs the carried-in frame exactly and takes the first whole frame's size as
-// the stride hypothesis; k_fused then checks every hypothesised header while
-// it unmasks the payloads it implies, writes the records, finishes each
-// segment's tail exactly and publishes a verdict.  A batch whose hypothesis
-// failed anywhere is undone by the same kernel in undo mode (it XORs exactly
-// the same bytes with the same masks: the hypothesised header bytes it reads
-// are never among the bytes it XORs) and re-run on the exact path.
-struct dfmid {
-    dcarry   st;        // parser state at pos (after the carried-in frame)
-    uint64_t pos;       // segment offset of the first hypothesised whole frame
-    uint64_t stride;    // its size (0: none)
-    uint64_t nwhole;    // hypothesised whole frames
-    uint32_t n_a;       // 1: the carried-in frame has a record (ra)
-    uint32_t tail;      // 1: the tail's header completes (a record is predicted)
-    int64_t  ra_hdr;    // the carried-in frame's record, segment-relative
-    uint64_t ra_off, ra_len, ra_length;
-    uint32_t ra_key, ra_info;
-    uint64_t a_po, a_pe; // the carried-in frame's masked payload span (rx offsets; empty: none)
-    uint64_t t_po, t_pe; // the tail frame's masked payload bytes in the segment
-    uint32_t a_kw, t_kw; // their 4-byte-aligned key words
-};
-struct dfctl {          // per table set, zeroed before k_fprep
-    uint64_t segs_done; // k_ffinish workgroups done (the last publishes)
-    uint64_t fail;      // a segment's hypothesis or count failed
-    uint64_t decline;   // k_ftile: a tile's segments or spans exceed its LDS (the batch runs exactly)
-    uint64_t pad[5];
-};
-constexpr uint32_t kFusedT = 512, kFusedU = 2;   // k_fused tile geometry (k_unmask<512,2>)
-constexpr uint64_t kFusedTile = (uint64_t)kFusedT * kFusedU * 16u;
-constexpr uint32_t kFusedMaxSegs = 64;    // segments per tile
-constexpr uint32_t kFusedMaxSpans = 256;  // payload spans per tile (frames >= 64 B on average)
-constexpr uint32_t FUSED_NOSEG = 0xFFFFFFFFu;
-struct dftile {            // per k_fused tile (k_ftile): its first segment's frames here
-    uint64_t j_lo, nj;     // whole frames overlapping the tile
-    uint64_t w0, stride, nwhole, rec0, off;   // the segment's hypothesis, record of whole frame 0, its offset
-    uint64_t a_po, a_pe, t_po, t_pe;          // its carried-in / tail payload spans (fmid)
-    uint64_t sp_po, sp_pe; // the masked payload span of the whole frame the tile starts inside (empty: none)
-    uint32_t a_kw, t_kw, sp_kw;
-    uint32_t s0;           // the first segment ending after the tile's start; FUSED_NOSEG: no segment bytes
-    uint32_t nin;          // segments with bytes in the tile
-    uint32_t fl;           // 1: carried-in span here, 2: tail span here, 4: s0 starts here, 8: s0 has records
-};
-constexpr uint32_t FUSED_GATED = 8u;      // status flag: not run (the previous fused batch failed)
-constexpr uint32_t FUSED_UNTOUCHED = 16u; // status flag: failed before any byte was XORed
-constexpr uint32_t FUSED_DECLINED = 32u;  // status flag (with UNTOUCHED): a tile's frames do not fit its LDS
-struct fused_args {
-    uint8_t*        rx;
-    uint64_t        rx_len;
-    const dseg*     segs;
-    const dfmid*    fmid;
-    const uint64_t* est;
-    const uint64_t* bases;
-    const uint64_t* total;
-    uint64_t*       first_fail;
-    uint64_t*       done_cnt;
-    dfctl*          ctl;
-    const dftile*   tiles;      // k_ftile: per tile, its first segment and the span it starts inside
-    uint64_t        ntiles;
-    dframes         fr;
-    dcarry*         carry_out;
-    uint64_t*       counts;
-    uint64_t*       gate;       // context word: 1 while a fused batch has failed and is not yet settled
-    dspec_status*   status;     // device-mapped pinned host
-    uint64_t        seq;
-    uint32_t        nseg;
-    uint32_t        vmask;
-    uint32_t        undo;
-    uint32_t        dbg;        // $HVWS_FUSED_DBG (probes): 2 no header parse, 4 no record stores, 8 loads only, 64 no data stores, 128 no header windows
-};
-hipError_t launch_fprep(const uint8_t* rx, uint64_t rx_len, const dseg* src_segs, const dcarry* src_carry, dseg* segs_w,
-                        dcarry* carry_w, uint32_t nseg, dfmid* fmid, uint64_t* est, uint64_t* first_fail,
-                        uint64_t* done_cnt, dcarry* carry_out, uint64_t* counts, dfctl* ctl, uint32_t vmask,
-                        hipStream_t st);
-hipError_t launch_ftile(const uint8_t* rx, const dseg* segs, const dfmid* fmid, const uint64_t* est,
-                        const uint64_t* bases, uint32_t nseg, uint64_t rx_len, dftile* tiles, dfctl* ctl,
-                        hipStream_t st);
-hipError_t launch_fused(const fused_args& a, hipStream_t st, hipEvent_t ev_start = nullptr,
-                        hipEvent_t ev_stop = nullptr);
-
 // Resident small-path worker ("door", k_door): one workgroup that stays on
 // the device between calls and takes one request at a time from a mailbox in
 // fine-grained pinned host memory, so a reference-API call (FeedRecvData,

@@ -1570,144 +1570,6 @@ __global__ void k_tile_fix_class(const uint64_t* __restrict__ off, const uint64_
                    (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
 }
 
-// ---------------------------------------------------------------- k_pscan
-//
-// The SPEC pass as ONE launch (pipelined and serial steps of uniform batches
-// alike).  As a chain of ~10 kernels the next batch's discovery could not
-// overlap the current unmask: a wide kernel queued on the second stream is
-// dispatched only once the unmask grid has been fully launched, so every
-// dependent kernel of the chain after the first waited for the unmask to
-// drain (profiles/r2b_raw/c2_piped_trace.txt).  One persistent launch of G
-// workgroups (2 per CU at most, all resident) is dispatched beside the unmask
-// grid once, and its phases are separated by grid barriers instead of kernel
-// boundaries:
-//   A  head<false> + est (+ zero-copy upload, last_masked cleared)   | barrier
-//   B  block 0: npred -> pbase, total_pred; block 1: est -> bases, total | barrier
-//   V  (only if some segment is long) verify<false> | barrier | verify<true> | barrier
-//   W  walk<true> (+ the carried-in frame's record: k_head<true>'s part)  | barrier
-//   C  block 0: spec check (status fields); all: tile scatter            | barrier
-//   T  tile fixup + classes; block 0 publishes the status sequence number
-// The bodies are the chain's kernels' own code (head_body, verify_body, ...),
-// so records, counts, carry and tiles are the chain's bit for bit.
-//
-// Visibility: a phase's outputs are plain stores; every workgroup's thread 0
-// makes an agent-scope release fence before it arrives at the barrier's
-// counter and an acquire fence after the count is complete (the 8 XCDs have
-// private L2s; cdna_hip_programming.md sec. 6 G16).  Values another
-// workgroup wrote in this launch that are read at a uniform address (totals)
-// are read with atomic loads, so they never come from the scalar cache.
-// Spins are bounded (~seconds): a barrier that cannot complete (a workgroup
-// never resident) sets err, every later barrier then passes at once, the
-// tiles are classified empty (the queued unmask does nothing) and the host
-// gets SPEC_ERR.  The barrier words are zeroed by the host before each launch.
-constexpr uint32_t PSCAN_THREADS = 256;
-constexpr uint32_t PSCAN_SPIN_MAX = 1u << 22;
-
-__device__ __forceinline__ bool pscan_sync(dpbar* __restrict__ b, uint32_t target) {
-    __shared__ uint32_t s_ok;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(&b->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t ok = 1;
-        for (uint32_t spin = 0;; ++spin) {
-            if (__hip_atomic_load(&b->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-            if (__hip_atomic_load(&b->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                ok = 0;
-                break;
-            }
-            if (spin >= PSCAN_SPIN_MAX) {
-                __hip_atomic_fetch_or(&b->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-__device__ __forceinline__ uint64_t ld_shared_u64(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(PSCAN_THREADS) void k_pscan(pscan_args a) {
-    const uint32_t G = gridDim.x, bid = blockIdx.x;
-    const uint32_t wpb = PSCAN_THREADS / 64;
-    const uint32_t w0 = bid * wpb + (threadIdx.x >> 6), wn = G * wpb;
-    scan_scratch& sc = a.sc;
-    dpbar* bar = a.bar;
-    uint32_t nbar = 0;
-    bool ok = true;
-    auto sync = [&]() { ok = pscan_sync(bar, ++nbar * G) && ok; };
-
-    // A: first whole frame, stride and estimate of every segment
-    head_body<false>(a.rx, a.rx_len, a.segs, a.nseg, a.carry_in, sc.mid, sc.npred, sc.first_fail, sc.last_masked,
-                     a.bases, a.fr, a.vmask, a.spec_min, sc.est, sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0,
-                     0, nullptr, w0, wn, HEAD_ZERO_LM);
-    sync();
-    // B: the two exclusive scans
-    if (bid == 0) offsets_body<PSCAN_THREADS>(sc.npred, sc.pbase, a.nseg, sc.total_pred);
-    if (bid == (G > 1 ? 1u : 0u)) {
-        __syncthreads();
-        offsets_body<PSCAN_THREADS>(sc.est, a.bases, a.nseg, a.total);
-    }
-    sync();
-    // V: grid-wide verification of long uniform runs (none at c2/c3 shapes)
-    const uint64_t tp = ok ? ld_shared_u64(sc.total_pred) : 0;
-    if (tp) {
-        verify_body<false>(a.rx, a.rx_len, a.segs, a.nseg, sc.mid, sc.pbase, tp, sc.first_fail, sc.last_masked, a.bases,
-                           a.fr, a.vmask, bid, G);
-        sync();
-        verify_body<true>(a.rx, a.rx_len, a.segs, a.nseg, sc.mid, sc.pbase, tp, sc.first_fail, sc.last_masked, a.bases,
-                          a.fr, a.vmask, bid, G);
-        sync();
-    }
-    // W: the walk, records at the estimated bases
-    walk_body<true>(a.rx, a.rx_len, a.segs, a.nseg, sc.mid, sc.npred, sc.first_fail, sc.last_masked, a.carry_out,
-                    a.counts, a.bases, a.fr, a.vmask, 1, nullptr, nullptr, a.carry_in, w0, wn);
-    sync();
-    // C: the check (block 0; zeroes *total when the table is not exact) beside
-    // the tile scatter over the estimated count (a rejected table's entries
-    // are harmless: T classifies every tile with the checked count)
-    // (capped at the table: a rejected estimate can exceed what was allocated)
-    const uint64_t est_raw = ok ? ld_shared_u64(a.total) : 0;
-    const uint64_t est_total = est_raw < a.fr.cap ? est_raw : a.fr.cap;
-    if (bid == 0)
-        spec_check_body<true, PSCAN_THREADS>(a.counts, sc.est, sc.npred, a.nseg, a.total, a.fr.cap, sc.status, sc.seq, false);
-    tile_scatter_body(a.fr.pay_off, a.fr.pay_len, est_total, a.tile_first, a.ntiles, a.tile,
-                      (uint64_t)bid * PSCAN_THREADS + threadIdx.x, (uint64_t)G * PSCAN_THREADS);
-    sync();
-    // T: tile fixup and classes with the checked count
-    const uint64_t nfr = ok ? ld_shared_u64(a.total) : 0;
-    fix_class_body(a.fr.pay_off, a.fr.pay_len, a.fr.keyrot, nfr, a.tile_first, a.tile_key, a.tile_kind, a.ntiles, a.tile,
-                   a.rx_len, (uint64_t)bid * PSCAN_THREADS + threadIdx.x, (uint64_t)G * PSCAN_THREADS);
-    if (bid == 0 && threadIdx.x == 0) {
-        if (!ok || __hip_atomic_load(&bar->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sc.status->flags = SPEC_ERR;
-        __hip_atomic_store(&sc.status->seq, sc.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-uint32_t pscan_threads() { return PSCAN_THREADS; }
-
-hipError_t launch_pscan(const pscan_args& a, uint32_t blocks, hipStream_t st) {
-    if (a.nseg == 0 || blocks == 0) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(a.bar, 0, sizeof(dpbar), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pscan, dim3(blocks), dim3(PSCAN_THREADS), 0, st, a);
-    return hipGetLastError();
-}
-
-// Workgroups of k_pscan that can be resident at once per CU (occupancy query).
-int pscan_blocks_per_cu() {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pscan, PSCAN_THREADS, 0) != hipSuccess) return 0;
-    return n;
-}
-
 // -------------------------------------------------------------- k_unmask
 //
 // One workgroup per tile of T*U*16 bytes.  Each thread owns U 16-byte chunks
@@ -1883,676 +1745,6 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
                 if (c + b < rx_len) rx[c + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
         }
     }
-}
-
-// ------------------------------------------------------------------ FUSED
-//
-// Uniform segments discovered inside the unmask pass (dfmid, hvws_internal.h).
-// The separate discovery walk of the SPEC path reads one 128-byte line per
-// header beside the previous batch's unmask; here the headers are read by the
-// pass that XORs the payloads around them, in its own tiles.
-//
-// k_fprep   one thread per segment: the carried-in frame (exact state
-//           machine), the first whole frame's size = the stride hypothesis,
-//           the number of whole frames it implies, the tail frame after them
-//           (parsed exactly from its header, which the hypothesis places), the
-//           record estimate est[s], and the XOR spans of the carried-in frame
-//           and the tail.  A segment with no record is finished here.
-// k_ftile   one thread per k_unmask-shaped tile (kFusedTile bytes): its first
-//           segment (segments sorted and disjoint, as hvws.h requires) and that
-//           segment's frames in the tile, incl. the span of the frame the tile
-//           starts inside (its header is in the tile before); declines the
-//           batch (untouched, exact path) when a tile's segments or spans
-//           exceed its LDS lists.
-// k_fused   one workgroup per tile, laid out like k_unmask<512,2>: the tile's
-//           16-byte chunks are loaded first; the threads holding a header's
-//           bytes stage them in LDS; wave 0 parses and checks every header
-//           that starts in the tile against the stride, stages the payload
-//           spans, writes the records (or marks the segment's first failure);
-//           then each chunk is XORed (xor_chunk) and written back by this
-//           workgroup alone -- tiles partition the bytes, so no atomics on
-//           payload.  A header whose size differs from the stride is not
-//           XORed and fails the batch.
-// k_ffinish one thread per segment, after k_fused in stream order: the tail
-//           record, carry-out, count and checks; the last workgroup publishes
-//           the verdict (dspec_status) and the context's gate.
-// Undo mode (a failed batch): k_fused again XORs the same bytes with the same
-// masks -- every mask and span comes from bytes the pass never XORs
-// (hypothesised header bytes, the tail's header, fprep's exact carried-in
-// frame) -- and writes nothing else.  Cross-workgroup state is atomics only
-// (first_fail, ctl): an agent-scope fence would write back the XCD's whole L2
-// (buffer_wbl2) per workgroup (measured: 14 ms per pass at config 2).
-constexpr uint64_t FUSED_NONE = ~0ull;
-
-__global__ __launch_bounds__(256) void k_fprep(const uint8_t* __restrict__ rx, uint64_t rx_len,
-                                               const dseg* __restrict__ src_segs, const dcarry* __restrict__ src_carry,
-                                               dseg* __restrict__ segs_w, dcarry* __restrict__ carry_w, uint32_t nseg,
-                                               dfmid* __restrict__ fmid, uint64_t* __restrict__ est,
-                                               uint64_t* __restrict__ first_fail, uint64_t* __restrict__ done_cnt,
-                                               dcarry* __restrict__ carry_out, uint64_t* __restrict__ counts,
-                                               dfctl* __restrict__ ctl, uint32_t vmask) {
-    const uint32_t s = blockIdx.x * 256u + threadIdx.x;
-    if (s >= nseg) return;
-    dseg sg;
-    dcarry st;
-    if (src_segs) {   // zero-copy upload: read the pinned slot, keep device copies
-        sg = src_segs[s];
-        st = src_carry[s];
-        segs_w[s] = sg;
-        carry_w[s] = st;
-    } else {
-        sg = segs_w[s];
-        st = carry_w[s];
-    }
-    st.started = 0;
-    const uint64_t L = sg.len;
-    const uint8_t* seg = rx + sg.off;
-    uint64_t pos = 0;
-    dfmid m;
-    m.n_a = 0;
-    m.tail = 0;
-    m.stride = 0;
-    m.nwhole = 0;
-    m.ra_hdr = -1;
-    m.ra_off = m.ra_len = m.ra_length = 0;
-    m.ra_key = m.ra_info = 0;
-    m.a_po = m.a_pe = m.t_po = m.t_pe = 0;
-    m.a_kw = m.t_kw = 0;
-    if (st.state != S_START) {
-        frec r;
-        if (scalar_frame(seg, L, st, pos, r, vmask)) {
-            m.n_a = 1;
-            m.ra_hdr = r.hdr_off;
-            m.ra_off = r.pay_off;
-            m.ra_len = r.pay_len;
-            m.ra_length = r.length;
-            m.ra_key = r.key;
-            m.ra_info = r.info;
-            if ((r.info & I_BODY) && (r.info & F_MASK) && r.pay_len) {
-                m.a_po = sg.off + r.pay_off;
-                m.a_pe = m.a_po + r.pay_len;
-                m.a_kw = key_for_aligned(r.key, m.a_po, (r.info >> 8) & 3u);
-            }
-        }
-    }
-    m.st = st;
-    m.pos = pos;
-    if (st.state == S_START && pos < L) {
-        hdr h;
-        if (parse_at(rx, rx_len, sg.off, L, pos, h)) {
-            m.stride = (uint64_t)h.hlen + h.length;
-            m.nwhole = (L - pos) / m.stride;
-        }
-        const uint64_t pt = pos + m.nwhole * m.stride;
-        if (pt < L && L - pt >= 2) {   // the tail's header completes iff its size byte says it fits
-            const uint32_t b1 = seg[pt + 1];
-            const uint32_t len7 = b1 & 0x7Fu;
-            const uint64_t hlen = 2u + (len7 == 126 ? 2u : (len7 == 127 ? 8u : 0u)) + ((b1 & 0x80u) ? 4u : 0u);
-            m.tail = hlen <= L - pt ? 1u : 0u;
-        }
-        if (m.tail) {   // its payload bytes here (the finisher checks the rest of the segment)
-            dcarry ts = st;
-            uint64_t tp = pt;
-            frec rt;
-            if (scalar_frame(seg, L, ts, tp, rt, vmask) && (rt.info & I_BODY) && (rt.info & F_MASK) && rt.pay_len) {
-                m.t_po = sg.off + rt.pay_off;
-                m.t_pe = m.t_po + rt.pay_len;
-                m.t_kw = key_for_aligned(rt.key, m.t_po, (rt.info >> 8) & 3u);
-            }
-        }
-    }
-    const uint64_t e = m.n_a + m.nwhole + m.tail;
-    fmid[s] = m;
-    est[s] = e;
-    first_fail[s] = FUSED_NONE;
-    done_cnt[s] = 0;
-    if (e == 0) {
-        // no record: what follows pos is at most a partial header
-        if (st.state == S_START && pos < L) {
-            frec r;
-            if (scalar_frame(seg, L, st, pos, r, vmask)) atomicOr((unsigned long long*)&ctl->fail, 1ull);
-        }
-        carry_out[s] = st;
-        counts[s] = 0;
-    }
-}
-
-hipError_t launch_fprep(const uint8_t* rx, uint64_t rx_len, const dseg* src_segs, const dcarry* src_carry, dseg* segs_w,
-                        dcarry* carry_w, uint32_t nseg, dfmid* fmid, uint64_t* est, uint64_t* first_fail,
-                        uint64_t* done_cnt, dcarry* carry_out, uint64_t* counts, dfctl* ctl, uint32_t vmask,
-                        hipStream_t st) {
-    if (nseg == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fprep, dim3((nseg + 255u) / 256u), dim3(256), 0, st, rx, rx_len, src_segs, src_carry, segs_w,
-                       carry_w, nseg, fmid, est, first_fail, done_cnt, carry_out, counts, ctl, vmask);
-    return hipGetLastError();
-}
-
-// The frames of segment (sg, m) whose bytes overlap [A, B): whole frames
-// j_lo .. j_lo + nj - 1, and whether the carried-in / tail payload spans do.
-struct fz_tile_seg {
-    uint64_t j_lo, nj;
-    uint32_t na, tl;
-};
-__device__ __forceinline__ fz_tile_seg fz_in_tile(const dseg& sg, const dfmid& m, uint64_t A, uint64_t B) {
-    fz_tile_seg r;
-    r.j_lo = r.nj = 0;
-    r.na = (m.a_pe > m.a_po && m.a_po < B && m.a_pe > A) ? 1u : 0u;
-    r.tl = (m.t_pe > m.t_po && m.t_po < B && m.t_pe > A) ? 1u : 0u;
-    if (m.nwhole) {
-        const uint64_t w0 = sg.off + m.pos, w1 = w0 + m.nwhole * m.stride;
-        const uint64_t lo = A > w0 ? A : w0, hi = B < w1 ? B : w1;
-        if (lo < hi) {
-            r.j_lo = (lo - w0) / m.stride;
-            r.nj = (hi - 1 - w0) / m.stride - r.j_lo + 1;
-        }
-    }
-    return r;
-}
-
-__global__ __launch_bounds__(256) void k_ftile(const uint8_t* __restrict__ rx, const dseg* __restrict__ segs,
-                                               const dfmid* __restrict__ fmid, const uint64_t* __restrict__ est,
-                                               const uint64_t* __restrict__ bases, uint32_t nseg, uint64_t rx_len,
-                                               uint64_t ntiles, dftile* __restrict__ tiles, dfctl* __restrict__ ctl) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (t >= ntiles) return;
-    const uint64_t A = t * kFusedTile, B = A + kFusedTile < rx_len ? A + kFusedTile : rx_len;
-    uint32_t lo = 0, hi = nseg;   // the first segment ending after A
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (segs[mid].off + segs[mid].len > A) hi = mid;
-        else lo = mid + 1;
-    }
-    dftile d = {};
-    d.s0 = FUSED_NOSEG;
-    uint32_t ns = 0;
-    uint64_t nsp = 0;
-    for (uint32_t s = lo; s < nseg && segs[s].off < B; ++s) {
-        if (++ns > kFusedMaxSegs) break;
-        if (!est[s]) continue;
-        const dseg sg = segs[s];
-        const dfmid m = fmid[s];
-        const fz_tile_seg q = fz_in_tile(sg, m, A, B);
-        nsp += q.na + q.tl + q.nj;
-        if (s != lo) continue;
-        // the first segment, whole: k_fused needs no load of its own for it
-        d.j_lo = q.j_lo;
-        d.nj = q.nj;
-        d.w0 = sg.off + m.pos;
-        d.stride = m.stride;
-        d.nwhole = m.nwhole;
-        d.rec0 = bases[s] + m.n_a;
-        d.off = sg.off;
-        d.a_po = m.a_po;
-        d.a_pe = m.a_pe;
-        d.a_kw = m.a_kw;
-        d.t_po = m.t_po;
-        d.t_pe = m.t_pe;
-        d.t_kw = m.t_kw;
-        d.fl = q.na | (q.tl << 1) | ((sg.off >= A) ? 4u : 0u) | 8u;
-        if (q.nj) {
-            // the whole frame the tile starts inside: its span here, from its
-            // header in the tile before (k_fused parses the others from its
-            // own bytes)
-            const uint64_t qf = d.w0 + q.j_lo * m.stride;
-            if (qf < A) {
-                uint64_t l0, h0;
-                ld16(rx, rx_len, qf, l0, h0);
-                const hdr h = parse_hdr(l0, h0);
-                const uint64_t fe = qf + m.stride;
-                d.sp_po = d.sp_pe = fe;
-                if ((uint64_t)h.hlen + h.length == m.stride && (h.flags & F_MASK) && h.length) {
-                    d.sp_po = qf + h.hlen;
-                    d.sp_kw = key_for_aligned(h.key, d.sp_po, 0u);
-                }
-            }
-        }
-    }
-    if (ns > kFusedMaxSegs || nsp > kFusedMaxSpans) atomicOr((unsigned long long*)&ctl->decline, 1ull);
-    if (ns) d.s0 = lo;
-    d.nin = ns;
-    tiles[t] = d;
-}
-
-hipError_t launch_ftile(const uint8_t* rx, const dseg* segs, const dfmid* fmid, const uint64_t* est,
-                        const uint64_t* bases, uint32_t nseg, uint64_t rx_len, dftile* tiles, dfctl* ctl,
-                        hipStream_t st) {
-    const uint64_t ntiles = (rx_len + kFusedTile - 1) / kFusedTile;
-    if (ntiles == 0) return hipSuccess;
-    if (ntiles > 0xFFFFFFFFull * 256u) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ftile, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256), 0, st, rx, segs, fmid, est, bases,
-                       nseg, rx_len, ntiles, tiles, ctl);
-    return hipGetLastError();
-}
-
-// Segment s's frames are all processed: finish it (thread 0).  No bytes are
-// XORed here: the tiles XORed the tail's payload with the rest.
-__device__ void fused_finish(const fused_args& a, uint32_t s) {
-    const dfmid m = a.fmid[s];
-    const dseg sg = a.segs[s];
-    const uint64_t L = sg.len;
-    // an atomic read-modify-write reads at the coherence point every
-    // workgroup's atomicMin reached
-    const uint64_t ff = atomicMin((unsigned long long*)&a.first_fail[s], (unsigned long long)FUSED_NONE);
-    bool fail = ff != FUSED_NONE;
-    if (!fail) {
-        dcarry st = m.st;
-        uint64_t pos = m.pos;
-        if (m.nwhole) {   // the state the whole frames leave (Q14: the last frame's fields persist)
-            uint64_t lo, hi;
-            const uint64_t ql = m.pos + (m.nwhole - 1) * m.stride;
-            ld16(a.rx, a.rx_len, sg.off + ql, lo, hi);
-            const hdr hl = parse_hdr(lo, hi);
-            st.state = S_START;
-            st.flags = hl.flags;
-            st.length = hl.length;
-            st.require = 0;
-            st.offset = 0;
-            st.mask_offset = (hl.flags & F_MASK) ? (uint32_t)(hl.length & 3u) : 0u;
-            st.started = 0;
-            if (hl.flags & F_MASK) {
-                st.mask = hl.key;
-            } else {   // the key of the last masked frame, if any
-                for (uint64_t k = m.nwhole - 1; k-- > 0;) {
-                    ld16(a.rx, a.rx_len, sg.off + m.pos + k * m.stride, lo, hi);
-                    const hdr hk = parse_hdr(lo, hi);
-                    if (hk.flags & F_MASK) {
-                        st.mask = hk.key;
-                        break;
-                    }
-                }
-            }
-            pos = m.pos + m.nwhole * m.stride;
-        }
-        bool has_t = false;
-        frec rt;
-        if (st.state == S_START && pos < L) has_t = scalar_frame(a.rx + sg.off, L, st, pos, rt, a.vmask);
-        // A tail frame that completed here is a whole frame to the exact walk
-        // (which leaves `started` clear); a frame after it means more records
-        // than estimated.
-        const bool more = st.state == S_START && pos < L;
-        if (st.state == S_START) st.started = 0;
-        const uint64_t actual = m.n_a + m.nwhole + (has_t ? 1u : 0u) + (more ? 1u : 0u);
-        if (actual != a.est[s]) fail = true;
-        else if (has_t) store_frame(a.fr, a.bases[s] + m.n_a + m.nwhole, sg.off, rt);
-        a.carry_out[s] = st;
-        a.counts[s] = actual;
-    }
-    if (fail) atomicOr((unsigned long long*)&a.ctl->fail, 1ull);
-}
-
-__device__ void fused_publish(const fused_args& a, uint32_t extra_flags) {
-    const uint64_t fail = atomicOr((unsigned long long*)&a.ctl->fail, 0ull);
-    const bool bad = fail || (extra_flags & (FUSED_GATED | FUSED_UNTOUCHED));
-    a.status->total = *a.total;
-    a.status->flags = (bad ? 0u : (SPEC_OK | SPEC_MATCH)) | extra_flags;
-    a.status->pad2[0] = 0;
-    a.status->pad2[1] = 0;
-    if (!(extra_flags & FUSED_GATED)) *a.gate = bad ? 1ull : 0ull;
-    __threadfence_system();
-    __hip_atomic_store(&a.status->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// One whole frame of a tile's segment: its header parsed (from global memory:
-// the line is being loaded by this workgroup anyway) and checked against the
-// stride; its payload span staged at span index k; its record written (or
-// the segment's first failure marked) when the header starts in the tile.
-__device__ __forceinline__ void fused_frame(const fused_args& a, uint64_t A, uint64_t B, uint32_t s, uint64_t j,
-                                                uint64_t w0, uint64_t stride, uint64_t off, uint64_t rec0,
-                                                uint64_t* s_off, uint64_t* s_end, uint32_t* s_key, uint32_t k,
-                                                uint64_t sp_po, uint64_t sp_pe, uint32_t sp_kw,
-                                                const uint32_t* win = nullptr) {
-    const uint64_t q = w0 + j * stride;
-    const uint64_t fe = q + stride;
-    if (q < A) {   // began in the tile before: its span came with the tile record
-        s_off[k] = sp_po;
-        s_end[k] = sp_pe;
-        s_key[k] = sp_kw;
-        return;
-    }
-    uint64_t lo, hi;
-    if (win && q + 16 <= A + kFusedTile) {
-        // the two chunks holding the header, staged by the threads that loaded them
-        const uint32_t sh = (uint32_t)(q & 15u);
-        const uint32_t w0i = sh >> 2, b = (sh & 3u) * 8u;
-        uint32_t x[5];
-#pragma unroll
-        for (int e = 0; e < 5; ++e) x[e] = win[w0i + e < 8 ? w0i + e : 7];
-        uint32_t y[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = b ? (x[e] >> b) | (x[e + 1] << (32u - b)) : x[e];
-        lo = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
-        hi = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
-    } else {
-        ld16(a.rx, a.rx_len, q, lo, hi);
-    }
-    hdr h = parse_hdr(lo, hi);
-    if (a.dbg & 2u) {   // probe: the hypothesis assumed, no parse
-        h.hlen = 8;
-        h.length = stride - 8;
-        h.flags = F_MASK | 2u;
-        h.key = 0x01020304u;
-    }
-    const bool ok = (uint64_t)h.hlen + h.length == stride;
-    if (ok && (h.flags & F_MASK) && h.length) {
-        s_off[k] = q + h.hlen;
-        s_end[k] = fe;
-        s_key[k] = key_for_aligned(h.key, q + h.hlen, 0u);
-    } else {   // nothing to XOR: an empty span at the frame end keeps the ends non-decreasing
-        s_off[k] = fe;
-        s_end[k] = fe;
-        s_key[k] = 0;
-    }
-    if (!a.undo && !(a.dbg & 4u)) {
-        if (ok) {
-            frec rr;
-            whole_frame_rec(rr, q - off, h, a.vmask);
-            store_frame(a.fr, rec0 + j, off, rr);
-        } else {
-            atomicMin((unsigned long long*)&a.first_fail[s], (unsigned long long)j);
-        }
-    }
-}
-
-__global__ __launch_bounds__(kFusedT, 8) void k_fused(fused_args a) {   // 8 waves per SIMD: <= 64 VGPRs
-    constexpr uint32_t T = kFusedT, U = kFusedU, MS = kFusedMaxSegs, MF = kFusedMaxSpans;
-    static_assert((uint64_t)T * U * 16u == kFusedTile, "tile geometry");
-    __shared__ uint64_t s_off[MF], s_end[MF];
-    __shared__ uint32_t s_key[MF];
-    __shared__ uint32_t g_seg[MS], g_base[MS + 1], g_na[MS];
-    __shared__ uint64_t g_jlo[MS], g_nj[MS], g_w0[MS], g_stride[MS], g_off[MS], g_rec[MS];
-    __shared__ uint32_t s_go, s_nst;
-    __shared__ uint32_t s_win[MF * 8];   // per frame of the first segment: the 32 bytes holding its header
-    const uint32_t tid = threadIdx.x;
-    // linear tile order (as k_unmask<512,2> below 16 GiB); probe 32: XCD-contiguous
-    const uint64_t t = (a.dbg & 32u) ? xcd_tile(blockIdx.x, a.ntiles) : (uint64_t)blockIdx.x;
-    const uint64_t A = t * kFusedTile;
-    const uint64_t B = A + kFusedTile < a.rx_len ? A + kFusedTile : a.rx_len;
-    const bool full = A + kFusedTile <= a.rx_len;
-
-    // 1. the tile's bytes (all threads) and, on wave 0, the control words and
-    // the tile record; then, still on wave 0 and while the bytes arrive, the
-    // first segment's frames in the tile: headers read and checked, spans
-    // staged, records written
-    // control words first (thread 0), so their round trip overlaps the data's
-    uint64_t c_total = 0, c_gate = 0, c_decl = 0;
-    if (tid == 0) {
-        c_total = *a.total;
-        c_gate = *a.gate;
-        c_decl = __hip_atomic_load(&a.ctl->decline, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    u32x4 v[U];
-    if (full) {
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i)
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.rx + A + ((uint64_t)i * T + tid) * 16u));
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
-            const uint64_t c = A + ((uint64_t)i * T + tid) * 16u;
-            uint32_t w4[4] = {0u, 0u, 0u, 0u};
-            for (int b = 0; b < 16; ++b)
-                if (c + b < a.rx_len) w4[b >> 2] |= (uint32_t)a.rx[c + b] << (8 * (b & 3));
-            v[i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
-        }
-    }
-    const dftile d = a.tiles[t];
-    // the first segment's header windows: each thread stages its chunks that
-    // hold the start (slot 2i) or the rest (slot 2i + 1) of frame j_lo + i's
-    // header -- no load of its own for any header inside the tile
-    if ((d.fl & 8u) && d.nj && d.nj <= MF && d.s0 != FUSED_NOSEG && !(a.dbg & 128u)) {
-        const uint64_t q_lo = d.w0 + d.j_lo * d.stride;   // <= A: frames index from the tile's first
-        const uint32_t stride = (uint32_t)(d.stride < 0xFFFFFFFFull ? d.stride : 0xFFFFFFFFull);
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
-            const uint64_t c = A + ((uint64_t)i * T + tid) * 16u;
-            if (c < q_lo) {   // before the segment's first whole frame: only its header can start here
-                if (q_lo < c + 16u) {
-                    uint32_t* w = s_win;
-                    w[0] = v[i].x; w[1] = v[i].y; w[2] = v[i].z; w[3] = v[i].w;
-                }
-                continue;
-            }
-            const uint64_t rel = c - q_lo;   // < 2 tiles
-            const uint32_t jj = (uint32_t)(rel / stride);
-            const uint32_t in = (uint32_t)(rel - (uint64_t)jj * stride);   // chunk start within frame jj
-            // frame jj starts in [c - 16, c]: this chunk is its slot 1 (or slot 0 when it starts at c)
-            if (in < 16u && in != 0u && jj < d.nj) {
-                uint32_t* w = s_win + (jj * 2u + 1u) * 4u;
-                w[0] = v[i].x; w[1] = v[i].y; w[2] = v[i].z; w[3] = v[i].w;
-            }
-            // the next frame to start in [c, c + 16): slot 0
-            const uint32_t jn = in == 0u ? jj : jj + 1u;
-            const uint64_t qn = in == 0u ? c : c + (stride - in);
-            if (qn < c + 16u && jn < d.nj) {
-                uint32_t* w = s_win + jn * 8u;
-                w[0] = v[i].x; w[1] = v[i].y; w[2] = v[i].z; w[3] = v[i].w;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid < 64) {
-        uint32_t go = 1;
-        if (tid == 0) {
-            // gated (the previous fused batch failed), declined (a tile's
-            // frames do not fit its LDS), the table too small for the
-            // estimate, or no records: nothing to do here (k_ffinish publishes)
-            if ((!a.undo && c_gate) || c_decl || c_total > a.fr.cap || c_total == 0 || d.s0 == FUSED_NOSEG) go = 0;
-            s_go = go;
-        }
-        go = (uint32_t)__shfl((int)go, 0, 64);
-        if (go && (a.dbg & 8u) && tid == 0) {   // probe: loads only
-            s_nst = 0;
-            g_base[0] = 0;
-        }
-        if (go && !(a.dbg & 8u)) {
-            uint32_t na = 0, tl = 0;
-            uint64_t nj = 0;
-            if (d.fl & 8u) {
-                na = d.fl & 1u;
-                tl = (d.fl >> 1) & 1u;
-                nj = d.nj;
-                if (na + nj + tl <= MF) {   // (k_ftile declined the batch otherwise)
-                    for (uint64_t i = tid; i < nj; i += 64)
-                        fused_frame(a, A, B, d.s0, d.j_lo + i, d.w0, d.stride, d.off, d.rec0, s_off, s_end,
-                                            s_key, na + (uint32_t)i, d.sp_po, d.sp_pe, d.sp_kw, s_win + i * 8u);
-                    if (tid == 0) {
-                        if (na) {
-                            s_off[0] = d.a_po;
-                            s_end[0] = d.a_pe;
-                            s_key[0] = d.a_kw;
-                        }
-                        if (tl) {
-                            const uint32_t k = na + (uint32_t)nj;
-                            s_off[k] = d.t_po;
-                            s_end[k] = d.t_pe;
-                            s_key[k] = d.t_kw;
-                        }
-                    }
-                }
-                if (tid == 0 && (d.fl & 4u) && !a.undo) {   // the segment starts here: its carried-in record
-                    const dfmid m = a.fmid[d.s0];
-                    if (m.n_a) {
-                        frec r;
-                        r.hdr_off = m.ra_hdr;
-                        r.pay_off = m.ra_off;
-                        r.pay_len = m.ra_len;
-                        r.length = m.ra_length;
-                        r.key = m.ra_key;
-                        r.info = m.ra_info;
-                        store_frame(a.fr, d.rec0 - 1, d.off, r);
-                    }
-                }
-            }
-            if (tid == 0) {
-                g_seg[0] = d.s0;
-                g_base[0] = 0;
-                g_base[1] = na + (uint32_t)nj + tl;
-                g_nj[0] = 0;   // done
-                s_nst = d.nin;
-            }
-            // 2. the other segments of the tile (tiles holding a segment
-            // boundary): lane k, from the segment tables
-            if (d.nin > 1) {
-                const uint32_t s = d.s0 + tid;
-                const bool in = tid >= 1 && tid < d.nin;
-                uint32_t cnt = 0;
-                uint32_t na2 = 0, tl2 = 0;
-                uint64_t j_lo = 0, nj2 = 0, rec0 = 0;
-                dseg sg = {};
-                dfmid m = {};
-                if (in && a.est[s]) {
-                    sg = a.segs[s];
-                    m = a.fmid[s];
-                    const fz_tile_seg q = fz_in_tile(sg, m, A, B);
-                    na2 = q.na;
-                    tl2 = q.tl;
-                    j_lo = q.j_lo;
-                    nj2 = q.nj;
-                    cnt = na2 + (uint32_t)nj2 + tl2;
-                    rec0 = a.bases[s] + m.n_a;
-                    if (sg.off >= A && sg.off < B) {   // its first byte is here: the carried-in record
-                        if (m.n_a && !a.undo) {
-                            frec r;
-                            r.hdr_off = m.ra_hdr;
-                            r.pay_off = m.ra_off;
-                            r.pay_len = m.ra_len;
-                            r.length = m.ra_length;
-                            r.key = m.ra_key;
-                            r.info = m.ra_info;
-                            store_frame(a.fr, rec0 - 1, sg.off, r);
-                        }
-                    }
-                }
-                uint32_t inc = cnt;
-#pragma unroll
-                for (uint32_t dd = 1; dd < 64; dd <<= 1) {
-                    const uint32_t o = (uint32_t)__shfl_up((int)inc, dd, 64);
-                    if (tid >= dd) inc += o;
-                }
-                const uint32_t base = na + (uint32_t)nj + tl + inc - cnt;   // after segment 0's spans
-                if (in) {
-                    g_seg[tid] = s;
-                    g_base[tid] = base;
-                    g_na[tid] = na2;
-                    g_jlo[tid] = j_lo;
-                    g_nj[tid] = nj2;
-                    g_w0[tid] = sg.off + m.pos;
-                    g_stride[tid] = m.stride;
-                    g_off[tid] = sg.off;
-                    g_rec[tid] = rec0;
-                    if (base + cnt <= MF) {
-                        if (na2) {
-                            s_off[base] = m.a_po;
-                            s_end[base] = m.a_pe;
-                            s_key[base] = m.a_kw;
-                        }
-                        if (tl2) {
-                            const uint32_t k = base + na2 + (uint32_t)nj2;
-                            s_off[k] = m.t_po;
-                            s_end[k] = m.t_pe;
-                            s_key[k] = m.t_kw;
-                        }
-                    }
-                }
-                if (tid == d.nin - 1) g_base[d.nin] = base + cnt;
-            }
-        }
-    }
-    __syncthreads();
-    if (!s_go) return;
-    const uint32_t nst = s_nst;
-
-    // 3. the other segments' whole frames, all threads
-    if (nst > 1) {
-        for (uint32_t k = 1; k < nst; ++k) {
-            const uint64_t nj = g_nj[k];
-            if (!nj) continue;
-            const uint32_t sb = g_base[k] + g_na[k];
-            if (sb + nj > MF) continue;   // cannot happen: k_ftile declined the batch
-            const uint32_t s = g_seg[k];
-            for (uint64_t i = tid; i < nj; i += T)
-                fused_frame(a, A, B, s, g_jlo[k] + i, g_w0[k], g_stride[k], g_off[k], g_rec[k], s_off, s_end,
-                                    s_key, sb + (uint32_t)i, 0, 0, 0);
-        }
-        __syncthreads();
-    }
-
-    // 5. XOR and write back (chunks with no masked byte are not written)
-    const uint32_t nf = g_base[nst] < MF ? g_base[nst] : MF;
-    bool dirty[U];
-#pragma unroll
-    for (uint32_t i = 0; i < U; ++i) {
-        const uint64_t c = A + ((uint64_t)i * T + tid) * 16u;
-        if (!full && c >= a.rx_len) {
-            dirty[i] = false;
-            continue;
-        }
-        dirty[i] = xor_chunk(
-            v[i], c, nf, [&](uint32_t k) { return s_off[k]; }, [&](uint32_t k) { return s_end[k]; },
-            [&](uint32_t k) { return s_key[k]; });
-    }
-    if (full && !(a.dbg & 64u)) {
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i)
-            if (dirty[i])
-                __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(a.rx + A + ((uint64_t)i * T + tid) * 16u));
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
-            if (!dirty[i]) continue;
-            const uint64_t c = A + ((uint64_t)i * T + tid) * 16u;
-            const uint32_t w4[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-            for (int b = 0; b < 16; ++b)
-                if (c + b < a.rx_len) a.rx[c + b] = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
-        }
-    }
-}
-
-// After k_fused (stream order: every header check and record is visible):
-// one thread per segment finishes it (tail record, carry-out, count, checks);
-// the last workgroup publishes the verdict -- or the reason k_fused did
-// nothing (gated, declined, table too small).
-__global__ __launch_bounds__(256) void k_ffinish(fused_args a) {
-    __shared__ uint32_t s_mode;
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) {
-        const uint64_t total = *a.total;
-        uint32_t mode = 0;   // 0 finish, else the flags to publish (block 0)
-        if (*a.gate) mode = FUSED_GATED | FUSED_UNTOUCHED;
-        else if (__hip_atomic_load(&a.ctl->decline, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            mode = FUSED_UNTOUCHED | FUSED_DECLINED;
-        else if (total > a.fr.cap) mode = FUSED_UNTOUCHED;
-        s_mode = mode;
-    }
-    __syncthreads();
-    if (s_mode) {
-        if (blockIdx.x == 0 && tid == 0) fused_publish(a, s_mode);
-        return;
-    }
-    const uint32_t s = blockIdx.x * 256u + tid;
-    if (s < a.nseg && a.est[s] && !(a.dbg & 8u)) fused_finish(a, s);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this block's atomicOr(fail) performed
-    __syncthreads();
-    if (tid == 0) {
-        const uint64_t old = atomicAdd((unsigned long long*)&a.ctl->segs_done, 1ull);   // blocks done
-        if (old + 1 == gridDim.x) fused_publish(a, 0u);
-    }
-}
-
-hipError_t launch_fused(const fused_args& a, hipStream_t st, hipEvent_t ev_start, hipEvent_t ev_stop) {
-    const uint64_t ntiles = a.ntiles ? a.ntiles : 1;
-    if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t fb = (a.nseg + 255u) / 256u ? (a.nseg + 255u) / 256u : 1u;
-    const bool fin = !a.undo;
-    if (ev_start || ev_stop) {
-        hipExtLaunchKernelGGL(k_fused, dim3((uint32_t)ntiles), dim3(kFusedT), 0, st, ev_start, fin ? nullptr : ev_stop, 0u,
-                              a);
-        if (fin) hipExtLaunchKernelGGL(k_ffinish, dim3(fb), dim3(256), 0, st, nullptr, ev_stop, 0u, a);
-    } else {
-        hipLaunchKernelGGL(k_fused, dim3((uint32_t)ntiles), dim3(kFusedT), 0, st, a);
-        if (fin) hipLaunchKernelGGL(k_ffinish, dim3(fb), dim3(256), 0, st, a);
-    }
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------- k_stream_xor

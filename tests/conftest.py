@@ -12,11 +12,6 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 # unmask tile index stands on (non-decreasing frame ends; include/hvws.h
 # hvws_set_table_checks) and fails loudly if a producer breaks it.
 os.environ.setdefault("HVWS_CHECK_TABLES", "1")
-# The FUSED scan path (include/hvws.h hvws_set_fused) is off unless a test
-# asks for it, so the path-specific tests keep the paths they assert; the
-# fused cases set it per context (SCAN_MODES "fused*", test_fused_*,
-# test_gpu_configs).
-os.environ.setdefault("HVWS_FUSED", "0")
 
 
 def pytest_configure(config):

@@ -191,33 +191,23 @@ def _oracle_batch(buf: np.ndarray, segs, carries):
 # path, without speculation (COUNT, read, EMIT) and with it (speculative
 # EMIT checked on the device, exact re-scan when the check fails): SPEC
 # (uniform estimates) and SLACK (per-segment regions, compacted).
-# SPEC runs as the kernel chain (default) and as the one-launch scan
-# ("_one_launch": k_pscan, hvws_set_one_launch_scan 1); the fourth field is
-# that mode.  The one-walk passes (SPEC, SLACK) run adaptively (default), with
-# the k_verify pair forced ("_verify", fifth field 1) and without it
+# The one-walk passes (SPEC, SLACK) run adaptively (default), with the
+# k_verify pair forced ("_verify", fourth field 1) and without it
 # ("_noverify", 0: head + walk, the walk records the carried-in frame).
-SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1), ("speculate_one_launch", 1, 1, 1),
-              ("speculate_verify", 1, 1, 0, 1), ("speculate_noverify", 1, 1, 0, 0),
-              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1), ("pipelined_speculate_one_launch", 1, 1, 1),
-              ("slack", 1, 2), ("slack_noverify", 1, 2, 0, 0), ("pipelined_slack", 1, 2),
-              ("pipelined_slack_verify", 1, 2, 0, 1),
-              # FUSED (hvws_set_fused 1: tried on every step): discovery inside the
-              # unmask pass; a batch whose frames are not uniform per segment is
-              # undone and re-run exactly (sixth field)
-              ("fused", 0, -1, 0, -1, 1), ("pipelined_fused", 0, -1, 0, -1, 1)]
+SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1),
+              ("speculate_verify", 1, 1, 1), ("speculate_noverify", 1, 1, 0),
+              ("pipelined", 0, -1), ("pipelined_speculate", 1, 1),
+              ("slack", 1, 2), ("slack_noverify", 1, 2, 0), ("pipelined_slack", 1, 2),
+              ("pipelined_slack_verify", 1, 2, 1)]
 
 
 def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, mode):
     L = libhv_amd.lib()
     bound, spec = mode[1], mode[2]
-    one_launch = mode[3] if len(mode) > 3 else 0
-    verify = mode[4] if len(mode) > 4 else -1
-    fused = mode[5] if len(mode) > 5 else 0
+    verify = mode[3] if len(mode) > 3 else -1
     old_b = L.hvws_set_fast_bound(eng.ctx, bound)
     old_s = L.hvws_set_speculation(eng.ctx, spec)
-    old_p = L.hvws_set_one_launch_scan(eng.ctx, one_launch)
     old_v = L.hvws_set_walk_verify(eng.ctx, verify)
-    old_f = L.hvws_set_fused(eng.ctx, fused)
     try:
         rx = eng.to_device(buf)
         if mode[0].startswith("pipelined"):
@@ -229,16 +219,10 @@ def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp
         cout, started = eng.carry(len(segs))
         rx.free()
         path = L.hvws_last_scan_path(eng.ctx)
-        launched = L.hvws_set_one_launch_scan(eng.ctx, -1)
     finally:
         L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
         L.hvws_set_speculation(eng.ctx, old_s)
-        L.hvws_set_one_launch_scan(eng.ctx, old_p)
         L.hvws_set_walk_verify(eng.ctx, old_v)
-        L.hvws_set_fused(eng.ctx, old_f)
-    # a SPEC scan used the one-launch kernel exactly when it was on
-    if path in (3, 4):
-        assert (launched > 0) == bool(one_launch), (mode, path, launched)
     assert len(frames) == len(exp_recs), mode
     for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
         assert np.array_equal(frames[f], exp_recs[f]), (mode, f)
@@ -515,8 +499,6 @@ def test_speculative_table_uniform(eng):
         buf, segs, carries = _cut_uniform(rng, nframes, size, nseg)
         paths = _compare_batch(eng, buf, segs, carries)
         assert paths["speculate"] == 3, paths   # HVWS_PATH_SPEC
-        assert paths["speculate_one_launch"] == 3, paths
-        assert paths["pipelined_speculate_one_launch"] == 3, paths
         assert paths["count_read"] == 1, paths
 
 
@@ -527,7 +509,6 @@ def test_speculative_table_rejected(eng):
     host = H.synth_cpu(plan)
     paths = _compare_batch(eng, host, plan.segments)
     assert paths["speculate"] == 4, paths       # HVWS_PATH_SPEC_FAILED
-    assert paths["speculate_one_launch"] == 4, paths
 
 
 def test_speculation_adapts(eng):
@@ -571,10 +552,9 @@ def test_pipelined_steps_back_to_back(eng):
         else:
             buf, segs, carries = _cut_uniform(rng, 400 + 50 * i, rng.choice([100, 1024, 3000]), 7 + i)
         batches.append((buf, segs, carries))
-    for bound, spec, fused in ((0, -1, 0), (1, 1, 0), (1, -1, 0), (0, -1, 1), (1, -1, 2)):
+    for bound, spec in ((0, -1), (1, 1), (1, -1)):
         old_b = L.hvws_set_fast_bound(eng.ctx, bound)
         old_s = L.hvws_set_speculation(eng.ctx, spec)
-        old_f = L.hvws_set_fused(eng.ctx, fused)
         try:
             devs = [eng.to_device(b) for b, _, _ in batches]
             for d, (b, segs, carries) in zip(devs, batches):
@@ -591,7 +571,6 @@ def test_pipelined_steps_back_to_back(eng):
         finally:
             L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
             L.hvws_set_speculation(eng.ctx, old_s)
-            L.hvws_set_fused(eng.ctx, old_f)
         assert np.array_equal(got[0], batches[0][0]), (bound, spec)
         for i in range(1, len(batches)):
             b, segs, carries = batches[i]
@@ -992,217 +971,3 @@ def test_slack_carried_partial_frames_ends_monotone(eng):
 
 
 
-# ------------------------------------------------------------- FUSED path
-def _fused_stats(eng):
-    out = (ctypes.c_uint64 * 2)()
-    assert libhv_amd.lib().hvws_fused_stats(eng.ctx, out) == 0
-    return list(out)
-
-
-def _check_step(eng, buf, segs, carries, piped, exp=None):
-    """One step of a host batch; frames, carries and bytes against the oracle.
-    Returns the scan path."""
-    if exp is None:
-        exp = _oracle_batch(buf, segs, carries)
-    exp_recs, exp_carry, exp_started, exp_bytes = exp
-    rx = eng.to_device(buf)
-    (eng.step_resident if piped else eng.step)(rx, len(buf), segs, carries)
-    frames = eng.frames()
-    cout, started = eng.carry(len(segs))
-    got = rx.download(len(buf))
-    rx.free()
-    assert np.array_equal(got, exp_bytes)
-    assert len(frames) == len(exp_recs)
-    for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
-        assert np.array_equal(frames[f], exp_recs[f]), f
-    for k in range(len(segs)):
-        assert cout[k].fields() == exp_carry[k].fields(), k
-        assert started[k] == exp_started[k], k
-    return libhv_amd.lib().hvws_last_scan_path(eng.ctx)
-
-
-@pytest.mark.parametrize("piped", [False, True], ids=["serial", "pipelined"])
-def test_fused_uniform_batches(eng, piped):
-    """Uniform streams cut anywhere (headers split across segments, carried-in
-    frames, tails): the first step's exact scan finds the estimates holding,
-    the next one takes the FUSED path (discovery inside the unmask pass) and
-    equals the oracle with no re-run."""
-    L = libhv_amd.lib()
-    old = L.hvws_set_fused(eng.ctx, 2)
-    try:
-        rng = random.Random(909)
-        for size, nframes, nseg in ((1024, 900, 13), (100, 3000, 64), (0, 500, 5), (125, 700, 70), (3000, 300, 4),
-                                    (7, 2000, 9), (30, 2000, 9), (15000, 40, 3)):
-            buf, segs, carries = _cut_uniform(rng, nframes, size, nseg)
-            exp = _oracle_batch(buf, segs, carries)
-            _check_step(eng, buf, segs, carries, False, exp)      # exact: learns that the estimates hold
-            before = _fused_stats(eng)
-            path = _check_step(eng, buf, segs, carries, piped, exp)
-            after = _fused_stats(eng)
-            if size + 6 < 64:
-                # frames this small are not tried (auto); forced, where a
-                # 16 KiB tile holds more of them than its LDS span list, the
-                # pass declines untouched and the batch runs exactly
-                assert path != 7 and after == before, (size, path)
-                L.hvws_set_fused(eng.ctx, 1)
-                path = _check_step(eng, buf, segs, carries, piped, exp)
-                L.hvws_set_fused(eng.ctx, 2)
-                after2 = _fused_stats(eng)
-                if min(nframes, 16384 // (size + 6)) > 256:   # a tile's frames overflow its LDS list
-                    assert path != 7 and after2[0] == after[0] + 1 and after2[1] == after[1] + 1, (size, path)
-                else:
-                    assert path == 7 and after2[0] == after[0] + 1 and after2[1] == after[1], (size, path)
-            else:
-                assert path == 7 and after[0] == before[0] + 1 and after[1] == before[1], (size, path, before, after)
-    finally:
-        L.hvws_set_fused(eng.ctx, old)
-
-
-@pytest.mark.parametrize("kind", ["longer", "shorter", "unmasked_same_size", "unmasked_other_size", "tail_longer",
-                                  "second_frame", "last_whole"])
-@pytest.mark.parametrize("piped", [False, True], ids=["serial", "pipelined"])
-def test_fused_forced_misprediction(eng, kind, piped):
-    """Segments whose frames are not all the size of their first whole frame,
-    on the FUSED path (forced, hvws_set_fused 1): the pass checks every
-    hypothesised header, publishes a failure, is undone byte for byte (the
-    same pass again) and the batch re-runs exactly -- bytes, frames and carries
-    equal the oracle's.  A frame of the same size but without a mask (a
-    different header length) still holds the hypothesis and is handled in the
-    pass."""
-    L = libhv_amd.lib()
-    rng = random.Random(hash(kind) & 0xFFFF)
-    size, nframes, nseg = 1024, 600, 6
-    frames = [(0x2 | 0x10 | 0x20, rng.randbytes(size), rng.randbytes(4)) for _ in range(nframes)]
-    at = {"longer": 250, "shorter": 250, "unmasked_same_size": 250, "unmasked_other_size": 250,
-          "tail_longer": nframes - 1, "second_frame": 101, "last_whole": 198}[kind]
-    if kind == "longer":
-        frames[at] = (frames[at][0], rng.randbytes(size + 3), frames[at][2])
-    elif kind == "shorter":
-        frames[at] = (frames[at][0], rng.randbytes(size - 40), frames[at][2])
-    elif kind == "unmasked_same_size":
-        frames[at] = (0x2 | 0x10, rng.randbytes(size + 4), None)   # 4-byte header + 1028 = 1032: same size
-    elif kind == "unmasked_other_size":
-        frames[at] = (0x1 | 0x10, rng.randbytes(size), None)
-    elif kind == "tail_longer":
-        frames[at] = (frames[at][0], rng.randbytes(size + 900), frames[at][2])
-    elif kind in ("second_frame", "last_whole"):
-        frames[at] = (frames[at][0], rng.randbytes(size + 1), frames[at][2])
-    data = H.build_frames_ref(frames)
-    # segments of 100 frames (the last one cut short, ending inside a frame)
-    offs = [0]
-    for f in frames:
-        offs.append(offs[-1] + len(H.build_frames_ref([f])))
-    segs = [(offs[100 * k], offs[100 * (k + 1)] - offs[100 * k]) for k in range(nseg - 1)]
-    segs.append((offs[100 * (nseg - 1)], len(data) - offs[100 * (nseg - 1)] - 5))
-    buf = np.frombuffer(data, np.uint8).copy()
-    old = L.hvws_set_fused(eng.ctx, 1)
-    try:
-        before = _fused_stats(eng)
-        _check_step(eng, buf, segs, None, piped)
-        after = _fused_stats(eng)
-    finally:
-        L.hvws_set_fused(eng.ctx, old)
-    assert after[0] == before[0] + 1
-    if kind == "unmasked_same_size":
-        assert after[1] == before[1], "a same-size unmasked frame holds the hypothesis"
-    else:
-        assert after[1] == before[1] + 1, "the misprediction was not caught"
-
-
-def test_fused_pipelined_failure_between_batches(eng):
-    """Pipelined FUSED steps A, B, C, D on four buffers, B mispredicted: B's
-    pass fails, C (queued behind it) sees the gate and does nothing, the next
-    call undoes B and re-runs B and C exactly, D takes the FUSED path again
-    (forced).  Every buffer ends exact; the last call's frames are D's."""
-    L = libhv_amd.lib()
-    rng = random.Random(4242)
-    batches = []
-    for i in range(4):
-        buf, segs, carries = _cut_uniform(rng, 500, 1024, 8)
-        if i == 1:   # one frame longer in the middle of B
-            frames = [(0x2 | 0x10 | 0x20, rng.randbytes(1024 if k != 250 else 1100), rng.randbytes(4))
-                      for k in range(500)]
-            data = H.build_frames_ref(frames)
-            buf = np.frombuffer(data, np.uint8).copy()
-            cuts = sorted(rng.sample(range(1, len(data)), 7))
-            bounds = [0] + cuts + [len(data)]
-            segs, carries = [], []
-            for a, b in zip(bounds[:-1], bounds[1:]):
-                segs.append((a, b - a))
-                carries.append(H.scan_segment(data[:a])[1])
-        batches.append((buf, segs, carries))
-    old = L.hvws_set_fused(eng.ctx, 1)
-    try:
-        before = _fused_stats(eng)
-        devs = [eng.to_device(b) for b, _, _ in batches]
-        for d, (b, segs, carries) in zip(devs, batches):
-            eng.step_resident(d, len(b), segs, carries)
-        frames = eng.frames()
-        got = [d.download(len(b)) for d, (b, _, _) in zip(devs, batches)]
-        for d in devs:
-            d.free()
-        after = _fused_stats(eng)
-    finally:
-        L.hvws_set_fused(eng.ctx, old)
-    assert after[0] == before[0] + 4 and after[1] == before[1] + 1, (before, after)
-    for i, (b, segs, carries) in enumerate(batches):
-        assert np.array_equal(got[i], _oracle_batch(b, segs, carries)[3]), i
-    exp_recs = _oracle_batch(*batches[3])[0]
-    assert len(frames) == len(exp_recs)
-    for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
-        assert np.array_equal(frames[f], exp_recs[f]), f
-
-
-def test_fused_grown_batch(eng):
-    """A batch with many more records than the last one: the frame table is
-    sized from the last count, so the pass declines untouched (and the batch
-    runs exactly) when the table cannot hold its estimate, and runs fused when
-    it can; either way the results are exact, and the next batch of that size
-    takes the FUSED path with no re-run."""
-    L = libhv_amd.lib()
-    rng = random.Random(515)
-    small = _cut_uniform(rng, 150, 1024, 6)
-    big = _cut_uniform(rng, 3000, 1024, 6)
-    old = L.hvws_set_fused(eng.ctx, 1)
-    try:
-        for piped in (False, True):
-            L.hvws_set_fused(eng.ctx, 0)
-            _check_step(eng, *small, False)
-            L.hvws_set_fused(eng.ctx, 1)
-            b0 = _fused_stats(eng)
-            _check_step(eng, *big, piped)
-            b1 = _fused_stats(eng)
-            assert b1[0] == b0[0] + 1 and b1[1] - b0[1] in (0, 1), (b0, b1)
-            path = _check_step(eng, *big, piped)
-            b2 = _fused_stats(eng)
-            assert path == 7 and b2[0] == b1[0] + 1 and b2[1] == b1[1], (b1, b2)
-    finally:
-        L.hvws_set_fused(eng.ctx, old)
-
-
-def test_fused_same_buffer_repeated(eng):
-    """The bench's shape: one resident uniform batch stepped 9 times,
-    pipelined, FUSED (auto): every pass unmasks or re-masks it in place
-    (XOR involution), so it ends unmasked; no batch re-run."""
-    L = libhv_amd.lib()
-    plan = synth.uniform_plan(20000, 1024, 17).split(64)
-    host = H.synth_cpu(plan)
-    exp = _oracle_batch(host, plan.segments, None)[3]
-    old = L.hvws_set_fused(eng.ctx, 2)
-    try:
-        rx = eng.to_device(host)
-        eng.step(rx, plan.total, plan.segments)      # exact: the estimates hold
-        eng.sync()                                   # (its published verdict is read without a wait)
-        before = _fused_stats(eng)
-        paths = []
-        for _ in range(8):
-            eng.step_resident(rx, plan.total, plan.segments)
-            paths.append(L.hvws_last_scan_path(eng.ctx))
-        eng.sync()
-        after = _fused_stats(eng)
-        got = rx.download(plan.total)
-        rx.free()
-    finally:
-        L.hvws_set_fused(eng.ctx, old)
-    assert after[0] == before[0] + 8 and after[1] == before[1], (before, after, paths)
-    assert np.array_equal(got, exp)
