@@ -692,6 +692,35 @@ def fixture_for(cfg: str, rank: int):
     return name, json.load(open(path)).get(name)
 
 
+def start_watchdog(period: float) -> None:
+    """A run still going after `period` seconds (and every `period` after)
+    leaves its state on stderr: every thread's Python stack, every thread's
+    native stack (hvws_debug_backtraces) and the library's contexts -- each
+    resident worker's mailbox and every stream's hipStreamQuery
+    (hvws_debug_dump, memory state first).  Diagnostics only ($HVWS_BENCH_WATCHDOG
+    seconds, 0: off)."""
+    import faulthandler
+
+    def run():
+        n = 0
+        while True:
+            time.sleep(period)
+            n += 1
+            print(f"[bench] watchdog: still running after {n * period:.0f} s", file=sys.stderr, flush=True)
+            faulthandler.dump_traceback(all_threads=True)
+            try:
+                import libhv_amd
+
+                L = libhv_amd.lib()
+                print(f"[bench] native stacks ({L.hvws_debug_backtraces(2)} threads answered above)",
+                      file=sys.stderr, flush=True)
+                L.hvws_debug_dump(2)
+            except Exception as e:   # noqa: BLE001 -- diagnostics must not end the run
+                print(f"[bench] watchdog: {e!r}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
+
+
 def dry_run(args, rank: int, world: int, local: int, dist) -> None:
     """--dry-run: the rank plumbing of a real run with the GPU legs stubbed --
     every rank builds its disjoint batch plan (CPU), the timing rows and the
@@ -727,9 +756,8 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     wd = float(os.environ.get("HVWS_BENCH_WATCHDOG", "150") or 0)
-    if wd > 0:   # a stuck run leaves every thread's Python stack on stderr (0: off)
-        import faulthandler
-        faulthandler.dump_traceback_later(wd, repeat=True)
+    if wd > 0:
+        start_watchdog(wd)
     rank, world, local, dist = init_dist()
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")

@@ -347,10 +347,21 @@ int hvws_set_door(hvws_ctx* ctx, int on);
 int hvws_door_stats(hvws_ctx* ctx, uint64_t out[4]);
 /* Idle time after which workers launched from now on park (microseconds;
  * 0 = the default, 5000).  Returns the previous value.  The runtime's frees
- * (hipFree, hipHostFree) wait for every stream, a resident worker's too: the
- * library parks the calling thread's own worker before each of its frees; a
- * worker of another thread holds such a free up to its idle time. */
+ * (hipFree, hipHostFree, hipHostUnregister) wait for every stream, a resident
+ * worker's too: before each of its frees the library parks every worker on
+ * that device, whichever thread owns it; a free outside this library waits
+ * for the workers to park themselves (at most their idle time). */
 uint64_t hvws_set_door_idle_us(uint64_t us);
+/* Diagnostics for a process that seems stuck (bench.py's watchdog): writes
+ * to fd the state of every context -- each resident worker's mailbox (seq,
+ * done, alive, exited epoch) and the host's view of it, then
+ * hipStreamQuery of every stream of the context (a query can itself block
+ * behind a stuck runtime call; the memory state is written first). */
+int hvws_debug_dump(int fd);
+/* Diagnostics: a native backtrace of every thread of the process to fd
+ * (SIGUSR2 to each thread in turn, backtrace_symbols_fd in the handler).
+ * Returns the number of threads that answered within 200 ms each. */
+int hvws_debug_backtraces(int fd);
 /* Diagnostics: 100 MHz device-clock stamps of the worker's last read request
  * -- seen, staged, walked, XORed, records written (before the release). */
 int hvws_door_stamps(hvws_ctx* ctx, uint64_t out[8]);

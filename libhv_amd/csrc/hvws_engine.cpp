@@ -7,6 +7,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dirent.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -42,10 +46,11 @@ int set_err(int code, const char* fmt, ...) {
                            __LINE__);                                                   \
     } while (0)
 
-// The runtime's frees (hipFree, hipHostFree) wait for every stream of the
-// device -- a resident k_door worker's too, until it parks.  Every free here
-// first parks the calling thread's own worker (defined with the worker).
-void door_park_self();
+// The runtime's frees (hipFree, hipHostFree, hipHostUnregister) wait for
+// every stream of the device -- a resident k_door worker's too, until it
+// parks.  Every free here first parks every worker on the current device,
+// whichever thread owns it (defined with the worker).
+void door_park_device();
 
 // Grow-only device allocation.
 struct dbuf {
@@ -54,7 +59,7 @@ struct dbuf {
     hipError_t ensure(uint64_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
         if (p) {
-            door_park_self();
+            door_park_device();
             hipFree(p);
         }
         p = nullptr;
@@ -66,7 +71,7 @@ struct dbuf {
     }
     void release() {
         if (p) {
-            door_park_self();
+            door_park_device();
             hipFree(p);
         }
         p = nullptr;
@@ -84,7 +89,7 @@ struct hbuf {   // grow-only pinned host allocation
     hipError_t ensure(uint64_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
         if (p) {
-            door_park_self();
+            door_park_device();
             hipHostFree(p);
         }
         p = nullptr;
@@ -97,7 +102,7 @@ struct hbuf {   // grow-only pinned host allocation
     }
     void release() {
         if (p) {
-            door_park_self();
+            door_park_device();
             hipHostFree(p);
         }
         p = nullptr;
@@ -262,6 +267,8 @@ struct hvws_ctx {
     dbuf d_door_slot;
     bool door_live = false;     // launched and not yet seen to have ended
     uint64_t door_seq = 0;      // last request number posted
+    uint64_t door_epoch = 0;    // launches so far; the worker writes its epoch to `exited` as it ends
+    std::mutex door_m;          // one caller at a time: the owning thread, a free on another thread, exit
     int door_mode = -1;         // hvws_set_door: -1 default ($HVWS_DOOR, off), 0 off, 1 on
     uint64_t door_launches = 0, door_calls = 0;
     // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
@@ -1311,27 +1318,16 @@ uint64_t door_idle_ticks() { return door_idle_us() * 100; }
 
 bool door_on(hvws_ctx* c) {
     if (c->door_mode >= 0) return c->door_mode != 0;
-    // Off unless asked for: two of four default bench runs after round 3's
-    // door_park change hung in the next leg's hvws_pipeline
     static const int env = getenv("HVWS_DOOR") ? atoi(getenv("HVWS_DOOR")) : 0;
     return env != 0;
 }
 
+// Contexts that own a worker stream.  Lock order: g_door_m, then a
+// context's door_m; nothing that holds a door_m takes g_door_m.
 std::mutex g_door_m;
-std::vector<hvws_ctx*> g_doors;   // contexts with a worker stream (parked at exit)
-void door_park(hvws_ctx* c);
-
-// At exit a worker still running is parked (no other HIP call here: an
-// exit handler that also destroyed the CU-masked streams hung a test
-// process's exit, profiles/r3ab_raw).
-void door_atexit() {
-    std::lock_guard<std::mutex> lk(g_door_m);
-    for (hvws_ctx* c : g_doors) {
-        if (!c->door_stream || !c->door_live) continue;
-        hipSetDevice(c->device);
-        door_park(c);
-    }
-}
+std::vector<hvws_ctx*> g_doors;
+std::atomic<int> g_door_count{0};   // g_doors.size(): frees skip the lock when no worker exists
+void door_atexit();
 
 int door_ensure(hvws_ctx* c) {
     if (c->door_stream) return HVWS_OK;
@@ -1342,7 +1338,6 @@ int door_ensure(hvws_ctx* c) {
     // other work.  The mask names every CU.
     std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0u);
     for (int i = 0; i < prop.multiProcessorCount; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-    HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
     // The mailbox is fine-grained (polled, uncached); the data and record
     // areas are ordinary pinned memory: the worker's system-scope acquire on
     // each request invalidates its caches before it stages the bytes, and its
@@ -1356,18 +1351,29 @@ int door_ensure(hvws_ctx* c) {
     memset(c->h_door.p, 0, sizeof(ddoor));
     if (!mapped<ddoor>(c->h_door) || !mapped<uint8_t>(c->h_door_data) || !mapped<drec>(c->h_door_rec))
         return set_err(HVWS_EHIP, "worker mailbox not device-mapped");
+    HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
     std::lock_guard<std::mutex> lk(g_door_m);
     // registered after the HIP runtime's own exit handlers, so it runs before them
     static const bool reg = (atexit(door_atexit), true);
     (void)reg;
     g_doors.push_back(c);
+    g_door_count.store((int)g_doors.size(), std::memory_order_release);
     return HVWS_OK;
 }
 
-// Post the request already written into the mailbox and wait for it.  The
-// worker is (re)launched when none is resident; one that parked just before
-// the request arrived is seen to have ended (stream idle, `done` behind) and
-// relaunched.  Kernel faults surface through the stream.
+uint64_t door_word(const hvws_ctx* c, const uint64_t& w) {
+    (void)c;
+    return __atomic_load_n(&w, __ATOMIC_ACQUIRE);
+}
+
+// Post the request already written into the mailbox and wait for it (the
+// caller holds c->door_m).  A worker is (re)launched when none is resident.
+// Whether the resident one has ended is read from the mailbox only: its last
+// store is `exited = epoch`.  Round 3 also took hipStreamQuery(door_stream)
+// == hipSuccess as "ended"; a worker that had cleared `alive` was then
+// treated as gone (its stream destroyed, its mailbox freed, or a second
+// worker queued behind it) while it could still be running.
+// The stream is asked only for errors (a kernel fault surfaces there).
 int door_call(hvws_ctx* c) {
     ddoor* b = c->h_door.as<ddoor>();
     const uint64_t seq = ++c->door_seq;
@@ -1381,45 +1387,55 @@ int door_call(hvws_ctx* c) {
         if (!c->door_live) {
             if (launches++ >= 4) return set_err(HVWS_EHIP, "k_door: the worker takes no requests");
             __atomic_store_n(&b->alive, 1ull, __ATOMIC_RELAXED);
+            ++c->door_epoch;
             HIP_OR(launch_door(mapped<ddoor>(c->h_door), mapped<uint8_t>(c->h_door_data), mapped<drec>(c->h_door_rec),
                                c->d_door_slot.as<drec>(), door_idle_ticks(), __atomic_load_n(&b->done, __ATOMIC_ACQUIRE),
-                               c->door_stream),
+                               c->door_epoch, c->door_stream),
                    HVWS_EHIP);
             c->door_live = true;
             ++c->door_launches;
             continue;
         }
-        const bool parked = __atomic_load_n(&b->alive, __ATOMIC_RELAXED) == 0;
-        if (parked || ((++spins & 63u) == 0 && std::chrono::steady_clock::now() >= next_query)) {
+        if (door_word(c, b->exited) == c->door_epoch) {
+            // The worker has ended; its last look at seq came before this
+            // request.  The stream drains (the wave retires) before the next
+            // launch, so two workers never share the mailbox.
+            if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+            HIP_OR(hipStreamSynchronize(c->door_stream), HVWS_EHIP);
+            c->door_live = false;
+            continue;
+        }
+        if ((++spins & 63u) == 0) {
             const auto now = std::chrono::steady_clock::now();
-            next_query = now + std::chrono::microseconds(100);
-            const hipError_t q = hipStreamQuery(c->door_stream);
-            if (q == hipSuccess) {   // the worker has ended
-                if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
-                c->door_live = false;
-                continue;
+            if (now >= next_query) {
+                next_query = now + std::chrono::microseconds(100);
+                const hipError_t q = hipStreamQuery(c->door_stream);
+                if (q != hipSuccess && q != hipErrorNotReady) return set_err(HVWS_EHIP, "k_door: %s", hipGetErrorString(q));
+                if (now - t0 > std::chrono::seconds(10)) return set_err(HVWS_EHIP, "k_door: no answer in 10 s");
             }
-            if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "k_door: %s", hipGetErrorString(q));
-            if (now - t0 > std::chrono::seconds(10)) return set_err(HVWS_EHIP, "k_door: no answer in 10 s");
         }
         __builtin_ia32_pause();
     }
 }
 
-// Send the resident worker home (context teardown, thread and process exit).
+// Send the resident worker home and wait until it has ended (the caller
+// holds c->door_m): context teardown, a free, a thread's exit, the door
+// switched off.
 void door_park(hvws_ctx* c) {
     if (!c->door_stream || !c->door_live) return;
-    // $HVWS_DOOR_PARK_FAST=1 (diagnostic only): take a worker that looks
-    // parked (alive == 0, stream idle) as parked without an exit request --
-    // the variant in use when the bench hung
-    static const bool fast = getenv("HVWS_DOOR_PARK_FAST") && atoi(getenv("HVWS_DOOR_PARK_FAST"));
-    if (fast && __atomic_load_n(&c->h_door.as<ddoor>()->alive, __ATOMIC_ACQUIRE) == 0 &&
-        hipStreamQuery(c->door_stream) == hipSuccess) {
-        c->door_live = false;
-        return;
+    ddoor* b = c->h_door.as<ddoor>();
+    if (door_word(c, b->exited) != c->door_epoch) {
+        b->op = DOOR_EXIT;
+        if (door_call(c) != HVWS_OK) {
+            (void)hipGetLastError();
+        } else {
+            // served: the worker's `exited` store follows `done`
+            const auto t0 = std::chrono::steady_clock::now();
+            while (door_word(c, b->exited) != c->door_epoch &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::seconds(1))
+                __builtin_ia32_pause();
+        }
     }
-    c->h_door.as<ddoor>()->op = DOOR_EXIT;
-    if (door_call(c) != HVWS_OK) (void)hipGetLastError();
     hipStreamSynchronize(c->door_stream);
     c->door_live = false;
 }
@@ -1428,21 +1444,62 @@ void door_park(hvws_ctx* c) {
 thread_local int t_device = -1;
 thread_local hvws_ctx* t_ctx = nullptr;
 
-void door_park_self() {
-    hvws_ctx* c = t_ctx;
-    if (c && c->door_live) {
-        hipSetDevice(c->device);
+// Park every worker on the current device before a free (whichever thread
+// owns it); the current device is restored afterwards.
+void door_park_device() {
+    if (g_door_count.load(std::memory_order_acquire) == 0) return;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_door_m);
+    for (hvws_ctx* c : g_doors) {
+        if (c->device != dev || !c->door_live) continue;
+        std::lock_guard<std::mutex> cl(c->door_m);
         door_park(c);
+    }
+    hipSetDevice(dev);
+}
+
+// At process exit: no HIP call at all (an exit handler that destroyed the
+// worker streams hung a process's exit, profiles/r3ab_raw).  A worker still
+// resident is asked to exit through the mailbox and given up to 100 ms to
+// say it has ended; a context whose owner holds its lock past 100 ms is left
+// as it is.
+void door_quit_nohip(hvws_ctx* c) {
+    if (!c->door_stream || !c->door_live) return;
+    ddoor* b = c->h_door.as<ddoor>();
+    if (door_word(c, b->exited) != c->door_epoch) {
+        b->op = DOOR_EXIT;
+        __atomic_store_n(&b->seq, ++c->door_seq, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (door_word(c, b->exited) != c->door_epoch &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(100))
+            __builtin_ia32_pause();
+    }
+    c->door_live = false;
+}
+
+void door_atexit() {
+    std::lock_guard<std::mutex> lk(g_door_m);
+    for (hvws_ctx* c : g_doors) {
+        std::unique_lock<std::mutex> cl(c->door_m, std::defer_lock);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!cl.try_lock() && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(100)) usleep(100);
+        if (cl.owns_lock()) door_quit_nohip(c);
     }
 }
 
 void door_release(hvws_ctx* c) {
     if (!c->door_stream) return;
-    door_park(c);
     {
         std::lock_guard<std::mutex> lk(g_door_m);
+        {
+            std::lock_guard<std::mutex> cl(c->door_m);
+            door_park(c);
+        }
         g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
+        g_door_count.store((int)g_doors.size(), std::memory_order_release);
     }
+    hipStreamSynchronize(c->door_stream);
     hipStreamDestroy(c->door_stream);
     c->door_stream = nullptr;
     c->h_door.release();
@@ -1456,6 +1513,7 @@ void door_release(hvws_ctx* c) {
 bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry, bool unmask,
                std::vector<hvws_frame>& frames, websocket_parser& carry_out, int& started) {
     if (!door_on(c) || len > kDoorMax || door_ensure(c) != HVWS_OK) return false;
+    std::lock_guard<std::mutex> cl(c->door_m);
     ddoor* b = c->h_door.as<ddoor>();
     uint8_t* data = c->h_door_data.as<uint8_t>();
     memcpy(data, buf, len);
@@ -1478,6 +1536,7 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
 
 bool door_xor(hvws_ctx* c, char* dst, const char* src, size_t n, uint32_t key, uint32_t phase) {
     if (!door_on(c) || n > kDoorMax || door_ensure(c) != HVWS_OK) return false;
+    std::lock_guard<std::mutex> cl(c->door_m);
     ddoor* b = c->h_door.as<ddoor>();
     uint8_t* data = c->h_door_data.as<uint8_t>();
     memcpy(data, src, n);
@@ -1557,10 +1616,102 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
 
 void stall_fn(void* usec) { usleep((useconds_t)(uintptr_t)usec); }
 
+
+// Every live context (hvws_debug_dump).
+std::mutex g_ctx_m;
+std::vector<hvws_ctx*> g_ctx_all;
+
+int g_bt_fd = 2;
+std::atomic<int> g_bt_done{0};
+
+void bt_handler(int) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    char hdr[64];
+    const int l = snprintf(hdr, sizeof(hdr), "--- thread %ld\n", (long)syscall(SYS_gettid));
+    if (l > 0) (void)!write(g_bt_fd, hdr, (size_t)l);
+    backtrace_symbols_fd(fr, n, g_bt_fd);
+    g_bt_done.fetch_add(1, std::memory_order_release);
+}
+
+const char* qname(hipError_t q) {
+    return q == hipSuccess ? "idle" : q == hipErrorNotReady ? "busy" : hipGetErrorString(q);
+}
+
 }  // namespace
 
 // ===================================================================== C ABI
 extern "C" {
+
+int hvws_debug_dump(int fd) {
+    std::vector<hvws_ctx*> all;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_m);
+        all = g_ctx_all;
+    }
+    dprintf(fd, "libhvws: %zu contexts, %d with a worker stream\n", all.size(), g_door_count.load());
+    // memory state first (no HIP call, no lock a stuck caller could hold)
+    for (hvws_ctx* c : all) {
+        dprintf(fd, "  ctx %p dev %d door_mode %d door_live %d door_seq %llu epoch %llu launches %llu calls %llu",
+                (void*)c, c->device, c->door_mode, (int)c->door_live, (unsigned long long)c->door_seq,
+                (unsigned long long)c->door_epoch, (unsigned long long)c->door_launches,
+                (unsigned long long)c->door_calls);
+        if (c->h_door.p) {
+            const ddoor* b = c->h_door.as<ddoor>();
+            dprintf(fd, " | mailbox seq %llu done %llu alive %llu exited %llu served %llu op %u",
+                    (unsigned long long)__atomic_load_n(&b->seq, __ATOMIC_ACQUIRE),
+                    (unsigned long long)__atomic_load_n(&b->done, __ATOMIC_ACQUIRE),
+                    (unsigned long long)__atomic_load_n(&b->alive, __ATOMIC_ACQUIRE),
+                    (unsigned long long)__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE),
+                    (unsigned long long)__atomic_load_n(&b->served, __ATOMIC_ACQUIRE), b->op);
+        }
+        dprintf(fd, " | last scan path %d, have_scan %d\n", c->scan_path, (int)c->have_scan);
+    }
+    for (hvws_ctx* c : all) {
+        dprintf(fd, "  ctx %p streams:", (void*)c);
+        const struct {
+            const char* n;
+            hipStream_t s;
+        } ss[] = {{"stream", c->stream}, {"sstream", c->sstream}, {"copy_in", c->copy_in},
+                  {"copy_out", c->copy_out}, {"door", c->door_stream}};
+        for (const auto& x : ss)
+            if (x.s) dprintf(fd, " %s=%s", x.n, qname(hipStreamQuery(x.s)));
+        dprintf(fd, "\n");
+    }
+    return (int)all.size();
+}
+
+int hvws_debug_backtraces(int fd) {
+    struct sigaction sa = {}, old = {};
+    sa.sa_handler = bt_handler;
+    sigemptyset(&sa.sa_mask);
+    sa.sa_flags = SA_RESTART;
+    void* warm[4];
+    (void)backtrace(warm, 4);   // loads the unwinder outside the handler
+    g_bt_fd = fd;
+    if (sigaction(SIGUSR2, &sa, &old) != 0) return -1;
+    const long self = (long)syscall(SYS_gettid);
+    int answered = 0;
+    if (DIR* d = opendir("/proc/self/task")) {
+        while (dirent* e = readdir(d)) {
+            const long tid = atol(e->d_name);
+            if (tid <= 0) continue;
+            if (tid == self) {
+                dprintf(fd, "--- thread %ld (the caller)\n", tid);
+                continue;
+            }
+            const int before = g_bt_done.load(std::memory_order_acquire);
+            if (syscall(SYS_tgkill, getpid(), tid, SIGUSR2) != 0) continue;
+            for (int i = 0; i < 200 && g_bt_done.load(std::memory_order_acquire) == before; ++i) usleep(1000);
+            if (g_bt_done.load(std::memory_order_acquire) != before) ++answered;
+            else dprintf(fd, "--- thread %ld: no answer\n", tid);
+        }
+        closedir(d);
+    }
+    sigaction(SIGUSR2, &old, nullptr);
+    return answered;
+}
+
 
 const char* hvws_last_error(void) { return g_err; }
 
@@ -1587,6 +1738,10 @@ hvws_ctx* hvws_ctx_create(int device) {
     }
     hvws_ctx* c = new hvws_ctx();
     c->device = device;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_m);
+        g_ctx_all.push_back(c);
+    }
     // Tables the device reads (upload slots) or writes (check verdict) in
     // host memory while the host uses them between launches: fine-grained,
     // so no stale copy can sit in a device cache across reuses.
@@ -1679,6 +1834,10 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     if (c->copy_out) hipStreamDestroy(c->copy_out);
     if (c->sstream) hipStreamDestroy(c->sstream);
     if (c->scan_done) hipEventDestroy(c->scan_done);
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_m);
+        g_ctx_all.erase(std::remove(g_ctx_all.begin(), g_ctx_all.end(), c), g_ctx_all.end());
+    }
     delete c;
 }
 
@@ -1698,8 +1857,8 @@ void* hvws_dev_alloc(hvws_ctx* c, uint64_t bytes) {
 
 void hvws_dev_free(hvws_ctx* c, void* p) {
     if (!c || !p) return;
-    door_park_self();
     hipSetDevice(c->device);
+    door_park_device();
     // The runtime holds the buffers of the last kernel dispatched on a stream
     // until the next dispatch there: without an empty launch on each of the
     // context's compute streams, a freed 68.7 GB batch stayed allocated.
@@ -1724,8 +1883,8 @@ void* hvws_host_alloc(hvws_ctx* c, uint64_t bytes) {
 
 void hvws_host_free(hvws_ctx* c, void* p) {
     if (!c || !p) return;
-    door_park_self();
     hipSetDevice(c->device);
+    door_park_device();
     pin_remove(p);
     hipHostFree(p);
 }
@@ -1749,7 +1908,7 @@ int hvws_host_unregister(hvws_ctx* c, void* p) {
     if (rc) return rc;
     const pinned_range r = pin_remove(p);
     if (!r.lo || !r.registered) return set_err(HVWS_EINVAL, "not a range from hvws_host_register");
-    door_park_self();
+    door_park_device();
     HIP_OR(hipHostUnregister(p), HVWS_EHIP);
     return HVWS_OK;
 }
@@ -2353,12 +2512,16 @@ uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {
 
 int hvws_set_door(hvws_ctx* c, int on) {
     if (!c) c = hvws::thread_ctx();
+    std::lock_guard<std::mutex> cl(c->door_m);
     const int old = door_on(c) ? 1 : 0;
-    if (on == 0 && c->door_live) {
+    c->door_mode = on < 0 ? -1 : (on ? 1 : 0);
+    if (!door_on(c) && c->door_live) {   // off (explicitly, or -1 resolving to off): park now
+        int dev = -1;
+        (void)hipGetDevice(&dev);
         hipSetDevice(c->device);
         door_park(c);
+        if (dev >= 0) hipSetDevice(dev);
     }
-    c->door_mode = on < 0 ? -1 : (on ? 1 : 0);
     return old;
 }
 
@@ -2500,9 +2663,15 @@ namespace hvws {
 
 // Parks the thread context's resident worker when the thread exits (the
 // context itself lives on until hvws_thread_release, as before).
+// The main thread's guard runs inside exit(): it only asks the worker to
+// exit through the mailbox (no HIP call, like door_atexit).
 struct thread_door_guard {
     ~thread_door_guard() {
-        if (t_ctx && t_ctx->door_live) {
+        if (!t_ctx || !t_ctx->door_live) return;
+        std::lock_guard<std::mutex> cl(t_ctx->door_m);
+        if ((pid_t)syscall(SYS_gettid) == getpid()) {
+            door_quit_nohip(t_ctx);
+        } else {
             hipSetDevice(t_ctx->device);
             door_park(t_ctx);
         }

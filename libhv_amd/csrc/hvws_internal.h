@@ -258,7 +258,10 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // then `seq` (release); the worker serves it and publishes `done = seq`
 // (system-scope release) after its results.  A worker idle for idle_ticks of
 // the 100 MHz realtime clock parks itself (alive = 0, after one last look at
-// seq) and the next request relaunches it.
+// seq) and the next request relaunches it.  Every launch carries an epoch;
+// a worker's last store before it returns is `exited = epoch`, and the host
+// takes that word -- not the stream's status -- as the sign that the worker
+// has ended ("Resident worker").
 enum : uint32_t { DOOR_FEED = 1u, DOOR_XOR = 2u, DOOR_EXIT = 3u };
 constexpr uint32_t kDoorThreads = 256;              // 4 waves: staging and XOR in parallel, walk on wave 0
 constexpr uint64_t kDoorMax = 32ull << 10;          // largest request (bytes)
@@ -281,7 +284,8 @@ struct ddoor {
     uint64_t count;     // DOOR_FEED: records written
     uint64_t served;    // requests served by this worker (diagnostic)
     dcarry   out;       // DOOR_FEED: carry out
-    uint64_t pad2[2];
+    uint64_t exited;    // epoch of the last worker that has ended (its last store before it returns)
+    uint64_t pad2[1];
     // realtime-clock stamps of the last request (100 MHz): seen, staged,
     // walked, xored, stored (before the release), and the sum of ticks spent
     // polling; read by hvws_door_stats' diagnostics
@@ -294,7 +298,7 @@ static_assert(offsetof(ddoor, carry) == 40 && offsetof(ddoor, len) == 16 && offs
 // data: kDoorMax + 64 bytes (pinned, 256-aligned); h_rec: kDoorRecords records
 // (pinned); d_slot: kDoorRecords records (device) for records past the LDS area.
 hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uint64_t idle_ticks, uint64_t first_seq,
-                       hipStream_t st);
+                       uint64_t epoch, hipStream_t st);
 
 // Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
 // copy_width() threads (the caller included; serial when another caller

@@ -986,11 +986,12 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // dispatch and no end-of-kernel signal, and the segment's work is spread
 // over four waves instead of one.  Parking: idle for idle_ticks of the
 // 100 MHz realtime clock, the worker clears `alive`, takes one last look at
-// `seq` (serving a request that arrived meanwhile) and exits; the host
-// relaunches it on the next request once the stream shows it has ended.
+// `seq` (serving a request that arrived meanwhile) and exits; its last store
+// is `exited = epoch`, and the host relaunches it on the next request once it
+// has seen that word.
 __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, uint8_t* __restrict__ data,
                                                        drec* __restrict__ h_rec, drec* __restrict__ d_slot,
-                                                       uint64_t idle_ticks, uint64_t first_seq) {
+                                                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch) {
     extern __shared__ u32x4 lds_door[];
     __shared__ drec lrec[SMALL_LREC];
     __shared__ uint64_t s_seq, s_len, s_n;
@@ -1031,7 +1032,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             if (!ex) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         __syncthreads();
-        if (s_exit) return;
+        if (s_exit) {   // parked (idle): `alive` is already 0; say this launch has ended
+            if (tid == 0) __hip_atomic_store(&box->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
         if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
             const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(box) + tid);
             reinterpret_cast<u32x4*>(s_req)[tid] = piece;
@@ -1059,6 +1063,8 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                 __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __threadfence_system();
                 __hip_atomic_store(&box->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+                __hip_atomic_store(&box->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             return;
         }
@@ -1189,9 +1195,9 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
 }
 
 hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uint64_t idle_ticks, uint64_t first_seq,
-                       hipStream_t st) {
+                       uint64_t epoch, hipStream_t st) {
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 16, st, box, data, h_rec, d_slot, idle_ticks,
-                       first_seq);
+                       first_seq, epoch);
     return hipGetLastError();
 }
 

@@ -228,3 +228,176 @@ def test_door_validation_rejects_like_per_launch_path(door):
         assert res[1] == res[0]
     finally:
         L.hvws_set_validation(None, old)
+
+
+def _in_thread(fn, timeout=120):
+    """fn() on a new thread (its own reference-API context); re-raises its
+    exception here."""
+    err = []
+
+    def run():
+        try:
+            fn()
+        except BaseException as e:   # noqa: BLE001
+            err.append(e)
+
+    t = threading.Thread(target=run)
+    t.start()
+    t.join(timeout=timeout)
+    assert not t.is_alive(), "thread did not finish"
+    if err:
+        raise err[0]
+
+
+def test_door_free_on_another_thread_parks_the_worker():
+    """A free on one thread while another thread's worker is resident: the
+    runtime's hipFree waits for every stream of the device, the worker's
+    too, so the library parks every worker of the device before its own
+    frees (round 3 parked only the calling thread's; with a 10 s idle time
+    this free would then have waited ~10 s).  The owner's next call
+    relaunches its worker; results stay the oracle's."""
+    L = libhv_amd.lib()
+    resident = threading.Event()
+    freed = threading.Event()
+    out = {}
+    rng = random.Random(41)
+    cases = _cases(rng, 6)
+
+    def owner():
+        old_idle = L.hvws_set_door_idle_us(10_000_000)
+        L.hvws_set_door(None, 1)
+        try:
+            data, chunks = cases[0]
+            assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks)
+            out["before"] = _stats()
+            resident.set()
+            assert freed.wait(60)
+            out["after_free"] = _stats()
+            for data, chunks in cases[1:]:
+                assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks)
+            out["end"] = _stats()
+        finally:
+            L.hvws_set_door(None, 0)
+            L.hvws_set_door_idle_us(old_idle)
+            L.hvws_thread_release()
+
+    errs = []
+
+    def run_owner():
+        try:
+            owner()
+        except BaseException as e:   # noqa: BLE001
+            errs.append(e)
+
+    t = threading.Thread(target=run_owner)
+    t.start()
+    try:
+        assert resident.wait(60), errs
+        assert out["before"][3] == 1, "the worker is not resident"
+        with libhv_amd.Engine(0) as eng:
+            t0 = time.perf_counter()
+            p = L.hvws_dev_alloc(eng.ctx, 1 << 20)
+            L.hvws_dev_free(eng.ctx, p)
+            h = L.hvws_host_alloc(eng.ctx, 1 << 20)
+            L.hvws_host_free(eng.ctx, h)
+            dt = time.perf_counter() - t0
+    finally:
+        freed.set()
+        t.join(120)
+    assert not errs, errs
+    assert dt < 2.0, f"frees beside another thread's resident worker took {dt:.2f} s"
+    assert out["after_free"][3] == 0, "the free did not park the other thread's worker"
+    assert out["end"][0] > out["before"][0], "the owner's next call did not relaunch its worker"
+
+
+def test_door_bench_sequence():
+    """bench.py's sequence when its drop-in leg ran (two of four such runs
+    hung in round 3, profiles/r3ae_raw): a thread context with the worker on
+    serves FeedRecvData and masked websocket_build_frame calls, switches it
+    off and on between passes, goes back to the default (-1) and releases
+    its context; then a feeder with registered pinned reads and a batched
+    feed; then hvws_pipeline calls (with their allocations and frees) on an
+    explicit context -- each call bounded, every result checked."""
+    from libhv_amd import synth
+
+    L = libhv_amd.lib()
+    rng = random.Random(71)
+    cases = _cases(rng, 8)
+
+    def dropin():
+        key = b"\x12\x34\x56\x78"
+        payload = bytes(range(125))
+        for rnd in range(3):
+            for on in (1, 0):
+                L.hvws_set_door(None, on)
+                for data, chunks in cases:
+                    assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks)
+                for _ in range(50):
+                    buf = ctypes.create_string_buffer(256)
+                    n = L.websocket_build_frame(buf, 0x2 | 0x10 | 0x20, key, payload, 125)
+                    assert buf.raw[:n] == H.build_frames_ref([(0x32, payload, key)])
+        L.hvws_set_door(None, -1)   # default ($HVWS_DOOR unset: off) parks the worker now
+        st = _stats()
+        assert st[3] == 0, "the worker is still resident after hvws_set_door(-1)"
+        L.hvws_thread_release()
+
+    t0 = time.perf_counter()
+    _in_thread(dropin)
+    t_dropin = time.perf_counter() - t0
+
+    # event loop: a feeder over registered pinned reads, then a batched feed
+    conns, per = 16, 8192
+    fp = synth.uniform_plan(conns * (per * 3 // 1032 + 2), 1024, 5).split(conns)
+    host = H.synth_cpu(fp)
+    streams = [host[o:o + 3 * per] for o, _ in fp.segments]
+    with libhv_amd.Engine(0) as eng:
+        arena = L.hvws_host_alloc(eng.ctx, conns * 3 * per)
+        try:
+            ring = np.ctypeslib.as_array((ctypes.c_uint8 * (conns * 3 * per)).from_address(arena))
+            for i, s in enumerate(streams):
+                ring[i * 3 * per:(i + 1) * 3 * per] = s
+            f = L.hvws_feeder_new()
+            hs = [L.hvws_wsp_new() for _ in range(conns)]
+            hv = (ctypes.c_void_p * conns)(*hs)
+            lens = (ctypes.c_size_t * conns)(*([per] * conns))
+            rets = (ctypes.c_int * conns)()
+            for it in range(3):
+                ds = (ctypes.c_void_p * conns)(*[arena + i * 3 * per + it * per for i in range(conns)])
+                if it < 2:
+                    assert L.hvws_wsp_feeder_submit(f, hv, ds, lens, conns, rets) == conns
+                else:
+                    assert L.hvws_feeder_flush(f) == 0
+                    assert L.hvws_wsp_feed_many(hv, ds, lens, conns, rets) == conns
+                    assert list(rets) == [per] * conns
+            L.hvws_feeder_free(f)
+            for h in hs:
+                L.hvws_wsp_free(h)
+        finally:
+            L.hvws_host_free(eng.ctx, arena)
+
+        # host-inclusive pipeline on the explicit context, toggling the bytes
+        plan = synth.mixed_plan(24 << 20, 33, hi=1 << 19)
+        hb = H.synth_cpu(plan)
+        _, _, _, exp = _oracle_batch_one(hb)
+        pinned = L.hvws_host_alloc(eng.ctx, plan.total)
+        try:
+            arr = np.ctypeslib.as_array((ctypes.c_uint8 * plan.total).from_address(pinned))
+            arr[:] = hb
+            for r in range(4):
+                carry = libhv_amd.WsParser()
+                L.websocket_parser_init(ctypes.byref(carry))
+                t = time.perf_counter()
+                assert L.hvws_pipeline(eng.ctx, pinned, plan.total, 4 << 20, ctypes.byref(carry)) == 0, \
+                    L.hvws_last_error()
+                assert time.perf_counter() - t < 10, f"pipeline call {r} took {time.perf_counter() - t:.1f} s"
+                assert np.array_equal(arr, exp if r % 2 == 0 else hb), r
+        finally:
+            L.hvws_host_free(eng.ctx, pinned)
+    assert t_dropin < 60
+
+
+def _oracle_batch_one(buf):
+    """The oracle's frames and unmasked bytes of one stream."""
+    import test_gpu_parity as P
+
+    return P._oracle_batch(buf, [(0, len(buf))], None)
