@@ -238,7 +238,7 @@ struct hvws_ctx {
     uint64_t zc_batch = kZcBatch;  // largest zero-copy batch ($HVWS_ZC_BATCH)
     uint32_t vmask = 0;         // protocol validation classes (V_*); 0 = reference behaviour
     // transmit side (hvws_build_frames)
-    dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat;
+    dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat, tx_span;
     hbuf h_tx;
     bool ev_build = false;
     int tx_path = 0;   // last hvws_build_frames: 0 k_build, 1 k_build_id (same-offset layout)
@@ -432,14 +432,23 @@ int step_times_at(hvws_ctx* c, int slot, float* out) {
 // write, so the host polls it instead of a stream event (an event marker
 // costs ~10 us of device idle between the check and the tile kernels).  A
 // stream that drains without publishing is an error, never a hang.
-int wait_status(hvws_ctx* c, uint64_t seq) {
+// Pipelined SPEC steps queue the unmask after the host has seen the scan
+// finish instead of behind a cross-stream event ($HVWS_HOST_ORDER=0: the
+// event, as in round 3).
+bool host_order() {
+    static const int v = getenv("HVWS_HOST_ORDER") ? atoi(getenv("HVWS_HOST_ORDER")) : 1;
+    return v != 0;
+}
+
+int wait_status(hvws_ctx* c, uint64_t seq, bool tiles = false) {
     const dspec_status* st = c->h_status.as<dspec_status>();
+    const uint64_t* w = tiles ? &st->tseq : &st->seq;
     for (uint64_t spin = 0;; ++spin) {
-        if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
         if ((spin & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(c->cs);
             if (q == hipSuccess) {
-                if (__atomic_load_n(&st->seq, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
+                if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
                 return set_err(HVWS_EHIP, "scan check did not publish (seq %llu)", (unsigned long long)seq);
             }
             if (q != hipErrorNotReady) return set_err(HVWS_EHIP, "stream error: %s", hipGetErrorString(q));
@@ -561,10 +570,12 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
 
 // Unmask kernel launch with its timing events (no argument checks).  The
 // events ride on the unmask's own dispatch (launch_unmask).
-hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
+// joined = false: the host has already seen the scan's last kernel publish
+// (host_order), so the unmask needs no cross-stream wait packet.
+hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined = false) {
     hipError_t e;
     const bool piped = c->cs != c->stream;
-    if (piped) {   // the scan ran on the side stream: join it
+    if (piped && !joined) {   // the scan ran on the side stream: join it
         if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
     }
@@ -842,7 +853,13 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             sc.no_verify = (c->verify_mode < 0 ? c->verify_hint : c->verify_mode != 0) ? 0u : 1u;
             HIP_OR(pass(SCAN_SPEC), HVWS_EHIP);
             if ((rc = tiles()) != HVWS_OK) return rc;
-            if (unmask_into) {
+            // Pipelined: the host waits for the scan's last kernel (it runs
+            // beside the previous unmask) and then queues this unmask with no
+            // cross-stream wait packet between the two unmasks.  Otherwise
+            // the unmask is queued behind the check at once.
+            const bool ordered = unmask_into && c->cs != c->stream && host_order();
+            if (ordered) HIP_OR(launch_publish_tiles(status_d, sc.seq, c->cs), HVWS_EHIP);
+            if (unmask_into && !ordered) {
                 HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
                 HIP_OR(issue_unmask(c, unmask_into, rx_len), HVWS_EHIP);
             }
@@ -852,6 +869,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
             done = (flags & SPEC_OK) != 0;
             c->spec_ok = done;
             c->scan_path = done ? HVWS_PATH_SPEC : HVWS_PATH_SPEC_FAILED;
+            if (done && ordered) {
+                if ((rc = wait_status(c, sc.seq, /*tiles=*/true)) != HVWS_OK) return rc;
+                HIP_OR(issue_unmask(c, unmask_into, rx_len, /*joined=*/true), HVWS_EHIP);
+            }
             if (done && unmask_into && unmasked) *unmasked = true;
             if (!done && (rc = join_rejected()) != HVWS_OK) return rc;
             tiles_done = done;
@@ -1807,7 +1828,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     for (hipEvent_t ev : c->pipe_ev)
         if (ev) hipEventDestroy(ev);
     for (dbuf* b : {&c->segs, &c->carry_in, &c->stage, &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad,
-                    &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->d_small_in, &c->d_small_slots})
+                    &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->tx_span, &c->d_small_in, &c->d_small_slots})
         b->release();
     c->h_tx.release();
     c->h_small_in.release();
@@ -2458,6 +2479,15 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     HIP_OR(launch_tile_index(off, c->tx_size.as<uint64_t>(), n, nullptr, c->tx_tiles.as<uint32_t>(), ntiles, tile,
                              c->stream),
            HVWS_EHIP);
+    // general layout: each tile's source span first ($HVWS_BUILD_SPANS=0: the records-first tiles)
+    const char* sp_env = getenv("HVWS_BUILD_SPANS");
+    const bool spans_ok = !sp_env || atoi(sp_env) != 0;
+    uint64_t* span = nullptr;
+    if (!same_off && spans_ok) {
+        HIP_OR(c->tx_span.ensure(ntiles * 16 + 16), HVWS_ENOMEM);
+        span = c->tx_span.as<uint64_t>();
+        HIP_OR(launch_tx_spans(d_pay_off, d_len, d_flags, off, n, ntiles, span, c->stream), HVWS_EHIP);
+    }
     HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
     if (same_off)
         HIP_OR(launch_build_id(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
@@ -2465,7 +2495,7 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
                HVWS_EHIP);
     else
         HIP_OR(launch_build(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
-                            c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), n, c->stream),
+                            c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), span, n, c->stream),
                HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
     c->ev_build = true;

@@ -108,7 +108,9 @@ struct dspec_status {
     uint64_t total;   // records of the batch (sum of the true counts)
     uint32_t flags;   // SPEC_*
     uint32_t pad;
-    uint64_t pad2[5];
+    uint64_t pad2[2];
+    uint64_t tseq;    // seq again, published after the scan's last kernel (tile index complete)
+    uint64_t pad3[2];
 };
 enum : uint32_t {
     SPEC_MATCH = 1u,   // every segment's record count equals k_head's estimate
@@ -229,6 +231,9 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);
 hipError_t launch_offsets(const uint64_t* counts, uint64_t* bases, uint32_t nseg, uint64_t* total,
                           hipStream_t st);
+// status->tseq = seq (system-scope release), after every earlier kernel of the stream:
+// the host sees that the scan's tables are complete without a stream event.
+hipError_t launch_publish_tiles(dspec_status* status, uint64_t seq, hipStream_t st);
 // *total > cap: *total = 0; publishes the count to status (SPEC_OK if within cap).
 hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st);
 hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uint64_t* nfr_dev,
@@ -360,8 +365,13 @@ hipError_t launch_build_id(uint8_t* out, uint64_t out_len, const uint8_t* pay, u
                            const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                            const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st);
 const char* build_kernel_name();   // k_build geometry in use ($HVWS_BUILD)
+// span: 2 words per k_build tile (ntiles of tx_tile() bytes), filled here.
+hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
+                           uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st);
+// span: from launch_tx_spans, or nullptr (boundary tiles load their records first)
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                        const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st);
+                        const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n,
+                        hipStream_t st);
 
 }  // namespace hvws

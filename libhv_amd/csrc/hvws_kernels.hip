@@ -1420,6 +1420,17 @@ __global__ void k_cap_check(uint64_t* __restrict__ total, uint64_t cap, dspec_st
     __hip_atomic_store(&status->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The scan's tables are complete: every earlier kernel of the stream has
+// ended (and released its writes) before this one starts.
+__global__ void k_publish_tiles(dspec_status* __restrict__ status, uint64_t seq) {
+    __hip_atomic_store(&status->tseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish_tiles(dspec_status* status, uint64_t seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_publish_tiles, dim3(1), dim3(1), 0, st, status, seq);
+    return hipGetLastError();
+}
+
 hipError_t launch_cap_check(uint64_t* total, uint64_t cap, dspec_status* status, uint64_t seq, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, st, total, cap, status, seq);
     return hipGetLastError();

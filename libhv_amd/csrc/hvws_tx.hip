@@ -256,6 +256,48 @@ __device__ __forceinline__ void build_chunk(uint8_t* __restrict__ out, uint64_t 
     }
 }
 
+// ---- per-tile source spans (the boundary tiles' payload bytes) ----------
+// span[2t], span[2t+1] = [lo, hi): the payload-buffer bytes tile t's frames
+// take their payload pieces from (lo = ~0 when it holds no payload byte).
+// Written frame by frame (atomics on the first and last tile a frame's
+// payload touches; a tile strictly inside one payload is inside no other
+// frame's and takes the streaming path or the records-first one),
+// so k_build's boundary tiles can issue their payload loads in the same
+// round trip as the frame records instead of one round trip after them.
+__global__ void k_tx_spans(const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len,
+                           const uint8_t* __restrict__ flags, const uint64_t* __restrict__ out_off, uint64_t n,
+                           uint64_t tile, unsigned long long* __restrict__ span) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t ln = len[k];
+    if (ln == 0) return;
+    const uint64_t ps = out_off[k] + tx_hdr_len(flags[k], ln), e = ps + ln, src = pay_off[k];
+    const uint64_t t0 = ps / tile, t1 = (e - 1) / tile;
+    for (uint64_t t = t0;; t = t1) {
+        const uint64_t pb = max(ps, t * tile), pe = min(e, (t + 1) * tile);
+        atomicMin(&span[2 * t], (unsigned long long)(src + (pb - ps)));
+        atomicMax(&span[2 * t + 1], (unsigned long long)(src + (pe - ps)));
+        if (t == t1) break;
+    }
+}
+
+__global__ void k_span_init(unsigned long long* __restrict__ span, uint64_t ntiles) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) {
+        span[2 * t] = ~0ull;
+        span[2 * t + 1] = 0ull;
+    }
+}
+
+// 16 bytes at byte offset q of an LDS area (q + 32 inside it)
+__device__ __forceinline__ void lds16(const uint8_t* a, uint32_t q, uint64_t& lo, uint64_t& hi) {
+    const u32x4 va = *reinterpret_cast<const u32x4*>(a + (q & ~15u));
+    const u32x4 vb = *reinterpret_cast<const u32x4*>(a + (q & ~15u) + 16);
+    const u32x4 v = (q & 15u) ? funnel16(va, vb, q & 15u) : va;
+    lo = v.x | ((uint64_t)v.y << 32);
+    hi = v.z | ((uint64_t)v.w << 32);
+}
+
 template <int U, bool SWZ, bool NT, bool SF>
 __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64_t out_len,
                                                const uint8_t* __restrict__ pay, uint64_t plen,
@@ -264,12 +306,18 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
                                                const uint32_t* __restrict__ mask,
                                                const uint64_t* __restrict__ out_off,
                                                const uint64_t* __restrict__ size,
-                                               const uint32_t* __restrict__ tile_first, uint64_t n, uint64_t tile0,
+                                               const uint32_t* __restrict__ tile_first,
+                                               const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
                                                uint64_t ntiles) {
     constexpr uint64_t TILE = 256ull * U * 16u;
     const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
+    uint64_t sp_lo = ~0ull, sp_hi = 0;
+    if (span) {   // loaded beside tile_first: no round trip of its own
+        sp_lo = span[2 * t];
+        sp_hi = span[2 * t + 1];
+    }
     const uint64_t k_lo = tile_first[t];
     // SF: both ends of the tile's frame range load together, and a tile that
     // more than one frame touches goes straight to staging (no dependent
@@ -319,12 +367,86 @@ __global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64
         }
     }
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
+    // staged source bytes per boundary tile (LDS): the tile's payload bytes,
+    // with room for gaps between payloads
+    constexpr uint64_t SPAN_MAX = TILE + 1024;
+    __shared__ uint64_t s_off[BUILD_MAXF], s_ps[BUILD_MAXF], s_end[BUILD_MAXF], s_src[BUILD_MAXF];
+    __shared__ uint32_t s_key[BUILD_MAXF], s_fl[BUILD_MAXF];
+    const uint64_t sa = sp_lo & ~15ull, sb = (sp_hi + 15) & ~15ull;   // staged source chunks [sa, sb)
+    const bool staged = span && nf && nf <= BUILD_MAXF && base + TILE <= out_len &&
+                        sp_lo < sp_hi && sb - sa <= SPAN_MAX && sb <= plen;
+    if (staged) {
+        // Boundary tile with its source span known up front: the span's
+        // payload chunks and the frame records load in one round trip into
+        // LDS, then every output chunk is assembled from LDS (header pieces
+        // from the records, payload pieces realigned from the staged bytes).
+        __shared__ u32x4 s_data[SPAN_MAX / 16 + 2];
+        constexpr int SPU = (int)((SPAN_MAX / 16 + 255) / 256);
+        const uint32_t nch = (uint32_t)((sb - sa) / 16);
+        u32x4 d[SPU];
+#pragma unroll
+        for (int i = 0; i < SPU; ++i) {
+            const uint32_t q = (uint32_t)i * 256u + tid;
+            if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
+        }
+        if (tid < nf) {
+            const uint64_t k = k_lo + tid;
+            const uint32_t fl = flags[k];
+            const uint64_t ln = len[k], o = out_off[k];
+            const uint64_t ps = o + tx_hdr_len(fl, ln);
+            s_off[tid] = o;
+            s_ps[tid] = ps;
+            s_end[tid] = ps + ln;
+            s_src[tid] = pay_off[k];
+            s_key[tid] = (fl & F_MASK) ? mask[k] : 0u;
+            s_fl[tid] = fl;
+        }
+#pragma unroll
+        for (int i = 0; i < SPU; ++i) {
+            const uint32_t q = (uint32_t)i * 256u + tid;
+            if (q < nch) s_data[q] = d[i];
+        }
+        if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
+        __syncthreads();
+        const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            const uint64_t ce = c + 16;
+            uint64_t lo = 0, hi = 0;
+            for (; j < nf && s_off[j] < ce; ++j) {
+                const uint64_t o = s_off[j], ps = s_ps[j], e = s_end[j];
+                const uint64_t hb = o > c ? o : c, he = ps < ce ? ps : ce;
+                if (hb < he) {   // header bytes
+                    uint64_t vlo, vhi;
+                    tx_hdr128(s_fl[j], e - ps, s_key[j], vlo, vhi);
+                    shr_bytes(vlo, vhi, (uint32_t)(hb - o));
+                    put_bytes(lo, hi, vlo, vhi, (uint32_t)(hb - c), (uint32_t)(he - c));
+                }
+                const uint64_t pb = ps > c ? ps : c, pe = e < ce ? e : ce;
+                if (pb < pe) {   // payload bytes, realigned out of the staged span
+                    uint64_t vlo, vhi;
+                    lds16(lb, (uint32_t)(s_src[j] + (pb - ps) - sa), vlo, vhi);
+                    const uint32_t kw = tx_rotr(s_key[j], (uint32_t)((pb - ps) & 3u) * 8u);
+                    const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                    put_bytes(lo, hi, vlo ^ kk, vhi ^ kk, (uint32_t)(pb - c), (uint32_t)(pe - c));
+                }
+            }
+            __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                        reinterpret_cast<u32x4*>(out + c));
+        }
+        return;
+    }
     if (nf && nf <= BUILD_MAXF && base + TILE <= out_len) {
         // Boundary tile: the tile's frames staged in LDS; chunks inside one
         // payload still stream (loads issued for all U chunks first), chunks
         // holding header bytes or a frame boundary are assembled byte by byte.
-        __shared__ uint64_t s_off[BUILD_MAXF], s_ps[BUILD_MAXF], s_end[BUILD_MAXF], s_src[BUILD_MAXF];
-        __shared__ uint32_t s_key[BUILD_MAXF], s_fl[BUILD_MAXF];
         if (tid < nf) {
             const uint64_t k = k_lo + tid;
             const uint32_t fl = flags[k];
@@ -638,9 +760,21 @@ const char* build_kernel_name() {
 
 uint64_t tx_tile() { return build_tile(build_variant()); }
 
+hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
+                           uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st) {
+    hipLaunchKernelGGL(k_span_init, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<unsigned long long*>(span), ntiles);
+    if (n == 0) return hipGetLastError();
+    hipLaunchKernelGGL(k_tx_spans, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, pay_off, len, flags, out_off, n,
+                       tx_tile(), reinterpret_cast<unsigned long long*>(span));
+    return hipGetLastError();
+}
+
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                        const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st) {
+                        const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n,
+                        hipStream_t st) {
+    const unsigned long long* sp = reinterpret_cast<const unsigned long long*>(span);
     const int v = build_variant();
     const uint64_t tile = build_tile(v);
     const uint64_t ntiles = (out_len + tile - 1) / tile;
@@ -652,7 +786,7 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
 #define X(I, U, S, N, F)                                                                                       \
     case I:                                                                                                    \
         hipLaunchKernelGGL((k_build<U, S, N, F>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off, \
-                           len, flags, mask, out_off, size, tile_first, n, t0, nt);                            \
+                           len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);                        \
         break;
             HVWS_BUILD_GEOMS(X)
 #undef X

@@ -231,3 +231,42 @@ def test_build_one_moved_payload_takes_general_kernel(eng):
     got, kern = _gpu_build_same_offset(eng, frames, rng, move=137)
     assert got == H.build_frames_ref(frames)
     assert not kern.startswith("k_build_id"), kern
+
+
+@pytest.mark.parametrize("spans", ["1", "0"])
+@pytest.mark.parametrize("order", ["packed", "gaps", "shuffled"])
+def test_build_boundary_tiles_span_staged(eng, spans, order, monkeypatch):
+    """Boundary tiles of the general layout stage their source span in LDS
+    together with the frame records (k_tx_spans; $HVWS_BUILD_SPANS=0: the
+    records-first tiles).  Small frames packed back to back, with gaps, and
+    with payloads in shuffled order (spans past the LDS area fall back to the
+    records-first path); every byte against the reference."""
+    monkeypatch.setenv("HVWS_BUILD_SPANS", spans)
+    rng = np.random.default_rng(31)
+    lens = np.concatenate([rng.integers(900, 1100, 1500), rng.integers(0, 130, 300)])
+    rng.shuffle(lens)
+    frames = _frames(rng, len(lens), lens=lens, p_mask=0.9)
+    if order == "shuffled":
+        perm = rng.permutation(len(frames))
+        pay = bytearray()
+        offs = [0] * len(frames)
+        for i in perm:
+            offs[i] = len(pay)
+            pay += frames[i][1]
+        flags = [f for f, _, _ in frames]
+        mask = [int.from_bytes(k, "little") if k else 0 for _, _, k in frames]
+        lns = [len(p) for _, p, _ in frames]
+        total = int(synth.frame_size(np.array(flags, dtype=np.uint8), np.array(lns, dtype=np.uint64)).sum())
+        payload = eng.to_device(np.frombuffer(bytes(pay), dtype=np.uint8))
+        tx = libhv_amd.TxPlan(eng, offs, lns, flags, mask)
+        out = eng.alloc(total + 64)
+        try:
+            assert eng.build_frames(out, total + 64, payload, len(pay), tx) == total
+            got = bytes(out.download(total))
+        finally:
+            payload.free()
+            out.free()
+            tx.free()
+    else:
+        got, _ = _gpu_build(eng, frames, gap_rng=rng if order == "gaps" else None)
+    assert got == H.build_frames_ref(frames)
