@@ -12,6 +12,8 @@ $S query_probe_$TAG 120 build/query_probe 300
 [ -f gpurun_out/.stop ] && exit 1
 $S pytest_door_$TAG 300 python -u -m pytest tests/test_gpu_door.py -x -v --timeout 120 --timeout-method thread
 [ -f gpurun_out/.stop ] && exit 1
+ASAN_OPTIONS=detect_leaks=0 $S asan_door_$TAG 180 build/asan/asan_driver door
+[ -f gpurun_out/.stop ] && exit 1
 $S pytest_gpu_$TAG 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 [ -f gpurun_out/.stop ] && exit 1
 HVWS_BENCH_DEVICE=0 $S rehearsal2_$TAG 500 python3 bench.py --gpus 2

@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <random>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -257,9 +258,43 @@ void test_tx_and_keys(std::mt19937_64& rng) {
     hvws_ctx_destroy(c);
 }
 
+// The resident worker (hvws_set_door) under ASan: this thread's context and
+// three loop threads with workers of their own feed through it; the threads
+// exit with their workers resident (the thread guard parks them), a free on
+// this thread parks the others' workers, and the process exits with this
+// thread's worker still resident and its context never released -- the path
+// of round 3's "corrupted double-linked list" at exit.
+void test_door(std::mt19937_64& rng) {
+    hvws_set_door(nullptr, 1);
+    test_feed(rng);
+    std::vector<std::thread> th;
+    for (int i = 0; i < 3; ++i) {
+        const uint64_t seed = rng();
+        th.emplace_back([seed] {
+            std::mt19937_64 r(seed);
+            hvws_set_door(nullptr, 1);
+            test_feed(r);
+        });
+    }
+    for (auto& t : th) t.join();
+    hvws_ctx* c = hvws_ctx_create(0);
+    void* p = hvws_dev_alloc(c, 1 << 20);
+    hvws_dev_free(c, p);
+    hvws_ctx_destroy(c);
+    test_feed(rng);   // relaunches this thread's worker, left resident at exit
+    uint64_t st[4];
+    CHECK(hvws_door_stats(nullptr, st) == 0 && st[0] >= 1 && st[3] == 1);
+}
+
 }  // namespace
 
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1 && strcmp(argv[1], "door") == 0) {   // the worker's paths and a process exit with one resident
+        std::mt19937_64 rng(20261017);
+        test_door(rng);
+        printf("asan_driver door: %s (%d failed checks)\n", g_fail ? "FAIL" : "ok", g_fail);
+        return g_fail ? 1 : 0;
+    }
     std::mt19937_64 rng(20261015);
     for (uint64_t limit : {0ull, ~0ull}) {   // small-batch path, then the general path
         hvws_set_small_batch_limit(nullptr, limit);
