@@ -10,6 +10,8 @@ export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONFAULTHANDLER=1
 rm -f gpurun_out/.stop
 $S query_probe_$TAG 120 build/query_probe 300
 [ -f gpurun_out/.stop ] && exit 1
+$S vram_probe_$TAG 120 build/vram_probe
+[ -f gpurun_out/.stop ] && exit 1
 $S pytest_door_$TAG 300 python -u -m pytest tests/test_gpu_door.py -x -v --timeout 120 --timeout-method thread
 [ -f gpurun_out/.stop ] && exit 1
 ASAN_OPTIONS=detect_leaks=0 $S asan_door_$TAG 180 build/asan/asan_driver door
