@@ -3,7 +3,8 @@
 # cross-stream event (HVWS_HOST_ORDER=0, round 3) vs after the host saw the
 # scan finish (default), interleaved; c2 step traffic (two --pmc passes) and a
 # kernel trace; transmit at the c2 shape, boundary tiles records-first
-# (HVWS_BUILD_SPANS=0) vs span-staged (default), interleaved
+# (HVWS_BUILD_SPANS=0) vs span-staged (default), interleaved; c4 as one
+# stream without (HVWS_SIEVE_STOP=0) and with the window early stop
 set -u
 S=scripts/gpu_step.sh
 TAG=${1:-r4b}
@@ -19,6 +20,13 @@ done
 for i in 1 2; do
   for sp in 0 1; do
     CONFIG=c2 HVWS_BUILD_SPANS=$sp $S tx_c2_sp${sp}_${i}_$TAG 120 python3 scripts/bench_tx.py
+    [ -f gpurun_out/.stop ] && exit 1
+  done
+done
+C4="--config c4 --segments 1 --steps 100 --warmup 10 --no-tx --host-gib 0 --cpu-seconds 0 --feed-conns 0"
+for i in 1 2; do
+  for ss in 0 1; do
+    HVWS_SIEVE_STOP=$ss $S c4s1_stop${ss}_${i}_$TAG 150 python3 bench.py $C4
     [ -f gpurun_out/.stop ] && exit 1
   done
 done
