@@ -265,6 +265,11 @@ struct hvws_ctx {
     hipStream_t door_stream = nullptr;
     hbuf h_door, h_door_data, h_door_rec;
     dbuf d_door_slot;
+    // Request block + request bytes in fine-grained device memory, written by
+    // the host through the PCIe BAR (round 4): the worker polls and stages
+    // from its own HBM instead of pulling them across the link.  nullptr: the
+    // request and its bytes go through the pinned box and data area (round 3).
+    void* d_door_req = nullptr;
     bool door_live = false;     // launched and not yet seen to have ended
     uint64_t door_seq = 0;      // last request number posted
     uint64_t door_epoch = 0;    // launches so far; the worker writes its epoch to `exited` as it ends
@@ -1358,6 +1363,27 @@ std::vector<hvws_ctx*> g_doors;
 std::atomic<int> g_door_count{0};   // g_doors.size(): frees skip the lock when no worker exists
 void door_atexit();
 
+// The request area in device memory: its 128-byte request block, then the
+// request bytes.
+constexpr uint64_t kDoorReqBytes = 256 + kDoorMax + 256;
+
+bool door_vram_enabled() {
+    static const int v = getenv("HVWS_DOOR_VRAM") ? atoi(getenv("HVWS_DOOR_VRAM")) : 1;
+    return v != 0;
+}
+
+// Host stores to device memory go through write-combining buffers: an sfence
+// makes them visible (the request bytes before seq, and seq itself; without
+// it a lone 8-byte seq store sat in a WC buffer for ~10 ms,
+// profiles/r4a_raw/vram_probe.jsonl).
+inline void door_flush_wc() { __builtin_ia32_sfence(); }
+
+// Where the host writes a request (block and bytes) and where the worker reads it.
+ddoor* door_req(hvws_ctx* c) { return c->d_door_req ? (ddoor*)c->d_door_req : c->h_door.as<ddoor>(); }
+uint8_t* door_din(hvws_ctx* c) {
+    return c->d_door_req ? (uint8_t*)c->d_door_req + 256 : c->h_door_data.as<uint8_t>();
+}
+
 int door_ensure(hvws_ctx* c) {
     if (c->door_stream) return HVWS_OK;
     hipDeviceProp_t prop;
@@ -1380,6 +1406,24 @@ int door_ensure(hvws_ctx* c) {
     memset(c->h_door.p, 0, sizeof(ddoor));
     if (!mapped<ddoor>(c->h_door) || !mapped<uint8_t>(c->h_door_data) || !mapped<drec>(c->h_door_rec))
         return set_err(HVWS_EHIP, "worker mailbox not device-mapped");
+    if (door_vram_enabled()) {
+        // Fine-grained device memory is host-accessible through the BAR on
+        // this platform (profiles/r4a_raw/vram_probe.jsonl); the pointer the
+        // runtime reports for the host is used, and the request area stays
+        // pinned when there is none.
+        void* p = nullptr;
+        if (hipExtMallocWithFlags(&p, kDoorReqBytes, hipDeviceMallocFinegrained) == hipSuccess) {
+            hipPointerAttribute_t a;
+            if (hipPointerGetAttributes(&a, p) == hipSuccess && a.hostPointer == p) {
+                c->d_door_req = p;
+                memset(p, 0, sizeof(ddoor));
+                door_flush_wc();
+            } else {
+                (void)hipFree(p);
+            }
+        }
+        (void)hipGetLastError();
+    }
     HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
     std::lock_guard<std::mutex> lk(g_door_m);
     // registered after the HIP runtime's own exit handlers, so it runs before them
@@ -1405,8 +1449,11 @@ uint64_t door_word(const hvws_ctx* c, const uint64_t& w) {
 // The stream is asked only for errors (a kernel fault surfaces there).
 int door_call(hvws_ctx* c) {
     ddoor* b = c->h_door.as<ddoor>();
+    ddoor* rq = door_req(c);
     const uint64_t seq = ++c->door_seq;
-    __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+    if (c->d_door_req) door_flush_wc();   // the request's bytes and fields first
+    __atomic_store_n(&rq->seq, seq, __ATOMIC_RELEASE);
+    if (c->d_door_req) door_flush_wc();
     ++c->door_calls;
     const auto t0 = std::chrono::steady_clock::now();
     auto next_query = t0 + std::chrono::microseconds(100);
@@ -1417,9 +1464,11 @@ int door_call(hvws_ctx* c) {
             if (launches++ >= 4) return set_err(HVWS_EHIP, "k_door: the worker takes no requests");
             __atomic_store_n(&b->alive, 1ull, __ATOMIC_RELAXED);
             ++c->door_epoch;
-            HIP_OR(launch_door(mapped<ddoor>(c->h_door), mapped<uint8_t>(c->h_door_data), mapped<drec>(c->h_door_rec),
-                               c->d_door_slot.as<drec>(), door_idle_ticks(), __atomic_load_n(&b->done, __ATOMIC_ACQUIRE),
-                               c->door_epoch, c->door_stream),
+            const ddoor* dreq = c->d_door_req ? (const ddoor*)c->d_door_req : mapped<ddoor>(c->h_door);
+            const uint8_t* ddin = c->d_door_req ? (const uint8_t*)c->d_door_req + 256 : mapped<uint8_t>(c->h_door_data);
+            HIP_OR(launch_door(dreq, mapped<ddoor>(c->h_door), ddin, mapped<uint8_t>(c->h_door_data),
+                               mapped<drec>(c->h_door_rec), c->d_door_slot.as<drec>(), door_idle_ticks(),
+                               __atomic_load_n(&b->done, __ATOMIC_ACQUIRE), c->door_epoch, c->door_stream),
                    HVWS_EHIP);
             c->door_live = true;
             ++c->door_launches;
@@ -1454,7 +1503,7 @@ void door_park(hvws_ctx* c) {
     if (!c->door_stream || !c->door_live) return;
     ddoor* b = c->h_door.as<ddoor>();
     if (door_word(c, b->exited) != c->door_epoch) {
-        b->op = DOOR_EXIT;
+        door_req(c)->op = DOOR_EXIT;
         if (door_call(c) != HVWS_OK) {
             (void)hipGetLastError();
         } else {
@@ -1497,8 +1546,11 @@ void door_quit_nohip(hvws_ctx* c) {
     if (!c->door_stream || !c->door_live) return;
     ddoor* b = c->h_door.as<ddoor>();
     if (door_word(c, b->exited) != c->door_epoch) {
-        b->op = DOOR_EXIT;
-        __atomic_store_n(&b->seq, ++c->door_seq, __ATOMIC_RELEASE);
+        ddoor* rq = door_req(c);
+        rq->op = DOOR_EXIT;
+        if (c->d_door_req) door_flush_wc();
+        __atomic_store_n(&rq->seq, ++c->door_seq, __ATOMIC_RELEASE);
+        if (c->d_door_req) door_flush_wc();
         const auto t0 = std::chrono::steady_clock::now();
         while (door_word(c, b->exited) != c->door_epoch &&
                std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(100))
@@ -1535,6 +1587,11 @@ void door_release(hvws_ctx* c) {
     c->h_door_data.release();
     c->h_door_rec.release();
     c->d_door_slot.release();
+    if (c->d_door_req) {
+        door_park_device();
+        hipFree(c->d_door_req);
+        c->d_door_req = nullptr;
+    }
 }
 
 // One read through the worker (gpu_feed's fast path): false when the worker
@@ -1544,13 +1601,16 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
     if (!door_on(c) || len > kDoorMax || door_ensure(c) != HVWS_OK) return false;
     std::lock_guard<std::mutex> cl(c->door_m);
     ddoor* b = c->h_door.as<ddoor>();
+    ddoor* rq = door_req(c);
     uint8_t* data = c->h_door_data.as<uint8_t>();
-    memcpy(data, buf, len);
-    b->op = DOOR_FEED;
-    b->unmask = unmask ? 1u : 0u;
-    b->len = len;
-    b->vmask = c->vmask;
-    to_dcarry(carry, b->carry);
+    memcpy(door_din(c), buf, len);
+    rq->op = DOOR_FEED;
+    rq->unmask = unmask ? 1u : 0u;
+    rq->len = len;
+    rq->vmask = c->vmask;
+    dcarry cin;
+    to_dcarry(carry, cin);
+    memcpy(&rq->carry, &cin, sizeof(dcarry));
     if (door_call(c) != HVWS_OK) hvws::fatal("k_door");
     const uint64_t n = b->count;
     frames.resize((size_t)n);
@@ -1566,13 +1626,13 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
 bool door_xor(hvws_ctx* c, char* dst, const char* src, size_t n, uint32_t key, uint32_t phase) {
     if (!door_on(c) || n > kDoorMax || door_ensure(c) != HVWS_OK) return false;
     std::lock_guard<std::mutex> cl(c->door_m);
-    ddoor* b = c->h_door.as<ddoor>();
+    ddoor* rq = door_req(c);
     uint8_t* data = c->h_door_data.as<uint8_t>();
-    memcpy(data, src, n);
-    b->op = DOOR_XOR;
-    b->len = n;
-    b->key = key;
-    b->phase = phase;
+    memcpy(door_din(c), src, n);
+    rq->op = DOOR_XOR;
+    rq->len = n;
+    rq->key = key;
+    rq->phase = phase;
     if (door_call(c) != HVWS_OK) hvws::fatal("k_door");
     memcpy(dst, data, n);
     return true;
@@ -1687,12 +1747,13 @@ int hvws_debug_dump(int fd) {
                 (unsigned long long)c->door_calls);
         if (c->h_door.p) {
             const ddoor* b = c->h_door.as<ddoor>();
-            dprintf(fd, " | mailbox seq %llu done %llu alive %llu exited %llu served %llu op %u",
-                    (unsigned long long)__atomic_load_n(&b->seq, __ATOMIC_ACQUIRE),
+            dprintf(fd, " | mailbox%s seq %llu done %llu alive %llu exited %llu served %llu op %u",
+                    c->d_door_req ? " (request in device memory)" : "",
+                    (unsigned long long)__atomic_load_n(&door_req(c)->seq, __ATOMIC_ACQUIRE),
                     (unsigned long long)__atomic_load_n(&b->done, __ATOMIC_ACQUIRE),
                     (unsigned long long)__atomic_load_n(&b->alive, __ATOMIC_ACQUIRE),
                     (unsigned long long)__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE),
-                    (unsigned long long)__atomic_load_n(&b->served, __ATOMIC_ACQUIRE), b->op);
+                    (unsigned long long)__atomic_load_n(&b->served, __ATOMIC_ACQUIRE), door_req(c)->op);
         }
         dprintf(fd, " | last scan path %d, have_scan %d\n", c->scan_path, (int)c->have_scan);
     }

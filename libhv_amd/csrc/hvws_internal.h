@@ -308,10 +308,14 @@ static_assert(sizeof(dcarry) == 48, "dcarry layout");
 static_assert(offsetof(ddoor, done) == 128, "ddoor: device fields on their own lines");
 static_assert(offsetof(ddoor, carry) == 40 && offsetof(ddoor, len) == 16 && offsetof(ddoor, vmask) == 24,
               "k_door reads the request as words 1-10");
-// data: kDoorMax + 64 bytes (pinned, 256-aligned); h_rec: kDoorRecords records
+// data areas: kDoorMax + 256 bytes (256-aligned); h_rec: kDoorRecords records
 // (pinned); d_slot: kDoorRecords records (device) for records past the LDS area.
-hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uint64_t idle_ticks, uint64_t first_seq,
-                       uint64_t epoch, hipStream_t st);
+// req: the request block (words 0-15 of a ddoor) -- fine-grained device
+// memory the host writes through the PCIe BAR, or the pinned box itself;
+// din: the request's bytes (same choice); dout: results (pinned host; may equal
+// din when both are the pinned area).
+hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
+                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st);
 
 // Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
 // copy_width() threads (the caller included; serial when another caller

@@ -989,7 +989,8 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // `seq` (serving a request that arrived meanwhile) and exits; its last store
 // is `exited = epoch`, and the host relaunches it on the next request once it
 // has seen that word.
-__global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, uint8_t* __restrict__ data,
+__global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__ req, ddoor* __restrict__ box,
+                                                       const uint8_t* __restrict__ din, uint8_t* __restrict__ dout,
                                                        drec* __restrict__ h_rec, drec* __restrict__ d_slot,
                                                        uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch) {
     extern __shared__ u32x4 lds_door[];
@@ -1009,12 +1010,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             uint64_t s;
             uint32_t ex = 0;
             for (;;) {
-                s = __hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (s != last) break;
                 if (wall_clock64() - t0 > idle_ticks) {
                     __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     __threadfence_system();
-                    s = __hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    s = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if (s != last) {   // arrived while parking: serve it
                         __hip_atomic_store(&box->alive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         break;
@@ -1037,7 +1038,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             return;
         }
         if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
-            const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(box) + tid);
+            const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(req) + tid);
             reinterpret_cast<u32x4*>(s_req)[tid] = piece;
         }
         __syncthreads();
@@ -1080,12 +1081,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
 #pragma unroll
             for (int u = 0; u < XB; ++u) {
                 const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
+                if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(din + c * 16u);
             }
 #pragma unroll
             for (int u = 0; u < XB; ++u) {
                 const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                if (c < nch) *reinterpret_cast<u32x4*>(data + c * 16u) = v[u] ^ k4;
+                if (c < nch) *reinterpret_cast<u32x4*>(dout + c * 16u) = v[u] ^ k4;
             }
         } else {
             // stage the segment in LDS: every chunk's load in flight at once
@@ -1095,7 +1096,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
                     const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                    if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(data + c * 16u);
+                    if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(din + c * 16u);
                 }
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
@@ -1128,6 +1129,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                         n = 1;
                     }
                 }
+                if (tid == 0) s_t[4] = wall_clock64();
                 walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
                 if (tid == 0) {
                     s_n = n;
@@ -1142,8 +1144,11 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
             }
             const uint64_t n = s_n;
             auto rec = [&](uint64_t i) -> drec { return i < SMALL_LREC ? lrec[i] : d_slot[i]; };
-            if (s_unmask && n) {
-                for (uint64_t c = (uint64_t)tid * 16u; c < L; c += (uint64_t)kDoorThreads * 16u) {
+            // every chunk of the read goes to dout (a separate area when the
+            // request came through device memory): masked bytes XORed
+            for (uint64_t c = (uint64_t)tid * 16u; c < L && s_unmask; c += (uint64_t)kDoorThreads * 16u) {
+                uint64_t mlo = 0, mhi = 0;
+                if (s_unmask && n) {
                     uint64_t k = 0, k_end = n;   // first record whose payload ends after c
                     while (k < k_end) {
                         const uint64_t mid = (k + k_end) >> 1;
@@ -1151,7 +1156,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                         if (m.pay_off + m.pay_len > c) k_end = mid;
                         else k = mid + 1;
                     }
-                    uint64_t mlo = 0, mhi = 0;
                     for (; k < n; ++k) {
                         const drec f = rec(k);
                         if (f.pay_off >= c + 16) break;
@@ -1166,10 +1170,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                         mhi |= kk & byte_range(a - 8, e - 8);
                         if (e == 16) break;   // this payload runs past the chunk
                     }
-                    if (!(mlo | mhi)) continue;   // no masked byte here: the data area already holds it
-                    const u32x4 m4 = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
-                    *reinterpret_cast<u32x4*>(data + c) = *reinterpret_cast<const u32x4*>(lds + c) ^ m4;
                 }
+                if (!(mlo | mhi) && din == dout) continue;   // no masked byte here: the data area already holds it
+                const u32x4 m4 = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+                *reinterpret_cast<u32x4*>(dout + c) = *reinterpret_cast<const u32x4*>(lds + c) ^ m4;
             }
             if (tid == 0) s_t[3] = wall_clock64();
             for (uint64_t i = tid; i < n; i += kDoorThreads) h_rec[i] = rec(i);
@@ -1184,6 +1188,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
                 box->stamp[4] = wall_clock64();
                 box->stamp[5] = s_t[5];
                 box->stamp[6] = s_m[1] - s_m[0];   // shader clocks from the request read to the walk's end
+                box->stamp[7] = s_t[4];            // carried-in frame done, speculative walk starts
             }
         }
         // every thread's stores reach host memory before `done` says so
@@ -1194,10 +1199,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(ddoor* __restrict__ box, 
     }
 }
 
-hipError_t launch_door(ddoor* box, uint8_t* data, drec* h_rec, drec* d_slot, uint64_t idle_ticks, uint64_t first_seq,
-                       uint64_t epoch, hipStream_t st) {
-    hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 16, st, box, data, h_rec, d_slot, idle_ticks,
-                       first_seq, epoch);
+hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
+                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st) {
+    hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 16, st, req, box, din, dout, h_rec, d_slot,
+                       idle_ticks, first_seq, epoch);
     return hipGetLastError();
 }
 
