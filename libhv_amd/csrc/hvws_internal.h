@@ -199,7 +199,7 @@ struct sieve_bufs {
 };
 constexpr uint32_t SV_STOP_TILES = 256;   // window tiles the early-stop bitmaps cover
 constexpr uint32_t SV_STOP_WORDS = 8;     // words per window (2 bitmaps x 4)
-bool sieve_stop_enabled();                // $HVWS_SIEVE_STOP (default on)
+bool sieve_stop_enabled();                // $HVWS_SIEVE_STOP (default off)
 uint64_t sieve_tiles_max(uint64_t rx_len);
 uint64_t sieve_slot_words(uint64_t rx_len);
 uint64_t sieve_min();                  // bytes after the first whole frame from which a mixed stream is sieved

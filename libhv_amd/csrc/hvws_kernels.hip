@@ -1822,11 +1822,19 @@ static uint32_t wave_blocks(uint32_t nseg) {
     return blocks > 65536u ? 65536u : (blocks ? blocks : 1u);
 }
 
+// $HVWS_WALK_BLOCKS (experiment): cap the walk's grid; each wave then walks
+// several segments in turn (fewer wave slots taken beside a running unmask).
+static uint32_t walk_blocks(uint32_t nseg) {
+    static const long cap = getenv("HVWS_WALK_BLOCKS") ? atol(getenv("HVWS_WALK_BLOCKS")) : 0;
+    const uint32_t b = wave_blocks(nseg);
+    return cap > 0 && (uint32_t)cap < b ? (uint32_t)cap : b;
+}
+
 hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
-    const uint32_t wb = wave_blocks(nseg);
+    const uint32_t wb = wave_blocks(nseg), wwb = walk_blocks(nseg);
     const uint32_t vb = 2048;
     // The frame sieve (one segment): its chain of whole frames is found in
     // parallel between the COUNT-side head and EMIT; k_walk resumes after it.
@@ -1855,7 +1863,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
             const hipError_t e = launch_sieve_emit(rx, rx_len, segs, sc.mid, *sc.sieve, fr, vmask, st);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+        hipLaunchKernelGGL(k_walk<true>, dim3(wwb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, emit_counts,
                            sv, sv_S, (const dcarry*)nullptr);
         return hipSuccess;
@@ -1871,7 +1879,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
                            pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, est, bases, nseg, total);
-        hipLaunchKernelGGL(k_walk<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+        hipLaunchKernelGGL(k_walk<true>, dim3(wwb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 1,
                            (const dsieve*)nullptr, (const uint64_t*)nullptr, carry_in);
     };
@@ -1894,7 +1902,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            fr.cap, sc.status, sc.seq);
     } else if (pass == SCAN_COUNT) {
         head_count(sc.status ? sc.est : nullptr);
-        hipLaunchKernelGGL(k_walk<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
+        hipLaunchKernelGGL(k_walk<false>, dim3(wwb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 0,
                            (const dsieve*)nullptr, (const uint64_t*)nullptr, (const dcarry*)nullptr);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, counts, bases, nseg, total);

@@ -803,8 +803,13 @@ __global__ __launch_bounds__(256) void k_sieve_emit_pos(const uint8_t* __restric
 
 uint64_t sieve_tiles_max(uint64_t rx_len) { return rx_len / SV_TILE + 2; }
 
+// Off by default: c4 as one stream ran 3.87 ms per step with it against
+// 1.57 without (profiles/r4b_raw): the window's tiles walked in order by 4
+// blocks make the count pass a long serial chain that no longer hides behind
+// the unmask, although the unmask beside it sped up (1.545 -> 1.450 ms) with
+// the traffic it saved.
 bool sieve_stop_enabled() {
-    static const int v = getenv("HVWS_SIEVE_STOP") ? atoi(getenv("HVWS_SIEVE_STOP")) : 1;
+    static const int v = getenv("HVWS_SIEVE_STOP") ? atoi(getenv("HVWS_SIEVE_STOP")) : 0;
     return v != 0;
 }
 uint64_t sieve_slot_words(uint64_t rx_len) { return sieve_tiles_max(rx_len) * SV_SLOT; }
