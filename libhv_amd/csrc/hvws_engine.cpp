@@ -199,7 +199,7 @@ struct hvws_ctx {
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
     // after each sieved scan (read as hints by the next one).
-    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_hops, sv_rank, sv_cnt, sv_tmp, sv_scr, sv_wmask;
+    dbuf sv_state, sv_tcount, sv_tbase, sv_slot, sv_pool, sv_keep, sv_kbase, sv_Spre, sv_S, sv_J0, sv_J1, sv_mark, sv_hops, sv_rank, sv_cnt, sv_tmp, sv_scr;
     uint64_t sv_cap = 0, sv_capc = 0;
     uint64_t sv_hint_pre = 0, sv_hint_surv = 0;   // counts of the latest sieved scan read back
     hbuf h_sv;
@@ -529,13 +529,6 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
     }
     c->sv_capc = capc;
     const uint64_t ntm = sieve_tiles_max(rx_len);
-    b.wmask = nullptr;
-    b.nwin = 0;
-    if (b.rt != b.wt && b.wt <= SV_STOP_TILES && sieve_stop_enabled()) {
-        b.nwin = ntm / b.rt + 2;
-        HIP_OR(c->sv_wmask.ensure(b.nwin * SV_STOP_WORDS * 8), HVWS_ENOMEM);
-        b.wmask = c->sv_wmask.as<unsigned long long>();
-    }
     const uint64_t nmax = std::max(cap, ntm);
     HIP_OR(c->sv_state.ensure(sizeof(dsieve)), HVWS_ENOMEM);
     HIP_OR(c->sv_tcount.ensure(ntm * 8), HVWS_ENOMEM);
@@ -794,8 +787,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                     (void)hipGetLastError();
                     for (dbuf* b : {&c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
                                     &c->sv_Spre, &c->sv_S,
-                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_tmp, &c->sv_scr,
-                                    &c->sv_wmask})
+                                    &c->sv_J0, &c->sv_J1, &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_tmp, &c->sv_scr})
                         b->release();
                     c->sv_ran = false;
                 }
@@ -1889,7 +1881,7 @@ void hvws_ctx_destroy(hvws_ctx* c) {
         b->release();
     for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
                     &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
-                    &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp, &c->sv_scr, &c->sv_wmask})
+                    &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp, &c->sv_scr})
         b->release();
     c->h_sv.release();
     if (c->sv_ev) hipEventDestroy(c->sv_ev);

@@ -191,15 +191,7 @@ struct sieve_bufs {
     uint32_t  rt, wt;    // windows: the first wt of every rt tiles are sieved (rt == wt: every tile)
     uint64_t* scr;       // windowed: each node's first 2^lgP frame offsets (capC << lgP), or nullptr
     uint32_t  lgP;
-    // Window early stop (windowed scans, wt <= SV_STOP_TILES): per window, 8
-    // words -- bitmaps of its tiles with >= 1 and with >= 2 survivors; a block
-    // stops sieving a window once earlier tiles hold 2 survivors.  nullptr: off.
-    unsigned long long* wmask;
-    uint64_t  nwin;      // windows the bitmaps cover (upper bound)
 };
-constexpr uint32_t SV_STOP_TILES = 256;   // window tiles the early-stop bitmaps cover
-constexpr uint32_t SV_STOP_WORDS = 8;     // words per window (2 bitmaps x 4)
-bool sieve_stop_enabled();                // $HVWS_SIEVE_STOP (default off)
 uint64_t sieve_tiles_max(uint64_t rx_len);
 uint64_t sieve_slot_words(uint64_t rx_len);
 uint64_t sieve_min();                  // bytes after the first whole frame from which a mixed stream is sieved

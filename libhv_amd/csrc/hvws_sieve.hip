@@ -61,7 +61,6 @@ constexpr int SV_DEPTH = 3;                            // hops a survivor's chai
 constexpr uint32_t SV_TERM = 0xFFFFFFFFu;
 constexpr uint32_t SV_GRID = 4096;
 constexpr uint32_t SV_HOP_CAP = 4096;                  // frames one link walk may cross
-constexpr uint32_t SV_STOP_G = 4;                      // blocks per window (window early stop)
 
 // Tiles of the segment that are sieved (the first wt of every rt of the NT
 // tiles from A0), and the stream tile of sieved tile t.
@@ -262,15 +261,10 @@ struct sieve_lds {
 // each thread's 32 positions waited for the busiest lane); survivors land in
 // the tile's bitmaps.  Two block barriers per tile: tile + candidate words
 // staged, and survivors complete.
-struct no_hook {
-    __device__ void operator()() const {}
-};
-
-// pre_final() runs on every thread right before the tile's last barrier.
-template <int MODE, typename Hook = no_hook>
+template <int MODE>
 __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, sieve_lds& sh, tile_regs& r, int par,
                                            uint64_t T0, bool have_next, uint64_t next_T0, uint64_t sb, uint64_t L,
-                                           uint64_t pos, Hook pre_final = Hook()) {
+                                           uint64_t pos) {
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     store_tile(sh.l, r);
     const uint32_t w0 = chunk_candidates(r.v[0], r.nx[0]);
@@ -284,7 +278,6 @@ __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, s
     __syncthreads();
     if (MODE == 2) {   // timing experiment: staging and candidate words only
         if (w0 == 0x12345678u) sh.sbits[par][0] = w1;
-        pre_final();
         __syncthreads();
         return;
     }
@@ -325,7 +318,6 @@ __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, s
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    pre_final();
     __syncthreads();
 }
 
@@ -335,9 +327,9 @@ __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, s
 // from one snapshot of the bytes, so S is exact and sorted even while a
 // concurrent unmask rewrites the payloads (only false survivors depend on
 // payload bytes).  Bit 31 of an entry: verify from HBM.
-__device__ __forceinline__ uint32_t record_tile(const sieve_lds& sh, int par, uint64_t t, uint64_t* tcount,
-                                                uint32_t* slot, uint32_t* pool, unsigned long long* pool_n,
-                                                uint64_t pool_cap) {
+__device__ __forceinline__ void record_tile(const sieve_lds& sh, int par, uint64_t t, uint64_t* tcount,
+                                            uint32_t* slot, uint32_t* pool, unsigned long long* pool_n,
+                                            uint64_t pool_cap) {
     const uint32_t lane = threadIdx.x;   // wave 0
     const uint32_t* sw = sh.sbits[par] + 4 * lane;
     const uint32_t* pw = sh.pbits[par] + 4 * lane;
@@ -347,7 +339,7 @@ __device__ __forceinline__ uint32_t record_tile(const sieve_lds& sh, int par, ui
     uint32_t k = wave_prefix(n, tot);
     if (tot == 0) {
         if (lane == 0) tcount[t] = 0;
-        return 0;
+        return;
     }
     uint32_t* dst = slot + t * SV_SLOT;
     uint32_t cap = SV_SLOT;
@@ -371,34 +363,9 @@ __device__ __forceinline__ uint32_t record_tile(const sieve_lds& sh, int par, ui
             ++k;
         }
     }
-    return tot;
 }
 
-// Window early stop: skip window tile i when the window's earlier tiles
-// already hold 2 survivors (one tile with >= 2, or two tiles with >= 1).  A
-// link walk entering the window from the previous region follows the exact
-// frames from the window's first true header on and stops at the first one
-// in S; any true header among the window's first survivors serves, so the
-// rest of the window need not be read (c4 as one stream).  The
-// bitmaps are read late and relaxed: a stale view only sieves a tile more.
-__device__ __forceinline__ bool window_done(const uint64_t* m, uint32_t i) {
-    uint32_t c1 = 0;
-    bool two = false;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t lo = 64u * (uint32_t)q;
-        const uint64_t below = i >= lo + 64 ? ~0ull : (i > lo ? (1ull << (i - lo)) - 1 : 0ull);
-        c1 += __builtin_popcountll(m[q] & below);
-        two |= (m[4 + q] & below) != 0;
-    }
-    return two || c1 >= 2;
-}
-
-// COUNT: tcount[t] = survivors of tile t, recorded by record_tile.  With
-// wmask (windowed scans): G blocks per window walk its tiles in order (block
-// g: window tiles g, g + G, ...) and stop once window_done() holds for their
-// next tile (tcount of the tiles left = 0).  Otherwise grid-stride over
-// every sieved tile.
+// COUNT: tcount[t] = survivors of tile t, recorded by record_tile.
 template <int MODE>
 __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_sieve_count(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                             const dseg* __restrict__ segs, const dmid* __restrict__ mid,
@@ -406,10 +373,8 @@ __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                                                             uint64_t* __restrict__ tcount, uint32_t* __restrict__ slot,
                                                             uint32_t* __restrict__ pool, unsigned long long* __restrict__ pool_n,
                                                             uint64_t pool_cap, uint64_t ntiles_max, dsieve* __restrict__ sv,
-                                                            uint32_t rt, uint32_t wt, unsigned long long* __restrict__ wmask,
-                                                            uint32_t G) {
+                                                            uint32_t rt, uint32_t wt) {
     __shared__ sieve_lds sh;
-    __shared__ uint64_t s_mv[SV_STOP_WORDS];
     uint64_t sb, L, pos;
     const bool want = sieve_wanted(segs, mid, npred, sieve_min, sb, L, pos);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -424,48 +389,6 @@ __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     for (uint64_t t = ntiles + blockIdx.x; t < ntiles_max; t += gridDim.x)
         if (threadIdx.x == 0) tcount[t] = 0;
     tile_regs r;
-    if (wmask) {
-        const uint64_t w = blockIdx.x / G;
-        const uint32_t g = blockIdx.x % G;
-        const uint64_t t0 = w * wt;
-        if (t0 >= ntiles) return;
-        const uint32_t wlen = (uint32_t)(ntiles - t0 < wt ? ntiles - t0 : wt);
-        unsigned long long* wm = wmask + w * SV_STOP_WORDS;
-        if (threadIdx.x < SV_STOP_WORDS) s_mv[threadIdx.x] = 0;
-        uint32_t i = g;
-        if (i >= wlen) return;
-        load_tile(rx, rx_len, A0 + sv_tile(t0 + i, rt, wt) * SV_TILE, r);
-        __syncthreads();   // s_mv initialised
-        for (int par = 0;; par ^= 1) {
-            const uint64_t t = t0 + i;
-            const uint32_t in = i + G;
-            uint64_t mv[SV_STOP_WORDS];
-            for (uint32_t k = 0; k < SV_STOP_WORDS; ++k) mv[k] = s_mv[k];   // the bitmaps as of the last tile
-            const bool have_next = in < wlen && !window_done(mv, in);
-            uint64_t nv[SV_STOP_WORDS] = {};
-            if (threadIdx.x == 0)   // issued now, used before the tile's last barrier
-                for (uint32_t k = 0; k < SV_STOP_WORDS; ++k)
-                    nv[k] = __hip_atomic_load(wm + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t T0 = A0 + sv_tile(t, rt, wt) * SV_TILE, Tn = A0 + sv_tile(t0 + in, rt, wt) * SV_TILE;
-            sieve_tile<MODE>(rx, rx_len, sh, r, par, T0, have_next, Tn, sb, L, pos, [&]() {
-                if (threadIdx.x == 0)
-                    for (uint32_t k = 0; k < SV_STOP_WORDS; ++k) s_mv[k] = nv[k];
-            });
-            if (threadIdx.x < 64) {
-                const uint32_t tot = record_tile(sh, par, t, tcount, slot, pool, pool_n, pool_cap);
-                if (threadIdx.x == 0 && tot) {
-                    atomicOr(wm + i / 64, 1ull << (i % 64));
-                    if (tot >= 2) atomicOr(wm + 4 + i / 64, 1ull << (i % 64));
-                }
-            }
-            if (!have_next) {   // the window's later tiles of this block: none sieved
-                for (uint32_t j = in; j < wlen; j += G)
-                    if (threadIdx.x == 0) tcount[t0 + j] = 0;
-                return;
-            }
-            i = in;
-        }
-    }
     uint64_t t = blockIdx.x;
     if (t < ntiles) load_tile(rx, rx_len, A0 + sv_tile(t, rt, wt) * SV_TILE, r);
     int par = 0;
@@ -802,16 +725,6 @@ __global__ __launch_bounds__(256) void k_sieve_emit_pos(const uint8_t* __restric
 // ---------------------------------------------------------------- launcher
 
 uint64_t sieve_tiles_max(uint64_t rx_len) { return rx_len / SV_TILE + 2; }
-
-// Off by default: c4 as one stream ran 3.87 ms per step with it against
-// 1.57 without (profiles/r4b_raw): the window's tiles walked in order by 4
-// blocks make the count pass a long serial chain that no longer hides behind
-// the unmask, although the unmask beside it sped up (1.545 -> 1.450 ms) with
-// the traffic it saved.
-bool sieve_stop_enabled() {
-    static const int v = getenv("HVWS_SIEVE_STOP") ? atoi(getenv("HVWS_SIEVE_STOP")) : 0;
-    return v != 0;
-}
 uint64_t sieve_slot_words(uint64_t rx_len) { return sieve_tiles_max(rx_len) * SV_SLOT; }
 
 static uint64_t g_sieve_min = 0;   // 0: not yet read from the environment
@@ -903,17 +816,10 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     // so the chain is empty and the exact walk does everything (results stay
     // exact, only slow); 4 = without the next tile's register prefetch.
     static const int mode = getenv("HVWS_SIEVE_MODE") ? atoi(getenv("HVWS_SIEVE_MODE")) : 0;
-    // window early stop: G blocks per window (the timing modes keep the grid-stride mapping)
-    const bool stop = b.wmask && b.rt != b.wt && b.wt <= SV_STOP_TILES && mode == 0 && b.nwin * SV_STOP_G < (1ull << 31);
-    uint32_t cgrid = grid;
-    if (stop) {
-        if ((e = hipMemsetAsync(b.wmask, 0, b.nwin * SV_STOP_WORDS * 8, st)) != hipSuccess) return e;
-        cgrid = (uint32_t)(b.nwin * SV_STOP_G);
-    }
 #define HVWS_SIEVE_COUNT(M)                                                                                     \
-    hipLaunchKernelGGL(k_sieve_count<M>, dim3(cgrid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,   \
+    hipLaunchKernelGGL(k_sieve_count<M>, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,    \
                        sieve_min(), b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), \
-                       b.capS, ntm, sv, b.rt, b.wt, stop ? b.wmask : nullptr, SV_STOP_G)
+                       b.capS, ntm, sv, b.rt, b.wt)
     switch (mode) {
         case 1: HVWS_SIEVE_COUNT(1); break;
         case 2: HVWS_SIEVE_COUNT(2); break;
