@@ -989,10 +989,52 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // `seq` (serving a request that arrived meanwhile) and exits; its last store
 // is `exited = epoch`, and the host relaunches it on the next request once it
 // has seen that word.
+// The worker's header walk over a read staged in LDS (walk != 0): one header
+// after the other, every lane of wave 0 on the same header (uniform control
+// flow), the header's 16 bytes from five dword loads realigned in registers;
+// whole frames only, the frame cut by the read's end through the exact state
+// machine.  Records and the carried fields (Q14) as walk_frames leaves them.
+template <typename Emit>
+__device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
+                                          uint32_t vmask, Emit&& emit) {
+    const uint32_t* l = reinterpret_cast<const uint32_t*>(lds);
+    while (st.state == S_START && pos + 2 <= L) {
+        const uint32_t q = (uint32_t)pos, w = q >> 2, sh = (q & 3u) * 8u;
+        const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
+        const uint32_t b0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
+        const uint32_t b1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
+        const uint32_t b2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
+        const uint32_t b3 = sh ? (d3 >> sh) | (d4 << (32u - sh)) : d3;
+        const hdr h = parse_hdr((uint64_t)b0 | ((uint64_t)b1 << 32), (uint64_t)b2 | ((uint64_t)b3 << 32));
+        const uint64_t rq = L - pos;
+        if (h.hlen > rq || h.length > rq - h.hlen) break;   // cut by the read's end
+        frec v;
+        whole_frame_rec(v, pos, h, vmask);
+        emit(n, v);
+        ++n;
+        pos += h.hlen + h.length;
+        st.flags = h.flags;
+        st.length = h.length;
+        st.require = 0;
+        st.offset = 0;
+        st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
+        if (h.flags & F_MASK) st.mask = h.key;
+        st.started = 0;
+    }
+    if (st.state == S_START && pos < L) {
+        frec r;
+        if (scalar_frame(lds, L, st, pos, r, vmask)) {
+            emit(n, r);
+            ++n;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__ req, ddoor* __restrict__ box,
                                                        const uint8_t* __restrict__ din, uint8_t* __restrict__ dout,
                                                        drec* __restrict__ h_rec, drec* __restrict__ d_slot,
-                                                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch) {
+                                                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch,
+                                                       uint32_t walk) {
     extern __shared__ u32x4 lds_door[];
     __shared__ drec lrec[SMALL_LREC];
     __shared__ uint64_t s_seq, s_len, s_n;
@@ -1130,7 +1172,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     }
                 }
                 if (tid == 0) s_t[4] = wall_clock64();
-                walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
+                if (walk)
+                    door_walk(lds, L, st, pos, n, vmask, [&](uint64_t idx, const frec& v) {
+                        if (tid == 0) emit(idx, v);
+                    });
+                else
+                    walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
                 if (tid == 0) {
                     s_n = n;
                     s_carry = st;
@@ -1201,8 +1248,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
 
 hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
                        uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st) {
-    hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 16, st, req, box, din, dout, h_rec, d_slot,
-                       idle_ticks, first_seq, epoch);
+    // $HVWS_DOOR_WALK=0: the speculative wave-wide walk (k_small's) instead of door_walk
+    static const uint32_t walk = getenv("HVWS_DOOR_WALK") ? (uint32_t)atoi(getenv("HVWS_DOOR_WALK")) : 1u;
+    hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
+                       idle_ticks, first_seq, epoch, walk);
     return hipGetLastError();
 }
 
