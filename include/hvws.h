@@ -362,6 +362,9 @@ int hvws_debug_dump(int fd);
  * (SIGUSR2 to each thread in turn, backtrace_symbols_fd in the handler).
  * Returns the number of threads that answered within 200 ms each. */
 int hvws_debug_backtraces(int fd);
+/* out = {requests go through device memory written across the PCIe BAR (1)
+ * or through pinned host memory (0), the context has a worker stream}. */
+int hvws_door_info(hvws_ctx* ctx, uint64_t out[2]);
 /* Diagnostics: 100 MHz device-clock stamps of the worker's last read request
  * -- seen, staged, walked, XORed, records written (before the release). */
 int hvws_door_stamps(hvws_ctx* ctx, uint64_t out[8]);

@@ -186,6 +186,7 @@ _SIGS = {
     "hvws_set_door": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_debug_dump": (ctypes.c_int, [ctypes.c_int]),
     "hvws_debug_backtraces": (ctypes.c_int, [ctypes.c_int]),
+    "hvws_door_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_door_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_door_idle_us": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_door_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),

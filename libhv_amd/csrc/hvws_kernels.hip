@@ -989,42 +989,116 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // `seq` (serving a request that arrived meanwhile) and exits; its last store
 // is `exited = epoch`, and the host relaunches it on the next request once it
 // has seen that word.
-// The worker's header walk over a read staged in LDS (walk != 0): one header
-// after the other, every lane of wave 0 on the same header (uniform control
-// flow), the header's 16 bytes from five dword loads realigned in registers;
-// whole frames only, the frame cut by the read's end through the exact state
-// machine.  Records and the carried fields (Q14) as walk_frames leaves them.
+// The worker's header walk over a read staged in LDS (walk != 0).  A single
+// wave walking headers one after the other is a chain of dependent
+// instructions (~8 cycles each): round 3's walks spent ~4.5 us on the 8
+// headers of an 8 KiB read (profiles/r4c_raw).  So the chain carries only
+// what the next position needs -- byte 1, the extended length, the mask bit
+// -- in 32-bit arithmetic, and the frames' positions go to LDS; then the
+// wave's lanes parse those headers in parallel and emit the records.  Up to
+// DOOR_CHASE positions per round; the frame cut by the read's end goes
+// through the exact state machine.  Records and the carried fields (Q14) as
+// walk_frames leaves them.
+constexpr uint32_t DOOR_CHASE = 512;
+
 template <typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
-                                          uint32_t vmask, Emit&& emit) {
+                                          uint32_t vmask, uint32_t* s_fpos, Emit&& emit) {
     const uint32_t* l = reinterpret_cast<const uint32_t*>(lds);
-    while (st.state == S_START && pos + 2 <= L) {
-        const uint32_t q = (uint32_t)pos, w = q >> 2, sh = (q & 3u) * 8u;
-        const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
-        const uint32_t b0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
-        const uint32_t b1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
-        const uint32_t b2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
-        const uint32_t b3 = sh ? (d3 >> sh) | (d4 << (32u - sh)) : d3;
-        const hdr h = parse_hdr((uint64_t)b0 | ((uint64_t)b1 << 32), (uint64_t)b2 | ((uint64_t)b3 << 32));
-        const uint64_t rq = L - pos;
-        if (h.hlen > rq || h.length > rq - h.hlen) break;   // cut by the read's end
-        frec v;
-        whole_frame_rec(v, pos, h, vmask);
-        emit(n, v);
-        ++n;
-        pos += h.hlen + h.length;
-        st.flags = h.flags;
-        st.length = h.length;
-        st.require = 0;
-        st.offset = 0;
-        st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
-        if (h.flags & F_MASK) st.mask = h.key;
-        st.started = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t Lw = (uint32_t)L;   // reads are <= kDoorMax
+    uint32_t q = (uint32_t)pos;
+    bool cut = false;
+    while (st.state == S_START && !cut && q + 2 <= Lw) {
+        // 1. positions only
+        uint32_t cnt = 0;
+        while (cnt < DOOR_CHASE && q + 2 <= Lw) {
+            const uint32_t w = q >> 2, sh = (q & 3u) * 8u;
+            const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3];
+            const uint32_t b0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
+            const uint32_t len7 = (b0 >> 8) & 0x7Fu, m4 = (b0 >> 13) & 4u;   // bit 7 of byte 1 -> 4 key bytes
+            const uint32_t rq = Lw - q;
+            uint32_t hl, len;
+            if (len7 < 126) {
+                hl = 2u + m4;
+                len = len7;
+            } else if (len7 == 126) {
+                hl = 4u + m4;
+                len = ((b0 >> 8) & 0xFF00u) | (b0 >> 24);
+            } else {   // 64-bit length: whole only if non-minimal and small
+                const uint32_t b1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
+                const uint32_t b2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
+                const uint64_t be = (uint64_t)(b0 >> 16) | ((uint64_t)b1 << 16) | ((uint64_t)(b2 & 0xFFFFu) << 48);
+                const uint64_t len64 = __builtin_bswap64(be);
+                hl = 10u + m4;
+                len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
+            }
+            if (hl > rq || len > rq - hl) {
+                cut = true;
+                break;
+            }
+            if (lane == 0) s_fpos[cnt] = q;
+            ++cnt;
+            q += hl + len;
+        }
+        if (!cnt) break;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // 2. the headers in parallel: records, and the last (masked) frame's fields
+        uint32_t lastm = 0, lastm_key = 0;   // 1 + index of this lane's last masked frame
+        for (uint32_t k = lane; k < cnt; k += 64) {
+            const uint32_t p = s_fpos[k], w = p >> 2, sh = (p & 3u) * 8u;
+            const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
+            const uint32_t c0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
+            const uint32_t c1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
+            const uint32_t c2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
+            const uint32_t c3 = sh ? (d3 >> sh) | (d4 << (32u - sh)) : d3;
+            const hdr h = parse_hdr((uint64_t)c0 | ((uint64_t)c1 << 32), (uint64_t)c2 | ((uint64_t)c3 << 32));
+            frec v;
+            whole_frame_rec(v, p, h, vmask);
+            emit(n + k, v);
+            if (h.flags & F_MASK) {
+                lastm = k + 1;
+                lastm_key = h.key;
+            }
+        }
+        // the round's last frame (its lane) and last masked frame (wave max)
+        const uint32_t lk = cnt - 1;
+        {
+            const uint32_t p = s_fpos[lk], w = p >> 2, sh = (p & 3u) * 8u;
+            const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
+            const uint32_t c0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
+            const uint32_t c1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
+            const uint32_t c2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
+            const uint32_t c3 = sh ? (d3 >> sh) | (d4 << (32u - sh)) : d3;
+            const hdr h = parse_hdr((uint64_t)c0 | ((uint64_t)c1 << 32), (uint64_t)c2 | ((uint64_t)c3 << 32));
+            st.flags = h.flags;
+            st.length = h.length;
+            st.require = 0;
+            st.offset = 0;
+            st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
+            st.started = 0;
+        }
+        uint32_t best = lastm, bkey = lastm_key;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t ob = __shfl_xor(best, o), ok = __shfl_xor(bkey, o);
+            if (ob > best) {
+                best = ob;
+                bkey = ok;
+            }
+        }
+        if (best) st.mask = bkey;
+        n += cnt;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // s_fpos is rewritten by the next round
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    pos = q;
     if (st.state == S_START && pos < L) {
         frec r;
         if (scalar_frame(lds, L, st, pos, r, vmask)) {
-            emit(n, r);
+            if (lane == 0) emit(n, r);
             ++n;
         }
     }
@@ -1046,6 +1120,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     uint64_t served = 0;
     __shared__ uint64_t s_t[6], s_m[2];
     __shared__ uint64_t s_req[16];
+    __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
     for (;;) {
         if (tid == 0) {
             uint64_t t0 = wall_clock64();
@@ -1173,9 +1248,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 }
                 if (tid == 0) s_t[4] = wall_clock64();
                 if (walk)
-                    door_walk(lds, L, st, pos, n, vmask, [&](uint64_t idx, const frec& v) {
-                        if (tid == 0) emit(idx, v);
-                    });
+                    door_walk(lds, L, st, pos, n, vmask, s_fpos, emit);
                 else
                     walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
                 if (tid == 0) {

@@ -40,7 +40,9 @@ for i in range(n):
 rows = np.array(rows[n // 10:], dtype=np.float64)
 t0, t1, t2, t3, t4, t5, clk, tw = (rows[:, i] for i in range(8))
 us = lambda a, b: round(float(np.median((b - a) * 0.01)), 2)   # noqa: E731  (ticks of 10 ns)
-out = {"reads": n, "request_in_device_memory": os.environ.get("HVWS_DOOR_VRAM", "1") != "0", "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
+info = (ctypes.c_uint64 * 2)()
+L.hvws_door_info(None, info)
+out = {"reads": n, "request_in_device_memory": bool(info[0]), "door_walk": os.environ.get("HVWS_DOOR_WALK", "1"), "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
        "device_us_median": {"request_read": us(t0, t5), "stage": us(t5, t1), "carried_in_frame": us(t1, tw),
                             "walk": us(tw, t2),
                             "xor_and_stores": us(t2, t3), "records": us(t3, t4)},
