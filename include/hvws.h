@@ -367,7 +367,7 @@ int hvws_debug_backtraces(int fd);
 int hvws_door_info(hvws_ctx* ctx, uint64_t out[2]);
 /* Diagnostics: 100 MHz device-clock stamps of the worker's last read request
  * -- seen, staged, walked, XORed, records written (before the release). */
-int hvws_door_stamps(hvws_ctx* ctx, uint64_t out[8]);
+int hvws_door_stamps(hvws_ctx* ctx, uint64_t out[12]);
 
 /* Small batches whose segments are all <= 32 KiB (total <= 1 MiB; an event
  * loop's reads) are read by the device straight from pinned host memory, each

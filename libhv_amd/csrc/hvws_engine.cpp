@@ -2619,11 +2619,11 @@ int hvws_door_info(hvws_ctx* c, uint64_t out[2]) {
     return HVWS_OK;
 }
 
-int hvws_door_stamps(hvws_ctx* c, uint64_t out[8]) {
+int hvws_door_stamps(hvws_ctx* c, uint64_t out[12]) {
     if (!c) c = hvws::thread_ctx();
     if (!out) return set_err(HVWS_EINVAL, "null output");
-    memset(out, 0, 8 * sizeof(uint64_t));
-    if (c->h_door.p) memcpy(out, c->h_door.as<ddoor>()->stamp, 8 * sizeof(uint64_t));
+    memset(out, 0, 12 * sizeof(uint64_t));
+    if (c->h_door.p) memcpy(out, c->h_door.as<ddoor>()->stamp, 12 * sizeof(uint64_t));
     return HVWS_OK;
 }
 

@@ -294,7 +294,7 @@ struct ddoor {
     // realtime-clock stamps of the last request (100 MHz): seen, staged,
     // walked, xored, stored (before the release), and the sum of ticks spent
     // polling; read by hvws_door_stats' diagnostics
-    uint64_t stamp[8];
+    uint64_t stamp[12];   // [8..10]: door_walk's chase, parallel parse, tail ends
 };
 static_assert(sizeof(dcarry) == 48, "dcarry layout");
 static_assert(offsetof(ddoor, done) == 128, "ddoor: device fields on their own lines");

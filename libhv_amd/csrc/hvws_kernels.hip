@@ -1003,7 +1003,7 @@ constexpr uint32_t DOOR_CHASE = 512;
 
 template <typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
-                                          uint32_t vmask, uint32_t* s_fpos, Emit&& emit) {
+                                          uint32_t vmask, uint32_t* s_fpos, uint64_t* stamps, Emit&& emit) {
     const uint32_t* l = reinterpret_cast<const uint32_t*>(lds);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t Lw = (uint32_t)L;   // reads are <= kDoorMax
@@ -1041,6 +1041,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             ++cnt;
             q += hl + len;
         }
+        if (threadIdx.x == 0) stamps[0] = wall_clock64();
         if (!cnt) break;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1090,6 +1091,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
         }
         if (best) st.mask = bkey;
         n += cnt;
+        if (threadIdx.x == 0) stamps[1] = wall_clock64();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // s_fpos is rewritten by the next round
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1102,6 +1104,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             ++n;
         }
     }
+    if (threadIdx.x == 0) stamps[2] = wall_clock64();
 }
 
 __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__ req, ddoor* __restrict__ box,
@@ -1121,6 +1124,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     __shared__ uint64_t s_t[6], s_m[2];
     __shared__ uint64_t s_req[16];
     __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
+    __shared__ uint64_t s_w[3];               // door_walk's stamps
     for (;;) {
         if (tid == 0) {
             uint64_t t0 = wall_clock64();
@@ -1248,7 +1252,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 }
                 if (tid == 0) s_t[4] = wall_clock64();
                 if (walk)
-                    door_walk(lds, L, st, pos, n, vmask, s_fpos, emit);
+                    door_walk(lds, L, st, pos, n, vmask, s_fpos, s_w, emit);
                 else
                     walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
                 if (tid == 0) {
@@ -1308,7 +1312,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 box->stamp[4] = wall_clock64();
                 box->stamp[5] = s_t[5];
                 box->stamp[6] = s_m[1] - s_m[0];   // shader clocks from the request read to the walk's end
-                box->stamp[7] = s_t[4];            // carried-in frame done, speculative walk starts
+                box->stamp[7] = s_t[4];            // carried-in frame done, the walk starts
+                box->stamp[8] = s_w[0];
+                box->stamp[9] = s_w[1];
+                box->stamp[10] = s_w[2];
             }
         }
         // every thread's stores reach host memory before `done` says so

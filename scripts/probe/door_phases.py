@@ -28,7 +28,7 @@ with libhv_amd.Engine(0) as eng:
 buf = ctypes.create_string_buffer(data.tobytes(), len(data))
 L.hvws_set_door(None, 1)
 h = L.hvws_wsp_new()
-st = (ctypes.c_uint64 * 8)()
+st = (ctypes.c_uint64 * 12)()
 rows, wall = [], []
 for i in range(n):
     t = time.perf_counter()
@@ -36,15 +36,17 @@ for i in range(n):
     wall.append(time.perf_counter() - t)
     assert r == 8192
     L.hvws_door_stamps(None, st)
-    rows.append(list(st[:8]))
+    rows.append(list(st[:11]))
 rows = np.array(rows[n // 10:], dtype=np.float64)
-t0, t1, t2, t3, t4, t5, clk, tw = (rows[:, i] for i in range(8))
+t0, t1, t2, t3, t4, t5, clk, tw, tc, tp, tt = (rows[:, i] for i in range(11))
 us = lambda a, b: round(float(np.median((b - a) * 0.01)), 2)   # noqa: E731  (ticks of 10 ns)
 info = (ctypes.c_uint64 * 2)()
 L.hvws_door_info(None, info)
 out = {"reads": n, "request_in_device_memory": bool(info[0]), "door_walk": os.environ.get("HVWS_DOOR_WALK", "1"), "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
        "device_us_median": {"request_read": us(t0, t5), "stage": us(t5, t1), "carried_in_frame": us(t1, tw),
                             "walk": us(tw, t2),
+                            "walk_parts": {"chase": us(tw, tc), "parse": us(tc, tp), "tail": us(tp, tt),
+                                           "to_barrier": us(tt, t2)},
                             "xor_and_stores": us(t2, t3), "records": us(t3, t4)},
        "device_us_total_median": us(t0, t4),
        "shader_clock_MHz_median": round(float(np.median(clk / ((t2 - t5) * 0.01))), 1)}
