@@ -1001,6 +1001,16 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // walk_frames leaves them.
 constexpr uint32_t DOOR_CHASE = 512;
 
+// 16 bytes at LDS byte q (dword-aligned loads, v_alignbyte realigns)
+__device__ __forceinline__ void lds_hdr16(const uint32_t* l, uint32_t q, uint64_t& lo, uint64_t& hi) {
+    const uint32_t w = q >> 2, r = q & 3u;
+    const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
+    const uint32_t c0 = __builtin_amdgcn_alignbyte(d1, d0, r), c1 = __builtin_amdgcn_alignbyte(d2, d1, r);
+    const uint32_t c2 = __builtin_amdgcn_alignbyte(d3, d2, r), c3 = __builtin_amdgcn_alignbyte(d4, d3, r);
+    lo = (uint64_t)c0 | ((uint64_t)c1 << 32);
+    hi = (uint64_t)c2 | ((uint64_t)c3 << 32);
+}
+
 template <typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
                                           uint32_t vmask, uint32_t* s_fpos, uint64_t* stamps, Emit&& emit) {
@@ -1010,13 +1020,13 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
     uint32_t q = (uint32_t)pos;
     bool cut = false;
     while (st.state == S_START && !cut && q + 2 <= Lw) {
-        // 1. positions only
+        // 1. positions only: byte 1, the extended length and the mask bit
         uint32_t cnt = 0;
         while (cnt < DOOR_CHASE && q + 2 <= Lw) {
-            const uint32_t w = q >> 2, sh = (q & 3u) * 8u;
-            const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3];
-            const uint32_t b0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
-            const uint32_t len7 = (b0 >> 8) & 0x7Fu, m4 = (b0 >> 13) & 4u;   // bit 7 of byte 1 -> 4 key bytes
+            const uint32_t w = q >> 2, r = q & 3u;
+            const uint32_t d0 = l[w], d1 = l[w + 1];
+            const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, r);   // bytes q .. q+3
+            const uint32_t len7 = (b0 >> 8) & 0x7Fu, m4 = (b0 >> 13) & 4u;
             const uint32_t rq = Lw - q;
             uint32_t hl, len;
             if (len7 < 126) {
@@ -1026,8 +1036,8 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
                 hl = 4u + m4;
                 len = ((b0 >> 8) & 0xFF00u) | (b0 >> 24);
             } else {   // 64-bit length: whole only if non-minimal and small
-                const uint32_t b1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
-                const uint32_t b2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
+                const uint32_t d2 = l[w + 2], d3 = l[w + 3];
+                const uint32_t b1 = __builtin_amdgcn_alignbyte(d2, d1, r), b2 = __builtin_amdgcn_alignbyte(d3, d2, r);
                 const uint64_t be = (uint64_t)(b0 >> 16) | ((uint64_t)b1 << 16) | ((uint64_t)(b2 & 0xFFFFu) << 48);
                 const uint64_t len64 = __builtin_bswap64(be);
                 hl = 10u + m4;
@@ -1046,16 +1056,16 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // 2. the headers in parallel: records, and the last (masked) frame's fields
+        // 2. the headers in parallel: records; the round's last frame and last
+        // masked frame give the carried fields (Q14)
         uint32_t lastm = 0, lastm_key = 0;   // 1 + index of this lane's last masked frame
+        uint32_t lfl = 0;
+        uint64_t llen = 0;
         for (uint32_t k = lane; k < cnt; k += 64) {
-            const uint32_t p = s_fpos[k], w = p >> 2, sh = (p & 3u) * 8u;
-            const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
-            const uint32_t c0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
-            const uint32_t c1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
-            const uint32_t c2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
-            const uint32_t c3 = sh ? (d3 >> sh) | (d4 << (32u - sh)) : d3;
-            const hdr h = parse_hdr((uint64_t)c0 | ((uint64_t)c1 << 32), (uint64_t)c2 | ((uint64_t)c3 << 32));
+            const uint32_t p = s_fpos[k];
+            uint64_t lo, hi;
+            lds_hdr16(l, p, lo, hi);
+            const hdr h = parse_hdr(lo, hi);
             frec v;
             whole_frame_rec(v, p, h, vmask);
             emit(n + k, v);
@@ -1063,24 +1073,16 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
                 lastm = k + 1;
                 lastm_key = h.key;
             }
+            lfl = h.flags;
+            llen = h.length;
         }
-        // the round's last frame (its lane) and last masked frame (wave max)
-        const uint32_t lk = cnt - 1;
-        {
-            const uint32_t p = s_fpos[lk], w = p >> 2, sh = (p & 3u) * 8u;
-            const uint32_t d0 = l[w], d1 = l[w + 1], d2 = l[w + 2], d3 = l[w + 3], d4 = l[w + 4];
-            const uint32_t c0 = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;
-            const uint32_t c1 = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
-            const uint32_t c2 = sh ? (d2 >> sh) | (d3 << (32u - sh)) : d2;
-            const uint32_t c3 = sh ? (d3 >> sh) | (d4 << (32u - sh)) : d3;
-            const hdr h = parse_hdr((uint64_t)c0 | ((uint64_t)c1 << 32), (uint64_t)c2 | ((uint64_t)c3 << 32));
-            st.flags = h.flags;
-            st.length = h.length;
-            st.require = 0;
-            st.offset = 0;
-            st.mask_offset = (h.flags & F_MASK) ? (uint32_t)(h.length & 3u) : 0u;
-            st.started = 0;
-        }
+        const int src = (int)((cnt - 1) & 63u);   // that lane parsed frame cnt - 1 last
+        st.flags = (uint32_t)__shfl((int)lfl, src);
+        st.length = (uint64_t)__shfl((long long)llen, src);
+        st.require = 0;
+        st.offset = 0;
+        st.mask_offset = (st.flags & F_MASK) ? (uint32_t)(st.length & 3u) : 0u;
+        st.started = 0;
         uint32_t best = lastm, bkey = lastm_key;
         for (int o = 32; o > 0; o >>= 1) {
             const uint32_t ob = __shfl_xor(best, o), ok = __shfl_xor(bkey, o);
@@ -1098,10 +1100,45 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
     }
     pos = q;
     if (st.state == S_START && pos < L) {
-        frec r;
-        if (scalar_frame(lds, L, st, pos, r, vmask)) {
+        const uint32_t rq = Lw - q;
+        uint64_t lo = 0, hi = 0;
+        hdr h;
+        h.hlen = 0xFFu;
+        if (rq >= 2) {
+            lds_hdr16(l, q, lo, hi);
+            h = parse_hdr(lo, hi);
+        }
+        if (h.hlen <= rq) {
+            // The common cut: the header is whole, the payload runs past the
+            // read.  What scalar_frame leaves behind, in one step: a record
+            // with the payload bytes here, S_BODY with the rest to come.
+            const uint32_t nb = rq - h.hlen;   // < h.length: the frame is cut
+            frec r;
+            r.hdr_off = (int64_t)q;
+            r.pay_off = q + h.hlen;
+            r.pay_len = nb;
+            r.length = h.length;
+            r.key = (h.flags & F_MASK) ? h.key : 0u;
+            r.info = I_START | (h.flags & 0xFFu) | I_HDR | invalid_bits(h.viol, vmask) | (nb ? I_BODY : 0u);
+            const uint32_t len7 = (uint32_t)(lo >> 8) & 0x7Fu;
+            st.state = S_BODY;
+            st.flags = h.flags;
+            st.length = h.length;
+            if (h.flags & F_MASK) st.mask = h.key;
+            st.mask_offset = (h.flags & F_MASK) ? (nb & 3u) : 0u;
+            st.require = h.length - nb;
+            st.offset = nb;
+            st.started = 1;
+            st.viol = h.viol | ((len7 == 127 ? 2u : (len7 == 126 ? 1u : 0u)) << V_ENC_SHIFT);
             if (lane == 0) emit(n, r);
             ++n;
+            pos = L;
+        } else {   // the header itself is cut: the exact state machine
+            frec r;
+            if (scalar_frame(lds, L, st, pos, r, vmask)) {
+                if (lane == 0) emit(n, r);
+                ++n;
+            }
         }
     }
     if (threadIdx.x == 0) stamps[2] = wall_clock64();
