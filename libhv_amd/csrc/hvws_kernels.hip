@@ -1011,6 +1011,29 @@ __device__ __forceinline__ void lds_hdr16(const uint32_t* l, uint32_t q, uint64_
     hi = (uint64_t)c2 | ((uint64_t)c3 << 32);
 }
 
+// Header length and payload length of the frame at LDS byte q (32-bit; a
+// 64-bit length past 2^32 - 1 clamps, which no whole frame of a read has).
+__device__ __forceinline__ void door_size(const uint32_t* l, uint32_t q, uint32_t& hl, uint32_t& len) {
+    const uint32_t w = q >> 2, r = q & 3u;
+    const uint32_t d0 = l[w], d1 = l[w + 1];
+    const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, r);   // bytes q .. q+3
+    const uint32_t len7 = (b0 >> 8) & 0x7Fu, m4 = (b0 >> 13) & 4u;   // bit 7 of byte 1 -> 4 key bytes
+    if (len7 < 126) {
+        hl = 2u + m4;
+        len = len7;
+    } else if (len7 == 126) {
+        hl = 4u + m4;
+        len = ((b0 >> 8) & 0xFF00u) | (b0 >> 24);
+    } else {
+        const uint32_t d2 = l[w + 2], d3 = l[w + 3];
+        const uint32_t b1 = __builtin_amdgcn_alignbyte(d2, d1, r), b2 = __builtin_amdgcn_alignbyte(d3, d2, r);
+        const uint64_t be = (uint64_t)(b0 >> 16) | ((uint64_t)b1 << 16) | ((uint64_t)(b2 & 0xFFFFu) << 48);
+        const uint64_t len64 = __builtin_bswap64(be);
+        hl = 10u + m4;
+        len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
+    }
+}
+
 template <typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
                                           uint32_t vmask, uint32_t* s_fpos, uint64_t* stamps, Emit&& emit) {
@@ -1020,36 +1043,34 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
     uint32_t q = (uint32_t)pos;
     bool cut = false;
     while (st.state == S_START && !cut && q + 2 <= Lw) {
-        // 1. positions only: byte 1, the extended length and the mask bit
+        // 1. positions only, a run of equal-size frames per step: every lane
+        // reads the header at q (its size is the stride), then lane j the
+        // header at q + j * stride; the first lane whose frame is not whole or
+        // not of that size ends the run, and the next step starts there.
         uint32_t cnt = 0;
         while (cnt < DOOR_CHASE && q + 2 <= Lw) {
-            const uint32_t w = q >> 2, r = q & 3u;
-            const uint32_t d0 = l[w], d1 = l[w + 1];
-            const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, r);   // bytes q .. q+3
-            const uint32_t len7 = (b0 >> 8) & 0x7Fu, m4 = (b0 >> 13) & 4u;
-            const uint32_t rq = Lw - q;
             uint32_t hl, len;
-            if (len7 < 126) {
-                hl = 2u + m4;
-                len = len7;
-            } else if (len7 == 126) {
-                hl = 4u + m4;
-                len = ((b0 >> 8) & 0xFF00u) | (b0 >> 24);
-            } else {   // 64-bit length: whole only if non-minimal and small
-                const uint32_t d2 = l[w + 2], d3 = l[w + 3];
-                const uint32_t b1 = __builtin_amdgcn_alignbyte(d2, d1, r), b2 = __builtin_amdgcn_alignbyte(d3, d2, r);
-                const uint64_t be = (uint64_t)(b0 >> 16) | ((uint64_t)b1 << 16) | ((uint64_t)(b2 & 0xFFFFu) << 48);
-                const uint64_t len64 = __builtin_bswap64(be);
-                hl = 10u + m4;
-                len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
-            }
+            door_size(l, q, hl, len);
+            const uint32_t rq = Lw - q;
             if (hl > rq || len > rq - hl) {
                 cut = true;
                 break;
             }
-            if (lane == 0) s_fpos[cnt] = q;
-            ++cnt;
-            q += hl + len;
+            const uint32_t stride = hl + len;
+            const uint32_t p = q + lane * stride;   // lane * stride < 64 * 2^15
+            bool ok = lane == 0;
+            if (lane && p + 2 <= Lw && p - q == lane * stride) {
+                uint32_t hj, lj;
+                door_size(l, p, hj, lj);
+                const uint32_t rj = Lw - p;
+                ok = hj <= rj && lj <= rj - hj && hj + lj == stride;
+            }
+            const unsigned long long bad = __ballot(!ok);
+            uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1u : 64u;
+            if (f > DOOR_CHASE - cnt) f = DOOR_CHASE - cnt;
+            if (lane < f) s_fpos[cnt + lane] = p;
+            cnt += f;
+            q += f * stride;
         }
         if (threadIdx.x == 0) stamps[0] = wall_clock64();
         if (!cnt) break;
