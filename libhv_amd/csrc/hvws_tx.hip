@@ -325,7 +325,7 @@ __device__ __forceinline__ void lds16(const uint8_t* a, uint32_t q, uint64_t& lo
 }
 
 template <int U, bool SWZ, bool NT, bool SF>
-__global__ __launch_bounds__(256) void k_build(uint8_t* __restrict__ out, uint64_t out_len,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(uint8_t* __restrict__ out, uint64_t out_len,
                                                const uint8_t* __restrict__ pay, uint64_t plen,
                                                const uint64_t* __restrict__ pay_off,
                                                const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,

@@ -26,6 +26,24 @@ with libhv_amd.Engine(0) as eng:
     b.free()
     dp.free()
 buf = ctypes.create_string_buffer(data.tobytes(), len(data))
+# DOOR_PHASES_BUSY=1: another context keeps the GPU busy with short kernels
+# meanwhile (does the worker's single workgroup run slower on an idle chip?)
+busy = os.environ.get("DOOR_PHASES_BUSY") == "1"
+stop = []
+if busy:
+    import threading
+
+    def keep_busy():
+        with libhv_amd.Engine(0) as e2:
+            bb = e2.alloc(1 << 20)
+            while not stop:
+                e2.stream_xor(bb, 1 << 20, 0x5A5A5A5A)
+                e2.sync()
+            bb.free()
+
+    th = threading.Thread(target=keep_busy, daemon=True)
+    th.start()
+    time.sleep(0.5)
 L.hvws_set_door(None, 1)
 h = L.hvws_wsp_new()
 st = (ctypes.c_uint64 * 12)()
@@ -37,12 +55,15 @@ for i in range(n):
     assert r == 8192
     L.hvws_door_stamps(None, st)
     rows.append(list(st[:11]))
+if busy:
+    stop.append(1)
+    th.join()
 rows = np.array(rows[n // 10:], dtype=np.float64)
 t0, t1, t2, t3, t4, t5, clk, tw, tc, tp, tt = (rows[:, i] for i in range(11))
 us = lambda a, b: round(float(np.median((b - a) * 0.01)), 2)   # noqa: E731  (ticks of 10 ns)
 info = (ctypes.c_uint64 * 2)()
 L.hvws_door_info(None, info)
-out = {"reads": n, "request_in_device_memory": bool(info[0]), "door_walk": os.environ.get("HVWS_DOOR_WALK", "1"), "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
+out = {"reads": n, "busy_chip": busy, "request_in_device_memory": bool(info[0]), "door_walk": os.environ.get("HVWS_DOOR_WALK", "1"), "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
        "device_us_median": {"request_read": us(t0, t5), "stage": us(t5, t1), "carried_in_frame": us(t1, tw),
                             "walk": us(tw, t2),
                             "walk_parts": {"chase": us(tw, tc), "parse": us(tc, tp), "tail": us(tp, tt),
