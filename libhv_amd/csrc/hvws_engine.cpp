@@ -1378,6 +1378,7 @@ uint8_t* door_din(hvws_ctx* c) {
 
 int door_ensure(hvws_ctx* c) {
     if (c->door_stream) return HVWS_OK;
+    HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
     hipDeviceProp_t prop;
     HIP_OR(hipGetDeviceProperties(&prop, c->device), HVWS_EHIP);
     // A CU-masked stream gets a hardware queue of its own instead of sharing
@@ -1449,6 +1450,7 @@ int door_call(hvws_ctx* c) {
         if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
         if (!c->door_live) {
             if (launches++ >= 4) return set_err(HVWS_EHIP, "k_door: the worker takes no requests");
+            HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
             __atomic_store_n(&b->alive, 1ull, __ATOMIC_RELAXED);
             ++c->door_epoch;
             const ddoor* dreq = c->d_door_req ? (const ddoor*)c->d_door_req : mapped<ddoor>(c->h_door);
@@ -2825,8 +2827,8 @@ char* pinned_stage(uint64_t bytes) {
 void gpu_xor_host(char* dst, const char* src, size_t n, uint32_t key, uint32_t phase) {
     if (n == 0) return;
     hvws_ctx* c = thread_ctx();
+    if (door_xor(c, dst, src, n, key, phase)) return;   // no HIP call on the worker's path
     if (hipSetDevice(c->device) != hipSuccess) fatal("hipSetDevice");
-    if (door_xor(c, dst, src, n, key, phase)) return;
     if (c->xor_stage.ensure(n + 64) != hipSuccess) fatal("device staging allocation");
     uint8_t* d = c->xor_stage.as<uint8_t>();
     if (hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
@@ -2843,8 +2845,8 @@ void gpu_xor_host(char* dst, const char* src, size_t n, uint32_t key, uint32_t p
 void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask, std::vector<hvws_frame>& frames,
               websocket_parser& carry_out, int& started) {
     hvws_ctx* c = thread_ctx();
+    if (door_feed(c, buf, len, carry, unmask, frames, carry_out, started)) return;   // no HIP call there
     if (hipSetDevice(c->device) != hipSuccess) fatal("hipSetDevice");
-    if (door_feed(c, buf, len, carry, unmask, frames, carry_out, started)) return;
     hvws_segment seg = {0, (uint64_t)len};
     websocket_parser cin;
     copy_parser(cin, carry);

@@ -1326,36 +1326,41 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             }
             const uint64_t n = s_n;
             auto rec = [&](uint64_t i) -> drec { return i < SMALL_LREC ? lrec[i] : d_slot[i]; };
-            // every chunk of the read goes to dout (a separate area when the
-            // request came through device memory): masked bytes XORed
-            for (uint64_t c = (uint64_t)tid * 16u; c < L && s_unmask; c += (uint64_t)kDoorThreads * 16u) {
-                uint64_t mlo = 0, mhi = 0;
-                if (s_unmask && n) {
-                    uint64_t k = 0, k_end = n;   // first record whose payload ends after c
-                    while (k < k_end) {
-                        const uint64_t mid = (k + k_end) >> 1;
-                        const drec m = rec(mid);
-                        if (m.pay_off + m.pay_len > c) k_end = mid;
-                        else k = mid + 1;
-                    }
-                    for (; k < n; ++k) {
-                        const drec f = rec(k);
-                        if (f.pay_off >= c + 16) break;
-                        if (!(f.info & F_MASK) || f.pay_len == 0) continue;
-                        const uint32_t phase = (f.info >> 8) & 3u;
+            // Unmask in LDS record by record (waves take records in turn, a
+            // wave's lanes a record's 16-byte chunks): no per-chunk search of
+            // the records.  A chunk inside one payload belongs to that record
+            // alone (plain read-modify-write); a payload's first and last
+            // chunks may hold another record's bytes too (LDS atomic XOR per
+            // dword).  Then every chunk of the read goes to dout.
+            if (s_unmask) {
+                uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+                const uint32_t wave = tid >> 6, lane = tid & 63u;
+                for (uint64_t k = wave; k < n; k += kDoorThreads / 64u) {
+                    const drec f = rec(k);
+                    if (!(f.info & F_MASK) || f.pay_len == 0) continue;
+                    const uint64_t pe = f.pay_off + f.pay_len;
+                    const uint32_t phase = (f.info >> 8) & 3u;
+                    for (uint64_t c = (f.pay_off & ~15ull) + (uint64_t)lane * 16u; c < pe; c += 64u * 16u) {
                         const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + c - f.pay_off) & 3u));
-                        const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
-                        const int64_t a = (int64_t)(f.pay_off > c ? f.pay_off - c : 0);
-                        const uint64_t pe = f.pay_off + f.pay_len;
-                        const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
-                        mlo |= kk & byte_range(a, e);
-                        mhi |= kk & byte_range(a - 8, e - 8);
-                        if (e == 16) break;   // this payload runs past the chunk
+                        if (c >= f.pay_off && c + 16 <= pe) {
+                            u32x4* q = reinterpret_cast<u32x4*>(lds + c);
+                            *q = *q ^ u32x4{kw, kw, kw, kw};
+                        } else {
+                            const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                            const int64_t a = (int64_t)(f.pay_off > c ? f.pay_off - c : 0);
+                            const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
+                            const uint64_t mlo = kk & byte_range(a, e), mhi = kk & byte_range(a - 8, e - 8);
+                            const uint32_t m[4] = {(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi,
+                                                   (uint32_t)(mhi >> 32)};
+#pragma unroll
+                            for (int d = 0; d < 4; ++d)
+                                if (m[d]) atomicXor(l32 + c / 4 + d, m[d]);
+                        }
                     }
                 }
-                if (!(mlo | mhi) && din == dout) continue;   // no masked byte here: the data area already holds it
-                const u32x4 m4 = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
-                *reinterpret_cast<u32x4*>(dout + c) = *reinterpret_cast<const u32x4*>(lds + c) ^ m4;
+                __syncthreads();
+                for (uint64_t c = (uint64_t)tid * 16u; c < L; c += (uint64_t)kDoorThreads * 16u)
+                    *reinterpret_cast<u32x4*>(dout + c) = *reinterpret_cast<const u32x4*>(lds + c);
             }
             if (tid == 0) s_t[3] = wall_clock64();
             for (uint64_t i = tid; i < n; i += kDoorThreads) h_rec[i] = rec(i);

@@ -740,24 +740,24 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // (profiles/): 256 x 2 linear reaches the copy ceiling; larger
 // tiles lose occupancy to the boundary-tile registers, and the XCD-contiguous
 // order that helps the in-place unmask halves this out-of-place stream.
-// Stage-first (index 0 vs 6, profiles/r1an_raw): c2 0.64 -> 0.60 ms, c3
+// Stage-first (index 0 vs 4, profiles/r1an_raw): c2 0.64 -> 0.60 ms, c3
 // 20.93 -> 20.50 ms.
+// Round 4: the 4 and 8 chunk variants (16 and 32 KiB tiles) are gone: with
+// span-staged boundary tiles the 16 KiB one ran 0.71 against 0.53 ms at the c2
+// shape (profiles/r4d_raw), and both had lost before.
 #define HVWS_BUILD_GEOMS(X)       \
     X(0, 2, false, false, true)   \
-    X(1, 4, false, false, false)  \
-    X(2, 1, false, false, false)  \
-    X(3, 2, true, false, false)   \
-    X(4, 2, false, true, false)   \
-    X(5, 8, false, false, false)  \
-    X(6, 2, false, false, false)  \
-    X(7, 4, false, false, true)
+    X(1, 1, false, false, false)  \
+    X(2, 2, true, false, false)   \
+    X(3, 2, false, true, false)   \
+    X(4, 2, false, false, false)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 8) ? x : 0;
+        return (x >= 0 && x < 5) ? x : 0;
     }();
     return v;
 }
