@@ -1034,6 +1034,29 @@ __device__ __forceinline__ void door_size(const uint32_t* l, uint32_t q, uint32_
     }
 }
 
+// k_door's flags (launch_door reads them from the environment once)
+constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames (HVWS_DOOR_WALK, default on)
+constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (HVWS_DOOR_NT)
+constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (HVWS_DOOR_PRELOAD)
+
+// Chunks [c_lo, c_hi) of the data area (both multiples of 64) into LDS at the
+// same offsets by LDS-DMA: no registers (an array of 16-byte values per
+// thread cost the worker ~1000 register moves, ~2 us per read); a wave
+// writes 64 consecutive chunks per instruction (lane-linear destination).
+// The caller waits for vmcnt(0) before a barrier.
+__device__ __forceinline__ void door_stage(const uint8_t* din, uint8_t* lds, uint32_t c_lo, uint32_t c_hi,
+                                           uint32_t flags) {
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t cb = c_lo + wave * 64u; cb < c_hi; cb += kDoorThreads) {
+        const auto* g = (const __attribute__((address_space(1))) void*)(din + (uint64_t)(cb + lane) * 16u);
+        auto* l = (__attribute__((address_space(3))) void*)(lds + (uint64_t)cb * 16u);
+        if (flags & DOOR_F_NT)
+            __builtin_amdgcn_global_load_lds(g, l, 16, 0, 2);
+        else
+            __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+    }
+}
+
 template <typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
                                           uint32_t vmask, uint32_t* s_fpos, uint64_t* stamps, Emit&& emit) {
@@ -1169,7 +1192,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                                                        const uint8_t* __restrict__ din, uint8_t* __restrict__ dout,
                                                        drec* __restrict__ h_rec, drec* __restrict__ d_slot,
                                                        uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch,
-                                                       uint32_t walk) {
+                                                       uint32_t flags) {
     extern __shared__ u32x4 lds_door[];
     __shared__ drec lrec[SMALL_LREC];
     __shared__ uint64_t s_seq, s_len, s_n;
@@ -1179,7 +1202,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     uint8_t* lds = reinterpret_cast<uint8_t*>(lds_door);
     uint64_t last = first_seq;
     uint64_t served = 0;
-    __shared__ uint64_t s_t[6], s_m[2];
+    const uint32_t walk = flags & DOOR_F_WALK;
+    // DOOR_F_PRELOAD: the first chunks of the data area are loaded in the
+    // request's own round trip, as many as the previous request had (up to one
+    // per thread); the data area follows the request block in device memory.
+    uint32_t guess = 0;
+    __shared__ uint64_t s_t[7], s_m[2];
     __shared__ uint64_t s_req[16];
     __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
     __shared__ uint64_t s_w[3];               // door_walk's stamps
@@ -1216,6 +1244,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             if (tid == 0) __hip_atomic_store(&box->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
+        if (guess) door_stage(din, lds, 0, guess, flags);   // beside the request's own load
         if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
             const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(req) + tid);
             reinterpret_cast<u32x4*>(s_req)[tid] = piece;
@@ -1250,39 +1279,20 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         }
         const uint64_t L = s_len;
         const uint64_t nch = (L + 15u) / 16u;   // the data area has slack past L: whole chunks throughout
+        const uint32_t ngr = (uint32_t)((nch + 63u) & ~63ull);   // whole wave groups of 64 chunks (<= kDoorMax)
+        // the rest of the data area into LDS (all in flight), then wait
+        door_stage(din, lds, guess, ngr, flags);
+        if (flags & DOOR_F_PRELOAD) guess = ngr < kDoorThreads ? ngr : kDoorThreads;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (op == DOOR_XOR) {
             // websocket_decode over the data area (16-byte aligned): byte i
             // uses mask[(i + phase) & 3]
+            __syncthreads();
             const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
             const u32x4 k4 = u32x4{kw, kw, kw, kw};
-            constexpr int XB = (int)(kDoorMax / 16u / kDoorThreads);
-            u32x4 v[XB];
-#pragma unroll
-            for (int u = 0; u < XB; ++u) {
-                const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(din + c * 16u);
-            }
-#pragma unroll
-            for (int u = 0; u < XB; ++u) {
-                const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                if (c < nch) *reinterpret_cast<u32x4*>(dout + c * 16u) = v[u] ^ k4;
-            }
+            for (uint64_t c = tid; c < nch; c += kDoorThreads)
+                *reinterpret_cast<u32x4*>(dout + c * 16u) = *reinterpret_cast<const u32x4*>(lds + c * 16u) ^ k4;
         } else {
-            // stage the segment in LDS: every chunk's load in flight at once
-            {
-                constexpr int SB = (int)(kDoorMax / 16u / kDoorThreads);
-                u32x4 v[SB];
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                    if (c < nch) v[u] = *reinterpret_cast<const u32x4*>(din + c * 16u);
-                }
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const uint64_t c = (uint64_t)u * kDoorThreads + tid;
-                    if (c < nch) *reinterpret_cast<u32x4*>(lds + c * 16u) = v[u];
-                }
-            }
             __syncthreads();
             if (tid == 0) s_t[1] = wall_clock64();
             if (tid < 64) {   // wave 0: carried-in frame, walk, tail (k_small's code)
@@ -1325,7 +1335,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 s_m[1] = __builtin_amdgcn_s_memtime();
             }
             const uint64_t n = s_n;
-            auto rec = [&](uint64_t i) -> drec { return i < SMALL_LREC ? lrec[i] : d_slot[i]; };
+            // records [0, nl) sit in LDS, the rest in d_slot: separate loops,
+            // so LDS records are read with ds loads (a select between the two
+            // pointers compiled to flat loads waiting on both counters)
+            const uint64_t nl = n < SMALL_LREC ? n : SMALL_LREC;
             // Unmask in LDS record by record (waves take records in turn, a
             // wave's lanes a record's 16-byte chunks): no per-chunk search of
             // the records.  A chunk inside one payload belongs to that record
@@ -1335,9 +1348,8 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             if (s_unmask) {
                 uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
                 const uint32_t wave = tid >> 6, lane = tid & 63u;
-                for (uint64_t k = wave; k < n; k += kDoorThreads / 64u) {
-                    const drec f = rec(k);
-                    if (!(f.info & F_MASK) || f.pay_len == 0) continue;
+                auto unmask_rec = [&](const drec& f) {
+                    if (!(f.info & F_MASK) || f.pay_len == 0) return;
                     const uint64_t pe = f.pay_off + f.pay_len;
                     const uint32_t phase = (f.info >> 8) & 3u;
                     for (uint64_t c = (f.pay_off & ~15ull) + (uint64_t)lane * 16u; c < pe; c += 64u * 16u) {
@@ -1357,13 +1369,19 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                                 if (m[d]) atomicXor(l32 + c / 4 + d, m[d]);
                         }
                     }
-                }
+                };
+                for (uint64_t k = wave; k < nl; k += kDoorThreads / 64u) unmask_rec(lrec[k]);
+                for (uint64_t k = nl + wave; k < n; k += kDoorThreads / 64u) unmask_rec(d_slot[k]);
                 __syncthreads();
+                if (tid == 0) s_t[6] = wall_clock64();
                 for (uint64_t c = (uint64_t)tid * 16u; c < L; c += (uint64_t)kDoorThreads * 16u)
                     *reinterpret_cast<u32x4*>(dout + c) = *reinterpret_cast<const u32x4*>(lds + c);
+            } else if (tid == 0) {
+                s_t[6] = s_t[2];
             }
             if (tid == 0) s_t[3] = wall_clock64();
-            for (uint64_t i = tid; i < n; i += kDoorThreads) h_rec[i] = rec(i);
+            for (uint64_t i = tid; i < nl; i += kDoorThreads) h_rec[i] = lrec[i];
+            for (uint64_t i = nl + tid; i < n; i += kDoorThreads) h_rec[i] = d_slot[i];
             if (tid == 0) {
                 box->count = n;
                 box->out = s_carry;
@@ -1379,6 +1397,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 box->stamp[8] = s_w[0];
                 box->stamp[9] = s_w[1];
                 box->stamp[10] = s_w[2];
+                box->stamp[11] = s_t[6];           // the XOR's barrier: stores to dout start
             }
         }
         // every thread's stores reach host memory before `done` says so
@@ -1392,9 +1411,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
 hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
                        uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st) {
     // $HVWS_DOOR_WALK=0: the speculative wave-wide walk (k_small's) instead of door_walk
-    static const uint32_t walk = getenv("HVWS_DOOR_WALK") ? (uint32_t)atoi(getenv("HVWS_DOOR_WALK")) : 1u;
+    auto knob = [](const char* name, uint32_t dflt) { return getenv(name) ? (uint32_t)atoi(getenv(name)) : dflt; };
+    static const uint32_t flags = (knob("HVWS_DOOR_WALK", 1) ? DOOR_F_WALK : 0u) |
+                                  (knob("HVWS_DOOR_NT", 0) ? DOOR_F_NT : 0u) |
+                                  (knob("HVWS_DOOR_PRELOAD", 0) ? DOOR_F_PRELOAD : 0u);
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
-                       idle_ticks, first_seq, epoch, walk);
+                       idle_ticks, first_seq, epoch, flags);
     return hipGetLastError();
 }
 

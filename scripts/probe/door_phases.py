@@ -54,12 +54,12 @@ for i in range(n):
     wall.append(time.perf_counter() - t)
     assert r == 8192
     L.hvws_door_stamps(None, st)
-    rows.append(list(st[:11]))
+    rows.append(list(st[:12]))
 if busy:
     stop.append(1)
     th.join()
 rows = np.array(rows[n // 10:], dtype=np.float64)
-t0, t1, t2, t3, t4, t5, clk, tw, tc, tp, tt = (rows[:, i] for i in range(11))
+t0, t1, t2, t3, t4, t5, clk, tw, tc, tp, tt, tx = (rows[:, i] for i in range(12))
 us = lambda a, b: round(float(np.median((b - a) * 0.01)), 2)   # noqa: E731  (ticks of 10 ns)
 info = (ctypes.c_uint64 * 2)()
 L.hvws_door_info(None, info)
@@ -68,7 +68,8 @@ out = {"reads": n, "busy_chip": busy, "request_in_device_memory": bool(info[0]),
                             "walk": us(tw, t2),
                             "walk_parts": {"chase": us(tw, tc), "parse": us(tc, tp), "tail": us(tp, tt),
                                            "to_barrier": us(tt, t2)},
-                            "xor_and_stores": us(t2, t3), "records": us(t3, t4)},
+                            "xor_and_stores": us(t2, t3), "xor_parts": {"xor": us(t2, tx), "stores": us(tx, t3)},
+                            "records": us(t3, t4)},
        "device_us_total_median": us(t0, t4),
        "shader_clock_MHz_median": round(float(np.median(clk / ((t2 - t5) * 0.01))), 1)}
 print(json.dumps(out))
