@@ -60,9 +60,9 @@ def parse():
     ap.add_argument("--feed-conns", type=int, default=1024,
                     help="event-loop leg: connections per poll iteration (0: skip)")
     ap.add_argument("--feed-iters", type=int, default=20, help="event-loop leg: poll iterations (8 KiB reads each)")
-    ap.add_argument("--dropin-reads", type=int, default=0,
-                    help="drop-in leg: FeedRecvData calls per pass, one 8 KiB read each (0: skip; "
-                         "scripts/bench_dropin.py runs it alone)")
+    ap.add_argument("--dropin-reads", type=int, default=2000,
+                    help="drop-in leg: FeedRecvData calls per pass, one 8 KiB read each, resident worker "
+                         "against a launch per call (0: skip; scripts/bench_dropin.py runs it alone)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
     ap.add_argument("--dry-run", action="store_true",
@@ -434,7 +434,8 @@ def dropin_leg(eng, device: int, seed: int, reads: int = 2000, builds: int = 400
         for impl in ("door", "launch", "ref"):
             res["feed_" + impl].append(feed_once(impl))
             res["build_" + impl].append(build_once(impl))
-    L.hvws_set_door(None, -1)
+    L.hvws_set_door(None, 0)    # the worker parks now, not after its idle time
+    L.hvws_set_door(None, -1)   # the default again (on), nothing resident
     # the leg's thread context goes now, worker and its CU-masked stream with
     # it (a process under rocprofv3 that still held such a stream at exit
     # crashed in its exit-time destructors, profiles/r3x_rocprof_c3.md)

@@ -333,12 +333,13 @@ uint64_t hvws_set_small_batch_limit(hvws_ctx* ctx, uint64_t bytes);
  * and websocket_parser_execute on a read of <= 32 KiB, websocket_decode,
  * websocket_parser_decode and a masked websocket_build_frame of <= 32 KiB --
  * are served by one workgroup (k_door) that stays on the device between
- * calls and takes requests from a mailbox in pinned host memory: no kernel
+ * calls and takes requests from a mailbox (in device memory written through
+ * the PCIe BAR on large-BAR devices, else in pinned host memory): no kernel
  * launch per call.  It runs on a stream of its own (its own hardware queue)
  * and parks itself after $HVWS_DOOR_IDLE_US (default 5000) without a
  * request; the next call relaunches it.  Context teardown, thread exit and
  * process exit park it too.  on = 1 / 0 (off: each call launches k_small, or
- * the XOR kernel, as before), -1 = default ($HVWS_DOOR, off).  ctx NULL = the
+ * the XOR kernel), -1 = default ($HVWS_DOOR, on unless set to 0).  ctx NULL = the
  * calling thread's context.  Returns the previous setting.  Results are
  * identical either way; only latency differs. */
 int hvws_set_door(hvws_ctx* ctx, int on);

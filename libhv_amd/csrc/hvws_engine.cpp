@@ -274,7 +274,7 @@ struct hvws_ctx {
     uint64_t door_seq = 0;      // last request number posted
     uint64_t door_epoch = 0;    // launches so far; the worker writes its epoch to `exited` as it ends
     std::mutex door_m;          // one caller at a time: the owning thread, a free on another thread, exit
-    int door_mode = -1;         // hvws_set_door: -1 default ($HVWS_DOOR, off), 0 off, 1 on
+    int door_mode = -1;         // hvws_set_door: -1 default ($HVWS_DOOR, on), 0 off, 1 on
     uint64_t door_launches = 0, door_calls = 0;
     // hvws_span_begin / hvws_span_end: a timed region's begin and end markers
     // on both of the context's compute streams
@@ -1344,7 +1344,7 @@ uint64_t door_idle_ticks() { return door_idle_us() * 100; }
 
 bool door_on(hvws_ctx* c) {
     if (c->door_mode >= 0) return c->door_mode != 0;
-    static const int env = getenv("HVWS_DOOR") ? atoi(getenv("HVWS_DOOR")) : 0;
+    static const int env = getenv("HVWS_DOOR") ? atoi(getenv("HVWS_DOOR")) : 1;   // on by default (round 4)
     return env != 0;
 }
 

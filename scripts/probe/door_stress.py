@@ -39,7 +39,7 @@ with libhv_amd.Engine(0) as eng:
             for i in range(200):
                 assert L.hvws_wsp_feed(h, ctypes.addressof(buf) + (i % 400) * 8192, 8192) == 8192
             L.hvws_wsp_free(h)
-        L.hvws_set_door(None, 0 if r % 2 else -1)
+        L.hvws_set_door(None, 0 if r % 2 else 1)
         t1 = time.perf_counter()
         pinned = L.hvws_host_alloc(eng.ctx, hbytes)
         assert L.hvws_d2h(eng.ctx, pinned, rx.ptr, hbytes) == 0

@@ -9,6 +9,7 @@ relaunching, and the resident kernel must hold up no other work."""
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 import threading
 import time
@@ -36,6 +37,23 @@ def door():
     yield L
     L.hvws_set_door(None, old)
     L.hvws_set_door_idle_us(0)
+
+
+@pytest.mark.skipif(os.environ.get("HVWS_DOOR", "1") == "0", reason="$HVWS_DOOR=0 turns the default off")
+def test_door_is_the_default():
+    """Round 4: a thread's first reference-API read goes to the resident
+    worker without hvws_set_door (a launch per call only when asked for)."""
+    def first_read():
+        L = libhv_amd.lib()
+        assert L.hvws_set_door(None, -1) == -1   # nothing set on this thread's context
+        before = _stats()
+        data = S.rand_stream(random.Random(5), 6, max_len=3000)
+        assert H.run_messages("gpu", data, [len(data)]) == H.run_messages("oracle", data, [len(data)])
+        after = _stats()
+        assert after[1] > before[1], "the read did not go to the worker"
+        L.hvws_thread_release()
+
+    _in_thread(first_read)
 
 
 def _cases(rng, n):
@@ -336,9 +354,10 @@ def test_door_bench_sequence():
                     buf = ctypes.create_string_buffer(256)
                     n = L.websocket_build_frame(buf, 0x2 | 0x10 | 0x20, key, payload, 125)
                     assert buf.raw[:n] == H.build_frames_ref([(0x32, payload, key)])
-        L.hvws_set_door(None, -1)   # default ($HVWS_DOOR unset: off) parks the worker now
+        L.hvws_set_door(None, 0)   # off parks the worker now
         st = _stats()
-        assert st[3] == 0, "the worker is still resident after hvws_set_door(-1)"
+        assert st[3] == 0, "the worker is still resident after hvws_set_door(0)"
+        L.hvws_set_door(None, -1)   # back to the default (on) without a relaunch
         L.hvws_thread_release()
 
     t0 = time.perf_counter()
