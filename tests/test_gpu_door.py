@@ -45,7 +45,7 @@ def test_door_is_the_default():
     worker without hvws_set_door (a launch per call only when asked for)."""
     def first_read():
         L = libhv_amd.lib()
-        assert L.hvws_set_door(None, -1) == -1   # nothing set on this thread's context
+        assert L.hvws_set_door(None, -1) == 1   # nothing set on this thread's context: the default, on
         before = _stats()
         data = S.rand_stream(random.Random(5), 6, max_len=3000)
         assert H.run_messages("gpu", data, [len(data)]) == H.run_messages("oracle", data, [len(data)])
