@@ -324,31 +324,45 @@ __device__ __forceinline__ void lds16(const uint8_t* a, uint32_t q, uint64_t& lo
     hi = v.z | ((uint64_t)v.w << 32);
 }
 
-template <int U, bool SWZ, bool NT, bool SF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(uint8_t* __restrict__ out, uint64_t out_len,
-                                               const uint8_t* __restrict__ pay, uint64_t plen,
-                                               const uint64_t* __restrict__ pay_off,
-                                               const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
-                                               const uint32_t* __restrict__ mask,
-                                               const uint64_t* __restrict__ out_off,
-                                               const uint64_t* __restrict__ size,
-                                               const uint32_t* __restrict__ tile_first,
-                                               const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
-                                               uint64_t ntiles) {
+// One output tile of k_build: its frame range [k_lo, k_hi) (tile_first of t
+// and t + 1) and its source span [sp_lo, sp_hi) (k_tx_spans) are loaded by the
+// caller -- per tile, or one tile ahead in the grid-stride loop.
+struct build_idx {
+    uint64_t k_lo, k_hi, sp_lo, sp_hi;
+};
+
+__device__ __forceinline__ build_idx build_load_idx(const uint32_t* __restrict__ tile_first,
+                                                    const unsigned long long* __restrict__ span, uint64_t t,
+                                                    uint64_t n) {
+    build_idx x;
+    x.sp_lo = ~0ull;
+    x.sp_hi = 0;
+    if (span) {   // loaded beside tile_first: no round trip of its own
+        x.sp_lo = span[2 * t];
+        x.sp_hi = span[2 * t + 1];
+    }
+    x.k_lo = tile_first[t];
+    x.k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
+    return x;
+}
+
+template <int U, bool NT, bool SF>
+__device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64_t out_len,
+                                           const uint8_t* __restrict__ pay, uint64_t plen,
+                                           const uint64_t* __restrict__ pay_off,
+                                           const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
+                                           const uint32_t* __restrict__ mask,
+                                           const uint64_t* __restrict__ out_off,
+                                           const uint64_t* __restrict__ size,
+                                           const unsigned long long* __restrict__ span, uint64_t n, uint64_t t,
+                                           const build_idx x) {
     constexpr uint64_t TILE = 256ull * U * 16u;
-    const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
-    uint64_t sp_lo = ~0ull, sp_hi = 0;
-    if (span) {   // loaded beside tile_first: no round trip of its own
-        sp_lo = span[2 * t];
-        sp_hi = span[2 * t + 1];
-    }
-    const uint64_t k_lo = tile_first[t];
+    const uint64_t sp_lo = x.sp_lo, sp_hi = x.sp_hi, k_lo = x.k_lo, k_hi = x.k_hi;
     // SF: both ends of the tile's frame range load together, and a tile that
     // more than one frame touches goes straight to staging (no dependent
     // load of its first frame's record to find out it is not one payload).
-    const uint64_t k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
     if (k_lo < n && base + TILE <= out_len && (!SF || k_hi == k_lo + 1)) {
         const uint32_t fl = flags[k_lo];
         const uint64_t ln = len[k_lo];
@@ -371,20 +385,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                 for (int i = 0; i < U; ++i)
                     v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * 256 + tid) * 16u));
             } else {
-                u32x4 w[U], x[U];
+                u32x4 w[U], xx[U];
 #pragma unroll
                 for (int i = 0; i < U; ++i) {
                     const u32x4* q = reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * 256 + tid) * 16u);
                     if (NT) {
                         w[i] = __builtin_nontemporal_load(q);
-                        x[i] = __builtin_nontemporal_load(q + 1);
+                        xx[i] = __builtin_nontemporal_load(q + 1);
                     } else {
                         w[i] = q[0];
-                        x[i] = q[1];
+                        xx[i] = q[1];
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < U; ++i) v[i] = funnel16(w[i], x[i], sft);
+                for (int i = 0; i < U; ++i) v[i] = funnel16(w[i], xx[i], sft);
             }
 #pragma unroll
             for (int i = 0; i < U; ++i)
@@ -545,6 +559,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
         if (c >= out_len) break;
         build_chunk(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, n, k_lo, k_hi, c);
+    }
+}
+
+// One workgroup per tile, tiles in linear or XCD-contiguous order.
+template <int U, bool SWZ, bool NT, bool SF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(
+    uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
+    const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
+    const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
+    const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
+    uint64_t ntiles) {
+    const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
+    build_one_tile<U, NT, SF>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
+                          build_load_idx(tile_first, span, t, n));
+}
+
+// Grid-stride form: a workgroup builds tiles t, t + G, t + 2G, ... and loads
+// the next tile's frame range and source span while it builds the current
+// one, so a boundary tile's chain is one dependent round trip (records and
+// payload span) instead of two.
+template <int U, bool NT, bool SF, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_build_loop(
+    uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
+    const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
+    const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
+    const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
+    uint64_t ntiles) {
+    const uint64_t G = gridDim.x;
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    build_idx cur = build_load_idx(tile_first, span, tile0 + t, n);
+    for (;;) {
+        const uint64_t tn = t + G;
+        build_idx nxt = cur;
+        if (tn < ntiles) nxt = build_load_idx(tile_first, span, tile0 + tn, n);
+        build_one_tile<U, NT, SF>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, tile0 + t,
+                              cur);
+        if (tn >= ntiles) break;
+        __syncthreads();   // the LDS of this tile is rewritten by the next
+        t = tn;
+        cur = nxt;
     }
 }
 
@@ -745,26 +800,31 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // Round 4: the 4 and 8 chunk variants (16 and 32 KiB tiles) are gone: with
 // span-staged boundary tiles the 16 KiB one ran 0.71 against 0.53 ms at the c2
 // shape (profiles/r4d_raw), and both had lost before.
-#define HVWS_BUILD_GEOMS(X)       \
-    X(0, 2, false, false, true)   \
-    X(1, 1, false, false, false)  \
-    X(2, 2, true, false, false)   \
-    X(3, 2, false, true, false)   \
-    X(4, 2, false, false, false)
+// Round 4: indices 5 and 6 are the grid-stride form (k_build_loop: the next
+// tile's frame range and span load while the current tile builds), LP = its
+// minimum waves per SIMD (8: 64 VGPRs, 5: 96).
+#define HVWS_BUILD_GEOMS(X)              \
+    X(0, 2, false, false, true, 0)       \
+    X(1, 1, false, false, false, 0)      \
+    X(2, 2, true, false, false, 0)       \
+    X(3, 2, false, true, false, 0)       \
+    X(4, 2, false, false, false, 0)      \
+    X(5, 2, false, false, true, 8)       \
+    X(6, 2, false, false, true, 5)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 5) ? x : 0;
+        return (x >= 0 && x < 7) ? x : 0;
     }();
     return v;
 }
 uint64_t build_tile(int v) {
     switch (v) {
-#define X(I, U, S, N, F) \
-    case I:              \
+#define X(I, U, S, N, F, LP) \
+    case I:                  \
         return 256ull * U * 16u;
         HVWS_BUILD_GEOMS(X)
 #undef X
@@ -775,9 +835,9 @@ uint64_t build_tile(int v) {
 
 const char* build_kernel_name() {
     switch (build_variant()) {
-#define X(I, U, S, N, F) \
-    case I:              \
-        return "k_build<" #U "," #S "," #N "," #F ">";
+#define X(I, U, S, N, F, LP) \
+    case I:                  \
+        return LP ? "k_build_loop<" #U "," #N "," #F "," #LP ">" : "k_build<" #U "," #S "," #N "," #F ">";
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
@@ -785,6 +845,26 @@ const char* build_kernel_name() {
 }
 
 uint64_t tx_tile() { return build_tile(build_variant()); }
+
+// k_build_loop's grid: every workgroup the device holds at once
+// ($HVWS_BUILD_LOOP_WGS: workgroups per CU instead of the occupancy limit)
+uint64_t build_loop_grid(int v) {
+    static uint64_t g[2] = {0, 0};
+    uint64_t& r = g[v == 6 ? 1 : 0];
+    if (!r) {
+        int dev = 0, cus = 256, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (const char* e = getenv("HVWS_BUILD_LOOP_WGS")) per = atoi(e);
+        else if ((v == 6 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_build_loop<2, false, true, 5>, 256, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_build_loop<2, false, true, 8>, 256, 0)) !=
+                 hipSuccess)
+            per = 0;
+        r = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 4);
+    }
+    return r;
+}
 
 hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
                            uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st) {
@@ -809,10 +889,15 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
         const uint64_t nt = min(per_launch, ntiles - t0);
         switch (v) {
-#define X(I, U, S, N, F)                                                                                       \
+#define X(I, U, S, N, F, LP)                                                                                   \
     case I:                                                                                                    \
-        hipLaunchKernelGGL((k_build<U, S, N, F>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off, \
-                           len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);                        \
+        if (LP)                                                                                                \
+            hipLaunchKernelGGL((k_build_loop<U, N, F, (LP ? LP : 8)>), dim3((uint32_t)min(nt, build_loop_grid(v))), dim3(256), 0, \
+                               st, out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, tile_first, sp, n, \
+                               t0, nt);                                                                        \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_build<U, S, N, F>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, \
+                               pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);           \
         break;
             HVWS_BUILD_GEOMS(X)
 #undef X
