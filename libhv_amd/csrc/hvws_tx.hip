@@ -315,6 +315,37 @@ __global__ void k_span_init(unsigned long long* __restrict__ span, uint64_t ntil
     }
 }
 
+// A boundary tile's frame in LDS (k_build's staged path, C): positions
+// relative to the tile's first output byte.  o and ps (header start and end)
+// clamp at -32 and e (payload end) into [-32, TILE + 32]: a header that ends
+// before the tile contributes no byte either way, and only min(e, chunk end)
+// is used.  q0 + (a tile-relative payload position) is that byte's offset in
+// the staged span.  len: the payload length for the header bytes.  fl's top
+// byte holds the key phase of the tile's first byte ((base - ps) mod 4).
+struct __attribute__((aligned(16))) tx_frel {
+    int32_t o, ps, e, q0;
+    uint32_t key, fl, len_lo, len_hi;
+};
+
+__device__ __forceinline__ tx_frel tx_frel_make(uint64_t o, uint64_t ps, uint64_t e, uint64_t src, uint64_t base,
+                                                uint64_t sa, uint64_t tile, uint32_t key, uint32_t fl, uint64_t ln) {
+    auto rel = [&](uint64_t x, int64_t hi) -> int32_t {
+        const int64_t r = (int64_t)(x - base);   // offsets < 2^63: no overflow in the difference
+        return (int32_t)(r < -32 ? -32 : (r > hi ? hi : r));
+    };
+    tx_frel f;
+    f.o = rel(o, (int64_t)tile + 32);
+    f.ps = rel(ps, (int64_t)tile + 32);
+    f.e = rel(e, (int64_t)tile + 32);
+    // staged byte of payload position p (tile-relative): src + (p + base - ps) - sa
+    f.q0 = (int32_t)((int64_t)(src - sa) + (int64_t)(base - ps));
+    f.key = key;
+    f.fl = (fl & 0xFFFFFFu) | ((uint32_t)((base - ps) & 3u) << 24);   // + the key phase of the tile's byte 0
+    f.len_lo = (uint32_t)ln;
+    f.len_hi = (uint32_t)(ln >> 32);
+    return f;
+}
+
 // 16 bytes at byte offset q of an LDS area (q + 32 inside it)
 __device__ __forceinline__ void lds16(const uint8_t* a, uint32_t q, uint64_t& lo, uint64_t& hi) {
     const u32x4 va = *reinterpret_cast<const u32x4*>(a + (q & ~15u));
@@ -346,7 +377,7 @@ __device__ __forceinline__ build_idx build_load_idx(const uint32_t* __restrict__
     return x;
 }
 
-template <int U, bool NT, bool SF>
+template <int U, bool NT, bool SF, bool C>
 __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64_t out_len,
                                            const uint8_t* __restrict__ pay, uint64_t plen,
                                            const uint64_t* __restrict__ pay_off,
@@ -412,6 +443,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     constexpr uint64_t SPAN_MAX = TILE + 1024;
     __shared__ uint64_t s_off[BUILD_MAXF], s_ps[BUILD_MAXF], s_end[BUILD_MAXF], s_src[BUILD_MAXF];
     __shared__ uint32_t s_key[BUILD_MAXF], s_fl[BUILD_MAXF];
+    __shared__ tx_frel s_rel[C ? BUILD_MAXF : 1];
     const uint64_t sa = sp_lo & ~15ull, sb = (sp_hi + 15) & ~15ull;   // staged source chunks [sa, sb)
     const bool staged = span && nf && nf <= BUILD_MAXF && base + TILE <= out_len &&
                         sp_lo < sp_hi && sb - sa <= SPAN_MAX && sb <= plen;
@@ -429,7 +461,18 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
             const uint32_t q = (uint32_t)i * 256u + tid;
             if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
         }
-        if (tid < nf) {
+        if (C) {
+            // one 32-byte record per frame, 32-bit fields relative to the
+            // tile (clamped where only their order matters) -- see tx_frel
+            if (tid < nf) {
+                const uint64_t k = k_lo + tid;
+                const uint32_t fl = flags[k];
+                const uint64_t ln = len[k], o = out_off[k];
+                const uint64_t ps = o + tx_hdr_len(fl, ln);
+                s_rel[tid] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mask[k] : 0u, fl,
+                                          ln);
+            }
+        } else if (tid < nf) {
             const uint64_t k = k_lo + tid;
             const uint32_t fl = flags[k];
             const uint64_t ln = len[k], o = out_off[k];
@@ -449,6 +492,52 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
         __syncthreads();
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
+        if (C) {
+            const uint32_t nf32 = (uint32_t)nf;
+#pragma unroll
+            for (int i = 0; i < U; ++i) {
+                const int32_t c = (int32_t)(((uint32_t)i * 256u + tid) * 16u);   // tile-relative
+                const int32_t ce = c + 16;
+                // first frame ending after c: a count over short ranges
+                // (independent broadcast reads), a binary search otherwise
+                uint32_t j = 0;
+                if (nf32 <= 16) {
+                    for (uint32_t m = 0; m < nf32; ++m) j += s_rel[m].e <= c ? 1u : 0u;
+                } else {
+                    uint32_t je = nf32;
+                    while (j < je) {
+                        const uint32_t mid = (j + je) >> 1;
+                        if (s_rel[mid].e > c) je = mid;
+                        else j = mid + 1;
+                    }
+                }
+                uint64_t lo = 0, hi = 0;
+                for (; j < nf32; ++j) {
+                    const tx_frel f = s_rel[j];
+                    if (f.o >= ce) break;
+                    const int32_t hb = f.o > c ? f.o : c, he = f.ps < ce ? f.ps : ce;
+                    if (hb < he) {   // header bytes
+                        uint64_t vlo, vhi;
+                        tx_hdr128(f.fl & 0xFFFFFFu, (uint64_t)f.len_lo | ((uint64_t)f.len_hi << 32), f.key, vlo, vhi);
+                        shr_bytes(vlo, vhi, (uint32_t)(hb - f.o));
+                        put_bytes(lo, hi, vlo, vhi, (uint32_t)(hb - c), (uint32_t)(he - c));
+                    }
+                    const int32_t pb = f.ps > c ? f.ps : c, pe = f.e < ce ? f.e : ce;
+                    if (pb < pe) {   // payload bytes, realigned out of the staged span
+                        uint64_t vlo, vhi;
+                        lds16(lb, (uint32_t)(f.q0 + pb), vlo, vhi);
+                        const uint32_t kw = tx_rotr(f.key, (((uint32_t)pb + (f.fl >> 24)) & 3u) * 8u);
+                        const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                        put_bytes(lo, hi, vlo ^ kk, vhi ^ kk, (uint32_t)(pb - c), (uint32_t)(pe - c));
+                    }
+                    if (f.e >= ce) break;   // the output is dense: the next frame starts at e
+                }
+                __builtin_nontemporal_store(
+                    u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                    reinterpret_cast<u32x4*>(out + base + (uint32_t)c));
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
@@ -563,7 +652,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
 }
 
 // One workgroup per tile, tiles in linear or XCD-contiguous order.
-template <int U, bool SWZ, bool NT, bool SF>
+template <int U, bool SWZ, bool NT, bool SF, bool C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(
     uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
@@ -571,37 +660,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
     uint64_t ntiles) {
     const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
-    build_one_tile<U, NT, SF>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
-                          build_load_idx(tile_first, span, t, n));
+    build_one_tile<U, NT, SF, C>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
+                                 build_load_idx(tile_first, span, t, n));
 }
 
-// Grid-stride form: a workgroup builds tiles t, t + G, t + 2G, ... and loads
-// the next tile's frame range and source span while it builds the current
-// one, so a boundary tile's chain is one dependent round trip (records and
-// payload span) instead of two.
-template <int U, bool NT, bool SF, int W>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_build_loop(
-    uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
-    const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
-    const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
-    const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
-    uint64_t ntiles) {
-    const uint64_t G = gridDim.x;
-    uint64_t t = blockIdx.x;
-    if (t >= ntiles) return;
-    build_idx cur = build_load_idx(tile_first, span, tile0 + t, n);
-    for (;;) {
-        const uint64_t tn = t + G;
-        build_idx nxt = cur;
-        if (tn < ntiles) nxt = build_load_idx(tile_first, span, tile0 + tn, n);
-        build_one_tile<U, NT, SF>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, tile0 + t,
-                              cur);
-        if (tn >= ntiles) break;
-        __syncthreads();   // the LDS of this tile is rewritten by the next
-        t = tn;
-        cur = nxt;
-    }
-}
 
 // ------------------------------------------------------------- k_build_id
 //
@@ -800,31 +862,33 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // Round 4: the 4 and 8 chunk variants (16 and 32 KiB tiles) are gone: with
 // span-staged boundary tiles the 16 KiB one ran 0.71 against 0.53 ms at the c2
 // shape (profiles/r4d_raw), and both had lost before.
-// Round 4: indices 5 and 6 are the grid-stride form (k_build_loop: the next
-// tile's frame range and span load while the current tile builds), LP = its
-// minimum waves per SIMD (8: 64 VGPRs, 5: 96).
-#define HVWS_BUILD_GEOMS(X)              \
-    X(0, 2, false, false, true, 0)       \
-    X(1, 1, false, false, false, 0)      \
-    X(2, 2, true, false, false, 0)       \
-    X(3, 2, false, true, false, 0)       \
-    X(4, 2, false, false, false, 0)      \
-    X(5, 2, false, false, true, 8)       \
-    X(6, 2, false, false, true, 5)
+// Round 4: C = boundary tiles' records kept in LDS as one 32-byte record of
+// tile-relative 32-bit fields (one round trip per frame, a linear count
+// instead of a binary search for short ranges); index 5 keeps the 64-bit
+// per-field arrays for A/B runs.  A grid-stride form that loaded the next
+// tile's frame range and span while building the current one ran 0.62-0.90
+// against 0.53 ms at the c2 shape (profiles/r4l_raw) and is gone.
+#define HVWS_BUILD_GEOMS(X)             \
+    X(0, 2, false, false, true, true)   \
+    X(1, 1, false, false, false, true)  \
+    X(2, 2, true, false, false, true)   \
+    X(3, 2, false, true, false, true)   \
+    X(4, 2, false, false, false, true)  \
+    X(5, 2, false, false, true, false)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 7) ? x : 0;
+        return (x >= 0 && x < 6) ? x : 0;
     }();
     return v;
 }
 uint64_t build_tile(int v) {
     switch (v) {
-#define X(I, U, S, N, F, LP) \
-    case I:                  \
+#define X(I, U, S, N, F, C) \
+    case I:                 \
         return 256ull * U * 16u;
         HVWS_BUILD_GEOMS(X)
 #undef X
@@ -835,9 +899,9 @@ uint64_t build_tile(int v) {
 
 const char* build_kernel_name() {
     switch (build_variant()) {
-#define X(I, U, S, N, F, LP) \
-    case I:                  \
-        return LP ? "k_build_loop<" #U "," #N "," #F "," #LP ">" : "k_build<" #U "," #S "," #N "," #F ">";
+#define X(I, U, S, N, F, C) \
+    case I:                 \
+        return C ? "k_build<" #U "," #S "," #N "," #F ">" : "k_build<" #U "," #S "," #N "," #F ",wide>";
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
@@ -845,26 +909,6 @@ const char* build_kernel_name() {
 }
 
 uint64_t tx_tile() { return build_tile(build_variant()); }
-
-// k_build_loop's grid: every workgroup the device holds at once
-// ($HVWS_BUILD_LOOP_WGS: workgroups per CU instead of the occupancy limit)
-uint64_t build_loop_grid(int v) {
-    static uint64_t g[2] = {0, 0};
-    uint64_t& r = g[v == 6 ? 1 : 0];
-    if (!r) {
-        int dev = 0, cus = 256, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        if (const char* e = getenv("HVWS_BUILD_LOOP_WGS")) per = atoi(e);
-        else if ((v == 6 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_build_loop<2, false, true, 5>, 256, 0)
-                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_build_loop<2, false, true, 8>, 256, 0)) !=
-                 hipSuccess)
-            per = 0;
-        r = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 4);
-    }
-    return r;
-}
 
 hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
                            uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st) {
@@ -889,15 +933,10 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
         const uint64_t nt = min(per_launch, ntiles - t0);
         switch (v) {
-#define X(I, U, S, N, F, LP)                                                                                   \
+#define X(I, U, S, N, F, C)                                                                                    \
     case I:                                                                                                    \
-        if (LP)                                                                                                \
-            hipLaunchKernelGGL((k_build_loop<U, N, F, (LP ? LP : 8)>), dim3((uint32_t)min(nt, build_loop_grid(v))), dim3(256), 0, \
-                               st, out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, tile_first, sp, n, \
-                               t0, nt);                                                                        \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_build<U, S, N, F>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, \
-                               pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);           \
+        hipLaunchKernelGGL((k_build<U, S, N, F, C>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, \
+                           pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);              \
         break;
             HVWS_BUILD_GEOMS(X)
 #undef X

@@ -161,6 +161,31 @@ def test_feed_recv_data_rejects(path, seed):
     assert msgs == omsgs
 
 
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_feed_recv_data_rejected_chunk_bytes(path, seed):
+    """What a caller may rely on in a chunk FeedRecvData rejected (DESIGN sec. 7,
+    validation): the bytes before the violating header are exactly what the
+    reference leaves there (the delivered frames' payloads unmasked), the
+    violating header's own bytes are as received, and everything after it is
+    either as received or unmasked with its frames' keys -- one or the other for
+    the whole rest of the chunk (the GPU unmasks a read in one pass)."""
+    good, bad, k = _valid_then_bad(seed)
+    data = good + bad
+    L = libhv_amd.lib()
+    L.hvws_set_validation(None, V.V_ALL)
+    _, rets, _, buf = H.run_messages("gpu", data, [len(data)])
+    off = V.violations(data)[k][0]
+    b1 = data[off + 1]
+    hlen = 2 + {126: 2, 127: 8}.get(b1 & 127, 0) + (4 if b1 & 128 else 0)
+    assert rets == [off + hlen - 1]
+    _, _, _, obuf = H.run_messages("oracle", good, [len(good)])
+    assert bytes(buf[:off]) == bytes(obuf[:off])
+    assert bytes(buf[off:off + hlen]) == data[off:off + hlen]
+    _, _, _, ubuf = H.run_messages("oracle", data, [len(data)])   # the reference validates nothing
+    rest = bytes(buf[off + hlen:])
+    assert rest in (data[off + hlen:], bytes(ubuf[off + hlen:]))
+
+
 @pytest.mark.parametrize("feeder", [False, True], ids=["many", "feeder"])
 def test_batched_feed_rejects(path, feeder):
     """hvws_feed_many and a feeder (whose worker context takes the creating
