@@ -1349,24 +1349,32 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
                 const uint32_t wave = tid >> 6, lane = tid & 63u;
                 auto unmask_rec = [&](const drec& f) {
-                    if (!(f.info & F_MASK) || f.pay_len == 0) return;
-                    const uint64_t pe = f.pay_off + f.pay_len;
-                    const uint32_t phase = (f.info >> 8) & 3u;
-                    for (uint64_t c = (f.pay_off & ~15ull) + (uint64_t)lane * 16u; c < pe; c += 64u * 16u) {
-                        const uint32_t kw = rotr32(f.key, 8u * (uint32_t)((phase + c - f.pay_off) & 3u));
-                        if (c >= f.pay_off && c + 16 <= pe) {
-                            u32x4* q = reinterpret_cast<u32x4*>(lds + c);
-                            *q = *q ^ u32x4{kw, kw, kw, kw};
-                        } else {
-                            const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
-                            const int64_t a = (int64_t)(f.pay_off > c ? f.pay_off - c : 0);
-                            const int64_t e = (int64_t)(pe < c + 16 ? pe - c : 16);
-                            const uint64_t mlo = kk & byte_range(a, e), mhi = kk & byte_range(a - 8, e - 8);
-                            const uint32_t m[4] = {(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi,
-                                                   (uint32_t)(mhi >> 32)};
+                    // 32-bit: offsets inside one read.  Chunks start at
+                    // multiples of 16, so one key word serves every chunk.
+                    const uint32_t po = (uint32_t)f.pay_off, pl = (uint32_t)f.pay_len, info = f.info;
+                    if (!(info & F_MASK) || pl == 0) return;
+                    const uint32_t pe = po + pl;
+                    const uint32_t kw = rotr32(f.key, 8u * ((((info >> 8) & 3u) - po) & 3u));
+                    const uint32_t cf = (po + 15u) & ~15u, cl = pe & ~15u;   // whole chunks [cf, cl)
+                    for (uint32_t c = cf + lane * 16u; c < cl; c += 64u * 16u) {
+                        u32x4* q = reinterpret_cast<u32x4*>(lds + c);
+                        *q = *q ^ u32x4{kw, kw, kw, kw};
+                    }
+                    // the partial chunks at either end (they may hold another
+                    // record's bytes): lane 0 the first, lane 1 the last
+                    const uint32_t c0 = po & ~15u;
+                    const bool head = (po & 15u) != 0, tail = (pe & 15u) != 0 && cl >= cf;
+                    if ((lane == 0 && head) || (lane == 1 && tail)) {
+                        const uint32_t cc = lane == 0 ? c0 : cl;
+                        const int32_t a = lane == 0 ? (int32_t)(po - c0) : 0;
+                        const int32_t e = (lane == 0 && cl < cf) ? (int32_t)(pe - c0) : (lane == 0 ? 16 : (int32_t)(pe - cl));
 #pragma unroll
-                            for (int d = 0; d < 4; ++d)
-                                if (m[d]) atomicXor(l32 + c / 4 + d, m[d]);
+                        for (int d = 0; d < 4; ++d) {
+                            const int32_t lo = a - 4 * d < 0 ? 0 : (a - 4 * d), hi = e - 4 * d > 4 ? 4 : (e - 4 * d);
+                            if (hi > lo) {
+                                const uint32_t m = (hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+                                atomicXor(l32 + cc / 4u + (uint32_t)d, kw & m);
+                            }
                         }
                     }
                 };
