@@ -241,7 +241,7 @@ struct hvws_ctx {
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat, tx_span;
     hbuf h_tx;
     bool ev_build = false;
-    int tx_path = 0;   // last hvws_build_frames: 0 k_build, 1 k_build_id (same-offset layout)
+    int tx_path = 0;   // last hvws_build_frames: 0 k_build, 1 k_build_id (same-offset layout), 2 k_build_uni
     // last scan
     uint32_t nseg = 0;
     uint64_t nfr = 0;
@@ -271,6 +271,7 @@ struct hvws_ctx {
     // request and its bytes go through the pinned box and data area (round 3).
     void* d_door_req = nullptr;
     bool door_live = false;     // launched and not yet seen to have ended
+    bool door_wedged = false;   // its stream stayed busy past every bound: stream and mailbox are left alone
     uint64_t door_seq = 0;      // last request number posted
     uint64_t door_epoch = 0;    // launches so far; the worker writes its epoch to `exited` as it ends
     std::mutex door_m;          // one caller at a time: the owning thread, a free on another thread, exit
@@ -1427,6 +1428,37 @@ uint64_t door_word(const hvws_ctx* c, const uint64_t& w) {
     return __atomic_load_n(&w, __ATOMIC_ACQUIRE);
 }
 
+// Wait up to `ms` for the worker stream to drain (hipStreamQuery, never an
+// unbounded hipStreamSynchronize: a worker that never ends must not hang its
+// host thread).  On a timeout the mailbox state goes to stderr and the
+// context is marked wedged: its stream and mailbox are never reused or freed.
+bool door_drain(hvws_ctx* c, int ms, const char* where) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(c->door_stream);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            set_err(HVWS_EHIP, "k_door: %s", hipGetErrorString(q));
+            return true;   // the stream failed: nothing of the worker runs any more
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms)) break;
+        usleep(20);
+    }
+    const ddoor* b = c->h_door.as<ddoor>();
+    const ddoor* rq = door_req(c);
+    fprintf(stderr,
+            "[hvws] k_door (%s): ctx %p worker stream still busy after %d ms: seq %llu done %llu alive %llu "
+            "exited %llu epoch %llu served %llu live %d\n",
+            where, (void*)c, ms, (unsigned long long)__atomic_load_n(&rq->seq, __ATOMIC_ACQUIRE),
+            (unsigned long long)door_word(c, b->done), (unsigned long long)door_word(c, b->alive),
+            (unsigned long long)door_word(c, b->exited), (unsigned long long)c->door_epoch,
+            (unsigned long long)door_word(c, b->served), (int)c->door_live);
+    c->door_wedged = true;
+    set_err(HVWS_EHIP, "k_door: the worker stream did not drain (%s)", where);
+    return false;
+}
+
 // Post the request already written into the mailbox and wait for it (the
 // caller holds c->door_m).  A worker is (re)launched when none is resident.
 // Whether the resident one has ended is read from the mailbox only: its last
@@ -1449,6 +1481,7 @@ int door_call(hvws_ctx* c) {
     for (;;) {
         if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
         if (!c->door_live) {
+            if (c->door_wedged) return set_err(HVWS_EHIP, "k_door: the worker stream is wedged");
             if (launches++ >= 4) return set_err(HVWS_EHIP, "k_door: the worker takes no requests");
             HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
             __atomic_store_n(&b->alive, 1ull, __ATOMIC_RELAXED);
@@ -1468,7 +1501,7 @@ int door_call(hvws_ctx* c) {
             // request.  The stream drains (the wave retires) before the next
             // launch, so two workers never share the mailbox.
             if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
-            HIP_OR(hipStreamSynchronize(c->door_stream), HVWS_EHIP);
+            if (!door_drain(c, 5000, "relaunch")) return HVWS_EHIP;
             c->door_live = false;
             continue;
         }
@@ -1503,8 +1536,7 @@ void door_park(hvws_ctx* c) {
                 __builtin_ia32_pause();
         }
     }
-    hipStreamSynchronize(c->door_stream);
-    c->door_live = false;
+    if (door_drain(c, 5000, "park")) c->door_live = false;
 }
 
 // The calling thread's context for the reference-API entry points.
@@ -1569,7 +1601,16 @@ void door_release(hvws_ctx* c) {
         g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
         g_door_count.store((int)g_doors.size(), std::memory_order_release);
     }
-    hipStreamSynchronize(c->door_stream);
+    if (c->door_wedged || !door_drain(c, 5000, "release")) {
+        // a worker that may still run: its stream and the memory it writes stay
+        fprintf(stderr, "[hvws] k_door: ctx %p released with its worker stream wedged; stream and mailbox leaked\n",
+                (void*)c);
+        c->door_stream = nullptr;
+        c->h_door.p = c->h_door_data.p = c->h_door_rec.p = nullptr;
+        c->d_door_slot.p = nullptr;
+        c->d_door_req = nullptr;
+        return;
+    }
     hipStreamDestroy(c->door_stream);
     c->door_stream = nullptr;
     c->h_door.release();
@@ -2502,22 +2543,23 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     const uint64_t nb = (n + 1023) / 1024;
     HIP_OR(c->tx_size.ensure(n * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->tx_scan.ensure((4 * nb + 64) * 8), HVWS_ENOMEM);
-    HIP_OR(c->tx_stat.ensure(24), HVWS_ENOMEM);
-    HIP_OR(c->h_tx.ensure(24), HVWS_ENOMEM);
+    HIP_OR(c->tx_stat.ensure(56), HVWS_ENOMEM);
+    HIP_OR(c->h_tx.ensure(56), HVWS_ENOMEM);
     uint64_t* off = d_out_off;
     if (!off) {
         HIP_OR(c->tx_off.ensure(n * 8 + 8), HVWS_ENOMEM);
         off = c->tx_off.as<uint64_t>();
     }
-    // [0] total bytes, [1] payload ranges out of bounds, [2] payloads not at their output offset
+    // [0] total bytes, [1] payload ranges out of bounds, [2] payloads not at their output offset,
+    // [3] frames off the uniform packed layout, [4..6] frame 0's payload length, header length, payload offset
     uint64_t* stat = c->tx_stat.as<uint64_t>();
-    HIP_OR(hipMemsetAsync(stat, 0, 24, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemsetAsync(stat, 0, 56, c->stream), HVWS_EHIP);
     HIP_OR(launch_frame_sizes(d_flags, d_len, n, c->tx_size.as<uint64_t>(), c->stream), HVWS_EHIP);
     HIP_OR(launch_exclusive_scan(c->tx_size.as<uint64_t>(), off, n, c->tx_scan.as<uint64_t>(), stat, c->stream),
            HVWS_EHIP);
     HIP_OR(launch_tx_check(d_pay_off, d_len, d_flags, d_mask, off, n, payload_len, stat + 1, c->stream), HVWS_EHIP);
     uint64_t* h = c->h_tx.as<uint64_t>();
-    HIP_OR(hipMemcpyAsync(h, stat, 24, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(h, stat, 56, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (h[1]) return set_err(HVWS_EINVAL, "build_frames: %llu frames read outside the payload buffer or lack a mask",
                              (unsigned long long)h[1]);
@@ -2530,6 +2572,20 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     // ($HVWS_BUILD_ID=0 keeps the general one, for A/B runs)
     static const bool id_ok = !getenv("HVWS_BUILD_ID") || atoi(getenv("HVWS_BUILD_ID")) != 0;
     const bool same_off = id_ok && h[2] == 0 && d_payload && payload_len >= total;
+    // every frame the same size, payloads back to back: tiles know their frames
+    // and source bytes from their position ($HVWS_BUILD_UNI=0: the general path)
+    const char* uni_env = getenv("HVWS_BUILD_UNI");
+    const bool uniform = !same_off && (!uni_env || atoi(uni_env) != 0) && h[3] == 0 && d_payload && h[4] + h[5] > 0;
+    if (uniform) {
+        c->tx_path = 2;
+        HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
+        HIP_OR(launch_build_uni(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
+                                c->tx_size.as<uint64_t>(), n, h[5], h[4], h[6], c->stream),
+               HVWS_EHIP);
+        HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
+        c->ev_build = true;
+        return HVWS_OK;
+    }
     c->tx_path = same_off ? 1 : 0;
     const uint64_t tile = same_off ? tx_id_tile() : tx_tile();
     const uint64_t ntiles = (total + tile - 1) / tile;
@@ -2588,7 +2644,7 @@ const char* hvws_build_kernel_name(void) { return build_kernel_name(); }
 
 const char* hvws_last_build_kernel(hvws_ctx* c) {
     if (!c) return "";
-    return c->tx_path == 1 ? build_id_kernel_name() : build_kernel_name();
+    return c->tx_path == 1 ? build_id_kernel_name() : (c->tx_path == 2 ? build_uni_kernel_name() : build_kernel_name());
 }
 
 uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {

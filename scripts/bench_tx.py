@@ -42,7 +42,11 @@ def main():
     eng.sync()
     alg = p.payload_bytes + p.total
     pack_off = np.concatenate([[0], np.cumsum(p.length)[:-1]]).astype(np.uint64)
-    for layout, offs in (("rx_layout", p.frame_off + hdr), ("packed", pack_off)):
+    # packed: payloads back to back (every frame the same size here, so the
+    # uniform-layout kernel); packed_general: the same with $HVWS_BUILD_UNI=0
+    for layout, offs in (("rx_layout", p.frame_off + hdr), ("packed", pack_off), ("packed_general", pack_off)):
+        if layout == "packed_general":
+            os.environ["HVWS_BUILD_UNI"] = "0"
         tx = libhv_amd.TxPlan(eng, offs, p.length, p.flags, p.mask)
         ms = []
         t0 = time.perf_counter()
@@ -56,7 +60,7 @@ def main():
             ok = eng.synth(out, p.total, p.seed, dp, 1) == 0
         k = float(np.mean(ms[1:]))
         print(json.dumps({
-            "bench": "build_frames", "kernel": libhv_amd.lib().hvws_build_kernel_name().decode(), "config": name,
+            "bench": "build_frames", "kernel": libhv_amd.lib().hvws_last_build_kernel(eng.ctx).decode(), "config": name,
             "layout": layout, "frames": p.n,
             "payload_bytes": p.payload_bytes, "out_bytes": p.total, "alg_bytes_per_launch": alg,
             "kernel_ms": round(k, 3), "kernel_GBps": round(alg / k / 1e6, 1),
@@ -65,6 +69,7 @@ def main():
             "verified": ok,
         }), flush=True)
         tx.free()
+        os.environ.pop("HVWS_BUILD_UNI", None)
     # ceilings: runtime D2D copy of the same bytes, and one huge unmasked frame
     # (k_build's streaming path as a plain realigning copy)
     import ctypes

@@ -261,7 +261,12 @@ def _in_thread(fn, timeout=120):
 
     t = threading.Thread(target=run)
     t.start()
-    t.join(timeout=timeout)
+    t.join(timeout=min(timeout, 60))
+    if t.is_alive():
+        # leave the native stacks and every context's mailbox on stderr
+        L = libhv_amd.lib()
+        L.hvws_debug_backtraces(2)
+        L.hvws_debug_dump(2)
     assert not t.is_alive(), "thread did not finish"
     if err:
         raise err[0]
