@@ -1353,6 +1353,12 @@ bool door_on(hvws_ctx* c) {
 // context's door_m; nothing that holds a door_m takes g_door_m.
 std::mutex g_door_m;
 std::vector<hvws_ctx*> g_doors;
+// Drained worker streams of released contexts, per device, for the next
+// context's worker: a CU-masked stream is created once per concurrent worker
+// and never destroyed (its creation is the costliest step of a context's
+// first call, and destroying one hung a process's exit in round 3,
+// profiles/r3ab_raw).  Guarded by g_door_m.
+std::vector<std::pair<int, hipStream_t>> g_door_pool;
 std::atomic<int> g_door_count{0};   // g_doors.size(): frees skip the lock when no worker exists
 void door_atexit();
 
@@ -1413,8 +1419,15 @@ int door_ensure(hvws_ctx* c) {
         }
         (void)hipGetLastError();
     }
-    HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
     std::lock_guard<std::mutex> lk(g_door_m);
+    for (size_t i = 0; i < g_door_pool.size(); ++i)
+        if (g_door_pool[i].first == c->device) {
+            c->door_stream = g_door_pool[i].second;
+            g_door_pool.erase(g_door_pool.begin() + (long)i);
+            break;
+        }
+    if (!c->door_stream)
+        HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
     // registered after the HIP runtime's own exit handlers, so it runs before them
     static const bool reg = (atexit(door_atexit), true);
     (void)reg;
@@ -1611,7 +1624,10 @@ void door_release(hvws_ctx* c) {
         c->d_door_req = nullptr;
         return;
     }
-    hipStreamDestroy(c->door_stream);
+    {
+        std::lock_guard<std::mutex> lk(g_door_m);
+        g_door_pool.emplace_back(c->device, c->door_stream);   // drained: the next context's worker takes it
+    }
     c->door_stream = nullptr;
     c->h_door.release();
     c->h_door_data.release();

@@ -676,14 +676,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
     const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
-    uint64_t n, uint64_t tile0, uint64_t ntiles, uint64_t S, uint64_t hl, uint64_t l0, uint64_t pay0) {
+    uint64_t n, uint64_t tile0, uint64_t ntiles, uint64_t S, uint64_t hl, uint64_t l0, uint64_t pay0, double invS) {
     constexpr uint64_t TILE = 256ull * U * 16u;
     const uint64_t t = tile0 + blockIdx.x;
     const uint64_t base = t * TILE;
+    // a / S from a double-precision reciprocal, corrected by one step either
+    // way (a 64-bit integer division is a ~150-instruction dependent chain,
+    // which every tile would pay before its first load)
+    auto div = [&](uint64_t a) -> uint64_t {
+        uint64_t q = (uint64_t)((double)a * invS);
+        if (q * S > a) --q;
+        else if ((q + 1) * S <= a) ++q;
+        return q;
+    };
     build_idx x;
-    x.k_lo = base / S;                                        // the frame holding output byte base
-    x.k_hi = min((base + TILE) / S + 1, n);                   // as tile_first[t + 1] + 1
-    const uint64_t kl = min((base + TILE - 1) / S, n - 1);    // the frame holding the tile's last byte
+    x.k_lo = div(base);                                       // the frame holding output byte base
+    const uint64_t kl = min(div(base + TILE - 1), n - 1);     // the frame holding the tile's last byte
+    x.k_hi = min(div(base + TILE) + 1, n);                    // as tile_first[t + 1] + 1
     auto clampl = [&](int64_t v) -> uint64_t { return v < 0 ? 0 : ((uint64_t)v > l0 ? l0 : (uint64_t)v); };
     // payload bytes of the tile: from its first frame's piece to its last frame's
     x.sp_lo = pay0 + x.k_lo * l0 + clampl((int64_t)(base - (x.k_lo * S + hl)));
@@ -967,7 +976,7 @@ hipError_t launch_build_uni(uint8_t* out, uint64_t out_len, const uint8_t* pay, 
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
         const uint64_t nt = min(per_launch, ntiles - t0);
         hipLaunchKernelGGL((k_build_uni<2, true>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off,
-                           len, flags, mask, out_off, size, n, t0, nt, S, hl, l0, pay0);
+                           len, flags, mask, out_off, size, n, t0, nt, S, hl, l0, pay0, 1.0 / (double)S);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
