@@ -241,7 +241,7 @@ struct hvws_ctx {
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat, tx_span;
     hbuf h_tx;
     bool ev_build = false;
-    int tx_path = 0;   // last hvws_build_frames: 0 k_build, 1 k_build_id (same-offset layout), 2 k_build_uni
+    int tx_path = 0;   // last hvws_build_frames: 0 k_build, 1 k_build_id (same-offset layout)
     // last scan
     uint32_t nseg = 0;
     uint64_t nfr = 0;
@@ -1624,9 +1624,15 @@ void door_release(hvws_ctx* c) {
         c->d_door_req = nullptr;
         return;
     }
-    {
+    // drained: the next context's worker takes it ($HVWS_DOOR_POOL=0: destroy
+    // it -- a profiled program that must leave no CU-masked stream to the
+    // runtime's teardown)
+    static const bool pool = !getenv("HVWS_DOOR_POOL") || atoi(getenv("HVWS_DOOR_POOL")) != 0;
+    if (pool) {
         std::lock_guard<std::mutex> lk(g_door_m);
-        g_door_pool.emplace_back(c->device, c->door_stream);   // drained: the next context's worker takes it
+        g_door_pool.emplace_back(c->device, c->door_stream);
+    } else {
+        hipStreamDestroy(c->door_stream);
     }
     c->door_stream = nullptr;
     c->h_door.release();
@@ -2559,23 +2565,22 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     const uint64_t nb = (n + 1023) / 1024;
     HIP_OR(c->tx_size.ensure(n * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->tx_scan.ensure((4 * nb + 64) * 8), HVWS_ENOMEM);
-    HIP_OR(c->tx_stat.ensure(56), HVWS_ENOMEM);
-    HIP_OR(c->h_tx.ensure(56), HVWS_ENOMEM);
+    HIP_OR(c->tx_stat.ensure(24), HVWS_ENOMEM);
+    HIP_OR(c->h_tx.ensure(24), HVWS_ENOMEM);
     uint64_t* off = d_out_off;
     if (!off) {
         HIP_OR(c->tx_off.ensure(n * 8 + 8), HVWS_ENOMEM);
         off = c->tx_off.as<uint64_t>();
     }
-    // [0] total bytes, [1] payload ranges out of bounds, [2] payloads not at their output offset,
-    // [3] frames off the uniform packed layout, [4..6] frame 0's payload length, header length, payload offset
+    // [0] total bytes, [1] payload ranges out of bounds, [2] payloads not at their output offset
     uint64_t* stat = c->tx_stat.as<uint64_t>();
-    HIP_OR(hipMemsetAsync(stat, 0, 56, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemsetAsync(stat, 0, 24, c->stream), HVWS_EHIP);
     HIP_OR(launch_frame_sizes(d_flags, d_len, n, c->tx_size.as<uint64_t>(), c->stream), HVWS_EHIP);
     HIP_OR(launch_exclusive_scan(c->tx_size.as<uint64_t>(), off, n, c->tx_scan.as<uint64_t>(), stat, c->stream),
            HVWS_EHIP);
     HIP_OR(launch_tx_check(d_pay_off, d_len, d_flags, d_mask, off, n, payload_len, stat + 1, c->stream), HVWS_EHIP);
     uint64_t* h = c->h_tx.as<uint64_t>();
-    HIP_OR(hipMemcpyAsync(h, stat, 56, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(h, stat, 24, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (h[1]) return set_err(HVWS_EINVAL, "build_frames: %llu frames read outside the payload buffer or lack a mask",
                              (unsigned long long)h[1]);
@@ -2588,20 +2593,6 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     // ($HVWS_BUILD_ID=0 keeps the general one, for A/B runs)
     static const bool id_ok = !getenv("HVWS_BUILD_ID") || atoi(getenv("HVWS_BUILD_ID")) != 0;
     const bool same_off = id_ok && h[2] == 0 && d_payload && payload_len >= total;
-    // every frame the same size, payloads back to back: tiles know their frames
-    // and source bytes from their position ($HVWS_BUILD_UNI=0: the general path)
-    const char* uni_env = getenv("HVWS_BUILD_UNI");
-    const bool uniform = !same_off && (!uni_env || atoi(uni_env) != 0) && h[3] == 0 && d_payload && h[4] + h[5] > 0;
-    if (uniform) {
-        c->tx_path = 2;
-        HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
-        HIP_OR(launch_build_uni(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
-                                c->tx_size.as<uint64_t>(), n, h[5], h[4], h[6], c->stream),
-               HVWS_EHIP);
-        HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
-        c->ev_build = true;
-        return HVWS_OK;
-    }
     c->tx_path = same_off ? 1 : 0;
     const uint64_t tile = same_off ? tx_id_tile() : tx_tile();
     const uint64_t ntiles = (total + tile - 1) / tile;
@@ -2660,7 +2651,7 @@ const char* hvws_build_kernel_name(void) { return build_kernel_name(); }
 
 const char* hvws_last_build_kernel(hvws_ctx* c) {
     if (!c) return "";
-    return c->tx_path == 1 ? build_id_kernel_name() : (c->tx_path == 2 ? build_uni_kernel_name() : build_kernel_name());
+    return c->tx_path == 1 ? build_id_kernel_name() : build_kernel_name();
 }
 
 uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {

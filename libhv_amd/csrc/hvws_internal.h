@@ -373,10 +373,6 @@ const char* build_kernel_name();   // k_build geometry in use ($HVWS_BUILD)
 hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
                            uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st);
 // span: from launch_tx_spans, or nullptr (boundary tiles load their records first)
-const char* build_uni_kernel_name();
-hipError_t launch_build_uni(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
-                            const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                            const uint64_t* size, uint64_t n, uint64_t hl, uint64_t l0, uint64_t pay0, hipStream_t st);
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                         const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n,

@@ -665,46 +665,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 }
 
 
-// Uniform packed layout (every frame the same payload length and header
-// length, payloads back to back from pay0; k_tx_check decides): a tile's
-// frames and source span follow from its position, so the tile issues its
-// payload and record loads at once -- one round trip, like k_build_id -- with
-// no tile index and no k_tx_spans pass.  The tile is then built by the same
-// code as k_build's (stage-first; staged boundary tiles).
-template <int U, bool C>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_uni(
-    uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
-    const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
-    const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
-    uint64_t n, uint64_t tile0, uint64_t ntiles, uint64_t S, uint64_t hl, uint64_t l0, uint64_t pay0, double invS) {
-    constexpr uint64_t TILE = 256ull * U * 16u;
-    const uint64_t t = tile0 + blockIdx.x;
-    const uint64_t base = t * TILE;
-    // a / S from a double-precision reciprocal, corrected by one step either
-    // way (a 64-bit integer division is a ~150-instruction dependent chain,
-    // which every tile would pay before its first load)
-    auto div = [&](uint64_t a) -> uint64_t {
-        uint64_t q = (uint64_t)((double)a * invS);
-        if (q * S > a) --q;
-        else if ((q + 1) * S <= a) ++q;
-        return q;
-    };
-    build_idx x;
-    x.k_lo = div(base);                                       // the frame holding output byte base
-    const uint64_t kl = min(div(base + TILE - 1), n - 1);     // the frame holding the tile's last byte
-    x.k_hi = min(div(base + TILE) + 1, n);                    // as tile_first[t + 1] + 1
-    auto clampl = [&](int64_t v) -> uint64_t { return v < 0 ? 0 : ((uint64_t)v > l0 ? l0 : (uint64_t)v); };
-    // payload bytes of the tile: from its first frame's piece to its last frame's
-    x.sp_lo = pay0 + x.k_lo * l0 + clampl((int64_t)(base - (x.k_lo * S + hl)));
-    x.sp_hi = pay0 + kl * l0 + clampl((int64_t)(base + TILE - (kl * S + hl)));
-    if (x.sp_lo >= x.sp_hi) {   // no payload byte in the tile: the records-first path
-        x.sp_lo = ~0ull;
-        x.sp_hi = 0;
-    }
-    build_one_tile<U, false, true, C>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, nullptr, n, t,
-                                      x);
-}
-
 // ------------------------------------------------------------- k_build_id
 //
 // Same-offset layout: every frame's payload sits in the source buffer at the
@@ -871,29 +831,17 @@ __global__ void k_tx_check(const uint64_t* __restrict__ pay_off, const uint64_t*
                            const uint64_t* __restrict__ out_off, uint64_t n, uint64_t plen,
                            unsigned long long* __restrict__ bad) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool b = false, moved = false, odd = false;
+    bool b = false, moved = false;
     if (i < n) {
         const uint64_t o = pay_off[i], l = len[i];
-        const uint32_t hl = tx_hdr_len(flags[i], l);
         b = o > plen || l > plen - o || ((flags[i] & F_MASK) && !mask);
         // same-offset layout (k_build_id): the payload where the output puts it
-        moved = l && o != out_off[i] + hl;
-        // uniform packed layout (k_build_uni): frame 0's payload length and
-        // header length for every frame, payloads back to back from frame 0's
-        const uint64_t l0 = len[0], o0 = pay_off[0];
-        odd = l != l0 || hl != tx_hdr_len(flags[0], l0) || o != o0 + i * l0;
-        if (i == 0) {
-            bad[3] = l0;
-            bad[4] = hl;
-            bad[5] = o0;
-        }
+        moved = l && o != out_off[i] + tx_hdr_len(flags[i], l);
     }
     const uint64_t m = __ballot(b);
     if (m && (threadIdx.x & 63) == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
     const uint64_t mv = __ballot(moved);
     if (mv && (threadIdx.x & 63) == 0) atomicAdd(bad + 1, (unsigned long long)__popcll(mv));
-    const uint64_t mo = __ballot(odd);
-    if (mo && (threadIdx.x & 63) == 0) atomicAdd(bad + 2, (unsigned long long)__popcll(mo));
 }
 
 hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
@@ -919,7 +867,10 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // instead of a binary search for short ranges); index 5 keeps the 64-bit
 // per-field arrays for A/B runs.  A grid-stride form that loaded the next
 // tile's frame range and span while building the current one ran 0.62-0.90
-// against 0.53 ms at the c2 shape (profiles/r4l_raw) and is gone.
+// against 0.53 ms at the c2 shape (profiles/r4l_raw) and is gone; so is a
+// kernel for uniform packed layouts that derived each tile's frames and span
+// from its position (no index round trip): 0.60 against 0.52 ms
+// (profiles/r4o_raw, r4p_raw).
 #define HVWS_BUILD_GEOMS(X)             \
     X(0, 2, false, false, true, true)   \
     X(1, 1, false, false, false, true)  \
@@ -961,27 +912,6 @@ const char* build_kernel_name() {
 }
 
 uint64_t tx_tile() { return build_tile(build_variant()); }
-
-const char* build_uni_kernel_name() { return "k_build_uni<2>"; }
-
-hipError_t launch_build_uni(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
-                            const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                            const uint64_t* size, uint64_t n, uint64_t hl, uint64_t l0, uint64_t pay0,
-                            hipStream_t st) {
-    constexpr uint64_t tile = 256ull * 2 * 16u;
-    const uint64_t S = hl + l0;
-    if (n == 0 || S == 0) return hipErrorInvalidValue;
-    const uint64_t ntiles = (out_len + tile - 1) / tile;
-    const uint64_t per_launch = 0xFFFFFFFFull / 256;
-    for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
-        const uint64_t nt = min(per_launch, ntiles - t0);
-        hipLaunchKernelGGL((k_build_uni<2, true>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, pay_off,
-                           len, flags, mask, out_off, size, n, t0, nt, S, hl, l0, pay0, 1.0 / (double)S);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
 
 hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
                            uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st) {

@@ -42,11 +42,7 @@ def main():
     eng.sync()
     alg = p.payload_bytes + p.total
     pack_off = np.concatenate([[0], np.cumsum(p.length)[:-1]]).astype(np.uint64)
-    # packed: payloads back to back (every frame the same size here, so the
-    # uniform-layout kernel); packed_general: the same with $HVWS_BUILD_UNI=0
-    for layout, offs in (("rx_layout", p.frame_off + hdr), ("packed", pack_off), ("packed_general", pack_off)):
-        if layout == "packed_general":
-            os.environ["HVWS_BUILD_UNI"] = "0"
+    for layout, offs in (("rx_layout", p.frame_off + hdr), ("packed", pack_off)):
         tx = libhv_amd.TxPlan(eng, offs, p.length, p.flags, p.mask)
         ms = []
         t0 = time.perf_counter()
@@ -69,7 +65,6 @@ def main():
             "verified": ok,
         }), flush=True)
         tx.free()
-        os.environ.pop("HVWS_BUILD_UNI", None)
     # ceilings: runtime D2D copy of the same bytes, and one huge unmasked frame
     # (k_build's streaming path as a plain realigning copy)
     import ctypes

@@ -270,75 +270,3 @@ def test_build_boundary_tiles_span_staged(eng, spans, order, monkeypatch):
     else:
         got, _ = _gpu_build(eng, frames, gap_rng=rng if order == "gaps" else None)
     assert got == H.build_frames_ref(frames)
-
-
-@pytest.mark.parametrize("uni", ["1", "0"])
-@pytest.mark.parametrize("ln,p_mask,lead", [(1024, 1.0, 0), (1024, 0.0, 7), (1000, 1.0, 3), (0, 1.0, 0), (1, 1.0, 0),
-                                            (5, 0.0, 0), (125, 1.0, 0), (126, 1.0, 9), (4093, 1.0, 0),
-                                            (65539, 1.0, 1), (200003, 0.0, 0)])
-def test_build_uniform_packed(eng, ln, p_mask, lead, uni, monkeypatch):
-    """Every frame the same payload and header length, payloads back to back
-    (from byte `lead` of the payload buffer): k_build_uni derives each tile's
-    frames and source span from its position ($HVWS_BUILD_UNI=0: the general
-    path); FIN and opcodes still vary per frame.  Every byte against the
-    reference."""
-    monkeypatch.setenv("HVWS_BUILD_UNI", uni)
-    L = libhv_amd.lib()
-    rng = np.random.default_rng(ln * 7 + lead)
-    n = max(4, min(20000, 3_000_000 // (ln + 14)))
-    frames = _frames(rng, n, lens=[ln] * n, p_mask=p_mask)
-    pay = bytes(rng.integers(0, 256, lead, dtype=np.uint8)) + b"".join(p for _, p, _ in frames)
-    offs = [lead + i * ln for i in range(n)]
-    flags = [f for f, _, _ in frames]
-    mask = [int.from_bytes(k, "little") if k else 0 for _, _, k in frames]
-    total = int(synth.frame_size(np.array(flags, dtype=np.uint8), np.array([ln] * n, dtype=np.uint64)).sum())
-    payload = eng.to_device(np.frombuffer(pay, dtype=np.uint8)) if pay else eng.alloc(16)
-    tx = libhv_amd.TxPlan(eng, offs, [ln] * n, flags, mask)
-    out = eng.alloc(total + 64)
-    try:
-        assert eng.build_frames(out, total + 64, payload, len(pay), tx) == total
-        got = bytes(out.download(total))
-        kern = L.hvws_last_build_kernel(eng.ctx).decode()
-    finally:
-        payload.free()
-        out.free()
-        tx.free()
-    assert got == H.build_frames_ref(frames)
-    if uni == "1":
-        assert kern.startswith("k_build_uni"), kern
-    else:
-        assert not kern.startswith("k_build_uni"), kern
-
-
-def test_build_almost_uniform_takes_general_kernel(eng):
-    """One frame one byte longer (or one payload moved) breaks the uniform
-    packed layout: the general kernel, same bytes as the reference."""
-    L = libhv_amd.lib()
-    rng = np.random.default_rng(5)
-    for case in ("longer", "moved"):
-        n = 3000
-        lens = [1024] * n
-        if case == "longer":
-            lens[1777] = 1025
-        frames = _frames(rng, n, lens=lens, p_mask=1.0)
-        offs = list(np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64))
-        pay = bytearray(b"".join(p for _, p, _ in frames) + b"\0")
-        if case == "moved":   # frame 2500's payload also copied past the end, and taken from there
-            offs[2500] = len(pay)
-            pay += frames[2500][1]
-        flags = [f for f, _, _ in frames]
-        mask = [int.from_bytes(k, "little") for _, _, k in frames]
-        total = int(synth.frame_size(np.array(flags, dtype=np.uint8), np.array(lens, dtype=np.uint64)).sum())
-        payload = eng.to_device(np.frombuffer(bytes(pay), dtype=np.uint8))
-        tx = libhv_amd.TxPlan(eng, [int(o) for o in offs], lens, flags, mask)
-        out = eng.alloc(total + 64)
-        try:
-            assert eng.build_frames(out, total + 64, payload, len(pay), tx) == total
-            got = bytes(out.download(total))
-            kern = L.hvws_last_build_kernel(eng.ctx).decode()
-        finally:
-            payload.free()
-            out.free()
-            tx.free()
-        assert got == H.build_frames_ref(frames), case
-        assert not kern.startswith("k_build_uni"), (case, kern)
