@@ -515,14 +515,6 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 for (; j < nf32; ++j) {
                     const tx_frel f = s_rel[j];
                     if (f.o >= ce) break;
-                    if (C >= 2 && f.ps <= c && f.e >= ce) {   // 16 payload bytes of one frame
-                        lds16(lb, (uint32_t)(f.q0 + c), lo, hi);
-                        const uint32_t kw = tx_rotr(f.key, (((uint32_t)c + (f.fl >> 24)) & 3u) * 8u);
-                        const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
-                        lo ^= kk;
-                        hi ^= kk;
-                        break;
-                    }
                     const int32_t hb = f.o > c ? f.o : c, he = f.ps < ce ? f.ps : ce;
                     if (hb < he) {   // header bytes
                         uint64_t vlo, vhi;
@@ -870,31 +862,30 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // Round 4: the 4 and 8 chunk variants (16 and 32 KiB tiles) are gone: with
 // span-staged boundary tiles the 16 KiB one ran 0.71 against 0.53 ms at the c2
 // shape (profiles/r4d_raw), and both had lost before.
-// Round 4: C >= 1 = boundary tiles' records kept in LDS as one 32-byte record
-// of tile-relative 32-bit fields (one round trip per frame, a linear count
-// instead of a binary search for short ranges), C = 2 with a short path for
-// chunks inside one payload; index 5 keeps the 64-bit per-field arrays and
-// index 6 the compact records without the short path, for A/B runs.  A grid-stride form that loaded the next
+// Round 4: C = boundary tiles' records kept in LDS as one 32-byte record of
+// tile-relative 32-bit fields (one round trip per frame, a linear count
+// instead of a binary search for short ranges); index 5 keeps the 64-bit
+// per-field arrays for A/B runs.  A short path for chunks inside one payload
+// measured no faster (c2 0.531-0.535 against 0.527-0.529 ms, r4r_raw).  A grid-stride form that loaded the next
 // tile's frame range and span while building the current one ran 0.62-0.90
 // against 0.53 ms at the c2 shape (profiles/r4l_raw) and is gone; so is a
 // kernel for uniform packed layouts that derived each tile's frames and span
 // from its position (no index round trip): 0.60 against 0.52 ms
 // (profiles/r4o_raw, r4p_raw).
 #define HVWS_BUILD_GEOMS(X)             \
-    X(0, 2, false, false, true, 2)      \
-    X(1, 1, false, false, false, 2)     \
-    X(2, 2, true, false, false, 2)      \
-    X(3, 2, false, true, false, 2)      \
-    X(4, 2, false, false, false, 2)     \
-    X(5, 2, false, false, true, 0)      \
-    X(6, 2, false, false, true, 1)
+    X(0, 2, false, false, true, 1)      \
+    X(1, 1, false, false, false, 1)     \
+    X(2, 2, true, false, false, 1)      \
+    X(3, 2, false, true, false, 1)      \
+    X(4, 2, false, false, false, 1)     \
+    X(5, 2, false, false, true, 0)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 7) ? x : 0;
+        return (x >= 0 && x < 6) ? x : 0;
     }();
     return v;
 }
@@ -914,8 +905,7 @@ const char* build_kernel_name() {
     switch (build_variant()) {
 #define X(I, U, S, N, F, C) \
     case I:                 \
-        return C == 2 ? "k_build<" #U "," #S "," #N "," #F ">"                  \
-                      : (C ? "k_build<" #U "," #S "," #N "," #F ",compact>" : "k_build<" #U "," #S "," #N "," #F ",wide>");
+        return C ? "k_build<" #U "," #S "," #N "," #F ">" : "k_build<" #U "," #S "," #N "," #F ",wide>";
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
