@@ -1120,19 +1120,27 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             lfl = h.flags;
             llen = h.length;
         }
+        // wave-uniform lane indices: s_readlane, not an LDS-routed shuffle
         const int src = (int)((cnt - 1) & 63u);   // that lane parsed frame cnt - 1 last
-        st.flags = (uint32_t)__shfl((int)lfl, src);
-        st.length = (uint64_t)__shfl((long long)llen, src);
+        st.flags = (uint32_t)__builtin_amdgcn_readlane((int)lfl, src);
+        st.length = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)llen, src) |
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(llen >> 32), src) << 32);
         st.require = 0;
         st.offset = 0;
         st.mask_offset = (st.flags & F_MASK) ? (uint32_t)(st.length & 3u) : 0u;
         st.started = 0;
         uint32_t best = lastm, bkey = lastm_key;
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t ob = __shfl_xor(best, o), ok = __shfl_xor(bkey, o);
-            if (ob > best) {
-                best = ob;
-                bkey = ok;
+        if (cnt <= 64) {   // one frame per lane: the last masked frame is the highest lane with one
+            const unsigned long long mm = __ballot(lastm != 0);
+            best = mm ? 1u : 0u;
+            if (mm) bkey = (uint32_t)__builtin_amdgcn_readlane((int)lastm_key, 63 - __clzll((long long)mm));
+        } else {
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint32_t ob = __shfl_xor(best, o), ok = __shfl_xor(bkey, o);
+                if (ob > best) {
+                    best = ob;
+                    bkey = ok;
+                }
             }
         }
         if (best) st.mask = bkey;
@@ -1311,7 +1319,30 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     if (idx < SMALL_LREC) lrec[idx] = o;
                     else d_slot[idx] = o;
                 };
-                if (st.state != S_START) {
+                if (st.state == S_BODY && st.require > 0 && L > 0) {
+                    // the common carry, a payload that continues into this
+                    // read: scalar_frame's S_BODY step without its state
+                    // dispatch (a chain of scalar branches, ~0.5 us)
+                    const uint64_t nb = st.require < L ? st.require : L;
+                    frec r;
+                    r.hdr_off = -1;
+                    r.pay_off = 0;
+                    r.pay_len = nb;
+                    r.length = st.length;
+                    r.key = (st.flags & F_MASK) ? st.mask : 0u;
+                    r.info = (st.flags & 0xFFu) | ((st.mask_offset & 3u) << 8) | I_BODY;
+                    if (st.flags & F_MASK) st.mask_offset = (uint32_t)((st.mask_offset + nb) & 3u);
+                    st.require -= nb;
+                    pos = nb;
+                    if (st.require == 0) {
+                        st.state = S_START;
+                        r.info |= I_END;
+                    } else {
+                        st.offset += L;   // http/websocket_parser.c:153
+                    }
+                    if (tid == 0) emit(0, r);
+                    n = 1;
+                } else if (st.state != S_START) {
                     frec r;
                     if (scalar_frame(lds, L, st, pos, r, vmask)) {
                         if (tid == 0) emit(0, r);
