@@ -377,7 +377,7 @@ __device__ __forceinline__ build_idx build_load_idx(const uint32_t* __restrict__
     return x;
 }
 
-template <int U, bool NT, bool SF, int C>
+template <int T, int U, bool NT, bool SF, int C>
 __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64_t out_len,
                                            const uint8_t* __restrict__ pay, uint64_t plen,
                                            const uint64_t* __restrict__ pay_off,
@@ -387,7 +387,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                                            const uint64_t* __restrict__ size,
                                            const unsigned long long* __restrict__ span, uint64_t n, uint64_t t,
                                            const build_idx x) {
-    constexpr uint64_t TILE = 256ull * U * 16u;
+    constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
     const uint64_t sp_lo = x.sp_lo, sp_hi = x.sp_hi, k_lo = x.k_lo, k_hi = x.k_hi;
@@ -414,12 +414,12 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
             if (sft == 0) {
 #pragma unroll
                 for (int i = 0; i < U; ++i)
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * 256 + tid) * 16u));
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * T + tid) * 16u));
             } else {
                 u32x4 w[U], xx[U];
 #pragma unroll
                 for (int i = 0; i < U; ++i) {
-                    const u32x4* q = reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * 256 + tid) * 16u);
+                    const u32x4* q = reinterpret_cast<const u32x4*>(sp + ((uint64_t)i * T + tid) * 16u);
                     if (NT) {
                         w[i] = __builtin_nontemporal_load(q);
                         xx[i] = __builtin_nontemporal_load(q + 1);
@@ -433,7 +433,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
             }
 #pragma unroll
             for (int i = 0; i < U; ++i)
-                __builtin_nontemporal_store(v[i] ^ kv, reinterpret_cast<u32x4*>(out + base + ((uint64_t)i * 256 + tid) * 16u));
+                __builtin_nontemporal_store(v[i] ^ kv, reinterpret_cast<u32x4*>(out + base + ((uint64_t)i * T + tid) * 16u));
             return;
         }
     }
@@ -441,11 +441,19 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     // staged source bytes per boundary tile (LDS): the tile's payload bytes,
     // with room for gaps between payloads
     constexpr uint64_t SPAN_MAX = TILE + 1024;
-    __shared__ uint64_t s_off[BUILD_MAXF], s_ps[BUILD_MAXF], s_end[BUILD_MAXF], s_src[BUILD_MAXF];
-    __shared__ uint32_t s_key[BUILD_MAXF], s_fl[BUILD_MAXF];
-    __shared__ tx_frel s_rel[C ? BUILD_MAXF : 1];
+    // the tile's frame records, 40 bytes each: the 64-bit per-field arrays,
+    // or (C) the compact records in the same storage
+    constexpr uint32_t MAXF = T >= 128 ? BUILD_MAXF : (uint32_t)T;
+    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * 5];
+    uint64_t* const s_off = s_rb;
+    uint64_t* const s_ps = s_rb + MAXF;
+    uint64_t* const s_end = s_rb + 2 * MAXF;
+    uint64_t* const s_src = s_rb + 3 * MAXF;
+    uint32_t* const s_key = reinterpret_cast<uint32_t*>(s_rb + 4 * MAXF);
+    uint32_t* const s_fl = s_key + MAXF;
+    tx_frel* const s_rel = reinterpret_cast<tx_frel*>(s_rb);
     const uint64_t sa = sp_lo & ~15ull, sb = (sp_hi + 15) & ~15ull;   // staged source chunks [sa, sb)
-    const bool staged = nf && nf <= BUILD_MAXF && base + TILE <= out_len &&
+    const bool staged = nf && nf <= MAXF && base + TILE <= out_len &&
                         sp_lo < sp_hi && sb - sa <= SPAN_MAX && sb <= plen;
     if (staged) {
         // Boundary tile with its source span known up front: the span's
@@ -453,40 +461,42 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         // LDS, then every output chunk is assembled from LDS (header pieces
         // from the records, payload pieces realigned from the staged bytes).
         __shared__ u32x4 s_data[SPAN_MAX / 16 + 2];
-        constexpr int SPU = (int)((SPAN_MAX / 16 + 255) / 256);
+        constexpr int SPU = (int)((SPAN_MAX / 16 + T - 1) / T);
         const uint32_t nch = (uint32_t)((sb - sa) / 16);
         u32x4 d[SPU];
 #pragma unroll
         for (int i = 0; i < SPU; ++i) {
-            const uint32_t q = (uint32_t)i * 256u + tid;
+            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
             if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
         }
         if (C) {
             // one 32-byte record per frame, 32-bit fields relative to the
             // tile (clamped where only their order matters) -- see tx_frel
-            if (tid < nf) {
-                const uint64_t k = k_lo + tid;
+            for (uint32_t r = tid; r < nf; r += T) {
+                const uint64_t k = k_lo + r;
                 const uint32_t fl = flags[k];
                 const uint64_t ln = len[k], o = out_off[k];
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
-                s_rel[tid] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mask[k] : 0u, fl,
+                s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mask[k] : 0u, fl,
                                           ln);
             }
-        } else if (tid < nf) {
-            const uint64_t k = k_lo + tid;
-            const uint32_t fl = flags[k];
-            const uint64_t ln = len[k], o = out_off[k];
-            const uint64_t ps = o + tx_hdr_len(fl, ln);
-            s_off[tid] = o;
-            s_ps[tid] = ps;
-            s_end[tid] = ps + ln;
-            s_src[tid] = pay_off[k];
-            s_key[tid] = (fl & F_MASK) ? mask[k] : 0u;
-            s_fl[tid] = fl;
+        } else {
+            for (uint32_t r = tid; r < nf; r += T) {
+                const uint64_t k = k_lo + r;
+                const uint32_t fl = flags[k];
+                const uint64_t ln = len[k], o = out_off[k];
+                const uint64_t ps = o + tx_hdr_len(fl, ln);
+                s_off[r] = o;
+                s_ps[r] = ps;
+                s_end[r] = ps + ln;
+                s_src[r] = pay_off[k];
+                s_key[r] = (fl & F_MASK) ? mask[k] : 0u;
+                s_fl[r] = fl;
+            }
         }
 #pragma unroll
         for (int i = 0; i < SPU; ++i) {
-            const uint32_t q = (uint32_t)i * 256u + tid;
+            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
             if (q < nch) s_data[q] = d[i];
         }
         if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
@@ -496,7 +506,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
             const uint32_t nf32 = (uint32_t)nf;
 #pragma unroll
             for (int i = 0; i < U; ++i) {
-                const int32_t c = (int32_t)(((uint32_t)i * 256u + tid) * 16u);   // tile-relative
+                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + tid) * 16u);   // tile-relative
                 const int32_t ce = c + 16;
                 // first frame ending after c: a count over short ranges
                 // (independent broadcast reads), a binary search otherwise
@@ -540,7 +550,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
 #pragma unroll
         for (int i = 0; i < U; ++i) {
-            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
             uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
             while (j < je) {
                 const uint32_t mid = (j + je) >> 1;
@@ -572,21 +582,21 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
         return;
     }
-    if (nf && nf <= BUILD_MAXF && base + TILE <= out_len) {
+    if (nf && nf <= MAXF && base + TILE <= out_len) {
         // Boundary tile: the tile's frames staged in LDS; chunks inside one
         // payload still stream (loads issued for all U chunks first), chunks
         // holding header bytes or a frame boundary are assembled byte by byte.
-        if (tid < nf) {
-            const uint64_t k = k_lo + tid;
+        for (uint32_t r = tid; r < nf; r += T) {
+            const uint64_t k = k_lo + r;
             const uint32_t fl = flags[k];
             const uint64_t ln = len[k], o = out_off[k];
             const uint64_t ps = o + tx_hdr_len(fl, ln);
-            s_off[tid] = o;
-            s_ps[tid] = ps;
-            s_end[tid] = ps + ln;
-            s_src[tid] = pay_off[k];
-            s_key[tid] = (fl & F_MASK) ? mask[k] : 0u;
-            s_fl[tid] = fl;
+            s_off[r] = o;
+            s_ps[r] = ps;
+            s_end[r] = ps + ln;
+            s_src[r] = pay_off[k];
+            s_key[r] = (fl & F_MASK) ? mask[k] : 0u;
+            s_fl[r] = fl;
         }
         __syncthreads();
         u32x4 w[U], x[U];
@@ -594,7 +604,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         uint32_t fastmask = 0;
 #pragma unroll
         for (int i = 0; i < U; ++i) {
-            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
             uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
             while (j < je) {
                 const uint32_t mid = (j + je) >> 1;
@@ -620,7 +630,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             if (!((fastmask >> i) & 1u)) continue;
-            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
             const u32x4 v = (sft[i] ? funnel16(w[i], x[i], sft[i]) : w[i]) ^ u32x4{kw[i], kw[i], kw[i], kw[i]};
             __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
         }
@@ -628,7 +638,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
 #pragma unroll 1
         for (int i = 0; i < U; ++i) {
             if ((fastmask >> i) & 1u) continue;
-            const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
             uint32_t j = 0, je = (uint32_t)nf;
             while (j < je) {
                 const uint32_t mid = (j + je) >> 1;
@@ -645,22 +655,22 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     }
 #pragma unroll 1
     for (int i = 0; i < U; ++i) {
-        const uint64_t c = base + ((uint64_t)i * 256 + tid) * 16u;
+        const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
         if (c >= out_len) break;
         build_chunk(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, n, k_lo, k_hi, c);
     }
 }
 
 // One workgroup per tile, tiles in linear or XCD-contiguous order.
-template <int U, bool SWZ, bool NT, bool SF, int C>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(
+template <int T, int U, bool SWZ, bool NT, bool SF, int C>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(
     uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
     const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
     const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
     uint64_t ntiles) {
     const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
-    build_one_tile<U, NT, SF, C>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
+    build_one_tile<T, U, NT, SF, C>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
                                  build_load_idx(tile_first, span, t, n));
 }
 
@@ -873,27 +883,30 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // from its position (no index round trip): 0.60 against 0.52 ms
 // (profiles/r4o_raw, r4p_raw).
 #define HVWS_BUILD_GEOMS(X)             \
-    X(0, 2, false, false, true, 1)      \
-    X(1, 1, false, false, false, 1)     \
-    X(2, 2, true, false, false, 1)      \
-    X(3, 2, false, true, false, 1)      \
-    X(4, 2, false, false, false, 1)     \
-    X(5, 2, false, false, true, 0)
+    X(0, 256, 2, false, false, true, 1)   \
+    X(1, 256, 1, false, false, false, 1)  \
+    X(2, 256, 2, true, false, false, 1)   \
+    X(3, 256, 2, false, true, false, 1)   \
+    X(4, 256, 2, false, false, false, 1)  \
+    X(5, 256, 2, false, false, true, 0)   \
+    X(6, 64, 2, false, false, true, 1)    \
+    X(7, 64, 4, false, false, true, 1)    \
+    X(8, 128, 2, false, false, true, 1)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 6) ? x : 0;
+        return (x >= 0 && x < 9) ? x : 0;
     }();
     return v;
 }
 uint64_t build_tile(int v) {
     switch (v) {
-#define X(I, U, S, N, F, C) \
-    case I:                 \
-        return 256ull * U * 16u;
+#define X(I, T, U, S, N, F, C) \
+    case I:                    \
+        return (uint64_t)T * U * 16u;
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
@@ -903,9 +916,10 @@ uint64_t build_tile(int v) {
 
 const char* build_kernel_name() {
     switch (build_variant()) {
-#define X(I, U, S, N, F, C) \
-    case I:                 \
-        return C ? "k_build<" #U "," #S "," #N "," #F ">" : "k_build<" #U "," #S "," #N "," #F ",wide>";
+#define X(I, T, U, S, N, F, C) \
+    case I:                    \
+        return T == 256 ? (C ? "k_build<" #U "," #S "," #N "," #F ">" : "k_build<" #U "," #S "," #N "," #F ",wide>") \
+                        : "k_build<" #U "," #S "," #N "," #F ",t" #T ">";
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
@@ -937,9 +951,9 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
         const uint64_t nt = min(per_launch, ntiles - t0);
         switch (v) {
-#define X(I, U, S, N, F, C)                                                                                    \
+#define X(I, T, U, S, N, F, C)                                                                                 \
     case I:                                                                                                    \
-        hipLaunchKernelGGL((k_build<U, S, N, F, C>), dim3((uint32_t)nt), dim3(256), 0, st, out, out_len, pay, plen, \
+        hipLaunchKernelGGL((k_build<T, U, S, N, F, C>), dim3((uint32_t)nt), dim3(T), 0, st, out, out_len, pay, plen, \
                            pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);              \
         break;
             HVWS_BUILD_GEOMS(X)
