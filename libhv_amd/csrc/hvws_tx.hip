@@ -440,10 +440,12 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
     // staged source bytes per boundary tile (LDS): the tile's payload bytes,
     // with room for gaps between payloads
-    constexpr uint64_t SPAN_MAX = TILE + 1024;
+    constexpr uint64_t SPAN_MAX = TILE + (C == 2 ? 256 : 1024);
     // the tile's frame records, 40 bytes each: the 64-bit per-field arrays,
     // or (C) the compact records in the same storage
-    constexpr uint32_t MAXF = T >= 128 ? BUILD_MAXF : (uint32_t)T;
+    // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
+    // workgroup's LDS leaves room for 8 waves per SIMD
+    constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
     __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * 5];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
@@ -862,43 +864,33 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     return hipGetLastError();
 }
 
-// Build geometries: X(index, chunks per thread, XCD order, nontemporal
-// realigning loads, stage-first); 0 is the default.  On-device sweeps
-// (profiles/): 256 x 2 linear reaches the copy ceiling; larger
-// tiles lose occupancy to the boundary-tile registers, and the XCD-contiguous
-// order that helps the in-place unmask halves this out-of-place stream.
-// Stage-first (index 0 vs 4, profiles/r1an_raw): c2 0.64 -> 0.60 ms, c3
-// 20.93 -> 20.50 ms.
-// Round 4: the 4 and 8 chunk variants (16 and 32 KiB tiles) are gone: with
-// span-staged boundary tiles the 16 KiB one ran 0.71 against 0.53 ms at the c2
-// shape (profiles/r4d_raw), and both had lost before.
-// Round 4: C = boundary tiles' records kept in LDS as one 32-byte record of
-// tile-relative 32-bit fields (one round trip per frame, a linear count
-// instead of a binary search for short ranges); index 5 keeps the 64-bit
-// per-field arrays for A/B runs.  A short path for chunks inside one payload
-// measured no faster (c2 0.531-0.535 against 0.527-0.529 ms, r4r_raw).  A grid-stride form that loaded the next
-// tile's frame range and span while building the current one ran 0.62-0.90
-// against 0.53 ms at the c2 shape (profiles/r4l_raw) and is gone; so is a
-// kernel for uniform packed layouts that derived each tile's frames and span
-// from its position (no index round trip): 0.60 against 0.52 ms
-// (profiles/r4o_raw, r4p_raw).
-#define HVWS_BUILD_GEOMS(X)             \
-    X(0, 256, 2, false, false, true, 1)   \
-    X(1, 256, 1, false, false, false, 1)  \
-    X(2, 256, 2, true, false, false, 1)   \
-    X(3, 256, 2, false, true, false, 1)   \
-    X(4, 256, 2, false, false, false, 1)  \
-    X(5, 256, 2, false, false, true, 0)   \
-    X(6, 64, 2, false, false, true, 1)    \
-    X(7, 64, 4, false, false, true, 1)    \
-    X(8, 128, 2, false, false, true, 1)
+// Build geometries: X(index, threads per workgroup, chunks per thread, XCD
+// order, nontemporal realigning loads, stage-first, compact records); 0 is the
+// default.  History (profiles/, DESIGN.md sec. 5 "Transmit side"): 256 x 2
+// linear was the default through round 3 (stage-first: c2 0.64 -> 0.60 ms, c3
+// 20.93 -> 20.50 ms, r1an_raw); larger 256-thread tiles lost occupancy, the
+// XCD-contiguous order halved this out-of-place stream.  Round 4: compact
+// tile-relative records (r4m_raw); then one-wave workgroups with 4 KiB tiles
+// -- no staging barrier across waves, every wave's tile independent: c2
+// packed 0.52 -> 0.455 ms, c3 packed 22.4 -> 20.6 ms, c4 1.40 -> 1.30 ms
+// (r4t_raw, r4u_raw).  Tried and gone in round 4: a grid-stride form with the
+// next tile's index prefetched (r4l_raw), a position-derived index for uniform
+// layouts (r4o_raw, r4p_raw), a short path for chunks inside one payload
+// (r4r_raw).
+#define HVWS_BUILD_GEOMS(X)               \
+    X(0, 64, 4, false, false, true, 1)    \
+    X(1, 256, 2, false, false, true, 1)   \
+    X(2, 256, 2, false, false, true, 0)   \
+    X(3, 64, 2, false, false, true, 1)    \
+    X(4, 128, 2, false, false, true, 1)   \
+    X(5, 64, 4, false, false, true, 2)
 
 namespace {
 int build_variant() {
     static const int v = [] {
         const char* e = getenv("HVWS_BUILD");
         const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 9) ? x : 0;
+        return (x >= 0 && x < 6) ? x : 0;
     }();
     return v;
 }
@@ -918,8 +910,7 @@ const char* build_kernel_name() {
     switch (build_variant()) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
-        return T == 256 ? (C ? "k_build<" #U "," #S "," #N "," #F ">" : "k_build<" #U "," #S "," #N "," #F ",wide>") \
-                        : "k_build<" #U "," #S "," #N "," #F ",t" #T ">";
+        return C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
