@@ -678,6 +678,7 @@ def tx_leg(eng, plan, dp, rx, rx_plain: bool, segs, tpath: str) -> dict:
         "kernel": bname, "traffic": tx_traffic,
         "achieved": round(tx_ach, 1), "unit": "GB/s", "frac": round(tx_ach / HBM_PEAK_GBS, 4),
         "alg_bytes_per_launch": tx_alg, "kernel_ms_mean": round(float(np.mean(tms[1:])), 3),
+        "timed": "tile index + source spans + k_build (the call's device work after its size check)",
         "verified": ok,
     }
 

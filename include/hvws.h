@@ -280,16 +280,15 @@ int hvws_build_frames(hvws_ctx* ctx, uint8_t* d_out, uint64_t out_cap, const uin
                       uint64_t payload_len, const uint64_t* d_pay_off, const uint64_t* d_len,
                       const uint8_t* d_flags, const uint32_t* d_mask, uint64_t n, uint64_t* d_out_off,
                       uint64_t* out_len);
-/* Device time (ms, HIP events on the ctx stream) of the last
- * hvws_build_frames or hvws_encode_keys kernel; the build kernel's name. */
+/* Device time (ms, HIP events on the ctx stream) of the last hvws_encode_keys
+ * kernel, or of the last hvws_build_frames' device work after its size check
+ * (tile index, source spans, k_build); the default build geometry's name. */
 int hvws_last_kernel_ms(hvws_ctx* ctx, float* ms);
 const char* hvws_build_kernel_name(void);
-/* The kernel the last hvws_build_frames on ctx ran: the general k_build, or
- * k_build_id when every frame's payload sat at its output offset in the
- * payload buffer (pay_off[i] == out_off[i] + header length, e.g. a relay
- * re-framing the batch it received): then the source bytes of every output
- * chunk are known before its frames, as in the unmask.
- * Results never depend on it. */
+/* The k_build geometry the last hvws_build_frames on ctx ran: one-wave
+ * workgroups of 4 KiB tiles, in a lean-LDS form for batches of small frames
+ * (mean frame < 4 KiB), or $HVWS_BUILD's.  Results never
+ * depend on it. */
 const char* hvws_last_build_kernel(hvws_ctx* ctx);
 
 /* ---- handshake, device resident --------------------------------------- */

@@ -241,7 +241,7 @@ struct hvws_ctx {
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat, tx_span;
     hbuf h_tx;
     bool ev_build = false;
-    int tx_path = 0;   // last hvws_build_frames: 0 k_build, 1 k_build_id (same-offset layout)
+    int tx_variant = 0;   // k_build geometry of the last hvws_build_frames
     // last scan
     uint32_t nseg = 0;
     uint64_t nfr = 0;
@@ -2565,22 +2565,22 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     const uint64_t nb = (n + 1023) / 1024;
     HIP_OR(c->tx_size.ensure(n * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->tx_scan.ensure((4 * nb + 64) * 8), HVWS_ENOMEM);
-    HIP_OR(c->tx_stat.ensure(24), HVWS_ENOMEM);
-    HIP_OR(c->h_tx.ensure(24), HVWS_ENOMEM);
+    HIP_OR(c->tx_stat.ensure(16), HVWS_ENOMEM);
+    HIP_OR(c->h_tx.ensure(16), HVWS_ENOMEM);
     uint64_t* off = d_out_off;
     if (!off) {
         HIP_OR(c->tx_off.ensure(n * 8 + 8), HVWS_ENOMEM);
         off = c->tx_off.as<uint64_t>();
     }
-    // [0] total bytes, [1] payload ranges out of bounds, [2] payloads not at their output offset
+    // [0] total bytes, [1] payload ranges out of bounds
     uint64_t* stat = c->tx_stat.as<uint64_t>();
-    HIP_OR(hipMemsetAsync(stat, 0, 24, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemsetAsync(stat, 0, 16, c->stream), HVWS_EHIP);
     HIP_OR(launch_frame_sizes(d_flags, d_len, n, c->tx_size.as<uint64_t>(), c->stream), HVWS_EHIP);
     HIP_OR(launch_exclusive_scan(c->tx_size.as<uint64_t>(), off, n, c->tx_scan.as<uint64_t>(), stat, c->stream),
            HVWS_EHIP);
     HIP_OR(launch_tx_check(d_pay_off, d_len, d_flags, d_mask, off, n, payload_len, stat + 1, c->stream), HVWS_EHIP);
     uint64_t* h = c->h_tx.as<uint64_t>();
-    HIP_OR(hipMemcpyAsync(h, stat, 24, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(h, stat, 16, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (h[1]) return set_err(HVWS_EINVAL, "build_frames: %llu frames read outside the payload buffer or lack a mask",
                              (unsigned long long)h[1]);
@@ -2589,35 +2589,31 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     if (total > out_cap)
         return set_err(HVWS_EINVAL, "build_frames: output needs %llu bytes, capacity %llu", (unsigned long long)total,
                        (unsigned long long)out_cap);
-    // every payload already at its output offset: the k_unmask-shaped kernel
-    // ($HVWS_BUILD_ID=0 keeps the general one, for A/B runs)
-    static const bool id_ok = !getenv("HVWS_BUILD_ID") || atoi(getenv("HVWS_BUILD_ID")) != 0;
-    const bool same_off = id_ok && h[2] == 0 && d_payload && payload_len >= total;
-    c->tx_path = same_off ? 1 : 0;
-    const uint64_t tile = same_off ? tx_id_tile() : tx_tile();
+    // the geometry by the batch's mean frame size (tx_variant); every layout
+    // takes k_build (round 4: it reached or beat the same-offset kernel
+    // k_build_id, which is gone, profiles/r4v_raw)
+    const int v = tx_variant(total, n);
+    c->tx_variant = v;
+    // each tile's source span first ($HVWS_BUILD_SPANS=0: the records-first tiles)
+    const char* sp_env = getenv("HVWS_BUILD_SPANS");
+    const bool spans_ok = !sp_env || atoi(sp_env) != 0;
+    const uint64_t tile = tx_tile(v);
     const uint64_t ntiles = (total + tile - 1) / tile;
     HIP_OR(c->tx_tiles.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+    if (spans_ok) HIP_OR(c->tx_span.ensure(ntiles * 16 + 16), HVWS_ENOMEM);
+    // the timed device work (hvws_last_kernel_ms): tile index, spans, build
+    HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
     HIP_OR(launch_tile_index(off, c->tx_size.as<uint64_t>(), n, nullptr, c->tx_tiles.as<uint32_t>(), ntiles, tile,
                              c->stream),
            HVWS_EHIP);
-    // general layout: each tile's source span first ($HVWS_BUILD_SPANS=0: the records-first tiles)
-    const char* sp_env = getenv("HVWS_BUILD_SPANS");
-    const bool spans_ok = !sp_env || atoi(sp_env) != 0;
     uint64_t* span = nullptr;
-    if (!same_off && spans_ok) {
-        HIP_OR(c->tx_span.ensure(ntiles * 16 + 16), HVWS_ENOMEM);
+    if (spans_ok) {
         span = c->tx_span.as<uint64_t>();
-        HIP_OR(launch_tx_spans(d_pay_off, d_len, d_flags, off, n, ntiles, span, c->stream), HVWS_EHIP);
+        HIP_OR(launch_tx_spans(d_pay_off, d_len, d_flags, off, n, ntiles, tile, span, c->stream), HVWS_EHIP);
     }
-    HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
-    if (same_off)
-        HIP_OR(launch_build_id(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
-                               c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), n, c->stream),
-               HVWS_EHIP);
-    else
-        HIP_OR(launch_build(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
-                            c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), span, n, c->stream),
-               HVWS_EHIP);
+    HIP_OR(launch_build(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
+                        c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), span, n, v, c->stream),
+           HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
     c->ev_build = true;
     return HVWS_OK;
@@ -2647,11 +2643,11 @@ int hvws_last_kernel_ms(hvws_ctx* c, float* ms) {
     return HVWS_OK;
 }
 
-const char* hvws_build_kernel_name(void) { return build_kernel_name(); }
+const char* hvws_build_kernel_name(void) { return build_kernel_name(tx_variant(0, 0)); }
 
 const char* hvws_last_build_kernel(hvws_ctx* c) {
     if (!c) return "";
-    return c->tx_path == 1 ? build_id_kernel_name() : build_kernel_name();
+    return build_kernel_name(c->tx_variant);
 }
 
 uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {

@@ -362,20 +362,18 @@ hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, 
 // *bad += frames whose payload range leaves [0, plen) or that are masked without a key table.
 hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
                            const uint64_t* out_off, uint64_t n, uint64_t plen, uint64_t* bad, hipStream_t st);
-uint64_t tx_tile();   // output bytes per k_build workgroup
-uint64_t tx_id_tile();   // output bytes per k_build_id workgroup
-const char* build_id_kernel_name();
-hipError_t launch_build_id(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
-                           const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                           const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st);
-const char* build_kernel_name();   // k_build geometry in use ($HVWS_BUILD)
-// span: 2 words per k_build tile (ntiles of tx_tile() bytes), filled here.
+// k_build geometry for a batch of out_len output bytes in n frames
+// ($HVWS_BUILD, else by the mean frame size), its tile and its name
+int tx_variant(uint64_t out_len, uint64_t n);
+uint64_t tx_tile(int v);   // output bytes per k_build workgroup
+const char* build_kernel_name(int v);
+// span: 2 words per k_build tile (ntiles of `tile` bytes), filled here.
 hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
-                           uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st);
+                           uint64_t n, uint64_t ntiles, uint64_t tile, uint64_t* span, hipStream_t st);
 // span: from launch_tx_spans, or nullptr (boundary tiles load their records first)
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                        const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n,
+                        const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,
                         hipStream_t st);
 
 }  // namespace hvws

@@ -677,151 +677,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
 }
 
 
-// ------------------------------------------------------------- k_build_id
-//
-// Same-offset layout: every frame's payload sits in the source buffer at the
-// offset its payload takes in the output (pay_off[k] = out_off[k] + header
-// length) -- a relay re-framing the batch it received, or a sender that
-// builds its payloads in place of the frames they go out in.  Then the source
-// bytes of output chunk c are pay[c, c+16): the tile's data loads are issued
-// before anything about its frames is known, exactly like k_unmask's (512 x
-// 2 geometry, the in-place read+write ceiling), and the frame records only
-// decide which bytes get a header byte, a key byte or nothing.  The general
-// k_build must find each chunk's source first: one dependent round trip more
-// per tile, which at 1 KiB frames every tile pays.
-constexpr int BID_T = 512, BID_U = 2;
-constexpr uint32_t BID_MAXF = 256;   // frames per tile staged in LDS
-
-__device__ __forceinline__ uint64_t bid_mask(int64_t lo, int64_t hi) {   // bytes [lo, hi) of an 8-byte word
-    lo = lo < 0 ? 0 : lo;
-    hi = hi > 8 ? 8 : hi;
-    if (hi <= lo) return 0;
-    const uint64_t top = hi >= 8 ? ~0ull : ((1ull << (8 * hi)) - 1);
-    return top & (~0ull << (8 * lo));
-}
-
-__global__ __launch_bounds__(BID_T) void k_build_id(uint8_t* __restrict__ out, uint64_t out_len,
-                                                    const uint8_t* __restrict__ pay, uint64_t plen,
-                                                    const uint64_t* __restrict__ pay_off,
-                                                    const uint64_t* __restrict__ len,
-                                                    const uint8_t* __restrict__ flags,
-                                                    const uint32_t* __restrict__ mask,
-                                                    const uint64_t* __restrict__ out_off,
-                                                    const uint64_t* __restrict__ size,
-                                                    const uint32_t* __restrict__ tile_first, uint64_t n,
-                                                    uint64_t tile0) {
-    constexpr uint64_t TILE = (uint64_t)BID_T * BID_U * 16u;
-    __shared__ uint64_t s_off[BID_MAXF], s_ps[BID_MAXF], s_end[BID_MAXF];
-    __shared__ uint32_t s_key[BID_MAXF], s_fl[BID_MAXF];
-    const uint64_t t = tile0 + blockIdx.x;
-    const uint64_t base = t * TILE;
-    const uint32_t tid = threadIdx.x;
-    const bool full = base + TILE <= out_len && base + TILE <= plen;
-    u32x4 v[BID_U];
-    if (full) {
-#pragma unroll
-        for (int i = 0; i < BID_U; ++i)
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + base + ((uint64_t)i * BID_T + tid) * 16u));
-    } else {
-#pragma unroll
-        for (int i = 0; i < BID_U; ++i) {
-            const uint64_t c = base + ((uint64_t)i * BID_T + tid) * 16u;
-            uint32_t w4[4] = {0u, 0u, 0u, 0u};
-            for (int b = 0; b < 16; ++b)
-                if (c + b < out_len && c + b < plen) w4[b >> 2] |= (uint32_t)pay[c + b] << (8 * (b & 3));
-            v[i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
-        }
-    }
-    const uint64_t k_lo = tile_first[t];
-    const uint64_t k_hi = min((uint64_t)tile_first[t + 1] + 1, n);   // frames touching the tile: [k_lo, k_hi)
-    const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
-    if (nf > BID_MAXF) {   // more frames than LDS holds: the general assembly, chunk by chunk
-#pragma unroll 1
-        for (int i = 0; i < BID_U; ++i) {
-            const uint64_t c = base + ((uint64_t)i * BID_T + tid) * 16u;
-            if (c >= out_len) break;
-            build_chunk(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, n, k_lo, k_hi, c);
-        }
-        return;
-    }
-    for (uint32_t i = tid; i < nf; i += BID_T) {
-        const uint64_t k = k_lo + i;
-        const uint32_t fl = flags[k];
-        const uint64_t ln = len[k], o = out_off[k];
-        const uint64_t ps = o + tx_hdr_len(fl, ln);
-        s_off[i] = o;
-        s_ps[i] = ps;
-        s_end[i] = ps + ln;
-        s_key[i] = (fl & F_MASK) ? mask[k] : 0u;
-        s_fl[i] = fl;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < BID_U; ++i) {
-        const uint64_t c = base + ((uint64_t)i * BID_T + tid) * 16u;
-        if (c >= out_len) break;
-        uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
-        while (j < je) {
-            const uint32_t mid = (j + je) >> 1;
-            if (s_end[mid] > c) je = mid;
-            else j = mid + 1;
-        }
-        u32x4 o4;
-        if (j < nf && s_ps[j] <= c && c + 16 <= s_end[j]) {   // 16 payload bytes of one frame
-            const uint32_t kw = tx_rotr(s_key[j], (uint32_t)((c - s_ps[j]) & 3u) * 8u);
-            o4 = v[i] ^ u32x4{kw, kw, kw, kw};
-        } else {   // headers / frame boundaries: piece by piece under byte masks
-            const uint64_t vlo = v[i].x | ((uint64_t)v[i].y << 32), vhi = v[i].z | ((uint64_t)v[i].w << 32);
-            const uint64_t ce = c + 16;
-            uint64_t olo = 0, ohi = 0;
-            for (; j < nf && s_off[j] < ce; ++j) {
-                const uint64_t o = s_off[j], ps = s_ps[j], e = s_end[j];
-                const uint64_t hb = o > c ? o : c, he = ps < ce ? ps : ce;
-                if (hb < he) {   // header bytes
-                    uint64_t hlo, hhi;
-                    tx_hdr128(s_fl[j], e - ps, s_key[j], hlo, hhi);
-                    shr_bytes(hlo, hhi, (uint32_t)(hb - o));
-                    put_bytes(olo, ohi, hlo, hhi, (uint32_t)(hb - c), (uint32_t)(he - c));
-                }
-                const uint64_t pb = ps > c ? ps : c, pe = e < ce ? e : ce;
-                if (pb < pe) {   // payload bytes: the source bytes at the same offsets, keyed
-                    const uint32_t kw = tx_rotr(s_key[j], ((uint32_t)(c - ps) & 3u) * 8u);
-                    const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
-                    const int64_t a0 = (int64_t)(pb - c), a1 = (int64_t)(pe - c);
-                    olo |= (vlo ^ kk) & bid_mask(a0, a1);
-                    ohi |= (vhi ^ kk) & bid_mask(a0 - 8, a1 - 8);
-                }
-            }
-            o4 = u32x4{(uint32_t)olo, (uint32_t)(olo >> 32), (uint32_t)ohi, (uint32_t)(ohi >> 32)};
-        }
-        if (c + 16 <= out_len) {
-            __builtin_nontemporal_store(o4, reinterpret_cast<u32x4*>(out + c));
-        } else {
-            const uint32_t w4[4] = {o4.x, o4.y, o4.z, o4.w};
-            for (uint32_t b = 0; b < 16 && c + b < out_len; ++b) out[c + b] = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
-        }
-    }
-}
-
-uint64_t tx_id_tile() { return (uint64_t)BID_T * BID_U * 16u; }
-const char* build_id_kernel_name() { return "k_build_id<512,2>"; }
-
-hipError_t launch_build_id(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
-                           const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                           const uint64_t* size, const uint32_t* tile_first, uint64_t n, hipStream_t st) {
-    const uint64_t tile = tx_id_tile();
-    const uint64_t ntiles = (out_len + tile - 1) / tile;
-    const uint64_t per_launch = 0xFFFFFFFFull / BID_T;
-    for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
-        const uint64_t nt = min(per_launch, ntiles - t0);
-        hipLaunchKernelGGL(k_build_id, dim3((uint32_t)nt), dim3(BID_T), 0, st, out, out_len, pay, plen, pay_off, len, flags,
-                           mask, out_off, size, tile_first, n, t0);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
 hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp, uint64_t* total,
                                  hipStream_t st) {
     if (n == 0) return hipMemsetAsync(total, 0, 8, st);
@@ -843,17 +698,13 @@ __global__ void k_tx_check(const uint64_t* __restrict__ pay_off, const uint64_t*
                            const uint64_t* __restrict__ out_off, uint64_t n, uint64_t plen,
                            unsigned long long* __restrict__ bad) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool b = false, moved = false;
+    bool b = false;
     if (i < n) {
         const uint64_t o = pay_off[i], l = len[i];
         b = o > plen || l > plen - o || ((flags[i] & F_MASK) && !mask);
-        // same-offset layout (k_build_id): the payload where the output puts it
-        moved = l && o != out_off[i] + tx_hdr_len(flags[i], l);
     }
     const uint64_t m = __ballot(b);
     if (m && (threadIdx.x & 63) == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
-    const uint64_t mv = __ballot(moved);
-    if (mv && (threadIdx.x & 63) == 0) atomicAdd(bad + 1, (unsigned long long)__popcll(mv));
 }
 
 hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
@@ -886,13 +737,14 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(5, 64, 4, false, false, true, 2)
 
 namespace {
-int build_variant() {
-    static const int v = [] {
-        const char* e = getenv("HVWS_BUILD");
-        const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x < 6) ? x : 0;
-    }();
-    return v;
+// $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
+// the lean one-wave form below 4 KiB per frame (c2: 0.43 against 0.46 ms),
+// the default above it (c3: 20.2-20.7 against 22.3 ms; profiles/r4v_raw)
+int build_pick(uint64_t out_len, uint64_t n) {
+    const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
+    const int forced = e ? atoi(e) : -1;
+    if (forced >= 0 && forced < 6) return forced;
+    return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
     switch (v) {
@@ -906,8 +758,8 @@ uint64_t build_tile(int v) {
 }
 }  // namespace
 
-const char* build_kernel_name() {
-    switch (build_variant()) {
+const char* build_kernel_name(int v) {
+    switch (v) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
         return C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
@@ -917,24 +769,24 @@ const char* build_kernel_name() {
     return "?";
 }
 
-uint64_t tx_tile() { return build_tile(build_variant()); }
+int tx_variant(uint64_t out_len, uint64_t n) { return build_pick(out_len, n); }
+uint64_t tx_tile(int v) { return build_tile(v); }
 
 hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
-                           uint64_t n, uint64_t ntiles, uint64_t* span, hipStream_t st) {
+                           uint64_t n, uint64_t ntiles, uint64_t tile, uint64_t* span, hipStream_t st) {
     hipLaunchKernelGGL(k_span_init, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256), 0, st,
                        reinterpret_cast<unsigned long long*>(span), ntiles);
     if (n == 0) return hipGetLastError();
     hipLaunchKernelGGL(k_tx_spans, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, pay_off, len, flags, out_off, n,
-                       tx_tile(), reinterpret_cast<unsigned long long*>(span));
+                       tile, reinterpret_cast<unsigned long long*>(span));
     return hipGetLastError();
 }
 
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
-                        const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n,
+                        const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,
                         hipStream_t st) {
     const unsigned long long* sp = reinterpret_cast<const unsigned long long*>(span);
-    const int v = build_variant();
     const uint64_t tile = build_tile(v);
     const uint64_t ntiles = (out_len + tile - 1) / tile;
     // a grid beyond 2^32-1 work-items is silently truncated: split the launch

@@ -166,7 +166,7 @@ def test_build_roundtrip_batch(eng, name, plan):
 
 
 def _gpu_build_same_offset(eng, frames, rng, move=None):
-    """Payloads placed where the output puts them (k_build_id's layout), the
+    """Payloads placed where the output puts them (a relay's layout), the
     bytes between them (the headers' places) random junk the build must not
     copy; `move` = a frame index whose payload is moved one byte instead."""
     L = libhv_amd.lib()
@@ -200,11 +200,11 @@ def _gpu_build_same_offset(eng, frames, rng, move=None):
 
 @pytest.mark.parametrize("kind", ["random", "small", "edges", "tiny", "large", "unmasked"])
 def test_build_same_offset_layout(eng, kind):
-    """Every payload already at its output offset: k_build_id (the source
-    bytes of each output chunk loaded before its frames are known), frame by
-    frame against the reference -- headers written over the junk between
-    payloads, keys at every phase, tiles with more frames than LDS holds
-    (tiny) taking its chunk-by-chunk fallback."""
+    """Every payload already at its output offset (a relay re-framing what it
+    received; round 3 had a kernel of its own for it), frame by frame against
+    the reference -- headers written over the junk between payloads, keys at
+    every phase, tiles with more frames than LDS holds (tiny) taking the
+    chunk-by-chunk fallback."""
     rng = np.random.default_rng(hash(kind) & 0xFFFF)
     if kind == "random":
         frames = _frames(rng, 400)
@@ -222,15 +222,43 @@ def test_build_same_offset_layout(eng, kind):
         frames = _frames(rng, 300, p_mask=0.0)
     got, kern = _gpu_build_same_offset(eng, frames, rng)
     assert got == H.build_frames_ref(frames)
-    assert kern.startswith("k_build_id"), kern
+    assert kern.startswith("k_build<"), kern
 
 
-def test_build_one_moved_payload_takes_general_kernel(eng):
+def test_build_one_moved_payload(eng):
     rng = np.random.default_rng(99)
     frames = _frames(rng, 200, lens=rng.integers(1, 3000, 200))
     got, kern = _gpu_build_same_offset(eng, frames, rng, move=137)
     assert got == H.build_frames_ref(frames)
-    assert not kern.startswith("k_build_id"), kern
+
+
+@pytest.mark.parametrize("v", ["0", "1", "2", "3", "4", "5"])
+def test_build_every_geometry(eng, v, monkeypatch):
+    """Every k_build geometry ($HVWS_BUILD) builds small frames, edge lengths
+    and misaligned payloads byte for byte like the reference and reports its
+    name; unset, the pick follows the mean frame size."""
+    monkeypatch.setenv("HVWS_BUILD", v)
+    L = libhv_amd.lib()
+    rng = np.random.default_rng(3)
+    lens = np.concatenate([rng.integers(0, 20, 200), rng.integers(1000, 2019, 300), np.array(EDGE_LENS)])
+    frames = _frames(rng, len(lens), lens=lens)
+    got, _ = _gpu_build(eng, frames, gap_rng=rng)
+    assert got == H.build_frames_ref(frames)
+    assert L.hvws_last_build_kernel(eng.ctx).decode().startswith("k_build<")
+
+
+def test_build_geometry_by_frame_size(eng, monkeypatch):
+    monkeypatch.delenv("HVWS_BUILD", raising=False)
+    L = libhv_amd.lib()
+    rng = np.random.default_rng(4)
+    small = _frames(rng, 300, lens=[1000] * 300)
+    got, _ = _gpu_build(eng, small)
+    assert got == H.build_frames_ref(small)
+    assert L.hvws_last_build_kernel(eng.ctx).decode().endswith(",lean>")
+    big = _frames(rng, 8, lens=[70001] * 8)
+    got, _ = _gpu_build(eng, big)
+    assert got == H.build_frames_ref(big)
+    assert not L.hvws_last_build_kernel(eng.ctx).decode().endswith(",lean>")
 
 
 @pytest.mark.parametrize("spans", ["1", "0"])
