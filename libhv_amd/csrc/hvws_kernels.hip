@@ -2240,7 +2240,10 @@ struct unmask_geom {
     X(8, 64, 8, true)                                                                     \
     X(9, 256, 4, false)                                                                   \
     X(10, 256, 2, false)                                                                  \
-    X(11, 512, 2, false)
+    X(11, 512, 2, false)                                                                  \
+    X(12, 64, 4, false)                                                                   \
+    X(13, 64, 8, false)                                                                   \
+    X(14, 64, 16, false)
 #define HVWS_GEOM_ENTRY(i, t, u, s) {t, u, s},
 static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
 
