@@ -2316,6 +2316,11 @@ static uint64_t max_tiles_per_launch(int threads) {
 #define HVWS_GEOM_CASE_EXT(i, t, u, s) \
     case i: hipExtLaunchKernelGGL((HVWS_K<t, u, s>), HVWS_EXT_ARGS); break;
 
+static uint32_t unmask_lds() {
+    static const uint32_t b = getenv("HVWS_UNMASK_LDS") ? (uint32_t)atoi(getenv("HVWS_UNMASK_LDS")) : 0u;
+    return b;
+}
+
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
                          const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st,
                          uint32_t pieces, hipEvent_t ev_start, hipEvent_t ev_stop) {
@@ -2340,11 +2345,13 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
         const hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
         const hipEvent_t e1 = tile0 + ntiles >= ntiles_all ? ev_stop : nullptr;
+// $HVWS_UNMASK_LDS (experiments): dynamic LDS bytes per workgroup, to cap how
+// many unmask workgroups a CU holds beside the next batch's scan
 #define HVWS_K k_unmask
-#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, fr.keyrot, \
-                  tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
-#define HVWS_EXT_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, e0, e1, 0u, rx, rx_len, fr.pay_off, fr.pay_len, \
-                      fr.keyrot, tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
+#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), unmask_lds(), st, rx, rx_len, fr.pay_off, fr.pay_len, \
+                  fr.keyrot, tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
+#define HVWS_EXT_ARGS dim3((uint32_t)ntiles), dim3(threads), unmask_lds(), st, e0, e1, 0u, rx, rx_len, fr.pay_off, \
+                      fr.pay_len, fr.keyrot, tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
         if (e0 || e1) {
             switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE_EXT) default: return hipErrorInvalidValue; }
         } else {
