@@ -734,7 +734,10 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(2, 256, 2, false, false, true, 0)   \
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
-    X(5, 64, 4, false, false, true, 2)
+    X(5, 64, 4, false, false, true, 2)    \
+    X(6, 64, 8, false, false, true, 2)    \
+    X(7, 64, 2, false, false, true, 2)    \
+    X(8, 64, 8, false, false, true, 1)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -743,7 +746,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 6) return forced;
+    if (forced >= 0 && forced < 9) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
