@@ -724,7 +724,8 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // tile-relative records (r4m_raw); then one-wave workgroups with 4 KiB tiles
 // -- no staging barrier across waves, every wave's tile independent: c2
 // packed 0.52 -> 0.455 ms, c3 packed 22.4 -> 20.6 ms, c4 1.40 -> 1.30 ms
-// (r4t_raw, r4u_raw).  Tried and gone in round 4: a grid-stride form with the
+// (r4t_raw, r4u_raw); 64 x 8 (LDS-bound to 3 waves per SIMD) and 64 x 2 ran
+// slower at every shape (r4aa_raw).  Tried and gone in round 4: a grid-stride form with the
 // next tile's index prefetched (r4l_raw), a position-derived index for uniform
 // layouts (r4o_raw, r4p_raw), a short path for chunks inside one payload
 // (r4r_raw).
@@ -734,10 +735,7 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(2, 256, 2, false, false, true, 0)   \
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
-    X(5, 64, 4, false, false, true, 2)    \
-    X(6, 64, 8, false, false, true, 2)    \
-    X(7, 64, 2, false, false, true, 2)    \
-    X(8, 64, 8, false, false, true, 1)
+    X(5, 64, 4, false, false, true, 2)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -746,7 +744,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 9) return forced;
+    if (forced >= 0 && forced < 6) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
