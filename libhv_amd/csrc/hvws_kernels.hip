@@ -1038,8 +1038,6 @@ __device__ __forceinline__ void door_size(const uint32_t* l, uint32_t q, uint32_
 constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames (HVWS_DOOR_WALK, default on)
 constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (HVWS_DOOR_NT)
 constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (HVWS_DOOR_PRELOAD)
-constexpr uint32_t DOOR_F_CHUNK = 8u;     // chunk-major unmask for reads of <= DOOR_XREC records (HVWS_DOOR_CHUNK)
-constexpr uint32_t DOOR_XREC = 64;
 
 // Chunks [c_lo, c_hi) of the data area (both multiples of 64) into LDS at the
 // same offsets by LDS-DMA: no registers (an array of 16-byte values per
@@ -1220,7 +1218,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     __shared__ uint64_t s_t[7], s_m[2];
     __shared__ uint64_t s_req[16];
     __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
-    __shared__ uint32_t s_xpo[DOOR_XREC], s_xpe[DOOR_XREC], s_xkw[DOOR_XREC];   // DOOR_F_CHUNK
     __shared__ uint64_t s_w[3];               // door_walk's stamps
     for (;;) {
         if (tid == 0) {
@@ -1321,13 +1318,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     o.info = v.info;
                     if (idx < SMALL_LREC) lrec[idx] = o;
                     else d_slot[idx] = o;
-                    if (idx < DOOR_XREC) {   // the chunk-major unmask's view: 32-bit span and key word
-                        const uint32_t po = (uint32_t)v.pay_off;
-                        const bool m = (v.info & F_MASK) && v.pay_len;
-                        s_xpo[idx] = po;
-                        s_xpe[idx] = m ? po + (uint32_t)v.pay_len : po;   // unmasked: an empty span
-                        s_xkw[idx] = rotr32(v.key, 8u * ((((v.info >> 8) & 3u) - po) & 3u));
-                    }
                 };
                 if (st.state == S_BODY && st.require > 0 && L > 0) {
                     // the common carry, a payload that continues into this
@@ -1386,41 +1376,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             // alone (plain read-modify-write); a payload's first and last
             // chunks may hold another record's bytes too (LDS atomic XOR per
             // dword).  Then every chunk of the read goes to dout.
-            if (s_unmask && (flags & DOOR_F_CHUNK) && n <= DOOR_XREC) {
-                // Chunk-major (n <= DOOR_XREC records): each thread takes its
-                // chunks, finds the records that overlap one (a count over
-                // the sorted, disjoint spans: independent broadcast reads),
-                // XORs them in registers and stores the chunk -- no atomics,
-                // no barrier before the stores.
-                const uint32_t n32 = (uint32_t)n;
-                for (uint32_t c = tid * 16u; c < (uint32_t)L; c += kDoorThreads * 16u) {
-                    uint32_t j = 0;
-                    for (uint32_t k = 0; k < n32; ++k) j += s_xpe[k] <= c ? 1u : 0u;
-                    u32x4 v = *reinterpret_cast<const u32x4*>(lds + c);
-                    for (; j < n32; ++j) {
-                        const uint32_t po = s_xpo[j], pe = s_xpe[j];
-                        if (po >= c + 16u) break;
-                        if (pe <= po) continue;   // unmasked or empty
-                        const uint32_t kw = s_xkw[j];
-                        if (po <= c && pe >= c + 16u) {
-                            v ^= u32x4{kw, kw, kw, kw};
-                            break;
-                        }
-                        const int32_t a = po > c ? (int32_t)(po - c) : 0, e = pe < c + 16u ? (int32_t)(pe - c) : 16;
-                        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) {
-                            const int32_t lo = a - 4 * d < 0 ? 0 : (a - 4 * d), hi = e - 4 * d > 4 ? 4 : (e - 4 * d);
-                            if (hi > lo)
-                                w[d] ^= kw & ((hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u));
-                        }
-                        v = u32x4{w[0], w[1], w[2], w[3]};
-                        if (pe >= c + 16u) break;
-                    }
-                    *reinterpret_cast<u32x4*>(dout + c) = v;
-                }
-                if (tid == 0) s_t[6] = s_t[2];
-            } else if (s_unmask) {
+            if (s_unmask) {
                 uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
                 const uint32_t wave = tid >> 6, lane = tid & 63u;
                 auto unmask_rec = [&](const drec& f) {
@@ -1497,8 +1453,7 @@ hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t
     auto knob = [](const char* name, uint32_t dflt) { return getenv(name) ? (uint32_t)atoi(getenv(name)) : dflt; };
     static const uint32_t flags = (knob("HVWS_DOOR_WALK", 1) ? DOOR_F_WALK : 0u) |
                                   (knob("HVWS_DOOR_NT", 0) ? DOOR_F_NT : 0u) |
-                                  (knob("HVWS_DOOR_PRELOAD", 0) ? DOOR_F_PRELOAD : 0u) |
-                                  (knob("HVWS_DOOR_CHUNK", 0) ? DOOR_F_CHUNK : 0u);
+                                  (knob("HVWS_DOOR_PRELOAD", 0) ? DOOR_F_PRELOAD : 0u);
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
                        idle_ticks, first_seq, epoch, flags);
     return hipGetLastError();
