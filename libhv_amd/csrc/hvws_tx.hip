@@ -440,12 +440,12 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
     // staged source bytes per boundary tile (LDS): the tile's payload bytes,
     // with room for gaps between payloads
-    constexpr uint64_t SPAN_MAX = TILE + ((C == 2 || C == 3) ? 256 : 1024);
+    constexpr uint64_t SPAN_MAX = TILE + (C == 2 ? 256 : 1024);
     // the tile's frame records, 40 bytes each: the 64-bit per-field arrays,
     // or (C) the compact records in the same storage
     // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
     // workgroup's LDS leaves room for 8 waves per SIMD
-    constexpr uint32_t MAXF = (C == 2 || C == 3) ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
+    constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
     __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * 5];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
@@ -465,25 +465,11 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         __shared__ u32x4 s_data[SPAN_MAX / 16 + 2];
         constexpr int SPU = (int)((SPAN_MAX / 16 + T - 1) / T);
         const uint32_t nch = (uint32_t)((sb - sa) / 16);
-        // GL (C >= 3, one-wave workgroups): the span goes to LDS by LDS-DMA
-        // (lane-linear, 64 chunks per instruction), no registers and no
-        // LDS store pass
-        constexpr bool GL = C >= 3 && T == 64;
-        u32x4 d[GL ? 1 : SPU];
-        if (GL) {
-            for (uint32_t q0 = 0; q0 < nch; q0 += 64u) {
-                if (q0 + tid < nch)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(pay + sa + (uint64_t)(q0 + tid) * 16u),
-                        (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(s_data) + (uint64_t)q0 * 16u),
-                        16, 0, 2);
-            }
-        } else {
+        u32x4 d[SPU];
 #pragma unroll
-            for (int i = 0; i < SPU; ++i) {
-                const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-                if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
-            }
+        for (int i = 0; i < SPU; ++i) {
+            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
+            if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
         }
         if (C) {
             // one 32-byte record per frame, 32-bit fields relative to the
@@ -510,15 +496,12 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 s_fl[r] = fl;
             }
         }
-        if (!GL) {
 #pragma unroll
-            for (int i = 0; i < SPU; ++i) {
-                const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-                if (q < nch) s_data[q] = d[i];
-            }
+        for (int i = 0; i < SPU; ++i) {
+            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
+            if (q < nch) s_data[q] = d[i];
         }
         if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
-        if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
         if (C) {
@@ -752,9 +735,7 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(2, 256, 2, false, false, true, 0)   \
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
-    X(5, 64, 4, false, false, true, 2)    \
-    X(6, 64, 4, false, false, true, 3)    \
-    X(7, 64, 4, false, false, true, 4)
+    X(5, 64, 4, false, false, true, 2)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -763,7 +744,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 8) return forced;
+    if (forced >= 0 && forced < 6) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
@@ -782,10 +763,7 @@ const char* build_kernel_name(int v) {
     switch (v) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
-        return C == 4   ? "k_build<" #T "x" #U ",glds>"                                        \
-               : C == 3 ? "k_build<" #T "x" #U ",lean,glds>"                                   \
-               : C == 2 ? "k_build<" #T "x" #U ",lean>"                                        \
-                        : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
+        return C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
