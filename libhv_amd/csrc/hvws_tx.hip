@@ -725,7 +725,8 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // -- no staging barrier across waves, every wave's tile independent: c2
 // packed 0.52 -> 0.455 ms, c3 packed 22.4 -> 20.6 ms, c4 1.40 -> 1.30 ms
 // (r4t_raw, r4u_raw); 64 x 8 (LDS-bound to 3 waves per SIMD) and 64 x 2 ran
-// slower at every shape (r4aa_raw).  Tried and gone in round 4: a grid-stride form with the
+// slower at every shape (r4aa_raw); staging the span by LDS-DMA changed
+// nothing measurable (r4ac_raw).  Tried and gone in round 4: a grid-stride form with the
 // next tile's index prefetched (r4l_raw), a position-derived index for uniform
 // layouts (r4o_raw, r4p_raw), a short path for chunks inside one payload
 // (r4r_raw).
