@@ -440,12 +440,12 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
     // staged source bytes per boundary tile (LDS): the tile's payload bytes,
     // with room for gaps between payloads
-    constexpr uint64_t SPAN_MAX = TILE + (C == 2 ? 256 : 1024);
+    constexpr uint64_t SPAN_MAX = TILE + (C >= 2 ? 256 : 1024);
     // the tile's frame records, 40 bytes each: the 64-bit per-field arrays,
     // or (C) the compact records in the same storage
     // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
     // workgroup's LDS leaves room for 8 waves per SIMD
-    constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
+    constexpr uint32_t MAXF = C >= 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
     __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * 5];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
@@ -584,7 +584,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
         return;
     }
-    if (nf && nf <= MAXF && base + TILE <= out_len) {
+    if (C != 3 && nf && nf <= MAXF && base + TILE <= out_len) {
         // Boundary tile: the tile's frames staged in LDS; chunks inside one
         // payload still stream (loads issued for all U chunks first), chunks
         // holding header bytes or a frame boundary are assembled byte by byte.
@@ -665,7 +665,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
 
 // One workgroup per tile, tiles in linear or XCD-contiguous order.
 template <int T, int U, bool SWZ, bool NT, bool SF, int C>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build(
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(C == 3 ? 7 : 8, 8))) void k_build(
     uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
     const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
@@ -736,7 +736,8 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(2, 256, 2, false, false, true, 0)   \
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
-    X(5, 64, 4, false, false, true, 2)
+    X(5, 64, 4, false, false, true, 2)    \
+    X(6, 64, 4, false, false, true, 3)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -745,7 +746,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 6) return forced;
+    if (forced >= 0 && forced < 7) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
@@ -764,7 +765,7 @@ const char* build_kernel_name(int v) {
     switch (v) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
-        return C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
+        return C == 3 ? "k_build<" #T "x" #U ",lean2>" : C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
