@@ -144,27 +144,27 @@ __device__ __attribute__((noinline)) sv_u32x4 load_chunk(const uint8_t* rx, uint
 __device__ __forceinline__ void load_tile(const uint8_t* rx, uint64_t rx_len, uint64_t T0, tile_regs& r) {
     const uint32_t t = threadIdx.x;
     const uint32_t hc = 2 * SV_THREADS + (t >> 3);   // halo chunk of a halo lane
-    const bool hl = halo_lane(t);
+    // Every lane loads a halo chunk (other lanes the first one, the same
+    // line): a load under the halo lanes' mask kept the register's old value
+    // for the rest, and the merge copy waited for the prefetch at once
+    // (s_waitcnt vmcnt(0) before the tile's sieve, so nothing overlapped).
+    const uint32_t hcu = halo_lane(t) ? hc : 2 * SV_THREADS;
     const uint8_t* p = rx + T0;
     if (T0 + SV_TILE + SV_HALO + 16 <= rx_len) {   // every tile but the last
         r.v[0] = *reinterpret_cast<const sv_u32x4*>(p + 16 * t);
         r.v[1] = *reinterpret_cast<const sv_u32x4*>(p + 16 * (t + SV_THREADS));
         r.nx[0] = *reinterpret_cast<const uint32_t*>(p + 16 * (t + 1));
         r.nx[1] = *reinterpret_cast<const uint32_t*>(p + 16 * (t + SV_THREADS + 1));
-        if (hl) {
-            r.v[2] = *reinterpret_cast<const sv_u32x4*>(p + 16 * hc);
-            r.nx[2] = *reinterpret_cast<const uint32_t*>(p + 16 * (hc + 1));
-        }
+        r.v[2] = *reinterpret_cast<const sv_u32x4*>(p + 16 * hcu);
+        r.nx[2] = *reinterpret_cast<const uint32_t*>(p + 16 * (hcu + 1));
         return;
     }
     r.v[0] = load_chunk(rx, rx_len, T0 + (uint64_t)t * 16);
     r.v[1] = load_chunk(rx, rx_len, T0 + (uint64_t)(t + SV_THREADS) * 16);
     r.nx[0] = load_chunk(rx, rx_len, T0 + (uint64_t)(t + 1) * 16).x;
     r.nx[1] = load_chunk(rx, rx_len, T0 + (uint64_t)(t + SV_THREADS + 1) * 16).x;
-    if (hl) {
-        r.v[2] = load_chunk(rx, rx_len, T0 + (uint64_t)hc * 16);
-        r.nx[2] = load_chunk(rx, rx_len, T0 + (uint64_t)(hc + 1) * 16).x;
-    }
+    r.v[2] = load_chunk(rx, rx_len, T0 + (uint64_t)hcu * 16);
+    r.nx[2] = load_chunk(rx, rx_len, T0 + (uint64_t)(hcu + 1) * 16).x;
 }
 
 __device__ __forceinline__ void store_tile(uint32_t* l, const tile_regs& r) {

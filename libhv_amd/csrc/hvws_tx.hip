@@ -128,6 +128,14 @@ constexpr uint32_t BUILD_MAXF = 128;   // frames per boundary tile staged in LDS
 
 __device__ __forceinline__ uint32_t tx_rotr(uint32_t x, uint32_t r) { return r ? (x >> r) | (x << (32u - r)) : x; }
 
+// The lane id, computed where it is used (volatile: not hoisted or merged
+// with another copy, so no register holds it across the kernel).
+__device__ __forceinline__ uint32_t lane_id_now() {
+    uint32_t v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
+}
+
 // OR bytes [0, b1 - b0) of the 16-byte little-endian value (vlo, vhi) into
 // bytes [b0, b1) of the chunk (olo, ohi); 0 <= b0 < b1 <= 16.
 __device__ __forceinline__ void put_bytes(uint64_t& olo, uint64_t& ohi, uint64_t vlo, uint64_t vhi, uint32_t b0,
@@ -394,7 +402,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     // SF: both ends of the tile's frame range load together, and a tile that
     // more than one frame touches goes straight to staging (no dependent
     // load of its first frame's record to find out it is not one payload).
-    if (k_lo < n && base + TILE <= out_len && (!SF || k_hi == k_lo + 1)) {
+    if (C != 4 && k_lo < n && base + TILE <= out_len && (!SF || k_hi == k_lo + 1)) {
         const uint32_t fl = flags[k_lo];
         const uint64_t ln = len[k_lo];
         const uint64_t ps = out_off[k_lo] + tx_hdr_len(fl, ln);
@@ -465,11 +473,25 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         __shared__ u32x4 s_data[SPAN_MAX / 16 + 2];
         constexpr int SPU = (int)((SPAN_MAX / 16 + T - 1) / T);
         const uint32_t nch = (uint32_t)((sb - sa) / 16);
-        u32x4 d[SPU];
+        // GL (C == 4, one-wave workgroups): the span goes to LDS by LDS-DMA
+        // (lane-linear, 64 chunks per instruction): no data registers and no
+        // LDS store pass
+        constexpr bool GL = C == 4 && T == 64;
+        u32x4 d[GL ? 1 : SPU];
+        if (GL) {
+            for (uint32_t q0 = 0; q0 < nch; q0 += 64u) {
+                if (q0 + tid < nch)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(pay + sa + (uint64_t)(q0 + tid) * 16u),
+                        (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(s_data) + (uint64_t)q0 * 16u),
+                        16, 0, 2);
+            }
+        } else {
 #pragma unroll
-        for (int i = 0; i < SPU; ++i) {
-            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-            if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
+            for (int i = 0; i < SPU; ++i) {
+                const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
+                if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
+            }
         }
         if (C) {
             // one 32-byte record per frame, 32-bit fields relative to the
@@ -477,38 +499,49 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
             for (uint32_t r = tid; r < nf; r += T) {
                 const uint64_t k = k_lo + r;
                 const uint32_t fl = flags[k];
+                // the key loads with the rest of the record, not after its
+                // flags (a second round trip per tile)
+                const uint32_t mk = mask ? mask[k] : 0u;
                 const uint64_t ln = len[k], o = out_off[k];
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
-                s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mask[k] : 0u, fl,
+                s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mk : 0u, fl,
                                           ln);
             }
         } else {
             for (uint32_t r = tid; r < nf; r += T) {
                 const uint64_t k = k_lo + r;
                 const uint32_t fl = flags[k];
+                const uint32_t mk = mask ? mask[k] : 0u;
                 const uint64_t ln = len[k], o = out_off[k];
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
                 s_off[r] = o;
                 s_ps[r] = ps;
                 s_end[r] = ps + ln;
                 s_src[r] = pay_off[k];
-                s_key[r] = (fl & F_MASK) ? mask[k] : 0u;
+                s_key[r] = (fl & F_MASK) ? mk : 0u;
                 s_fl[r] = fl;
             }
         }
+        if (!GL) {
 #pragma unroll
-        for (int i = 0; i < SPU; ++i) {
-            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-            if (q < nch) s_data[q] = d[i];
+            for (int i = 0; i < SPU; ++i) {
+                const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
+                if (q < nch) s_data[q] = d[i];
+            }
         }
         if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
+        if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
         if (C) {
             const uint32_t nf32 = (uint32_t)nf;
 #pragma unroll
             for (int i = 0; i < U; ++i) {
-                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + tid) * 16u);   // tile-relative
+                // (C == 4: the lane id recomputed here -- held from the
+                // kernel's start it was spilled and reloaded from scratch,
+                // with a wait, inside this loop)
+                const uint32_t ln = C == 4 ? lane_id_now() : tid;
+                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + ln) * 16u);   // tile-relative
                 const int32_t ce = c + 16;
                 // first frame ending after c: a count over short ranges
                 // (independent broadcast reads), a binary search otherwise
@@ -584,20 +617,21 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
         return;
     }
-    if (C != 3 && nf && nf <= MAXF && base + TILE <= out_len) {
+    if (C < 3 && nf && nf <= MAXF && base + TILE <= out_len) {
         // Boundary tile: the tile's frames staged in LDS; chunks inside one
         // payload still stream (loads issued for all U chunks first), chunks
         // holding header bytes or a frame boundary are assembled byte by byte.
         for (uint32_t r = tid; r < nf; r += T) {
             const uint64_t k = k_lo + r;
             const uint32_t fl = flags[k];
+            const uint32_t mk = mask ? mask[k] : 0u;
             const uint64_t ln = len[k], o = out_off[k];
             const uint64_t ps = o + tx_hdr_len(fl, ln);
             s_off[r] = o;
             s_ps[r] = ps;
             s_end[r] = ps + ln;
             s_src[r] = pay_off[k];
-            s_key[r] = (fl & F_MASK) ? mask[k] : 0u;
+            s_key[r] = (fl & F_MASK) ? mk : 0u;
             s_fl[r] = fl;
         }
         __syncthreads();
@@ -737,7 +771,8 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
     X(5, 64, 4, false, false, true, 2)    \
-    X(6, 64, 4, false, false, true, 3)
+    X(6, 64, 4, false, false, true, 3)    \
+    X(7, 64, 4, false, false, true, 4)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -746,7 +781,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 7) return forced;
+    if (forced >= 0 && forced < 8) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
@@ -765,7 +800,7 @@ const char* build_kernel_name(int v) {
     switch (v) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
-        return C == 3 ? "k_build<" #T "x" #U ",lean2>" : C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
+        return C == 4 ? "k_build<" #T "x" #U ",lean2,glds>" : C == 3 ? "k_build<" #T "x" #U ",lean2>" : C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
