@@ -128,14 +128,6 @@ constexpr uint32_t BUILD_MAXF = 128;   // frames per boundary tile staged in LDS
 
 __device__ __forceinline__ uint32_t tx_rotr(uint32_t x, uint32_t r) { return r ? (x >> r) | (x << (32u - r)) : x; }
 
-// The lane id, computed where it is used (volatile: not hoisted or merged
-// with another copy, so no register holds it across the kernel).
-__device__ __forceinline__ uint32_t lane_id_now() {
-    uint32_t v;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
-    return v;
-}
-
 // OR bytes [0, b1 - b0) of the 16-byte little-endian value (vlo, vhi) into
 // bytes [b0, b1) of the chunk (olo, ohi); 0 <= b0 < b1 <= 16.
 __device__ __forceinline__ void put_bytes(uint64_t& olo, uint64_t& ohi, uint64_t vlo, uint64_t vhi, uint32_t b0,
@@ -385,6 +377,98 @@ __device__ __forceinline__ build_idx build_load_idx(const uint32_t* __restrict__
     return x;
 }
 
+// A boundary tile from its records alone (the span not staged): records to
+// LDS, chunks inside one payload streamed, the rest assembled frame by frame.
+template <int T, int U, uint32_t MAXF, int G>
+__device__ __forceinline__ void records_first_tile(uint8_t* __restrict__ out, const uint8_t* __restrict__ pay,
+                                                   uint64_t plen, const uint64_t* __restrict__ pay_off,
+                                                   const uint64_t* __restrict__ len,
+                                                   const uint8_t* __restrict__ flags,
+                                                   const uint32_t* __restrict__ mask,
+                                                   const uint64_t* __restrict__ out_off, uint64_t k_lo, uint64_t nf,
+                                                   uint64_t base, uint64_t* s_rb) {
+    const uint32_t tid = threadIdx.x;
+    uint64_t* const s_off = s_rb;
+    uint64_t* const s_ps = s_rb + MAXF;
+    uint64_t* const s_end = s_rb + 2 * MAXF;
+    uint64_t* const s_src = s_rb + 3 * MAXF;
+    uint32_t* const s_key = reinterpret_cast<uint32_t*>(s_rb + 4 * MAXF);
+    uint32_t* const s_fl = s_key + MAXF;
+    for (uint32_t r = tid; r < nf; r += T) {
+        const uint64_t k = k_lo + r;
+        const uint32_t fl = flags[k];
+        const uint32_t mk = mask ? mask[k] : 0u;
+        const uint64_t ln = len[k], o = out_off[k];
+        const uint64_t ps = o + tx_hdr_len(fl, ln);
+        s_off[r] = o;
+        s_ps[r] = ps;
+        s_end[r] = ps + ln;
+        s_src[r] = pay_off[k];
+        s_key[r] = (fl & F_MASK) ? mk : 0u;
+        s_fl[r] = fl;
+    }
+    __syncthreads();
+    // chunks inside one payload: their loads issued G at a time (G < U keeps
+    // the lean form's registers down), then realigned, XORed and stored
+    uint32_t fastmask = 0;
+#pragma unroll
+    for (int g = 0; g < U; g += G) {
+        u32x4 w[G], x[G];
+        uint32_t kw[G], sft[G];
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const int i = g + h;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            w[h] = x[h] = u32x4{0, 0, 0, 0};
+            kw[h] = 0;
+            sft[h] = 0;
+            if (j < nf) {
+                const uint64_t ps = s_ps[j];
+                const uint64_t src = s_src[j] + (c - ps);
+                if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
+                    fastmask |= 1u << i;
+                    sft[h] = (uint32_t)(src & 15u);
+                    const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
+                    w[h] = q[0];
+                    if (sft[h]) x[h] = q[1];
+                    kw[h] = tx_rotr(s_key[j], (uint32_t)((c - ps) & 3u) * 8u);
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const int i = g + h;
+            if (!((fastmask >> i) & 1u)) continue;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            const u32x4 v = (sft[h] ? funnel16(w[h], x[h], sft[h]) : w[h]) ^ u32x4{kw[h], kw[h], kw[h], kw[h]};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
+        }
+    }
+    // chunks holding header bytes or a frame boundary, one at a time
+#pragma unroll 1
+    for (int i = 0; i < U; ++i) {
+        if ((fastmask >> i) & 1u) continue;
+        const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+        uint32_t j = 0, je = (uint32_t)nf;
+        while (j < je) {
+            const uint32_t mid = (j + je) >> 1;
+            if (s_end[mid] > c) je = mid;
+            else j = mid + 1;
+        }
+        uint64_t lo = 0, hi = 0;
+        for (; j < nf && s_off[j] < c + 16; ++j)
+            frame_piece(lo, hi, c, s_off[j], s_ps[j], s_end[j], s_src[j], s_key[j], s_fl[j], pay, plen);
+        __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                    reinterpret_cast<u32x4*>(out + c));
+    }
+}
+
 template <int T, int U, bool NT, bool SF, int C>
 __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64_t out_len,
                                            const uint8_t* __restrict__ pay, uint64_t plen,
@@ -402,7 +486,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     // SF: both ends of the tile's frame range load together, and a tile that
     // more than one frame touches goes straight to staging (no dependent
     // load of its first frame's record to find out it is not one payload).
-    if (C != 4 && k_lo < n && base + TILE <= out_len && (!SF || k_hi == k_lo + 1)) {
+    if (k_lo < n && base + TILE <= out_len && (!SF || k_hi == k_lo + 1)) {
         const uint32_t fl = flags[k_lo];
         const uint64_t ln = len[k_lo];
         const uint64_t ps = out_off[k_lo] + tx_hdr_len(fl, ln);
@@ -448,12 +532,12 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
     // staged source bytes per boundary tile (LDS): the tile's payload bytes,
     // with room for gaps between payloads
-    constexpr uint64_t SPAN_MAX = TILE + (C >= 2 ? 256 : 1024);
+    constexpr uint64_t SPAN_MAX = TILE + (C == 2 ? 256 : 1024);
     // the tile's frame records, 40 bytes each: the 64-bit per-field arrays,
     // or (C) the compact records in the same storage
     // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
-    // workgroup's LDS leaves room for 8 waves per SIMD
-    constexpr uint32_t MAXF = C >= 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
+    // workgroup's LDS leaves room for 8 waves per SIMD (its 66 VGPRs allow 7)
+    constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
     __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * 5];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
@@ -473,25 +557,11 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         __shared__ u32x4 s_data[SPAN_MAX / 16 + 2];
         constexpr int SPU = (int)((SPAN_MAX / 16 + T - 1) / T);
         const uint32_t nch = (uint32_t)((sb - sa) / 16);
-        // GL (C == 4, one-wave workgroups): the span goes to LDS by LDS-DMA
-        // (lane-linear, 64 chunks per instruction): no data registers and no
-        // LDS store pass
-        constexpr bool GL = C == 4 && T == 64;
-        u32x4 d[GL ? 1 : SPU];
-        if (GL) {
-            for (uint32_t q0 = 0; q0 < nch; q0 += 64u) {
-                if (q0 + tid < nch)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(pay + sa + (uint64_t)(q0 + tid) * 16u),
-                        (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(s_data) + (uint64_t)q0 * 16u),
-                        16, 0, 2);
-            }
-        } else {
+        u32x4 d[SPU];
 #pragma unroll
-            for (int i = 0; i < SPU; ++i) {
-                const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-                if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
-            }
+        for (int i = 0; i < SPU; ++i) {
+            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
+            if (q < nch) d[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + sa) + q);
         }
         if (C) {
             // one 32-byte record per frame, 32-bit fields relative to the
@@ -522,26 +592,19 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 s_fl[r] = fl;
             }
         }
-        if (!GL) {
 #pragma unroll
-            for (int i = 0; i < SPU; ++i) {
-                const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-                if (q < nch) s_data[q] = d[i];
-            }
+        for (int i = 0; i < SPU; ++i) {
+            const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
+            if (q < nch) s_data[q] = d[i];
         }
         if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
-        if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
         if (C) {
             const uint32_t nf32 = (uint32_t)nf;
 #pragma unroll
             for (int i = 0; i < U; ++i) {
-                // (C == 4: the lane id recomputed here -- held from the
-                // kernel's start it was spilled and reloaded from scratch,
-                // with a wait, inside this loop)
-                const uint32_t ln = C == 4 ? lane_id_now() : tid;
-                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + ln) * 16u);   // tile-relative
+                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + tid) * 16u);   // tile-relative
                 const int32_t ce = c + 16;
                 // first frame ending after c: a count over short ranges
                 // (independent broadcast reads), a binary search otherwise
@@ -617,76 +680,17 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
         return;
     }
-    if (C < 3 && nf && nf <= MAXF && base + TILE <= out_len) {
-        // Boundary tile: the tile's frames staged in LDS; chunks inside one
-        // payload still stream (loads issued for all U chunks first), chunks
-        // holding header bytes or a frame boundary are assembled byte by byte.
-        for (uint32_t r = tid; r < nf; r += T) {
-            const uint64_t k = k_lo + r;
-            const uint32_t fl = flags[k];
-            const uint32_t mk = mask ? mask[k] : 0u;
-            const uint64_t ln = len[k], o = out_off[k];
-            const uint64_t ps = o + tx_hdr_len(fl, ln);
-            s_off[r] = o;
-            s_ps[r] = ps;
-            s_end[r] = ps + ln;
-            s_src[r] = pay_off[k];
-            s_key[r] = (fl & F_MASK) ? mk : 0u;
-            s_fl[r] = fl;
-        }
-        __syncthreads();
-        u32x4 w[U], x[U];
-        uint32_t kw[U], sft[U];
-        uint32_t fastmask = 0;
-#pragma unroll
-        for (int i = 0; i < U; ++i) {
-            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
-            while (j < je) {
-                const uint32_t mid = (j + je) >> 1;
-                if (s_end[mid] > c) je = mid;
-                else j = mid + 1;
-            }
-            w[i] = x[i] = u32x4{0, 0, 0, 0};
-            kw[i] = 0;
-            sft[i] = 0;
-            if (j < nf) {
-                const uint64_t ps = s_ps[j];
-                const uint64_t src = s_src[j] + (c - ps);
-                if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
-                    fastmask |= 1u << i;
-                    sft[i] = (uint32_t)(src & 15u);
-                    const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
-                    w[i] = q[0];
-                    if (sft[i]) x[i] = q[1];
-                    kw[i] = tx_rotr(s_key[j], (uint32_t)((c - ps) & 3u) * 8u);
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < U; ++i) {
-            if (!((fastmask >> i) & 1u)) continue;
-            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-            const u32x4 v = (sft[i] ? funnel16(w[i], x[i], sft[i]) : w[i]) ^ u32x4{kw[i], kw[i], kw[i], kw[i]};
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
-        }
-        // chunks holding header bytes or a frame boundary, one at a time
-#pragma unroll 1
-        for (int i = 0; i < U; ++i) {
-            if ((fastmask >> i) & 1u) continue;
-            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-            uint32_t j = 0, je = (uint32_t)nf;
-            while (j < je) {
-                const uint32_t mid = (j + je) >> 1;
-                if (s_end[mid] > c) je = mid;
-                else j = mid + 1;
-            }
-            uint64_t lo = 0, hi = 0;
-            for (; j < nf && s_off[j] < c + 16; ++j)
-                frame_piece(lo, hi, c, s_off[j], s_ps[j], s_end[j], s_src[j], s_key[j], s_fl[j], pay, plen);
-            __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
-                                        reinterpret_cast<u32x4*>(out + c));
-        }
+    // Boundary tile whose span does not fit: the tile's frames staged in LDS;
+    // chunks inside one payload still stream (loads issued for all U chunks
+    // first), chunks holding header bytes or a frame boundary are assembled
+    // byte by byte.  The lean form (C == 2) calls it out of line: inlined,
+    // its register arrays made the whole kernel spill 253 VGPRs at 8 waves
+    // per SIMD, and the spilled lane index was reloaded from scratch between
+    // the staged loads, each reload waiting for every load before it
+    // (r4ae_raw / r4af_raw: c2 0.46-0.47 -> 0.42-0.45 ms without it).
+    if (nf && nf <= MAXF && base + TILE <= out_len) {
+        records_first_tile<T, U, MAXF, C == 2 ? 1 : U>(out, pay, plen, pay_off, len, flags, mask, out_off, k_lo, nf,
+                                                       base, s_rb);
         return;
     }
 #pragma unroll 1
@@ -699,7 +703,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
 
 // One workgroup per tile, tiles in linear or XCD-contiguous order.
 template <int T, int U, bool SWZ, bool NT, bool SF, int C>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(C == 3 ? 7 : 8, 8))) void k_build(
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(C == 2 ? 7 : 8, 8))) void k_build(
     uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
     const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
@@ -760,7 +764,10 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 // packed 0.52 -> 0.455 ms, c3 packed 22.4 -> 20.6 ms, c4 1.40 -> 1.30 ms
 // (r4t_raw, r4u_raw); 64 x 8 (LDS-bound to 3 waves per SIMD) and 64 x 2 ran
 // slower at every shape (r4aa_raw); staging the span by LDS-DMA changed
-// nothing measurable (r4ac_raw).  Tried and gone in round 4: a grid-stride form with the
+// nothing measurable (r4ac_raw).  The lean form without the records-first
+// path: no VGPR spills, c2 0.46-0.47 -> 0.42-0.45 ms (r4ae_raw, r4af_raw;
+// with LDS-DMA staging and no streaming path as well, the same at c2 and
+// 1.6x slower at c3).  Tried and gone in round 4: a grid-stride form with the
 // next tile's index prefetched (r4l_raw), a position-derived index for uniform
 // layouts (r4o_raw, r4p_raw), a short path for chunks inside one payload
 // (r4r_raw).
@@ -770,9 +777,7 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(2, 256, 2, false, false, true, 0)   \
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
-    X(5, 64, 4, false, false, true, 2)    \
-    X(6, 64, 4, false, false, true, 3)    \
-    X(7, 64, 4, false, false, true, 4)
+    X(5, 64, 4, false, false, true, 2)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -781,7 +786,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 8) return forced;
+    if (forced >= 0 && forced < 6) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
@@ -800,7 +805,7 @@ const char* build_kernel_name(int v) {
     switch (v) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
-        return C == 4 ? "k_build<" #T "x" #U ",lean2,glds>" : C == 3 ? "k_build<" #T "x" #U ",lean2>" : C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
+        return C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
         HVWS_BUILD_GEOMS(X)
 #undef X
     }
