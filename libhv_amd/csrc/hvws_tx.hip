@@ -377,97 +377,6 @@ __device__ __forceinline__ build_idx build_load_idx(const uint32_t* __restrict__
     return x;
 }
 
-// A boundary tile from its records alone (the span not staged): records to
-// LDS, chunks inside one payload streamed, the rest assembled frame by frame.
-template <int T, int U, uint32_t MAXF, int G>
-__device__ __forceinline__ void records_first_tile(uint8_t* __restrict__ out, const uint8_t* __restrict__ pay,
-                                                   uint64_t plen, const uint64_t* __restrict__ pay_off,
-                                                   const uint64_t* __restrict__ len,
-                                                   const uint8_t* __restrict__ flags,
-                                                   const uint32_t* __restrict__ mask,
-                                                   const uint64_t* __restrict__ out_off, uint64_t k_lo, uint64_t nf,
-                                                   uint64_t base, uint64_t* s_rb) {
-    const uint32_t tid = threadIdx.x;
-    uint64_t* const s_off = s_rb;
-    uint64_t* const s_ps = s_rb + MAXF;
-    uint64_t* const s_end = s_rb + 2 * MAXF;
-    uint64_t* const s_src = s_rb + 3 * MAXF;
-    uint32_t* const s_key = reinterpret_cast<uint32_t*>(s_rb + 4 * MAXF);
-    uint32_t* const s_fl = s_key + MAXF;
-    for (uint32_t r = tid; r < nf; r += T) {
-        const uint64_t k = k_lo + r;
-        const uint32_t fl = flags[k];
-        const uint32_t mk = mask ? mask[k] : 0u;
-        const uint64_t ln = len[k], o = out_off[k];
-        const uint64_t ps = o + tx_hdr_len(fl, ln);
-        s_off[r] = o;
-        s_ps[r] = ps;
-        s_end[r] = ps + ln;
-        s_src[r] = pay_off[k];
-        s_key[r] = (fl & F_MASK) ? mk : 0u;
-        s_fl[r] = fl;
-    }
-    __syncthreads();
-    // chunks inside one payload: their loads issued G at a time (G < U keeps
-    // the lean form's registers down), then realigned, XORed and stored
-    uint32_t fastmask = 0;
-#pragma unroll
-    for (int g = 0; g < U; g += G) {
-        u32x4 w[G], x[G];
-        uint32_t kw[G], sft[G];
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const int i = g + h;
-            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
-            while (j < je) {
-                const uint32_t mid = (j + je) >> 1;
-                if (s_end[mid] > c) je = mid;
-                else j = mid + 1;
-            }
-            w[h] = x[h] = u32x4{0, 0, 0, 0};
-            kw[h] = 0;
-            sft[h] = 0;
-            if (j < nf) {
-                const uint64_t ps = s_ps[j];
-                const uint64_t src = s_src[j] + (c - ps);
-                if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
-                    fastmask |= 1u << i;
-                    sft[h] = (uint32_t)(src & 15u);
-                    const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
-                    w[h] = q[0];
-                    if (sft[h]) x[h] = q[1];
-                    kw[h] = tx_rotr(s_key[j], (uint32_t)((c - ps) & 3u) * 8u);
-                }
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const int i = g + h;
-            if (!((fastmask >> i) & 1u)) continue;
-            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-            const u32x4 v = (sft[h] ? funnel16(w[h], x[h], sft[h]) : w[h]) ^ u32x4{kw[h], kw[h], kw[h], kw[h]};
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
-        }
-    }
-    // chunks holding header bytes or a frame boundary, one at a time
-#pragma unroll 1
-    for (int i = 0; i < U; ++i) {
-        if ((fastmask >> i) & 1u) continue;
-        const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-        uint32_t j = 0, je = (uint32_t)nf;
-        while (j < je) {
-            const uint32_t mid = (j + je) >> 1;
-            if (s_end[mid] > c) je = mid;
-            else j = mid + 1;
-        }
-        uint64_t lo = 0, hi = 0;
-        for (; j < nf && s_off[j] < c + 16; ++j)
-            frame_piece(lo, hi, c, s_off[j], s_ps[j], s_end[j], s_src[j], s_key[j], s_fl[j], pay, plen);
-        __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
-                                    reinterpret_cast<u32x4*>(out + c));
-    }
-}
 
 template <int T, int U, bool NT, bool SF, int C>
 __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64_t out_len,
@@ -680,17 +589,140 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
         return;
     }
-    // Boundary tile whose span does not fit: the tile's frames staged in LDS;
-    // chunks inside one payload still stream (loads issued for all U chunks
-    // first), chunks holding header bytes or a frame boundary are assembled
-    // byte by byte.  The lean form (C == 2) calls it out of line: inlined,
-    // its register arrays made the whole kernel spill 253 VGPRs at 8 waves
-    // per SIMD, and the spilled lane index was reloaded from scratch between
-    // the staged loads, each reload waiting for every load before it
-    // (r4ae_raw / r4af_raw: c2 0.46-0.47 -> 0.42-0.45 ms without it).
-    if (nf && nf <= MAXF && base + TILE <= out_len) {
-        records_first_tile<T, U, MAXF, C == 2 ? 1 : U>(out, pay, plen, pay_off, len, flags, mask, out_off, k_lo, nf,
-                                                       base, s_rb);
+    // The lean form's boundary tiles whose span does not fit: as below, but
+    // one chunk load in flight at a time.  With all U in flight (below) its
+    // register arrays made the whole kernel spill 253 VGPRs at 8 waves per
+    // SIMD, and the spilled lane index was reloaded from scratch between the
+    // staged loads above, each reload waiting for every load before it
+    // (r4ae_raw / r4af_raw / r4ag_raw: c2 0.46-0.47 -> 0.41-0.44 ms).
+    if (C == 2 && nf && nf <= MAXF && base + TILE <= out_len) {
+        for (uint32_t r = tid; r < nf; r += T) {
+            const uint64_t k = k_lo + r;
+            const uint32_t fl = flags[k];
+            const uint32_t mk = mask ? mask[k] : 0u;
+            const uint64_t ln = len[k], o = out_off[k];
+            const uint64_t ps = o + tx_hdr_len(fl, ln);
+            s_off[r] = o;
+            s_ps[r] = ps;
+            s_end[r] = ps + ln;
+            s_src[r] = pay_off[k];
+            s_key[r] = (fl & F_MASK) ? mk : 0u;
+            s_fl[r] = fl;
+        }
+        __syncthreads();
+        uint32_t fastmask = 0;
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            if (j >= nf) continue;
+            const uint64_t ps = s_ps[j];
+            const uint64_t src = s_src[j] + (c - ps);
+            if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
+                fastmask |= 1u << i;
+                const uint32_t sft = (uint32_t)(src & 15u);
+                const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
+                const u32x4 w = q[0];
+                const u32x4 x = sft ? q[1] : w;
+                const uint32_t kw = tx_rotr(s_key[j], (uint32_t)((c - ps) & 3u) * 8u);
+                const u32x4 v = (sft ? funnel16(w, x, sft) : w) ^ u32x4{kw, kw, kw, kw};
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
+            }
+        }
+        // chunks holding header bytes or a frame boundary, one at a time
+#pragma unroll 1
+        for (int i = 0; i < U; ++i) {
+            if ((fastmask >> i) & 1u) continue;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            uint64_t lo = 0, hi = 0;
+            for (; j < nf && s_off[j] < c + 16; ++j)
+                frame_piece(lo, hi, c, s_off[j], s_ps[j], s_end[j], s_src[j], s_key[j], s_fl[j], pay, plen);
+            __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                        reinterpret_cast<u32x4*>(out + c));
+        }
+        return;
+    }
+    if (C != 2 && nf && nf <= MAXF && base + TILE <= out_len) {
+        // Boundary tile: the tile's frames staged in LDS; chunks inside one
+        // payload still stream (loads issued for all U chunks first), chunks
+        // holding header bytes or a frame boundary are assembled byte by byte.
+        for (uint32_t r = tid; r < nf; r += T) {
+            const uint64_t k = k_lo + r;
+            const uint32_t fl = flags[k];
+            const uint32_t mk = mask ? mask[k] : 0u;
+            const uint64_t ln = len[k], o = out_off[k];
+            const uint64_t ps = o + tx_hdr_len(fl, ln);
+            s_off[r] = o;
+            s_ps[r] = ps;
+            s_end[r] = ps + ln;
+            s_src[r] = pay_off[k];
+            s_key[r] = (fl & F_MASK) ? mk : 0u;
+            s_fl[r] = fl;
+        }
+        __syncthreads();
+        u32x4 w[U], x[U];
+        uint32_t kw[U], sft[U];
+        uint32_t fastmask = 0;
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;   // first frame ending after c
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            w[i] = x[i] = u32x4{0, 0, 0, 0};
+            kw[i] = 0;
+            sft[i] = 0;
+            if (j < nf) {
+                const uint64_t ps = s_ps[j];
+                const uint64_t src = s_src[j] + (c - ps);
+                if (ps <= c && c + 16 <= s_end[j] && (src & ~15ull) + 32 <= plen) {
+                    fastmask |= 1u << i;
+                    sft[i] = (uint32_t)(src & 15u);
+                    const u32x4* q = reinterpret_cast<const u32x4*>(pay + (src & ~15ull));
+                    w[i] = q[0];
+                    if (sft[i]) x[i] = q[1];
+                    kw[i] = tx_rotr(s_key[j], (uint32_t)((c - ps) & 3u) * 8u);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            if (!((fastmask >> i) & 1u)) continue;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            const u32x4 v = (sft[i] ? funnel16(w[i], x[i], sft[i]) : w[i]) ^ u32x4{kw[i], kw[i], kw[i], kw[i]};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + c));
+        }
+        // chunks holding header bytes or a frame boundary, one at a time
+#pragma unroll 1
+        for (int i = 0; i < U; ++i) {
+            if ((fastmask >> i) & 1u) continue;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            uint32_t j = 0, je = (uint32_t)nf;
+            while (j < je) {
+                const uint32_t mid = (j + je) >> 1;
+                if (s_end[mid] > c) je = mid;
+                else j = mid + 1;
+            }
+            uint64_t lo = 0, hi = 0;
+            for (; j < nf && s_off[j] < c + 16; ++j)
+                frame_piece(lo, hi, c, s_off[j], s_ps[j], s_end[j], s_src[j], s_key[j], s_fl[j], pay, plen);
+            __builtin_nontemporal_store(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                        reinterpret_cast<u32x4*>(out + c));
+        }
         return;
     }
 #pragma unroll 1
