@@ -511,9 +511,9 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
         if (C) {
             const uint32_t nf32 = (uint32_t)nf;
-            // output chunk at tile-relative byte c, assembled from the records
-            // and the staged span
-            auto assemble = [&](int32_t c) -> u32x4 {
+#pragma unroll
+            for (int i = 0; i < U; ++i) {
+                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + tid) * 16u);   // tile-relative
                 const int32_t ce = c + 16;
                 // first frame ending after c: a count over short ranges
                 // (independent broadcast reads), a binary search otherwise
@@ -549,58 +549,9 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                     }
                     if (f.e >= ce) break;   // the output is dense: the next frame starts at e
                 }
-                return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-            };
-            if constexpr (C == 2 && T == 64) {
-                // Lean one-wave tiles: the general assembly above costs some
-                // 470 instructions per chunk, and a wave ran it for all U of
-                // its chunks although only the few that hold header bytes or
-                // a frame end need it (issue-bound, ~5 TB/s).  Chunks inside
-                // one payload take the short form here; the others are
-                // gathered into a list and assembled together, 64 per pass.
-                __shared__ uint16_t s_bl[U * 64];
-                uint32_t bm = 0, j = 0;
-#pragma unroll
-                for (int i = 0; i < U; ++i) {
-                    const int32_t c = (int32_t)(((uint32_t)i * 64u + tid) * 16u);   // tile-relative
-                    while (j < nf32 && s_rel[j].e <= c) ++j;   // c grows with i: j only advances
-                    bool inner = false;
-                    if (j < nf32) {
-                        const tx_frel f = s_rel[j];
-                        if (f.ps <= c && c + 16 <= f.e) {
-                            inner = true;
-                            uint64_t vlo, vhi;
-                            lds16(lb, (uint32_t)(f.q0 + c), vlo, vhi);
-                            const uint32_t kw = tx_rotr(f.key, (((uint32_t)c + (f.fl >> 24)) & 3u) * 8u);
-                            const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
-                            vlo ^= kk;
-                            vhi ^= kk;
-                            __builtin_nontemporal_store(
-                                u32x4{(uint32_t)vlo, (uint32_t)(vlo >> 32), (uint32_t)vhi, (uint32_t)(vhi >> 32)},
-                                reinterpret_cast<u32x4*>(out + base + (uint32_t)c));
-                        }
-                    }
-                    if (!inner) bm |= 1u << i;
-                }
-                const uint64_t below = (1ull << tid) - 1ull;   // lanes before this one
-                uint32_t nb = 0;
-#pragma unroll
-                for (int i = 0; i < U; ++i) {
-                    const uint64_t m = __ballot((bm >> i) & 1u);
-                    if ((bm >> i) & 1u) s_bl[nb + (uint32_t)__popcll(m & below)] = (uint16_t)(i * 64 + (int)tid);
-                    nb += (uint32_t)__popcll(m);
-                }
-                __syncthreads();
-                for (uint32_t k = tid; k < nb; k += 64u) {
-                    const int32_t c = (int32_t)s_bl[k] * 16;
-                    __builtin_nontemporal_store(assemble(c), reinterpret_cast<u32x4*>(out + base + (uint32_t)c));
-                }
-                return;
-            }
-#pragma unroll
-            for (int i = 0; i < U; ++i) {
-                const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + tid) * 16u);   // tile-relative
-                __builtin_nontemporal_store(assemble(c), reinterpret_cast<u32x4*>(out + base + (uint32_t)c));
+                __builtin_nontemporal_store(
+                    u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                    reinterpret_cast<u32x4*>(out + base + (uint32_t)c));
             }
             return;
         }
