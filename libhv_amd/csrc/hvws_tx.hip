@@ -447,7 +447,8 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
     // workgroup's LDS leaves room for 8 waves per SIMD (its 66 VGPRs allow 7)
     constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
-    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * 5];
+    // (lean: 16 more bytes per frame for its header bytes, built once)
+    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * (C == 2 ? 6 : 5)];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
     uint64_t* const s_end = s_rb + 2 * MAXF;
@@ -455,6 +456,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     uint32_t* const s_key = reinterpret_cast<uint32_t*>(s_rb + 4 * MAXF);
     uint32_t* const s_fl = s_key + MAXF;
     tx_frel* const s_rel = reinterpret_cast<tx_frel*>(s_rb);
+    u32x4* const s_hdr = reinterpret_cast<u32x4*>(s_rb + 4 * MAXF);   // lean: after the MAXF records
     const uint64_t sa = sp_lo & ~15ull, sb = (sp_hi + 15) & ~15ull;   // staged source chunks [sa, sb)
     const bool staged = nf && nf <= MAXF && base + TILE <= out_len &&
                         sp_lo < sp_hi && sb - sa <= SPAN_MAX && sb <= plen;
@@ -485,6 +487,11 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
                 s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mk : 0u, fl,
                                           ln);
+                if (C == 2) {   // the header's bytes, once per frame instead of per chunk and lane
+                    uint64_t hlo, hhi;
+                    tx_hdr128(fl, ln, mk, hlo, hhi);
+                    s_hdr[r] = u32x4{(uint32_t)hlo, (uint32_t)(hlo >> 32), (uint32_t)hhi, (uint32_t)(hhi >> 32)};
+                }
             }
         } else {
             for (uint32_t r = tid; r < nf; r += T) {
@@ -511,14 +518,19 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
         if (C) {
             const uint32_t nf32 = (uint32_t)nf;
+            uint32_t jb = 0;   // lean: the first frame ending after the previous chunk (chunks rise with i)
 #pragma unroll
             for (int i = 0; i < U; ++i) {
                 const int32_t c = (int32_t)(((uint32_t)i * (uint32_t)T + tid) * 16u);   // tile-relative
                 const int32_t ce = c + 16;
                 // first frame ending after c: a count over short ranges
-                // (independent broadcast reads), a binary search otherwise
+                // (independent broadcast reads), a binary search otherwise;
+                // lean: advanced from the previous chunk's
                 uint32_t j = 0;
-                if (nf32 <= 16) {
+                if (C == 2) {
+                    while (jb < nf32 && s_rel[jb].e <= c) ++jb;
+                    j = jb;
+                } else if (nf32 <= 16) {
                     for (uint32_t m = 0; m < nf32; ++m) j += s_rel[m].e <= c ? 1u : 0u;
                 } else {
                     uint32_t je = nf32;
@@ -535,7 +547,14 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                     const int32_t hb = f.o > c ? f.o : c, he = f.ps < ce ? f.ps : ce;
                     if (hb < he) {   // header bytes
                         uint64_t vlo, vhi;
-                        tx_hdr128(f.fl & 0xFFFFFFu, (uint64_t)f.len_lo | ((uint64_t)f.len_hi << 32), f.key, vlo, vhi);
+                        if (C == 2) {
+                            const u32x4 hv = s_hdr[j];
+                            vlo = hv.x | ((uint64_t)hv.y << 32);
+                            vhi = hv.z | ((uint64_t)hv.w << 32);
+                        } else {
+                            tx_hdr128(f.fl & 0xFFFFFFu, (uint64_t)f.len_lo | ((uint64_t)f.len_hi << 32), f.key, vlo,
+                                      vhi);
+                        }
                         shr_bytes(vlo, vhi, (uint32_t)(hb - f.o));
                         put_bytes(lo, hi, vlo, vhi, (uint32_t)(hb - c), (uint32_t)(he - c));
                     }
