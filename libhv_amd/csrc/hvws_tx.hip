@@ -447,8 +447,9 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
     // workgroup's LDS leaves room for 8 waves per SIMD (its 66 VGPRs allow 7)
     constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
-    // (lean: 16 more bytes per frame for its header bytes, built once)
-    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * (C == 2 ? 6 : 5)];
+    // (lean: 32 more bytes per frame for its header bytes, built once and
+    // placed in the two output chunks they can touch)
+    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * (C == 2 ? 8 : 5)];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
     uint64_t* const s_end = s_rb + 2 * MAXF;
@@ -456,7 +457,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     uint32_t* const s_key = reinterpret_cast<uint32_t*>(s_rb + 4 * MAXF);
     uint32_t* const s_fl = s_key + MAXF;
     tx_frel* const s_rel = reinterpret_cast<tx_frel*>(s_rb);
-    u32x4* const s_hdr = reinterpret_cast<u32x4*>(s_rb + 4 * MAXF);   // lean: after the MAXF records
+    u32x4* const s_win = reinterpret_cast<u32x4*>(s_rb + 4 * MAXF);   // lean: 2 per frame, after the records
     const uint64_t sa = sp_lo & ~15ull, sb = (sp_hi + 15) & ~15ull;   // staged source chunks [sa, sb)
     const bool staged = nf && nf <= MAXF && base + TILE <= out_len &&
                         sp_lo < sp_hi && sb - sa <= SPAN_MAX && sb <= plen;
@@ -465,7 +466,17 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         // payload chunks and the frame records load in one round trip into
         // LDS, then every output chunk is assembled from LDS (header pieces
         // from the records, payload pieces realigned from the staged bytes).
-        __shared__ u32x4 s_data[SPAN_MAX / 16 + 2];
+        // (lean: the span one chunk in, so a payload read aligned to its
+        // output chunk may start up to 15 bytes before the span; and a table
+        // of byte masks, entry n = bytes [0, n))
+        constexpr uint32_t LPAD = C == 2 ? 1u : 0u;
+        __shared__ u32x4 s_data[SPAN_MAX / 16 + 2 + LPAD];
+        __shared__ u32x4 s_mtab[C == 2 ? 17 : 1];
+        if (C == 2 && tid < 17) {
+            const uint64_t mlo = tid >= 8 ? ~0ull : (1ull << (8u * tid)) - 1ull;
+            const uint64_t mhi = tid <= 8 ? 0ull : (tid >= 16 ? ~0ull : (1ull << (8u * (tid - 8u))) - 1ull);
+            s_mtab[tid] = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+        }
         constexpr int SPU = (int)((SPAN_MAX / 16 + T - 1) / T);
         const uint32_t nch = (uint32_t)((sb - sa) / 16);
         u32x4 d[SPU];
@@ -487,10 +498,27 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
                 s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mk : 0u, fl,
                                           ln);
-                if (C == 2) {   // the header's bytes, once per frame instead of per chunk and lane
+                if (C == 2) {
+                    // the header's bytes, once per frame instead of per chunk
+                    // and lane, already where they go in the two 16-byte
+                    // output chunks from floor(o / 16) on (zeros around them)
                     uint64_t hlo, hhi;
                     tx_hdr128(fl, ln, mk, hlo, hhi);
-                    s_hdr[r] = u32x4{(uint32_t)hlo, (uint32_t)(hlo >> 32), (uint32_t)hhi, (uint32_t)(hhi >> 32)};
+                    const int32_t orel = s_rel[r].o;
+                    const uint32_t sb = (uint32_t)(orel - ((orel >> 4) << 4)) * 8u;   // bits, 0..120
+                    uint64_t w0, w1, w2, w3;
+                    if (sb == 0) {
+                        w0 = hlo, w1 = hhi, w2 = 0, w3 = 0;
+                    } else if (sb < 64) {
+                        w0 = hlo << sb, w1 = (hhi << sb) | (hlo >> (64u - sb)), w2 = hhi >> (64u - sb), w3 = 0;
+                    } else {
+                        const uint32_t s2 = sb - 64u;
+                        w0 = 0, w1 = hlo << s2;
+                        w2 = s2 ? (hhi << s2) | (hlo >> (64u - s2)) : hhi;
+                        w3 = s2 ? hhi >> (64u - s2) : 0;
+                    }
+                    s_win[2 * r] = u32x4{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+                    s_win[2 * r + 1] = u32x4{(uint32_t)w2, (uint32_t)(w2 >> 32), (uint32_t)w3, (uint32_t)(w3 >> 32)};
                 }
             }
         } else {
@@ -511,9 +539,9 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
 #pragma unroll
         for (int i = 0; i < SPU; ++i) {
             const uint32_t q = (uint32_t)i * (uint32_t)T + tid;
-            if (q < nch) s_data[q] = d[i];
+            if (q < nch) s_data[q + LPAD] = d[i];
         }
-        if (tid < 2) s_data[nch + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
+        if (tid < 2) s_data[nch + LPAD + tid] = u32x4{0, 0, 0, 0};   // lds16 may read 16 bytes past the span
         __syncthreads();
         const uint8_t* lb = reinterpret_cast<const uint8_t*>(s_data);
         if (C) {
@@ -546,25 +574,36 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                     if (f.o >= ce) break;
                     const int32_t hb = f.o > c ? f.o : c, he = f.ps < ce ? f.ps : ce;
                     if (hb < he) {   // header bytes
-                        uint64_t vlo, vhi;
-                        if (C == 2) {
-                            const u32x4 hv = s_hdr[j];
-                            vlo = hv.x | ((uint64_t)hv.y << 32);
-                            vhi = hv.z | ((uint64_t)hv.w << 32);
+                        if (C == 2) {   // the chunk is the first or second of the frame's window
+                            const u32x4 hv = s_win[2 * j + (c > ((f.o >> 4) << 4) ? 1 : 0)];
+                            lo |= hv.x | ((uint64_t)hv.y << 32);
+                            hi |= hv.z | ((uint64_t)hv.w << 32);
                         } else {
+                            uint64_t vlo, vhi;
                             tx_hdr128(f.fl & 0xFFFFFFu, (uint64_t)f.len_lo | ((uint64_t)f.len_hi << 32), f.key, vlo,
                                       vhi);
+                            shr_bytes(vlo, vhi, (uint32_t)(hb - f.o));
+                            put_bytes(lo, hi, vlo, vhi, (uint32_t)(hb - c), (uint32_t)(he - c));
                         }
-                        shr_bytes(vlo, vhi, (uint32_t)(hb - f.o));
-                        put_bytes(lo, hi, vlo, vhi, (uint32_t)(hb - c), (uint32_t)(he - c));
                     }
                     const int32_t pb = f.ps > c ? f.ps : c, pe = f.e < ce ? f.e : ce;
                     if (pb < pe) {   // payload bytes, realigned out of the staged span
                         uint64_t vlo, vhi;
-                        lds16(lb, (uint32_t)(f.q0 + pb), vlo, vhi);
-                        const uint32_t kw = tx_rotr(f.key, (((uint32_t)pb + (f.fl >> 24)) & 3u) * 8u);
-                        const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
-                        put_bytes(lo, hi, vlo ^ kk, vhi ^ kk, (uint32_t)(pb - c), (uint32_t)(pe - c));
+                        if (C == 2) {
+                            // read aligned to the output chunk (bytes land in
+                            // place) and keep [pb, pe) by two table masks
+                            lds16(lb, (uint32_t)(f.q0 + c + 16), vlo, vhi);
+                            const uint32_t kw = tx_rotr(f.key, (((uint32_t)c + (f.fl >> 24)) & 3u) * 8u);
+                            const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                            const u32x4 ms = s_mtab[pb - c], me = s_mtab[pe - c];
+                            lo |= (vlo ^ kk) & ~(ms.x | ((uint64_t)ms.y << 32)) & (me.x | ((uint64_t)me.y << 32));
+                            hi |= (vhi ^ kk) & ~(ms.z | ((uint64_t)ms.w << 32)) & (me.z | ((uint64_t)me.w << 32));
+                        } else {
+                            lds16(lb, (uint32_t)(f.q0 + pb), vlo, vhi);
+                            const uint32_t kw = tx_rotr(f.key, (((uint32_t)pb + (f.fl >> 24)) & 3u) * 8u);
+                            const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+                            put_bytes(lo, hi, vlo ^ kk, vhi ^ kk, (uint32_t)(pb - c), (uint32_t)(pe - c));
+                        }
                     }
                     if (f.e >= ce) break;   // the output is dense: the next frame starts at e
                 }
