@@ -1038,7 +1038,6 @@ __device__ __forceinline__ void door_size(const uint32_t* l, uint32_t q, uint32_
 constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames (HVWS_DOOR_WALK, default on)
 constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (HVWS_DOOR_NT)
 constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (HVWS_DOOR_PRELOAD)
-constexpr uint32_t DOOR_F_CXOR = 8u;      // XOR fused into the stores, chunk by chunk (HVWS_DOOR_CXOR, default on)
 
 // Chunks [c_lo, c_hi) of the data area (both multiples of 64) into LDS at the
 // same offsets by LDS-DMA: no registers (an array of 16-byte values per
@@ -1377,39 +1376,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             // alone (plain read-modify-write); a payload's first and last
             // chunks may hold another record's bytes too (LDS atomic XOR per
             // dword).  Then every chunk of the read goes to dout.
-            if (s_unmask && (flags & DOOR_F_CXOR) && n <= nl) {
-                // Chunk by chunk, fused with the stores (no XOR pass over LDS
-                // and no barrier before the stores): each thread's chunks rise,
-                // so its first record that ends after the chunk only moves on;
-                // every masked payload the chunk meets contributes its key word
-                // cut to the bytes it covers.
-                if (tid == 0) s_t[6] = s_t[2];
-                uint32_t jb = 0;
-                const uint32_t n32 = (uint32_t)n;
-                for (uint64_t c64 = (uint64_t)tid * 16u; c64 < L; c64 += (uint64_t)kDoorThreads * 16u) {
-                    const uint32_t c = (uint32_t)c64;
-                    while (jb < n32 && (uint32_t)(lrec[jb].pay_off + lrec[jb].pay_len) <= c) ++jb;
-                    uint32_t x[4] = {0u, 0u, 0u, 0u};
-                    for (uint32_t j = jb; j < n32; ++j) {
-                        const drec& f = lrec[j];
-                        const uint32_t po = (uint32_t)f.pay_off;
-                        if (po >= c + 16u) break;
-                        const uint32_t pl = (uint32_t)f.pay_len, info = f.info;
-                        if (!(info & F_MASK) || pl == 0) continue;
-                        const uint32_t pe = po + pl;
-                        const uint32_t kw = rotr32(f.key, 8u * ((((info >> 8) & 3u) - po) & 3u));
-                        const int32_t a = po > c ? (int32_t)(po - c) : 0, e = pe < c + 16u ? (int32_t)(pe - c) : 16;
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) {
-                            const int32_t lo = a - 4 * d < 0 ? 0 : (a - 4 * d), hi = e - 4 * d > 4 ? 4 : (e - 4 * d);
-                            if (hi > lo)
-                                x[d] ^= kw & (hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
-                        }
-                    }
-                    *reinterpret_cast<u32x4*>(dout + c64) =
-                        *reinterpret_cast<const u32x4*>(lds + c64) ^ u32x4{x[0], x[1], x[2], x[3]};
-                }
-            } else if (s_unmask) {
+            if (s_unmask) {
                 uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
                 const uint32_t wave = tid >> 6, lane = tid & 63u;
                 auto unmask_rec = [&](const drec& f) {
@@ -1486,8 +1453,7 @@ hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t
     auto knob = [](const char* name, uint32_t dflt) { return getenv(name) ? (uint32_t)atoi(getenv(name)) : dflt; };
     static const uint32_t flags = (knob("HVWS_DOOR_WALK", 1) ? DOOR_F_WALK : 0u) |
                                   (knob("HVWS_DOOR_NT", 0) ? DOOR_F_NT : 0u) |
-                                  (knob("HVWS_DOOR_PRELOAD", 0) ? DOOR_F_PRELOAD : 0u) |
-                                  (knob("HVWS_DOOR_CXOR", 1) ? DOOR_F_CXOR : 0u);
+                                  (knob("HVWS_DOOR_PRELOAD", 0) ? DOOR_F_PRELOAD : 0u);
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
                        idle_ticks, first_seq, epoch, flags);
     return hipGetLastError();
