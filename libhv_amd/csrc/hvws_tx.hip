@@ -128,14 +128,6 @@ constexpr uint32_t BUILD_MAXF = 128;   // frames per boundary tile staged in LDS
 
 __device__ __forceinline__ uint32_t tx_rotr(uint32_t x, uint32_t r) { return r ? (x >> r) | (x << (32u - r)) : x; }
 
-// The lane id, computed where it is used (volatile: not hoisted or merged,
-// so no register holds it across the kernel for the allocator to spill).
-__device__ __forceinline__ uint32_t lane_id_now() {
-    uint32_t v;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
-    return v;
-}
-
 // OR bytes [0, b1 - b0) of the 16-byte little-endian value (vlo, vhi) into
 // bytes [b0, b1) of the chunk (olo, ohi); 0 <= b0 < b1 <= 16.
 __device__ __forceinline__ void put_bytes(uint64_t& olo, uint64_t& ohi, uint64_t vlo, uint64_t vhi, uint32_t b0,
@@ -449,16 +441,15 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     const uint64_t nf = k_hi > k_lo ? k_hi - k_lo : 0;
     // staged source bytes per boundary tile (LDS): the tile's payload bytes,
     // with room for gaps between payloads
-    constexpr bool LEAN = C >= 2;   // 3: the lean form cut to 8 records and 64 B of slack (8 tiles per SIMD)
-    constexpr uint64_t SPAN_MAX = TILE + (C == 3 ? 64 : (C == 2 ? 256 : 1024));
+    constexpr uint64_t SPAN_MAX = TILE + (C == 2 ? 256 : 1024);
     // the tile's frame records, 40 bytes each: the 64-bit per-field arrays,
     // or (C) the compact records in the same storage
     // C == 2 (lean): 16 records and 256 bytes of span slack, so a one-wave
     // workgroup's LDS leaves room for 8 waves per SIMD (its 66 VGPRs allow 7)
-    constexpr uint32_t MAXF = C == 3 ? 8u : (C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T));
+    constexpr uint32_t MAXF = C == 2 ? 16u : (T >= 128 ? BUILD_MAXF : (uint32_t)T);
     // (lean: 32 more bytes per frame for its header bytes, built once and
     // placed in the two output chunks they can touch)
-    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * (LEAN ? 8 : 5)];
+    __shared__ __attribute__((aligned(16))) uint64_t s_rb[MAXF * (C == 2 ? 8 : 5)];
     uint64_t* const s_off = s_rb;
     uint64_t* const s_ps = s_rb + MAXF;
     uint64_t* const s_end = s_rb + 2 * MAXF;
@@ -471,8 +462,6 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     const bool staged = nf && nf <= MAXF && base + TILE <= out_len &&
                         sp_lo < sp_hi && sb - sa <= SPAN_MAX && sb <= plen;
     if (staged) {
-        // (C == 3: the lane id recomputed in this block, T == 64)
-        const uint32_t tid = C == 3 ? lane_id_now() : threadIdx.x;
         // Boundary tile with its source span known up front: the span's
         // payload chunks and the frame records load in one round trip into
         // LDS, then every output chunk is assembled from LDS (header pieces
@@ -480,10 +469,10 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         // (lean: the span one chunk in, so a payload read aligned to its
         // output chunk may start up to 15 bytes before the span; and a table
         // of byte masks, entry n = bytes [0, n))
-        constexpr uint32_t LPAD = LEAN ? 1u : 0u;
+        constexpr uint32_t LPAD = C == 2 ? 1u : 0u;
         __shared__ u32x4 s_data[SPAN_MAX / 16 + 2 + LPAD];
-        __shared__ u32x4 s_mtab[LEAN ? 17 : 1];
-        if (LEAN && tid < 17) {
+        __shared__ u32x4 s_mtab[C == 2 ? 17 : 1];
+        if (C == 2 && tid < 17) {
             const uint64_t mlo = tid >= 8 ? ~0ull : (1ull << (8u * tid)) - 1ull;
             const uint64_t mhi = tid <= 8 ? 0ull : (tid >= 16 ? ~0ull : (1ull << (8u * (tid - 8u))) - 1ull);
             s_mtab[tid] = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
@@ -509,7 +498,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
                 s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mk : 0u, fl,
                                           ln);
-                if (LEAN) {
+                if (C == 2) {
                     // the header's bytes, once per frame instead of per chunk
                     // and lane, already where they go in the two 16-byte
                     // output chunks from floor(o / 16) on (zeros around them)
@@ -566,7 +555,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 // (independent broadcast reads), a binary search otherwise;
                 // lean: advanced from the previous chunk's
                 uint32_t j = 0;
-                if (LEAN) {
+                if (C == 2) {
                     while (jb < nf32 && s_rel[jb].e <= c) ++jb;
                     j = jb;
                 } else if (nf32 <= 16) {
@@ -585,7 +574,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                     if (f.o >= ce) break;
                     const int32_t hb = f.o > c ? f.o : c, he = f.ps < ce ? f.ps : ce;
                     if (hb < he) {   // header bytes
-                        if (LEAN) {   // the chunk is the first or second of the frame's window
+                        if (C == 2) {   // the chunk is the first or second of the frame's window
                             const u32x4 hv = s_win[2 * j + (c > ((f.o >> 4) << 4) ? 1 : 0)];
                             lo |= hv.x | ((uint64_t)hv.y << 32);
                             hi |= hv.z | ((uint64_t)hv.w << 32);
@@ -600,7 +589,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                     const int32_t pb = f.ps > c ? f.ps : c, pe = f.e < ce ? f.e : ce;
                     if (pb < pe) {   // payload bytes, realigned out of the staged span
                         uint64_t vlo, vhi;
-                        if (LEAN) {
+                        if (C == 2) {
                             // read aligned to the output chunk (bytes land in
                             // place) and keep [pb, pe) by two table masks
                             lds16(lb, (uint32_t)(f.q0 + c + 16), vlo, vhi);
@@ -664,7 +653,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     // SIMD, and the spilled lane index was reloaded from scratch between the
     // staged loads above, each reload waiting for every load before it
     // (r4ae_raw / r4af_raw / r4ag_raw: c2 0.46-0.47 -> 0.41-0.44 ms).
-    if (LEAN && nf && nf <= MAXF && base + TILE <= out_len) {
+    if (C == 2 && nf && nf <= MAXF && base + TILE <= out_len) {
         for (uint32_t r = tid; r < nf; r += T) {
             const uint64_t k = k_lo + r;
             const uint32_t fl = flags[k];
@@ -722,7 +711,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
         }
         return;
     }
-    if (!LEAN && nf && nf <= MAXF && base + TILE <= out_len) {
+    if (C != 2 && nf && nf <= MAXF && base + TILE <= out_len) {
         // Boundary tile: the tile's frames staged in LDS; chunks inside one
         // payload still stream (loads issued for all U chunks first), chunks
         // holding header bytes or a frame boundary are assembled byte by byte.
@@ -878,8 +867,7 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(2, 256, 2, false, false, true, 0)   \
     X(3, 64, 2, false, false, true, 1)    \
     X(4, 128, 2, false, false, true, 1)   \
-    X(5, 64, 4, false, false, true, 2)    \
-    X(6, 64, 4, false, false, true, 3)
+    X(5, 64, 4, false, false, true, 2)
 
 namespace {
 // $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
@@ -888,7 +876,7 @@ namespace {
 int build_pick(uint64_t out_len, uint64_t n) {
     const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
-    if (forced >= 0 && forced < 7) return forced;
+    if (forced >= 0 && forced < 6) return forced;
     return n && out_len / n < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
@@ -907,7 +895,7 @@ const char* build_kernel_name(int v) {
     switch (v) {
 #define X(I, T, U, S, N, F, C) \
     case I:                    \
-        return C == 3 ? "k_build<" #T "x" #U ",lean8>" : C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
+        return C == 2 ? "k_build<" #T "x" #U ",lean>" : (C ? "k_build<" #T "x" #U ">" : "k_build<" #T "x" #U ",wide>");
         HVWS_BUILD_GEOMS(X)
 #undef X
     }

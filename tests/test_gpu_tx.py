@@ -232,7 +232,7 @@ def test_build_one_moved_payload(eng):
     assert got == H.build_frames_ref(frames)
 
 
-@pytest.mark.parametrize("v", ["0", "1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("v", ["0", "1", "2", "3", "4", "5"])
 def test_build_every_geometry(eng, v, monkeypatch):
     """Every k_build geometry ($HVWS_BUILD) builds small frames, edge lengths
     and misaligned payloads byte for byte like the reference and reports its
