@@ -2603,14 +2603,10 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     if (spans_ok) HIP_OR(c->tx_span.ensure(ntiles * 16 + 16), HVWS_ENOMEM);
     // the timed device work (hvws_last_kernel_ms): tile index, spans, build
     HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
-    HIP_OR(launch_tile_index(off, c->tx_size.as<uint64_t>(), n, nullptr, c->tx_tiles.as<uint32_t>(), ntiles, tile,
-                             c->stream),
+    uint64_t* span = spans_ok ? c->tx_span.as<uint64_t>() : nullptr;
+    HIP_OR(launch_tx_index(off, c->tx_size.as<uint64_t>(), d_pay_off, d_len, d_flags, n, ntiles, tile,
+                           c->tx_tiles.as<uint32_t>(), span, c->stream),
            HVWS_EHIP);
-    uint64_t* span = nullptr;
-    if (spans_ok) {
-        span = c->tx_span.as<uint64_t>();
-        HIP_OR(launch_tx_spans(d_pay_off, d_len, d_flags, off, n, ntiles, tile, span, c->stream), HVWS_EHIP);
-    }
     HIP_OR(launch_build(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
                         c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), span, n, v, c->stream),
            HVWS_EHIP);

@@ -240,6 +240,13 @@ hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uin
                              unsigned long long* bad, hipStream_t st);
 hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t nfr, const uint64_t* nfr_dev,
                              uint32_t* tile_first, uint64_t ntiles, uint64_t tile, hipStream_t st);
+// Tile index marks: a tile no frame's scatter reached (k_tile_fixup searches
+// it); a frame scatters itself into at most TILE_SPAN_MAX tiles.
+constexpr uint32_t TILE_MARK = 0xFFFFFFFFu;
+constexpr uint64_t TILE_SPAN_MAX = 64;
+// k_tile_fixup alone (tile_first already scattered).
+hipError_t launch_tile_fixup(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
+                             uint64_t ntiles, uint64_t tile, hipStream_t st);
 // Small batches, whole path in one launch (one wave per segment): records
 // into slots[slot_base[s]..], then compacted into h_rec (pinned host) when
 // they fit h_rec_cap; results into h_out[s]; unmasked chunks into h_rx
@@ -367,10 +374,14 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
 int tx_variant(uint64_t out_len, uint64_t n);
 uint64_t tx_tile(int v);   // output bytes per k_build workgroup
 const char* build_kernel_name(int v);
-// span: 2 words per k_build tile (ntiles of `tile` bytes), filled here.
-hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
-                           uint64_t n, uint64_t ntiles, uint64_t tile, uint64_t* span, hipStream_t st);
-// span: from launch_tx_spans, or nullptr (boundary tiles load their records first)
+// The transmit tile index and (span != nullptr: 2 words per k_build tile)
+// source spans in three launches: one fill of both, one pass over the frames
+// doing the tile scatter and the span runs together, k_tile_fixup (in place
+// of a tile index's fill, scatter and fixup plus a span fill and pass).
+hipError_t launch_tx_index(const uint64_t* out_off, const uint64_t* size, const uint64_t* pay_off, const uint64_t* len,
+                           const uint8_t* flags, uint64_t n, uint64_t ntiles, uint64_t tile, uint32_t* tile_first,
+                           uint64_t* span, hipStream_t st);
+// span: from launch_tx_index, or nullptr (boundary tiles load their records first)
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                         const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,

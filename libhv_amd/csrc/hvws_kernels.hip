@@ -1730,8 +1730,7 @@ hipError_t launch_ends_check(const uint64_t* off, const uint64_t* len, const uin
 // config 3 (4M tiles x 20 dependent loads).
 // nfr_p (device) overrides nfr_v when given: the frame count of a batch can
 // stay on the device, so a small batch needs no host round trip before EMIT.
-constexpr uint32_t TILE_MARK = 0xFFFFFFFFu;
-constexpr uint64_t TILE_SPAN_MAX = 64;
+// (TILE_MARK, TILE_SPAN_MAX: hvws_internal.h)
 
 __device__ __forceinline__ void tile_scatter_body(const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
                                                   uint64_t nfr, uint32_t* __restrict__ tile_first, uint64_t ntiles,
@@ -2194,6 +2193,14 @@ hipError_t launch_tile_index(const uint64_t* off, const uint64_t* len, uint64_t 
     hipLaunchKernelGGL(k_tile_scatter, dim3(2048), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_tile_fixup, dim3(blocks), dim3(256), 0, st, off, len, nfr, nfr_dev, tile_first, ntiles, tile);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_fixup(const uint64_t* off, const uint64_t* len, uint64_t nfr, uint32_t* tile_first,
+                             uint64_t ntiles, uint64_t tile, hipStream_t st) {
+    const uint32_t blocks = (uint32_t)((ntiles + 1 + 255) / 256);
+    hipLaunchKernelGGL(k_tile_fixup, dim3(blocks), dim3(256), 0, st, off, len, nfr, (const uint64_t*)nullptr, tile_first,
+                       ntiles, tile);
     return hipGetLastError();
 }
 

@@ -287,10 +287,39 @@ __device__ __forceinline__ void span_run_atomics(unsigned long long* span, uint6
     }
 }
 
-__global__ void k_tx_spans(const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len,
-                           const uint8_t* __restrict__ flags, const uint64_t* __restrict__ out_off, uint64_t n,
-                           uint64_t tile, unsigned long long* __restrict__ span) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // whole waves run the shuffles
+
+// The transmit tile index and spans together.  Fill: tile_first[0..ntiles]
+// marked, spans empty.  Pass: frame k scatters itself into tile_first (as
+// k_tile_scatter: the tiles whose first byte its output covers, at most
+// TILE_SPAN_MAX) and its payload's span runs (one atomic min/max pair per run
+// of lanes sharing a tile, span_run_atomics); the marked
+// tiles are left to k_tile_fixup.
+__global__ void k_tx_index_fill(uint32_t* __restrict__ tile_first, unsigned long long* __restrict__ span,
+                                uint64_t ntiles) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t <= ntiles) tile_first[t] = TILE_MARK;
+    if (span && t < ntiles) {
+        span[2 * t] = ~0ull;
+        span[2 * t + 1] = 0ull;
+    }
+}
+
+__global__ void k_tx_index(const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
+                           const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len,
+                           const uint8_t* __restrict__ flags, uint64_t n, uint64_t ntiles, uint64_t tile,
+                           uint32_t* __restrict__ tile_first, unsigned long long* __restrict__ span) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // whole waves run the span shuffles
+    if (k < n) {
+        const uint64_t lo = k ? out_off[k - 1] + size[k - 1] : 0, hi = out_off[k] + size[k];
+        if (hi > lo) {
+            const uint64_t t0 = (lo + tile - 1) / tile;
+            uint64_t t1 = (hi + tile - 1) / tile;
+            if (t1 > ntiles + 1) t1 = ntiles + 1;
+            if (t1 > t0 && t1 - t0 <= TILE_SPAN_MAX)
+                for (uint64_t t = t0; t < t1; ++t) tile_first[t] = (uint32_t)k;
+        }
+    }
+    if (!span) return;
     const uint64_t ln = k < n ? len[k] : 0;
     uint64_t t0 = ~0ull, t1 = ~0ull, l0 = 0, h0 = 0, l1 = 0, h1 = 0;
     if (ln) {
@@ -303,17 +332,9 @@ __global__ void k_tx_spans(const uint64_t* __restrict__ pay_off, const uint64_t*
         h1 = src + ln;
     }
     span_run_atomics(span, t0, l0, h0);
-    // last payload tile, when it is another one (else its piece is in the first run)
     span_run_atomics(span, t1 != t0 ? t1 : ~0ull, l1, h1);
 }
 
-__global__ void k_span_init(unsigned long long* __restrict__ span, uint64_t ntiles) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < ntiles) {
-        span[2 * t] = ~0ull;
-        span[2 * t + 1] = 0ull;
-    }
-}
 
 // A boundary tile's frame in LDS (k_build's staged path, C): positions
 // relative to the tile's first output byte.  o and ps (header start and end)
@@ -356,7 +377,7 @@ __device__ __forceinline__ void lds16(const uint8_t* a, uint32_t q, uint64_t& lo
 }
 
 // One output tile of k_build: its frame range [k_lo, k_hi) (tile_first of t
-// and t + 1) and its source span [sp_lo, sp_hi) (k_tx_spans) are loaded by the
+// and t + 1) and its source span [sp_lo, sp_hi) (k_tx_index) are loaded by the
 // caller -- per tile, or one tile ahead in the grid-stride loop.
 struct build_idx {
     uint64_t k_lo, k_hi, sp_lo, sp_hi;
@@ -905,14 +926,18 @@ const char* build_kernel_name(int v) {
 int tx_variant(uint64_t out_len, uint64_t n) { return build_pick(out_len, n); }
 uint64_t tx_tile(int v) { return build_tile(v); }
 
-hipError_t launch_tx_spans(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint64_t* out_off,
-                           uint64_t n, uint64_t ntiles, uint64_t tile, uint64_t* span, hipStream_t st) {
-    hipLaunchKernelGGL(k_span_init, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256), 0, st,
-                       reinterpret_cast<unsigned long long*>(span), ntiles);
-    if (n == 0) return hipGetLastError();
-    hipLaunchKernelGGL(k_tx_spans, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, pay_off, len, flags, out_off, n,
-                       tile, reinterpret_cast<unsigned long long*>(span));
-    return hipGetLastError();
+
+hipError_t launch_tx_index(const uint64_t* out_off, const uint64_t* size, const uint64_t* pay_off, const uint64_t* len,
+                           const uint8_t* flags, uint64_t n, uint64_t ntiles, uint64_t tile, uint32_t* tile_first,
+                           uint64_t* span, hipStream_t st) {
+    unsigned long long* sp = reinterpret_cast<unsigned long long*>(span);
+    hipLaunchKernelGGL(k_tx_index_fill, dim3((uint32_t)((ntiles + 1 + 255) / 256)), dim3(256), 0, st, tile_first, sp,
+                       ntiles);
+    if (n) hipLaunchKernelGGL(k_tx_index, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, out_off, size, pay_off,
+                              len, flags, n, ntiles, tile, tile_first, sp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_tile_fixup(out_off, size, n, tile_first, ntiles, tile, st);
 }
 
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,

@@ -265,7 +265,7 @@ def test_build_geometry_by_frame_size(eng, monkeypatch):
 @pytest.mark.parametrize("order", ["packed", "gaps", "shuffled"])
 def test_build_boundary_tiles_span_staged(eng, spans, order, monkeypatch):
     """Boundary tiles of the general layout stage their source span in LDS
-    together with the frame records (k_tx_spans; $HVWS_BUILD_SPANS=0: the
+    together with the frame records (k_tx_index; $HVWS_BUILD_SPANS=0: the
     records-first tiles).  Small frames packed back to back, with gaps, and
     with payloads in shuffled order (spans past the LDS area fall back to the
     records-first path); every byte against the reference."""
