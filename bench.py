@@ -122,42 +122,75 @@ def launch_ranks(args) -> int:
     port = s.getsockname()[1]
     s.close()
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
-                                      start_new_session=True))
-    chunks = []   # rank 0's stdout, read beside the polling loop (a failed rank must not wait on it)
-    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read().decode()), daemon=True)
-    reader.start()
-    rcs = [None] * n
-    failed = False
-    while any(rc is None for rc in rcs):
-        for r, p in enumerate(procs):
-            if rcs[r] is None:
-                rcs[r] = p.poll()
-                if rcs[r] not in (None, 0):
-                    failed = True
-        if failed:
-            break
-        time.sleep(0.05)
-    if failed:
-        for r, p in enumerate(procs):
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
             if p.poll() is None:
-                os.killpg(p.pid, signal.SIGTERM)
-        for r, p in enumerate(procs):
-            try:
-                rcs[r] = p.wait(timeout=30)
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-                rcs[r] = p.wait()
-        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr, flush=True)
-        return 1
-    reader.join(timeout=30)
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    # a launcher stopped by a signal (the driver's timeout) stops its ranks
+    # too: they run in sessions of their own and would keep their GPUs
+    def forward(signum, _frame):
+        stop_all(signum)
+        raise SystemExit(128 + signum)
+
+    old_handlers = {sg: signal.signal(sg, forward) for sg in (signal.SIGTERM, signal.SIGINT)}
+    limit = float(os.environ.get("HVWS_BENCH_RANK_TIMEOUT", "0") or 0)   # seconds, 0 = none
+    t_start = time.monotonic()
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                          stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                          start_new_session=True))
+        chunks = []   # rank 0's stdout, read beside the polling loop (a failed rank must not wait on it)
+        reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read().decode()), daemon=True)
+        reader.start()
+        rcs = [None] * n
+        failed = False
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+                    if rcs[r] not in (None, 0):
+                        failed = True
+            if limit and time.monotonic() - t_start > limit:
+                print(f"bench.py: ranks still running after {limit:.0f} s (HVWS_BENCH_RANK_TIMEOUT)",
+                      file=sys.stderr, flush=True)
+                failed = True
+            if failed:
+                break
+            time.sleep(0.05)
+        if failed:
+            stop_all()
+            for r, p in enumerate(procs):
+                try:
+                    rcs[r] = p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    rcs[r] = p.wait()
+            print(f"bench.py: rank exit codes {rcs}", file=sys.stderr, flush=True)
+            return 1
+        reader.join(timeout=30)
+    finally:
+        stop_all(signal.SIGKILL)
+        for sg, h in old_handlers.items():
+            signal.signal(sg, h)
     line = [ln for ln in "".join(chunks).splitlines() if ln.startswith("{")]
     if not line:
         print("bench.py: rank 0 printed no result line", file=sys.stderr, flush=True)
+        return 1
+    # the line must name N distinct cards (outside a rehearsal)
+    try:
+        buses = [r.get("pci_bus_id") for r in json.loads(line[-1]).get("timing", {}).get("per_rank", [])]
+    except ValueError:
+        buses = []
+    if len(buses) != n or ("HVWS_BENCH_DEVICE" not in os.environ and len(set(buses)) != n):
+        print(f"bench.py: rank 0's line names devices {buses} for {n} ranks", file=sys.stderr, flush=True)
         return 1
     print(line[-1], flush=True)
     return 0
@@ -683,6 +716,27 @@ def tx_leg(eng, plan, dp, rx, rx_plain: bool, segs, tpath: str) -> dict:
     }
 
 
+def bus_number(bus_id: str) -> int:
+    """PCI bus id "dddd:bb:dd.f" as one integer (gathered over gloo as a float)."""
+    dom, bus, df = bus_id.split(":")
+    dv, fn = df.split(".")
+    return (int(dom, 16) << 16) | (int(bus, 16) << 8) | (int(dv, 16) << 3) | int(fn, 16)
+
+
+def bus_name(n: int) -> str:
+    return f"{n >> 16:04x}:{(n >> 8) & 0xFF:02x}:{(n >> 3) & 0x1F:02x}.{n & 7:x}"
+
+
+def check_distinct_devices(bus_ids, rank: int) -> None:
+    """An N-rank line must come from N cards: two ranks on one PCI bus id
+    end the run (exit status 3), except in a rehearsal (HVWS_BENCH_DEVICE
+    pins every rank to one card on purpose)."""
+    if "HVWS_BENCH_DEVICE" in os.environ or len(set(bus_ids)) == len(bus_ids):
+        return
+    print(f"bench.py: rank {rank}: ranks share a device: {bus_ids}", file=sys.stderr, flush=True)
+    raise SystemExit(3)
+
+
 def fixture_for(cfg: str, rank: int):
     """(name, entry) of the committed reference digests for this rank's batch
     (tests/golden/configs.json: c5_rank<r> = the c3-shaped batch of seed
@@ -735,7 +789,11 @@ def dry_run(args, rank: int, world: int, local: int, dist) -> None:
         dist.barrier()
     t0 = time.perf_counter()
     t1 = time.perf_counter()
-    trows = gather_rows(dist, [t0, t1, 0.0])
+    # no device: a stand-in bus id per local rank ($HVWS_BENCH_DRYRUN_BUS pins
+    # every rank to one, as two ranks on one card would report)
+    bus = os.environ.get("HVWS_BENCH_DRYRUN_BUS", f"0000:{local + 1:02x}:00.0")
+    trows = gather_rows(dist, [t0, t1, 0.0, local, local, bus_number(bus)])
+    check_distinct_devices([bus_name(int(b)) for b in trows[:, 5]], rank)
     fx_name, fx = fixture_for("c3", rank)
     vrows = gather_rows(dist, [rank, local, int(plan.seed), -1 if fx is None else 1])
     if rank == 0:
@@ -743,7 +801,9 @@ def dry_run(args, rank: int, world: int, local: int, dist) -> None:
             "metric": "device-resident WS unmask GiB/s, 64 KiB masked frames, 1/2/4/8 MI355X",
             "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": True,
             "timing": {"elapsed_s": span_of(trows),
-                       "per_rank": [{"rank": int(r), "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3)}
+                       "per_rank": [{"rank": int(r), "device": int(trows[r, 3]), "hip_device": int(trows[r, 4]),
+                                     "pci_bus_id": bus_name(int(trows[r, 5])),
+                                     "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3)}
                                     for r in range(trows.shape[0])]},
             "verified": {"ranks": [{"rank": int(v[0]), "local_rank": int(v[1]), "seed": int(v[2]),
                                     "fixture": f"c5_rank{int(v[0])}" if v[3] >= 0 else None} for v in vrows]},
@@ -789,6 +849,7 @@ def main():
     # works); HVWS_BENCH_DEVICE pins every rank to one card for rehearsals.
     ndev = max(1, libhv_amd.device_count())
     device = int(os.environ.get("HVWS_BENCH_DEVICE", local % ndev))
+    bus_id, hip_device = libhv_amd.device_identity(device)
     eng = libhv_amd.Engine(device)
     t = time.perf_counter()
     plan = rank_plan(cfg, rank, args.segments)
@@ -834,8 +895,10 @@ def main():
     eng.sync()
     t1 = time.perf_counter()
     barrier()
-    trows = gather_rows(dist, [t0, t1, span_ms.value])
+    trows = gather_rows(dist, [t0, t1, span_ms.value, device, hip_device, bus_number(bus_id)])
     elapsed = span_of(trows)
+    # every rank on its own card (a rehearsal under HVWS_BENCH_DEVICE excepted)
+    check_distinct_devices([bus_name(int(b)) for b in trows[:, 5]], rank)
     scan_path = L.hvws_last_scan_path(eng.ctx)
     times = eng.step_times(min(args.steps, 32))
     scan_ms = [t[0] for t in times]
@@ -909,7 +972,9 @@ def main():
             "method": "per device: hvws_span_begin/end markers on the context's streams (HIP events); "
                       "across devices: latest end - earliest start on the host CLOCK_MONOTONIC after a barrier",
             "elapsed_s": round(elapsed, 6),
-            "per_rank": [{"rank": int(r), "device_span_ms": round(float(trows[r, 2]), 3),
+            "per_rank": [{"rank": int(r), "device": int(trows[r, 3]), "hip_device": int(trows[r, 4]),
+                          "pci_bus_id": bus_name(int(trows[r, 5])),
+                          "device_span_ms": round(float(trows[r, 2]), 3),
                           "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3),
                           "end_offset_ms": round(float(trows[r, 1] - trows[:, 0].min()) * 1e3, 3)}
                          for r in range(trows.shape[0])],

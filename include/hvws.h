@@ -96,6 +96,10 @@ void        hvws_ctx_destroy(hvws_ctx* ctx);
 const char* hvws_last_error(void);                /* thread-local */
 void*       hvws_ctx_stream(hvws_ctx* ctx);       /* hipStream_t */
 int         hvws_ctx_device(hvws_ctx* ctx);
+/* The PCI bus id ("dddd:bb:dd.f", NUL-terminated, len >= 13) of HIP device
+ * `device` and, in *cur, the device hipGetDevice reports once it is selected:
+ * a multi-GPU run names the physical card each rank used. */
+int         hvws_device_identity(int device, char* bus_id, int len, int* cur);
 
 void* hvws_dev_alloc(hvws_ctx* ctx, uint64_t bytes);
 void  hvws_dev_free(hvws_ctx* ctx, void* p);
@@ -290,6 +294,11 @@ const char* hvws_build_kernel_name(void);
  * (mean frame < 4 KiB), or $HVWS_BUILD's.  Results never
  * depend on it. */
 const char* hvws_last_build_kernel(hvws_ctx* ctx);
+/* 1 when the last hvws_build_frames on ctx found a uniform layout (every frame
+ * the same size and payload length, payload offsets a + k*b with b >= 0) and
+ * built it without a tile index (each tile finds its frames from its
+ * position); 0 otherwise.  Results never depend on it. */
+int hvws_last_build_uniform(hvws_ctx* ctx);
 
 /* ---- handshake, device resident --------------------------------------- */
 /* Sec-WebSocket-Accept for n upgrade requests: accept + 32*i receives the 28
@@ -345,6 +354,14 @@ int hvws_set_door(hvws_ctx* ctx, int on);
 /* out = {worker launches, requests posted, requests the current worker
  * served, worker resident now} (tests, benchmarks). */
 int hvws_door_stats(hvws_ctx* ctx, uint64_t out[4]);
+/* Process-wide worker failures since the process started: out = {worker
+ * streams that did not drain within 5 s (their context keeps the stream and
+ * mailbox and never reuses them), requests a worker did not answer (that
+ * context launches per call from then on)}.  Each is also reported on stderr
+ * when it happens; both are 0 in a healthy process (the test session fails
+ * otherwise).  At most $HVWS_DOOR_MAX (default 8) contexts per device hold a
+ * worker stream at once; reads on further contexts launch per call. */
+int hvws_door_health(uint64_t out[2]);
 /* Idle time after which workers launched from now on park (microseconds;
  * 0 = the default, 5000).  Returns the previous value.  The runtime's frees
  * (hipFree, hipHostFree, hipHostUnregister) wait for every stream, a resident

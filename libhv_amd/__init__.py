@@ -84,6 +84,7 @@ _SIGS = {
     "hvws_last_error": (ctypes.c_char_p, []),
     "hvws_ctx_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "hvws_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "hvws_device_identity": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "hvws_dev_alloc": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint64]),
     "hvws_dev_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "hvws_host_alloc": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -181,6 +182,7 @@ _SIGS = {
     "hvws_last_sieve_windows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_build_kernel_name": (ctypes.c_char_p, []),
     "hvws_last_build_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "hvws_last_build_uniform": (ctypes.c_int, [ctypes.c_void_p]),
     "hvws_span_begin": (ctypes.c_int, [ctypes.c_void_p]),
     "hvws_span_end": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "hvws_set_door": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -188,6 +190,7 @@ _SIGS = {
     "hvws_debug_backtraces": (ctypes.c_int, [ctypes.c_int]),
     "hvws_door_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_door_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hvws_door_health": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_door_idle_us": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_door_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hvws_set_small_batch_limit": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -497,3 +500,12 @@ class TxPlan:
 
 def device_count() -> int:
     return lib().hvws_device_count()
+
+
+def device_identity(device: int) -> tuple:
+    """(PCI bus id, the device hipGetDevice reports once `device` is
+    selected): which physical card a rank ran on."""
+    buf = ctypes.create_string_buffer(64)
+    cur = ctypes.c_int(-1)
+    _check(lib().hvws_device_identity(device, buf, 64, ctypes.byref(cur)), "hvws_device_identity")
+    return buf.value.decode(), int(cur.value)

@@ -242,6 +242,7 @@ struct hvws_ctx {
     hbuf h_tx;
     bool ev_build = false;
     int tx_variant = 0;   // k_build geometry of the last hvws_build_frames
+    bool tx_uniform = false;   // ... and whether it built a uniform layout without a tile index
     // last scan
     uint32_t nseg = 0;
     uint64_t nfr = 0;
@@ -272,6 +273,10 @@ struct hvws_ctx {
     void* d_door_req = nullptr;
     bool door_live = false;     // launched and not yet seen to have ended
     bool door_wedged = false;   // its stream stayed busy past every bound: stream and mailbox are left alone
+    bool door_broken = false;   // a request went unanswered: this context launches per call from now on
+    // The HIP runtime call this context's worker lifecycle or teardown is
+    // in (nullptr: none): a wedge report or hvws_debug_dump names the call.
+    std::atomic<const char*> at{nullptr};
     uint64_t door_seq = 0;      // last request number posted
     uint64_t door_epoch = 0;    // launches so far; the worker writes its epoch to `exited` as it ends
     std::mutex door_m;          // one caller at a time: the owning thread, a free on another thread, exit
@@ -1344,6 +1349,7 @@ uint64_t door_idle_us() {
 uint64_t door_idle_ticks() { return door_idle_us() * 100; }
 
 bool door_on(hvws_ctx* c) {
+    if (c->door_broken) return false;
     if (c->door_mode >= 0) return c->door_mode != 0;
     static const int env = getenv("HVWS_DOOR") ? atoi(getenv("HVWS_DOOR")) : 1;   // on by default (round 4)
     return env != 0;
@@ -1361,6 +1367,38 @@ std::vector<hvws_ctx*> g_doors;
 std::vector<std::pair<int, hipStream_t>> g_door_pool;
 std::atomic<int> g_door_count{0};   // g_doors.size(): frees skip the lock when no worker exists
 void door_atexit();
+// Process-wide failure counts (hvws_door_health; the test session fails on
+// either): worker streams that did not drain within their bound (left
+// wedged), and requests a worker did not answer (the context then launches
+// per call).  Both are printed to stderr as they happen.
+std::atomic<uint64_t> g_door_wedged{0};
+std::atomic<uint64_t> g_door_failed{0};
+
+// Worker streams per device at most ($HVWS_DOOR_MAX, default 8): each is a
+// hardware queue of its own, and queues beyond what the hardware scheduler
+// maps at once are time-sliced -- a resident worker could then go
+// unscheduled.  A context past the cap serves its reads with a launch each.
+int door_cap() {
+    static const int cap = getenv("HVWS_DOOR_MAX") && atoi(getenv("HVWS_DOOR_MAX")) > 0 ? atoi(getenv("HVWS_DOOR_MAX")) : 8;
+    return cap;
+}
+
+// EXPERIMENT (round 5, to be removed): $HVWS_DOOR_LEGACY_RELEASE = 1: round
+// 4's r4k park/release waits (unbounded hipStreamSynchronize, stream pooled);
+// 2: the same plus hipStreamDestroy of the CU-masked stream (r4k as it was).
+int door_legacy() {
+    static const int v = getenv("HVWS_DOOR_LEGACY_RELEASE") ? atoi(getenv("HVWS_DOOR_LEGACY_RELEASE")) : 0;
+    return v;
+}
+
+// Marks the runtime call a context is in for the wedge report and
+// hvws_debug_dump (a hang then names its call, not only its thread).
+struct in_call {
+    hvws_ctx* c;
+    const char* prev;
+    in_call(hvws_ctx* c_, const char* what) : c(c_), prev(c_->at.exchange(what)) {}
+    ~in_call() { c->at.store(prev); }
+};
 
 // The request area in device memory: its 128-byte request block, then the
 // request bytes.
@@ -1385,6 +1423,12 @@ uint8_t* door_din(hvws_ctx* c) {
 
 int door_ensure(hvws_ctx* c) {
     if (c->door_stream) return HVWS_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_door_m);
+        int same = 0;
+        for (const hvws_ctx* o : g_doors) same += o->device == c->device;
+        if (same >= door_cap()) return set_err(HVWS_EINVAL, "k_door: %d worker streams on device %d already", same, c->device);
+    }
     HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
     hipDeviceProp_t prop;
     HIP_OR(hipGetDeviceProperties(&prop, c->device), HVWS_EHIP);
@@ -1420,14 +1464,19 @@ int door_ensure(hvws_ctx* c) {
         (void)hipGetLastError();
     }
     std::lock_guard<std::mutex> lk(g_door_m);
+    int same = 0;   // again, under the lock that also registers this context
+    for (const hvws_ctx* o : g_doors) same += o->device == c->device;
+    if (same >= door_cap()) return set_err(HVWS_EINVAL, "k_door: %d worker streams on device %d already", same, c->device);
     for (size_t i = 0; i < g_door_pool.size(); ++i)
         if (g_door_pool[i].first == c->device) {
             c->door_stream = g_door_pool[i].second;
             g_door_pool.erase(g_door_pool.begin() + (long)i);
             break;
         }
-    if (!c->door_stream)
+    if (!c->door_stream) {
+        in_call ic(c, "hipExtStreamCreateWithCUMask");
         HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
+    }
     // registered after the HIP runtime's own exit handlers, so it runs before them
     static const bool reg = (atexit(door_atexit), true);
     (void)reg;
@@ -1447,6 +1496,7 @@ uint64_t door_word(const hvws_ctx* c, const uint64_t& w) {
 // context is marked wedged: its stream and mailbox are never reused or freed.
 bool door_drain(hvws_ctx* c, int ms, const char* where) {
     const auto t0 = std::chrono::steady_clock::now();
+    in_call ic(c, "hipStreamQuery(worker stream)");
     for (;;) {
         const hipError_t q = hipStreamQuery(c->door_stream);
         if (q == hipSuccess) return true;
@@ -1468,6 +1518,7 @@ bool door_drain(hvws_ctx* c, int ms, const char* where) {
             (unsigned long long)door_word(c, b->exited), (unsigned long long)c->door_epoch,
             (unsigned long long)door_word(c, b->served), (int)c->door_live);
     c->door_wedged = true;
+    g_door_wedged.fetch_add(1);
     set_err(HVWS_EHIP, "k_door: the worker stream did not drain (%s)", where);
     return false;
 }
@@ -1501,6 +1552,7 @@ int door_call(hvws_ctx* c) {
             ++c->door_epoch;
             const ddoor* dreq = c->d_door_req ? (const ddoor*)c->d_door_req : mapped<ddoor>(c->h_door);
             const uint8_t* ddin = c->d_door_req ? (const uint8_t*)c->d_door_req + 256 : mapped<uint8_t>(c->h_door_data);
+            in_call ic(c, "hipLaunchKernel(k_door)");
             HIP_OR(launch_door(dreq, mapped<ddoor>(c->h_door), ddin, mapped<uint8_t>(c->h_door_data),
                                mapped<drec>(c->h_door_rec), c->d_door_slot.as<drec>(), door_idle_ticks(),
                                __atomic_load_n(&b->done, __ATOMIC_ACQUIRE), c->door_epoch, c->door_stream),
@@ -1535,7 +1587,7 @@ int door_call(hvws_ctx* c) {
 // holds c->door_m): context teardown, a free, a thread's exit, the door
 // switched off.
 void door_park(hvws_ctx* c) {
-    if (!c->door_stream || !c->door_live) return;
+    if (!c->door_stream || !c->door_live || c->door_wedged) return;
     ddoor* b = c->h_door.as<ddoor>();
     if (door_word(c, b->exited) != c->door_epoch) {
         door_req(c)->op = DOOR_EXIT;
@@ -1548,6 +1600,12 @@ void door_park(hvws_ctx* c) {
                    std::chrono::steady_clock::now() - t0 < std::chrono::seconds(1))
                 __builtin_ia32_pause();
         }
+    }
+    if (door_legacy()) {   // EXPERIMENT (round 5): r4k's unbounded wait
+        in_call ic(c, "hipStreamSynchronize(worker stream) in park");
+        hipStreamSynchronize(c->door_stream);
+        c->door_live = false;
+        return;
     }
     if (door_drain(c, 5000, "park")) c->door_live = false;
 }
@@ -1614,7 +1672,23 @@ void door_release(hvws_ctx* c) {
         g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
         g_door_count.store((int)g_doors.size(), std::memory_order_release);
     }
-    if (c->door_wedged || !door_drain(c, 5000, "release")) {
+    // EXPERIMENT (round 5, to be removed): round 4's r4k release -- unbounded
+    // hipStreamSynchronize + hipStreamDestroy of the CU-masked stream -- to
+    // find which call the r4k/r4n hang blocked in (scripts/probe/door_first.cpp).
+    const int legacy = door_legacy();
+    if (legacy && !c->door_wedged) {
+        {
+            in_call ic(c, "hipStreamSynchronize(worker stream)");
+            hipStreamSynchronize(c->door_stream);
+        }
+        if (legacy == 2) {
+            in_call ic(c, "hipStreamDestroy(worker stream)");
+            hipStreamDestroy(c->door_stream);
+        } else {
+            std::lock_guard<std::mutex> lk(g_door_m);
+            g_door_pool.emplace_back(c->device, c->door_stream);
+        }
+    } else if (c->door_wedged || !door_drain(c, 5000, "release")) {
         // a worker that may still run: its stream and the memory it writes stay
         fprintf(stderr, "[hvws] k_door: ctx %p released with its worker stream wedged; stream and mailbox leaked\n",
                 (void*)c);
@@ -1623,18 +1697,15 @@ void door_release(hvws_ctx* c) {
         c->d_door_slot.p = nullptr;
         c->d_door_req = nullptr;
         return;
-    }
-    // drained: the next context's worker takes it ($HVWS_DOOR_POOL=0: destroy
-    // it -- a profiled program that must leave no CU-masked stream to the
-    // runtime's teardown)
-    static const bool pool = !getenv("HVWS_DOOR_POOL") || atoi(getenv("HVWS_DOOR_POOL")) != 0;
-    if (pool) {
+    } else {
+        // drained: the next context's worker takes it.  A CU-masked stream is
+        // never destroyed (destroying one is what the r4k /
+        // r4n hangs and the round-3 exit hang have in common).
         std::lock_guard<std::mutex> lk(g_door_m);
         g_door_pool.emplace_back(c->device, c->door_stream);
-    } else {
-        hipStreamDestroy(c->door_stream);
     }
     c->door_stream = nullptr;
+    in_call ic(c, "hipHostFree / hipFree (worker mailbox and areas)");
     c->h_door.release();
     c->h_door_data.release();
     c->h_door_rec.release();
@@ -1644,6 +1715,18 @@ void door_release(hvws_ctx* c) {
         hipFree(c->d_door_req);
         c->d_door_req = nullptr;
     }
+}
+
+// A request the worker did not answer (the caller holds c->door_m): counted
+// and reported, and the context launches per call from now on.  The caller's
+// buffer is untouched until a request succeeds, so the caller serves this
+// call on the launch path itself (advisor r4: no abort).
+void door_fail(hvws_ctx* c, const char* what) {
+    g_door_failed.fetch_add(1);
+    fprintf(stderr, "[hvws] k_door: ctx %p: %s request unanswered (%s); this context launches per call from now on\n",
+            (void*)c, what, g_err);
+    c->door_broken = true;
+    if (c->door_live && !c->door_wedged && door_drain(c, 1000, "failed request")) c->door_live = false;
 }
 
 // One read through the worker (gpu_feed's fast path): false when the worker
@@ -1663,7 +1746,10 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
     dcarry cin;
     to_dcarry(carry, cin);
     memcpy(&rq->carry, &cin, sizeof(dcarry));
-    if (door_call(c) != HVWS_OK) hvws::fatal("k_door");
+    if (door_call(c) != HVWS_OK) {
+        door_fail(c, "read");
+        return false;
+    }
     const uint64_t n = b->count;
     frames.resize((size_t)n);
     if (n) memcpy(frames.data(), c->h_door_rec.p, (size_t)n * sizeof(drec));
@@ -1685,7 +1771,10 @@ bool door_xor(hvws_ctx* c, char* dst, const char* src, size_t n, uint32_t key, u
     rq->len = n;
     rq->key = key;
     rq->phase = phase;
-    if (door_call(c) != HVWS_OK) hvws::fatal("k_door");
+    if (door_call(c) != HVWS_OK) {
+        door_fail(c, "XOR");
+        return false;
+    }
     memcpy(dst, data, n);
     return true;
 }
@@ -1807,9 +1896,17 @@ int hvws_debug_dump(int fd) {
                     (unsigned long long)__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE),
                     (unsigned long long)__atomic_load_n(&b->served, __ATOMIC_ACQUIRE), door_req(c)->op);
         }
-        dprintf(fd, " | last scan path %d, have_scan %d\n", c->scan_path, (int)c->have_scan);
+        const char* at = c->at.load();
+        dprintf(fd, " | wedged %d broken %d | in %s | last scan path %d, have_scan %d\n", (int)c->door_wedged,
+                (int)c->door_broken, at ? at : "-", c->scan_path, (int)c->have_scan);
     }
+    dprintf(fd, "libhvws: worker streams wedged %llu, requests unanswered %llu (process)\n",
+            (unsigned long long)g_door_wedged.load(), (unsigned long long)g_door_failed.load());
     for (hvws_ctx* c : all) {
+        if (c->at.load()) {   // its streams may be going away under that call: not queried
+            dprintf(fd, "  ctx %p streams: not queried (in %s)\n", (void*)c, c->at.load());
+            continue;
+        }
         dprintf(fd, "  ctx %p streams:", (void*)c);
         const struct {
             const char* n;
@@ -1850,7 +1947,11 @@ int hvws_debug_backtraces(int fd) {
         }
         closedir(d);
     }
-    sigaction(SIGUSR2, &old, nullptr);
+    // A thread that had SIGUSR2 blocked, or sat in a long system call, takes
+    // it after this returns: with the default action (terminate) restored,
+    // that would kill a healthy process from its own diagnostics (advisor
+    // r4).  So the handler stays installed unless the program had one.
+    if (old.sa_handler != SIG_DFL || (old.sa_flags & SA_SIGINFO)) sigaction(SIGUSR2, &old, nullptr);
     return answered;
 }
 
@@ -1861,6 +1962,16 @@ int hvws_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+int hvws_device_identity(int device, char* bus_id, int len, int* cur) {
+    if (!bus_id || len < 13) return set_err(HVWS_EINVAL, "bus id buffer too small");
+    HIP_OR(hipSetDevice(device), HVWS_EHIP);
+    int d = -1;
+    HIP_OR(hipGetDevice(&d), HVWS_EHIP);
+    if (cur) *cur = d;
+    HIP_OR(hipDeviceGetPCIBusId(bus_id, len, d), HVWS_EHIP);
+    return HVWS_OK;
 }
 
 hvws_ctx* hvws_ctx_create(int device) {
@@ -1931,51 +2042,75 @@ void hvws_ctx_destroy(hvws_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     door_release(c);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->sstream) hipStreamSynchronize(c->sstream);
-    for (tset& t : c->ts) {
-        t.release();
-        if (t.free_ev) hipEventDestroy(t.free_ev);
+    // Each runtime call of the teardown is named while it runs (c->at): a
+    // teardown that hangs names its call in the wedge report and
+    // hvws_debug_dump (round 5: the r4k hang was inside this teardown).
+    {
+        in_call ic(c, "hipStreamSynchronize(stream)");
+        if (c->stream) hipStreamSynchronize(c->stream);
     }
-    for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length, &c->sl_key, &c->sl_keyrot, &c->sl_info, &c->sl_bx})
-        b->release();
-    for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
-                    &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
-                    &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp, &c->sv_scr})
-        b->release();
-    c->h_sv.release();
-    if (c->sv_ev) hipEventDestroy(c->sv_ev);
-    for (dbuf* b : {&c->pipe_slot[0], &c->pipe_slot[1], &c->pipe_slot[2], &c->pipe_segs}) b->release();
-    for (hipEvent_t ev : c->pipe_ev)
-        if (ev) hipEventDestroy(ev);
-    for (dbuf* b : {&c->segs, &c->carry_in, &c->stage, &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad,
-                    &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->tx_span, &c->d_small_in, &c->d_small_slots})
-        b->release();
-    c->h_tx.release();
-    c->h_small_in.release();
-    c->h_small_done.release();
-    c->h_small_out.release();
-    c->h_feed.release();
-    c->h_segs.release();
-    for (hbuf& b : c->h_up) b.release();
-    c->h_total.release();
-    c->chk.release();
-    c->h_chk.release();
-    for (auto& ev : c->ev)
-        if (ev) hipEventDestroy(ev);
-    for (auto& row : c->tev)
-        for (auto& ev : row)
+    {
+        in_call ic(c, "hipStreamSynchronize(sstream)");
+        if (c->sstream) hipStreamSynchronize(c->sstream);
+    }
+    {
+        in_call ic(c, "hipFree (table sets)");
+        for (tset& t : c->ts) t.release();
+    }
+    {
+        in_call ic(c, "hipFree (scratch, sieve, pipeline, staging)");
+        for (dbuf* b : {&c->sl_hdr, &c->sl_off, &c->sl_len, &c->sl_length, &c->sl_key, &c->sl_keyrot, &c->sl_info, &c->sl_bx})
+            b->release();
+        for (dbuf* b : {&c->sv_state, &c->sv_tcount, &c->sv_tbase, &c->sv_slot, &c->sv_pool, &c->sv_keep, &c->sv_kbase,
+                        &c->sv_Spre, &c->sv_S, &c->sv_J0, &c->sv_J1,
+                        &c->sv_mark, &c->sv_hops, &c->sv_rank, &c->sv_cnt, &c->sv_tmp, &c->sv_scr})
+            b->release();
+        for (dbuf* b : {&c->pipe_slot[0], &c->pipe_slot[1], &c->pipe_slot[2], &c->pipe_segs}) b->release();
+        for (dbuf* b : {&c->segs, &c->carry_in, &c->stage, &c->xor_stage, &c->synth_sizes, &c->synth_tiles, &c->synth_bad,
+                        &c->tx_size, &c->tx_off, &c->tx_scan, &c->tx_tiles, &c->tx_stat, &c->tx_span, &c->d_small_in,
+                        &c->d_small_slots})
+            b->release();
+        c->chk.release();
+    }
+    {
+        in_call ic(c, "hipHostFree (pinned buffers)");
+        c->h_sv.release();
+        c->h_tx.release();
+        c->h_small_in.release();
+        c->h_small_done.release();
+        c->h_small_out.release();
+        c->h_feed.release();
+        c->h_segs.release();
+        for (hbuf& b : c->h_up) b.release();
+        c->h_total.release();
+        c->h_chk.release();
+        c->h_status.release();
+    }
+    {
+        in_call ic(c, "hipEventDestroy");
+        for (tset& t : c->ts)
+            if (t.free_ev) hipEventDestroy(t.free_ev);
+        if (c->sv_ev) hipEventDestroy(c->sv_ev);
+        for (hipEvent_t ev : c->pipe_ev)
             if (ev) hipEventDestroy(ev);
-    for (auto& ev : c->up_ev)
-        if (ev) hipEventDestroy(ev);
-    for (auto& ev : c->span_ev)
-        if (ev) hipEventDestroy(ev);
-    c->h_status.release();
-    if (c->stream) hipStreamDestroy(c->stream);
-    if (c->copy_in) hipStreamDestroy(c->copy_in);
-    if (c->copy_out) hipStreamDestroy(c->copy_out);
-    if (c->sstream) hipStreamDestroy(c->sstream);
-    if (c->scan_done) hipEventDestroy(c->scan_done);
+        for (auto& ev : c->ev)
+            if (ev) hipEventDestroy(ev);
+        for (auto& row : c->tev)
+            for (auto& ev : row)
+                if (ev) hipEventDestroy(ev);
+        for (auto& ev : c->up_ev)
+            if (ev) hipEventDestroy(ev);
+        for (auto& ev : c->span_ev)
+            if (ev) hipEventDestroy(ev);
+        if (c->scan_done) hipEventDestroy(c->scan_done);
+    }
+    {
+        in_call ic(c, "hipStreamDestroy (context streams)");
+        if (c->stream) hipStreamDestroy(c->stream);
+        if (c->copy_in) hipStreamDestroy(c->copy_in);
+        if (c->copy_out) hipStreamDestroy(c->copy_out);
+        if (c->sstream) hipStreamDestroy(c->sstream);
+    }
     {
         std::lock_guard<std::mutex> lk(g_ctx_m);
         g_ctx_all.erase(std::remove(g_ctx_all.begin(), g_ctx_all.end(), c), g_ctx_all.end());
@@ -2565,22 +2700,25 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     const uint64_t nb = (n + 1023) / 1024;
     HIP_OR(c->tx_size.ensure(n * 8 + 8), HVWS_ENOMEM);
     HIP_OR(c->tx_scan.ensure((4 * nb + 64) * 8), HVWS_ENOMEM);
-    HIP_OR(c->tx_stat.ensure(16), HVWS_ENOMEM);
-    HIP_OR(c->h_tx.ensure(16), HVWS_ENOMEM);
+    HIP_OR(c->tx_stat.ensure(64), HVWS_ENOMEM);
+    HIP_OR(c->h_tx.ensure(64), HVWS_ENOMEM);
     uint64_t* off = d_out_off;
     if (!off) {
         HIP_OR(c->tx_off.ensure(n * 8 + 8), HVWS_ENOMEM);
         off = c->tx_off.as<uint64_t>();
     }
-    // [0] total bytes, [1] payload ranges out of bounds
+    // [0] total bytes, [1] payload ranges out of bounds, [2] frames breaking
+    // the uniform layout, [3..5] pay_off[0], its step, len[0] (k_tx_check)
     uint64_t* stat = c->tx_stat.as<uint64_t>();
-    HIP_OR(hipMemsetAsync(stat, 0, 16, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemsetAsync(stat, 0, 64, c->stream), HVWS_EHIP);
     HIP_OR(launch_frame_sizes(d_flags, d_len, n, c->tx_size.as<uint64_t>(), c->stream), HVWS_EHIP);
     HIP_OR(launch_exclusive_scan(c->tx_size.as<uint64_t>(), off, n, c->tx_scan.as<uint64_t>(), stat, c->stream),
            HVWS_EHIP);
-    HIP_OR(launch_tx_check(d_pay_off, d_len, d_flags, d_mask, off, n, payload_len, stat + 1, c->stream), HVWS_EHIP);
+    HIP_OR(launch_tx_check(d_pay_off, d_len, d_flags, d_mask, c->tx_size.as<uint64_t>(), n, payload_len, stat,
+                           c->stream),
+           HVWS_EHIP);
     uint64_t* h = c->h_tx.as<uint64_t>();
-    HIP_OR(hipMemcpyAsync(h, stat, 16, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
+    HIP_OR(hipMemcpyAsync(h, stat, 48, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
     if (h[1]) return set_err(HVWS_EINVAL, "build_frames: %llu frames read outside the payload buffer or lack a mask",
                              (unsigned long long)h[1]);
@@ -2599,16 +2737,28 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     const bool spans_ok = !sp_env || atoi(sp_env) != 0;
     const uint64_t tile = tx_tile(v);
     const uint64_t ntiles = (total + tile - 1) / tile;
-    HIP_OR(c->tx_tiles.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
-    if (spans_ok) HIP_OR(c->tx_span.ensure(ntiles * 16 + 16), HVWS_ENOMEM);
+    // A uniform layout (every frame the same size and length, payload offsets
+    // a + k * b, b >= 0) needs no tile index: each tile finds its frames and
+    // source span from its position ($HVWS_BUILD_UNI=0: the index anyway).
+    static const bool uni_ok = !getenv("HVWS_BUILD_UNI") || atoi(getenv("HVWS_BUILD_UNI")) != 0;
+    // (payload steps shorter than a payload would make a tile's pieces
+    // overlap out of order: the index handles those)
+    const bool uniform = uni_ok && h[2] == 0 && total % n == 0 && (n == 1 || h[4] >= h[5]);
+    const uint64_t uni[4] = {uniform ? total / n : 0, uniform ? total / n - h[5] : 0, h[3], h[4]};
+    c->tx_uniform = uniform;
+    if (!uniform) {
+        HIP_OR(c->tx_tiles.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+        if (spans_ok) HIP_OR(c->tx_span.ensure(ntiles * 16 + 16), HVWS_ENOMEM);
+    }
     // the timed device work (hvws_last_kernel_ms): tile index, spans, build
     HIP_OR(hipEventRecord(c->ev[4], c->stream), HVWS_EHIP);
-    uint64_t* span = spans_ok ? c->tx_span.as<uint64_t>() : nullptr;
-    HIP_OR(launch_tx_index(off, c->tx_size.as<uint64_t>(), d_pay_off, d_len, d_flags, n, ntiles, tile,
-                           c->tx_tiles.as<uint32_t>(), span, c->stream),
-           HVWS_EHIP);
+    uint64_t* span = spans_ok && !uniform ? c->tx_span.as<uint64_t>() : nullptr;
+    if (!uniform)
+        HIP_OR(launch_tx_index(off, c->tx_size.as<uint64_t>(), d_pay_off, d_len, d_flags, n, ntiles, tile,
+                               c->tx_tiles.as<uint32_t>(), span, c->stream),
+               HVWS_EHIP);
     HIP_OR(launch_build(d_out, total, d_payload, payload_len, d_pay_off, d_len, d_flags, d_mask, off,
-                        c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), span, n, v, c->stream),
+                        c->tx_size.as<uint64_t>(), c->tx_tiles.as<uint32_t>(), span, n, v, c->stream, uni),
            HVWS_EHIP);
     HIP_OR(hipEventRecord(c->ev[5], c->stream), HVWS_EHIP);
     c->ev_build = true;
@@ -2645,6 +2795,8 @@ const char* hvws_last_build_kernel(hvws_ctx* c) {
     if (!c) return "";
     return build_kernel_name(c->tx_variant);
 }
+
+int hvws_last_build_uniform(hvws_ctx* c) { return c && c->tx_uniform ? 1 : 0; }
 
 uint32_t hvws_set_validation(hvws_ctx* c, uint32_t classes) {
     if (!c) c = hvws::thread_ctx();
@@ -2688,6 +2840,13 @@ uint64_t hvws_set_door_idle_us(uint64_t us) {
     const uint64_t old = door_idle_us();
     g_door_idle_us.store(us ? us : 5000, std::memory_order_relaxed);
     return old;
+}
+
+int hvws_door_health(uint64_t out[2]) {
+    if (!out) return set_err(HVWS_EINVAL, "null output");
+    out[0] = g_door_wedged.load();
+    out[1] = g_door_failed.load();
+    return HVWS_OK;
 }
 
 int hvws_door_stats(hvws_ctx* c, uint64_t out[4]) {

@@ -366,9 +366,12 @@ uint64_t synth_tile();
 // out[i] = sum(in[0..i)), *total = sum(in); tmp >= 4 * ceil(n / 1024) + 64 words.
 hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp, uint64_t* total,
                                  hipStream_t st);
-// *bad += frames whose payload range leaves [0, plen) or that are masked without a key table.
+// stat[1] += frames whose payload range leaves [0, plen) or that are masked
+// without a key table; stat[2] += frames breaking the uniform layout (size
+// or length other than frame 0's, payload offset step other than frame 1's or
+// negative); stat[3..5] = pay_off[0], pay_off[1] - pay_off[0], len[0].
 hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
-                           const uint64_t* out_off, uint64_t n, uint64_t plen, uint64_t* bad, hipStream_t st);
+                           const uint64_t* size, uint64_t n, uint64_t plen, uint64_t* stat, hipStream_t st);
 // k_build geometry for a batch of out_len output bytes in n frames
 // ($HVWS_BUILD, else by the mean frame size), its tile and its name
 int tx_variant(uint64_t out_len, uint64_t n);
@@ -381,10 +384,13 @@ const char* build_kernel_name(int v);
 hipError_t launch_tx_index(const uint64_t* out_off, const uint64_t* size, const uint64_t* pay_off, const uint64_t* len,
                            const uint8_t* flags, uint64_t n, uint64_t ntiles, uint64_t tile, uint32_t* tile_first,
                            uint64_t* span, hipStream_t st);
-// span: from launch_tx_index, or nullptr (boundary tiles load their records first)
+// span: from launch_tx_index, or nullptr (boundary tiles load their records
+// first).  uni (host array {stride, header bytes, pay_off[0], payload offset
+// step}, stride != 0): a uniform layout -- every tile finds its frame range and
+// span from its position, tile_first and span are not read (no index pass).
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                         const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,
-                        hipStream_t st);
+                        hipStream_t st, const uint64_t* uni = nullptr);
 
 }  // namespace hvws

@@ -383,6 +383,52 @@ struct build_idx {
     uint64_t k_lo, k_hi, sp_lo, sp_hi;
 };
 
+// Uniform layouts (every frame the same size, payload offsets affine in the
+// frame index with a non-negative step: packed payloads, the rx layout, any
+// fixed gap; k_tx_check finds them): the tile's frame range and source span
+// follow from its position -- no tile index or span pass, no index round trip.
+// Frame k's output is [k * stride, (k + 1) * stride), its header hdr bytes,
+// its payload from pay_a + k * pay_b.
+struct build_uni {
+    uint64_t stride, hdr, pay_a, pay_b;
+    double inv;   // 1 / stride
+};
+
+// floor(x / stride) from the double reciprocal, corrected to exact
+__device__ __forceinline__ uint64_t uni_div(uint64_t x, const build_uni& u) {
+    uint64_t k = (uint64_t)((double)x * u.inv);
+    while (k && k * u.stride > x) --k;
+    while ((k + 1) * u.stride <= x) ++k;
+    return k;
+}
+
+__device__ __forceinline__ build_idx build_uni_idx(const build_uni& u, uint64_t base, uint64_t tile, uint64_t n,
+                                                   uint64_t out_len) {
+    build_idx x;
+    const uint64_t te = base + tile < out_len ? base + tile : out_len;   // base < out_len
+    const uint64_t k0 = uni_div(base, u), k1 = uni_div(te - 1, u);     // first and last frame touching the tile
+    x.k_lo = k0;
+    x.k_hi = k1 + 1 < n ? k1 + 1 : n;
+    x.sp_lo = ~0ull;
+    x.sp_hi = 0;
+    const uint64_t len = u.stride - u.hdr;
+    if (len) {
+        // first payload piece: frame k0's if its payload starts before te
+        // (it ends past base), else none at all (later frames start later)
+        const uint64_t ps0 = k0 * u.stride + u.hdr;
+        if (ps0 < te) {
+            x.sp_lo = u.pay_a + k0 * u.pay_b + (ps0 > base ? 0 : base - ps0);
+            // last piece: frame k1's if its payload starts before te, else
+            // the whole payload of frame k1 - 1 (>= k0 here)
+            const uint64_t ps1 = k1 * u.stride + u.hdr;
+            const uint64_t e1 = (k1 + 1) * u.stride;
+            x.sp_hi = ps1 < te ? u.pay_a + k1 * u.pay_b + ((e1 < te ? e1 : te) - ps1)
+                               : u.pay_a + (k1 - 1) * u.pay_b + len;
+        }
+    }
+    return x;
+}
+
 __device__ __forceinline__ build_idx build_load_idx(const uint32_t* __restrict__ tile_first,
                                                     const unsigned long long* __restrict__ span, uint64_t t,
                                                     uint64_t n) {
@@ -812,17 +858,23 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
     }
 }
 
-// One workgroup per tile, tiles in linear or XCD-contiguous order.
-template <int T, int U, bool SWZ, bool NT, bool SF, int C>
+// One workgroup per tile, tiles in linear order (an order giving each XCD
+// runs of 8 adjacent tiles, so neighbours' records share one L2, measured
+// slower at c2: 0.370-0.391 against 0.353-0.386 ms, profiles/r5a_raw).
+// uni.stride != 0: a uniform layout, the tile's frame
+// range and span from its position (build_uni_idx); else from the tile index.
+template <int T, int U, bool NT, bool SF, int C>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(C == 2 ? 7 : 8, 8))) void k_build(
     uint8_t* __restrict__ out, uint64_t out_len, const uint8_t* __restrict__ pay, uint64_t plen,
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
     const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
     const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
-    uint64_t ntiles) {
-    const uint64_t t = tile0 + (SWZ ? xcd_tile(blockIdx.x, ntiles) : (uint64_t)blockIdx.x);
+    uint64_t ntiles, build_uni uni) {
+    const uint64_t t = tile0 + blockIdx.x;
+    constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     build_one_tile<T, U, NT, SF, C>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
-                                 build_load_idx(tile_first, span, t, n));
+                                 uni.stride ? build_uni_idx(uni, t * TILE, TILE, n, out_len)
+                                            : build_load_idx(tile_first, span, t, n));
 }
 
 
@@ -842,25 +894,41 @@ hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, 
     return hipGetLastError();
 }
 
+// stat[1] += frames whose payload range leaves [0, plen) or that are masked
+// without a key table; stat[2] += frames that break the uniform layout (a
+// size other than frame 0's, or a payload offset step other than frame 1's,
+// or a negative one, or a payload length other than frame 0's); stat[3],
+// stat[4], stat[5] = pay_off[0], pay_off[1] - pay_off[0], len[0].
 __global__ void k_tx_check(const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len,
                            const uint8_t* __restrict__ flags, const uint32_t* __restrict__ mask,
-                           const uint64_t* __restrict__ out_off, uint64_t n, uint64_t plen,
-                           unsigned long long* __restrict__ bad) {
+                           const uint64_t* __restrict__ size, uint64_t n, uint64_t plen,
+                           unsigned long long* __restrict__ stat) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool b = false;
+    bool b = false, nu = false;
     if (i < n) {
         const uint64_t o = pay_off[i], l = len[i];
         b = o > plen || l > plen - o || ((flags[i] & F_MASK) && !mask);
+        if (i) {
+            const uint64_t p0 = pay_off[0], p1 = pay_off[1], pp = pay_off[i - 1];
+            nu = size[i] != size[0] || l != len[0] || p1 < p0 || o < pp || o - pp != p1 - p0;
+        } else {
+            stat[3] = o;
+            stat[4] = n > 1 ? pay_off[1] - o : 0;
+            stat[5] = l;
+        }
     }
-    const uint64_t m = __ballot(b);
-    if (m && (threadIdx.x & 63) == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
+    const uint64_t m = __ballot(b), mu = __ballot(nu);
+    if ((threadIdx.x & 63) == 0) {
+        if (m) atomicAdd(stat + 1, (unsigned long long)__popcll(m));
+        if (mu) atomicAdd(stat + 2, (unsigned long long)__popcll(mu));
+    }
 }
 
 hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
-                           const uint64_t* out_off, uint64_t n, uint64_t plen, uint64_t* bad, hipStream_t st) {
+                           const uint64_t* size, uint64_t n, uint64_t plen, uint64_t* stat, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_tx_check, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, pay_off, len, flags, mask,
-                       out_off, n, plen, reinterpret_cast<unsigned long long*>(bad));
+                       size, n, plen, reinterpret_cast<unsigned long long*>(stat));
     return hipGetLastError();
 }
 
@@ -943,8 +1011,16 @@ hipError_t launch_tx_index(const uint64_t* out_off, const uint64_t* size, const 
 hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint64_t plen, const uint64_t* pay_off,
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                         const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,
-                        hipStream_t st) {
+                        hipStream_t st, const uint64_t* uni) {
     const unsigned long long* sp = reinterpret_cast<const unsigned long long*>(span);
+    build_uni u = {0, 0, 0, 0, 0.0};
+    if (uni && uni[0]) {
+        u.stride = uni[0];
+        u.hdr = uni[1];
+        u.pay_a = uni[2];
+        u.pay_b = uni[3];
+        u.inv = 1.0 / (double)uni[0];
+    }
     const uint64_t tile = build_tile(v);
     const uint64_t ntiles = (out_len + tile - 1) / tile;
     // a grid beyond 2^32-1 work-items is silently truncated: split the launch
@@ -954,8 +1030,8 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
         switch (v) {
 #define X(I, T, U, S, N, F, C)                                                                                 \
     case I:                                                                                                    \
-        hipLaunchKernelGGL((k_build<T, U, S, N, F, C>), dim3((uint32_t)nt), dim3(T), 0, st, out, out_len, pay, plen, \
-                           pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt);              \
+        hipLaunchKernelGGL((k_build<T, U, N, F, C>), dim3((uint32_t)nt), dim3(T), 0, st, out, out_len, pay, plen, \
+                           pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt, u);           \
         break;
             HVWS_BUILD_GEOMS(X)
 #undef X

@@ -7,8 +7,11 @@ Two payload layouts:
     unmasked rx batch) -- payload and output 16-B phases agree;
   * "packed": payloads back to back in a send arena -- every 64 KiB frame's
     14-byte header shifts the output phase, so loads are realigned.
-Algorithmic bytes per launch = payload read + frames written.  Device time
-from HIP events around the kernel on the ctx stream.  Prints JSON lines.
+Both layouts build from real payload bytes and every output byte is checked
+against the masked batch.  Algorithmic bytes per launch = payload read +
+frames written.  Device time from HIP events around the call's device work
+after its size check (tile index and spans when the layout needs them, and
+k_build) on the ctx stream.  Prints JSON lines.
 """
 from __future__ import annotations
 
@@ -32,6 +35,7 @@ def main():
     reps = int(os.environ.get("REPS", "5"))
     name = os.environ.get("CONFIG", "c3")
     eng = libhv_amd.Engine(int(os.environ.get("HVWS_BENCH_DEVICE", "0")))
+    L = libhv_amd.lib()
     p = synth.config_plan(name, 1).split(4096)
     dp = libhv_amd.DevicePlan(eng, p)
     hdr = synth.frame_size(p.flags, p.length) - p.length
@@ -42,21 +46,39 @@ def main():
     eng.sync()
     alg = p.payload_bytes + p.total
     pack_off = np.concatenate([[0], np.cumsum(p.length)[:-1]]).astype(np.uint64)
-    for layout, offs in (("rx_layout", p.frame_off + hdr), ("packed", pack_off)):
+    # a real packed send arena: every frame's plaintext payload back to back,
+    # compacted on the host out of the unmasked rx batch
+    host = rx.download(p.total)
+    packed = np.empty(max(p.payload_bytes, 1), dtype=np.uint8)
+    src = (p.frame_off + hdr).astype(np.int64)
+    if len(set(np.unique(p.length).tolist())) == 1 and np.all(np.diff(src) == src[1] - src[0] if p.n > 1 else True):
+        ln, st = int(p.length[0]), int(src[1] - src[0]) if p.n > 1 else 0
+        view = np.lib.stride_tricks.as_strided(host[int(src[0]):], shape=(p.n, ln), strides=(st, 1))
+        packed[:p.payload_bytes] = view.reshape(-1)
+    else:
+        for k in range(p.n):
+            o, ln = int(pack_off[k]), int(p.length[k])
+            packed[o:o + ln] = host[src[k]:src[k] + ln]
+    del host
+    arena = eng.to_device(packed)
+    del packed
+    for layout, offs, pay in (("rx_layout", p.frame_off + hdr, rx), ("packed", pack_off, arena)):
         tx = libhv_amd.TxPlan(eng, offs, p.length, p.flags, p.mask)
         ms = []
         t0 = time.perf_counter()
+        plen = p.total if pay is rx else p.payload_bytes
         for _ in range(reps + 1):
-            n = eng.build_frames(out, p.total + 64, rx, p.total, tx)
+            n = eng.build_frames(out, p.total + 64, pay, plen, tx)
             ms.append(eng.last_kernel_ms())
         wall = (time.perf_counter() - t0) / (reps + 1)
         assert n == p.total
-        ok = None
-        if layout == "rx_layout":
-            ok = eng.synth(out, p.total, p.seed, dp, 1) == 0
+        # every output byte against the masked batch (device synth VERIFY)
+        ok = eng.synth(out, p.total, p.seed, dp, 1) == 0
+        L.hvws_memset(eng.ctx, out.ptr, 0, p.total)   # the next layout must write every byte itself
         k = float(np.mean(ms[1:]))
         print(json.dumps({
             "bench": "build_frames", "kernel": libhv_amd.lib().hvws_last_build_kernel(eng.ctx).decode(), "config": name,
+            "index": "none (uniform layout)" if L.hvws_last_build_uniform(eng.ctx) else "tile index + spans",
             "layout": layout, "frames": p.n,
             "payload_bytes": p.payload_bytes, "out_bytes": p.total, "alg_bytes_per_launch": alg,
             "kernel_ms": round(k, 3), "kernel_GBps": round(alg / k / 1e6, 1),
@@ -65,10 +87,11 @@ def main():
             "verified": ok,
         }), flush=True)
         tx.free()
+        if not ok:
+            raise SystemExit(f"{layout}: the built frames differ from the masked batch")
+    arena.free()
     # ceilings: runtime D2D copy of the same bytes, and one huge unmasked frame
     # (k_build's streaming path as a plain realigning copy)
-    import ctypes
-    L = libhv_amd.lib()
     ev = []
     for _ in range(reps + 1):
         t0 = time.perf_counter()

@@ -19,6 +19,46 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: full-size (BASELINE.json) configurations")
 
 
+def _door_health():
+    import ctypes
+
+    import libhv_amd
+
+    out = (ctypes.c_uint64 * 2)()
+    libhv_amd.lib().hvws_door_health(out)
+    return int(out[0]), int(out[1])
+
+
+@pytest.fixture(autouse=True)
+def _no_wedged_worker(request):
+    """Every GPU test fails if a resident worker's stream wedged or a worker
+    left a request unanswered during it (include/hvws.h hvws_door_health):
+    the library recovers from both without hanging, so without this check a
+    recurrence would pass silently (What's weak 1)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    before = _door_health()
+    yield
+    after = _door_health()
+    assert after == before, (f"resident worker failure during this test: wedged streams {before[0]} -> {after[0]}, "
+                             f"unanswered requests {before[1]} -> {after[1]} (stderr has the mailbox)")
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """The whole session fails when any worker wedged, inside or between tests."""
+    if "libhv_amd" not in sys.modules or getattr(sys.modules["libhv_amd"], "_lib", None) is None:
+        return
+    try:
+        wedged, failed = _door_health()
+    except Exception:   # noqa: BLE001 -- the library did not load: nothing ran on it
+        return
+    if wedged or failed:
+        print(f"\nlibhvws: {wedged} worker stream(s) wedged, {failed} request(s) unanswered in this session",
+              file=sys.stderr)
+        session.exitstatus = 1
+
+
 @pytest.fixture(scope="session")
 def eng():
     import libhv_amd

@@ -88,7 +88,11 @@ def test_bench_launcher_two_ranks():
     assert len(lines) == 1, p.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["dry_run"] is True
-    assert [r["rank"] for r in out["timing"]["per_rank"]] == [0, 1]
+    pr = out["timing"]["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    # each rank names its card: HIP device index, hipGetDevice, PCI bus id (distinct)
+    assert [(r["device"], r["hip_device"]) for r in pr] == [(0, 0), (1, 1)]
+    assert [r["pci_bus_id"] for r in pr] == ["0000:01:00.0", "0000:02:00.0"]
     v = out["verified"]["ranks"]
     assert [r["fixture"] for r in v] == ["c5_rank0", "c5_rank1"]
     assert [r["local_rank"] for r in v] == [0, 1] and v[0]["seed"] != v[1]["seed"]
@@ -108,3 +112,20 @@ def test_bench_launcher_refuses_too_few_gpus():
     p = _bench(["--gpus", "4"], {"HIP_VISIBLE_DEVICES": "0"}, timeout=60)
     assert p.returncode == 2 and "refusing" in p.stderr
     assert not p.stdout.strip()
+
+
+def test_bench_launcher_refuses_ranks_sharing_a_device():
+    """Two ranks that report one PCI bus id end the run non-zero with no
+    result line: an N-rank line must come from N cards."""
+    p = _bench(["--gpus", "2", "--dry-run"], {"HVWS_BENCH_DRYRUN_BUS": "0000:05:00.0"})
+    assert p.returncode != 0
+    assert "share a device" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bus_id_round_trip():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for b in ("0000:05:00.0", "0001:c3:1f.7", "0000:ff:00.1"):
+        assert bench.bus_name(bench.bus_number(b)) == b

@@ -54,6 +54,56 @@ def test_door_is_the_default():
         L.hvws_thread_release()
 
     _in_thread(first_read)
+    assert _health() == (0, 0), "a worker stream wedged or a request went unanswered (stderr has the mailbox)"
+
+
+def _health():
+    out = (ctypes.c_uint64 * 2)()
+    assert libhv_amd.lib().hvws_door_health(out) == 0
+    return int(out[0]), int(out[1])
+
+
+def test_door_many_threads_capped():
+    """24 loop threads at once (advisor r4): at most $HVWS_DOOR_MAX (8) of
+    them hold a worker stream on the device -- each is a hardware queue of its
+    own -- and the rest launch per call; every thread's messages equal the
+    oracle's, and no worker wedges or leaves a request unanswered."""
+    n = 24
+    work = [_cases(random.Random(100 + i), 6) for i in range(n)]
+    fed = threading.Barrier(n + 1, timeout=120)
+    done = threading.Event()
+    has_stream, errs = [0] * n, []
+
+    def loop(i):
+        L = libhv_amd.lib()
+        try:
+            for data, chunks in work[i]:
+                if H.run_messages("gpu", data, chunks) != H.run_messages("oracle", data, chunks):
+                    errs.append(f"thread {i}: mismatch")
+            info = (ctypes.c_uint64 * 2)()
+            L.hvws_door_info(None, info)
+            has_stream[i] = int(info[1])
+        except Exception as e:   # noqa: BLE001
+            errs.append(f"thread {i}: {e!r}")
+        finally:
+            try:
+                fed.wait()          # every thread has fed: count the streams held at once
+                done.wait(120)
+            finally:
+                L.hvws_thread_release()
+
+    ths = [threading.Thread(target=loop, args=(i,)) for i in range(n)]
+    for t in ths:
+        t.start()
+    fed.wait()
+    held = sum(has_stream)
+    done.set()
+    for t in ths:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ths), "a loop thread did not finish"
+    assert not errs, errs
+    assert 1 <= held <= 8, f"{held} loop threads hold a worker stream at once (cap 8)"
+    assert _health() == (0, 0)
 
 
 def _cases(rng, n):

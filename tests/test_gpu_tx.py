@@ -298,3 +298,80 @@ def test_build_boundary_tiles_span_staged(eng, spans, order, monkeypatch):
     else:
         got, _ = _gpu_build(eng, frames, gap_rng=rng if order == "gaps" else None)
     assert got == H.build_frames_ref(frames)
+
+
+def _build_at(eng, frames, offs, pay: bytes):
+    """hvws_build_frames with explicit payload offsets into `pay`; returns the
+    output bytes and whether the call took the index-free uniform path."""
+    flags = [f for f, _, _ in frames]
+    mask = [int.from_bytes(k, "little") if k else 0 for _, _, k in frames]
+    lens = [len(p) for _, p, _ in frames]
+    total = int(synth.frame_size(np.array(flags, dtype=np.uint8), np.array(lens, dtype=np.uint64)).sum())
+    payload = eng.to_device(np.frombuffer(pay, dtype=np.uint8)) if pay else eng.alloc(16)
+    tx = libhv_amd.TxPlan(eng, offs, lens, flags, mask)
+    out = eng.alloc(total + 64)
+    try:
+        assert eng.build_frames(out, total + 64, payload, len(pay), tx) == total
+        got = bytes(out.download(total))
+    finally:
+        for b in (payload, out):
+            b.free()
+        tx.free()
+    return got, libhv_amd.lib().hvws_last_build_uniform(eng.ctx)
+
+
+@pytest.mark.parametrize("ln", [0, 1, 7, 125, 1024, 3000, 70001])
+@pytest.mark.parametrize("layout", ["packed", "gap", "rx", "shared", "one"])
+def test_build_uniform_layouts(eng, ln, layout):
+    """Uniform layouts (every frame the same size and payload length, payload
+    offsets a + k*b with b >= the payload length) build without a tile index
+    -- each tile finds its frames and source span from its position -- frame by
+    frame equal to the reference's websocket_build_frame: payloads packed, with
+    a fixed gap, where an rx batch holds them, a single frame; all frames
+    sharing one payload (b = 0) take the index and are equal too."""
+    rng = np.random.default_rng(ln * 7 + len(layout))
+    n = 1 if layout == "one" else max(3, min(3000, (4 << 20) // (ln + 14)))
+    fl = 0x2 | 0x10 | 0x20
+    body = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
+    frames = [(fl, body if layout == "shared" else bytes(rng.integers(0, 256, ln, dtype=np.uint8)),
+               bytes(rng.integers(0, 256, 4, dtype=np.uint8))) for _ in range(n)]
+    a = int(rng.integers(0, 40))
+    step = {"packed": ln, "gap": ln + 13, "rx": len(H.build_frames_ref([frames[0]])),
+            "shared": 0, "one": 0}[layout]
+    offs = [a + k * step for k in range(n)]
+    pay = bytearray(a + (n - 1) * step + ln + 8)
+    for k, (_, p, _) in enumerate(frames):
+        pay[offs[k]:offs[k] + ln] = p
+    got, uni = _build_at(eng, frames, offs, bytes(pay))
+    assert got == H.build_frames_ref(frames)
+    # one payload shared by every frame (a step shorter than a payload): the index
+    assert uni == (0 if layout == "shared" and ln else 1)
+
+
+@pytest.mark.parametrize("kind", ["same_size_other_lengths", "descending", "one_longer", "shuffled"])
+def test_build_not_uniform_takes_the_index(eng, kind):
+    """Layouts that only look uniform take the tile index and still equal the
+    reference: equal sizes from different lengths (masked L, unmasked L + 4),
+    descending payload offsets, one frame longer, shuffled offsets."""
+    rng = np.random.default_rng(77)
+    n, ln = 2000, 1000
+    frames = []
+    for k in range(n):
+        masked = kind != "same_size_other_lengths" or k % 2 == 0
+        m = ln + (0 if masked else 4) + (5 if kind == "one_longer" and k == 1234 else 0)
+        frames.append((0x2 | 0x10 | (0x20 if masked else 0), bytes(rng.integers(0, 256, m, dtype=np.uint8)),
+                       bytes(rng.integers(0, 256, 4, dtype=np.uint8)) if masked else None))
+    lens = [len(p) for _, p, _ in frames]
+    offs = list(np.concatenate([[0], np.cumsum(lens)[:-1]]))
+    if kind in ("descending", "shuffled"):
+        perm = list(range(n))[::-1] if kind == "descending" else list(rng.permutation(n))
+        pos = np.concatenate([[0], np.cumsum([lens[i] for i in perm])[:-1]])
+        offs = [0] * n
+        for j, i in enumerate(perm):
+            offs[i] = int(pos[j])
+        pay = b"".join(frames[i][1] for i in perm)
+    else:
+        pay = b"".join(p for _, p, _ in frames)
+    got, uni = _build_at(eng, frames, [int(o) for o in offs], pay)
+    assert got == H.build_frames_ref(frames)
+    assert uni == 0
