@@ -967,7 +967,7 @@ def main():
             extra["validation"] = "HVWS_V_ALL"
         extra["other_step_call_ms"] = round(other_ms, 3) if other_ms is not None else None
         extra["scan_path"] = {0: "count_emit", 1: "count_read_emit", 2: "single", 3: "speculative",
-                              4: "speculative_rejected", 5: "slack", 6: "slack_rejected"}.get(scan_path, scan_path)
+                              4: "speculative_rejected", 5: "slack", 6: "slack_rejected", 7: "run"}.get(scan_path, scan_path)
         extra["timing"] = {
             "method": "per device: hvws_span_begin/end markers on the context's streams (HIP events); "
                       "across devices: latest end - earliest start on the host CLOCK_MONOTONIC after a barrier",

@@ -246,9 +246,32 @@ enum {
     HVWS_PATH_SPEC = 3,             /* speculative table checked exact on the device */
     HVWS_PATH_SPEC_FAILED = 4,      /* speculation rejected by the check, then COUNT/EMIT */
     HVWS_PATH_SLACK = 5,            /* mixed sizes: one EMIT walk into per-segment regions, compacted on the device */
-    HVWS_PATH_SLACK_FAILED = 6      /* a segment outgrew its region, then COUNT/EMIT */
+    HVWS_PATH_SLACK_FAILED = 6,     /* a segment outgrew its region, then COUNT/EMIT */
+    HVWS_PATH_RUN = 7               /* step of small uniform frames: per-segment run descriptors, headers
+                                       checked by the unmask itself, records built when read */
 };
 int hvws_last_scan_path(hvws_ctx* ctx);
+
+/* RUN path for hvws_step / hvws_step_resident: a batch of many segments whose
+ * last exact scan found each segment one run of equal frames (and frames of at
+ * most 8 KiB) is discovered by k_head alone -- the carried-in frame and the
+ * frame cut by the segment end exactly, the run in between as a hypothesis --
+ * and the unmask parses every run header from the bytes it loads anyway,
+ * checks it against the hypothesis and takes its key from it: no per-frame
+ * records and no second pass over the header lines.  A repair pass queued on
+ * the context stream right behind undoes and redoes exactly any segment whose
+ * hypothesis failed, so work queued after the step sees the reference's bytes
+ * either way; the next steps then scan exactly until a check sees uniform
+ * frames again.  The frame records, counts and carry of a RUN step are built
+ * (an exact scan of the unchanged headers) when hvws_get_* first asks.  mode
+ * -1 = automatic (default; $HVWS_RUN=0 turns it off), 0 = never, 1 = every
+ * step batch of several segments, whatever the last scan saw (tests).  ctx
+ * NULL = the calling thread's context.  Returns the previous mode. */
+int hvws_set_run(hvws_ctx* ctx, int mode);
+/* Segments of the last step that the RUN path's repair pass put back and
+ * unmasked exactly (their hypothesis failed, or k_head saw they were not one
+ * run); -1 if the last scan was not a RUN step.  Waits for the step. */
+int64_t hvws_last_run_repairs(hvws_ctx* ctx);
 
 /* Device span of a timed region: hvws_span_begin records a marker on each of
  * the context's compute streams, hvws_span_end records the end markers, waits

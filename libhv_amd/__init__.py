@@ -115,6 +115,8 @@ _SIGS = {
     "hvws_last_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "hvws_step_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "hvws_set_speculation": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hvws_set_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hvws_last_run_repairs": (ctypes.c_int64, [ctypes.c_void_p]),
     "hvws_set_walk_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_last_scan_path": (ctypes.c_int, [ctypes.c_void_p]),
     "hvws_set_fast_bound": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),

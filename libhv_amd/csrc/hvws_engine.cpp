@@ -130,6 +130,7 @@ struct tset {
     dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total, sc_est;
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first, tile_key, tile_kind;
+    dbuf runs, run_fail, run_tseg;   // RUN path: per-segment run descriptors, failure words, tile -> segment
     uint64_t frame_cap = 0;
     hipEvent_t free_ev = nullptr;   // recorded after the last kernel reading the set (pipelined steps)
     hipEvent_t free_wait = nullptr; // what the next scan into the set waits for: free_ev, or the stop
@@ -138,7 +139,7 @@ struct tset {
     void release() {
         for (dbuf* b : {&carry_out, &counts, &bases, &total, &sc_mid, &sc_npred, &sc_pbase, &sc_fail, &sc_masked,
                         &sc_total, &sc_est, &f_hdr, &f_off, &f_len, &f_length, &f_key, &f_keyrot, &f_info,
-                        &tile_first, &tile_key, &tile_kind})
+                        &tile_first, &tile_key, &tile_kind, &runs, &run_fail, &run_tseg})
             b->release();
         frame_cap = 0;
     }
@@ -196,6 +197,15 @@ struct hvws_ctx {
     int scan_path = -1;        // HVWS_PATH_* of the last scan
     int prev_path = -1;        // ... and of the one before (set when a scan starts)
     uint64_t single_hint = 0;  // records of the last one-segment scan whose count was read
+    // RUN path (hvws_internal.h, drun): the last scan left no frame table (its
+    // records are built on demand), its unmask is k_unmask_run + k_run_fix
+    bool run_active = false;
+    bool run_call = false;     // the scan belongs to a step call (the only callers RUN serves)
+    int run_mode = -1;         // hvws_set_run: -1 auto, 0 never, 1 whenever a step's batch allows it
+    uint32_t run_skip = 0;     // steps left before RUN is tried again after a failed hypothesis
+    uint64_t run_seq = 0;      // the current RUN step's verdict number
+    uint64_t run_seen = 0;     // the last verdict read (status pad3)
+    uint64_t last_mean = 0;    // bytes per record of the last exact (or SPEC) scan: RUN is for small frames
     // frame sieve (hvws_sieve.hip): one long mixed-size segment discovered in
     // parallel.  h_sv receives the device state + survivor and chain counts
     // after each sieved scan (read as hints by the next one).
@@ -446,6 +456,12 @@ int step_times_at(hvws_ctx* c, int slot, float* out) {
 // Pipelined SPEC steps queue the unmask after the host has seen the scan
 // finish instead of behind a cross-stream event ($HVWS_HOST_ORDER=0: the
 // event, as in round 3).
+// $HVWS_RUN=0: the RUN path off (A/B runs); hvws_set_run overrides per context.
+bool run_env() {
+    static const int v = getenv("HVWS_RUN") ? atoi(getenv("HVWS_RUN")) : 1;
+    return v != 0;
+}
+
 bool host_order() {
     static const int v = getenv("HVWS_HOST_ORDER") ? atoi(getenv("HVWS_HOST_ORDER")) : 1;
     return v != 0;
@@ -605,11 +621,18 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
     const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED || path == HVWS_PATH_SPEC_FAILED ||
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
-    if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
-                           c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(), c->T().total.as<uint64_t>(),
-                           c->stream, pieces, timed ? c->tev[c->t_cur][2] : nullptr,
-                           timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess)
+    if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
+        if ((e = launch_unmask_run(c->variant, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_tseg.as<uint32_t>(),
+                                   c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
+                                   c->run_seq, c->stream, timed ? c->tev[c->t_cur][2] : nullptr,
+                                   timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess)
+            return e;
+    } else if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
+                                  c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(),
+                                  c->T().total.as<uint64_t>(), c->stream, pieces, timed ? c->tev[c->t_cur][2] : nullptr,
+                                  timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess) {
         return e;
+    }
     if (timed) c->t_rec[c->t_cur] |= (uint8_t)(4u | 8u);
     c->t_unmask[c->t_cur] = true;
     if (piped) {   // the next pipelined scan into this set waits for this unmask
@@ -638,6 +661,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     // unmask may still be running (pipelined steps).
     c->cur ^= 1;
     c->prev_path = c->scan_path;
+    c->run_active = false;
     if (c->cs == c->stream) c->piped = false;   // a later pipelined step re-arms the set events
     if (c->cs != c->stream && c->T().free_pending) {
         HIP_OR(hipStreamWaitEvent(c->cs, c->T().free_wait, 0), HVWS_EHIP);
@@ -677,6 +701,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.bases_x = nullptr;
     sc.est_u = nullptr;
     sc.no_verify = 0;
+    sc.runs = nullptr;
+    sc.run_fail = nullptr;
+    sc.run_tseg = nullptr;
+    sc.run_ntiles = sc.run_tile = 0;
     dspec_status* status_d = mapped<dspec_status>(c->h_status);
     const dspec_status* status_h = c->h_status.as<dspec_status>();
     if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
@@ -854,6 +882,60 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         uint32_t flags = 0;
         sc.status = status_d;
         bool done = false;
+        // The last RUN verdict the device has published: a failed hypothesis
+        // turns RUN off for the next 16 steps and the next scan exact.
+        const uint64_t vseq = __atomic_load_n(&status_h->pad3[0], __ATOMIC_ACQUIRE);
+        if (vseq != c->run_seen) {
+            c->run_seen = vseq;
+            if (status_h->pad3[1]) {
+                c->run_skip = 16;
+                c->spec_ok = false;
+            }
+        }
+        // RUN: a step's batch of small uniform frames (the last exact or SPEC
+        // scan matched the uniform estimates): discovery is k_head alone, the
+        // unmask checks every header it loads (hvws_internal.h, drun).
+        const bool run_auto = c->run_mode < 0 && c->spec_ok && c->spec_mode != 0 && !c->run_skip && c->last_mean &&
+                              c->last_mean <= RUN_MAX_FRAME && run_env();
+        if (c->run_skip) --c->run_skip;
+        if (unmask_into && c->run_call && c->vmask == 0 && (run_auto || c->run_mode == 1)) {
+            c->scan_path = HVWS_PATH_RUN;
+            HIP_OR(c->T().runs.ensure((uint64_t)nseg * sizeof(drun) + 64), HVWS_ENOMEM);
+            {
+                const void* was = c->T().run_fail.p;
+                const uint64_t had = c->T().run_fail.cap;
+                HIP_OR(c->T().run_fail.ensure((uint64_t)nseg * 4 + 64), HVWS_ENOMEM);
+                if (c->T().run_fail.p != was || c->T().run_fail.cap != had)
+                    HIP_OR(hipMemsetAsync(c->T().run_fail.p, 0, c->T().run_fail.cap, c->cs), HVWS_EHIP);
+            }
+            HIP_OR(c->T().run_tseg.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+            sc.runs = c->T().runs.as<drun>();
+            sc.run_fail = c->T().run_fail.as<uint32_t>();
+            sc.run_tseg = c->T().run_tseg.as<uint32_t>();
+            sc.run_ntiles = ntiles;
+            sc.run_tile = tile;
+            HIP_OR(pass(SCAN_RUN), HVWS_EHIP);
+            c->run_seq = ++c->scan_seq;
+            c->run_active = true;
+            c->nseg = nseg;
+            const bool ordered = c->cs != c->stream && host_order();
+            if (ordered) {
+                HIP_OR(launch_publish_tiles(status_d, c->run_seq, c->cs), HVWS_EHIP);
+                if ((rc = wait_status(c, c->run_seq, /*tiles=*/true)) != HVWS_OK) return rc;
+                HIP_OR(issue_unmask(c, unmask_into, rx_len, /*joined=*/true), HVWS_EHIP);
+            } else {
+                HIP_OR(tev_record(c, 1, c->cs), HVWS_EHIP);
+                HIP_OR(issue_unmask(c, unmask_into, rx_len), HVWS_EHIP);
+            }
+            if (unmasked) *unmasked = true;
+            c->nfr = 0;
+            c->nfr_known = false;
+            c->rx = d_rx;
+            c->rx_len = rx_len;
+            c->have_scan = true;
+            c->hcache_valid = false;
+            return HVWS_OK;
+        }
         c->scan_path = HVWS_PATH_COUNT_READ_EMIT;
         if ((c->spec_ok && c->spec_mode != 0) || c->spec_mode == 1) {
             // a set not used yet gets the other set's capacity (the table
@@ -986,12 +1068,33 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     c->rx_len = rx_len;
     c->have_scan = true;
     c->hcache_valid = false;
+    if (c->nfr_known && nfr) c->last_mean = rx_len / nfr;
     return HVWS_OK;
+}
+
+// The records of a RUN step, built when a reader asks for them: an exact scan
+// of the same batch (its headers never change; its segment and carry tables
+// are the device copies the RUN scan wrote) on the context stream, behind
+// the unmask and its repair.  The scan path stays RUN.
+int run_materialize(hvws_ctx* c) {
+    if (!c->run_active) return HVWS_OK;
+    c->run_active = false;
+    const int path = c->scan_path;
+    hipStream_t cs = c->cs;
+    c->cs = c->stream;
+    const bool call = c->run_call;
+    c->run_call = false;
+    const int rc = scan_device_carry(c, c->rx, c->rx_len, c->nseg);
+    c->run_call = call;
+    c->cs = cs;
+    c->scan_path = path;
+    return rc;
 }
 
 // The frame count of the last scan on the host (one small read-back when the
 // scan left it on the device).
 int ensure_count(hvws_ctx* c) {
+    if (int rc = run_materialize(c)) return rc;
     if (c->nfr_known) return HVWS_OK;
     HIP_OR(hipMemcpyAsync(c->h_total.p, c->T().total.p, 8, hipMemcpyDeviceToHost, c->stream), HVWS_EHIP);
     HIP_OR(hipStreamSynchronize(c->stream), HVWS_EHIP);
@@ -1004,6 +1107,7 @@ int ensure_count(hvws_ctx* c) {
 // count, per-segment first/count, carry-out, and the frame table up to the
 // record bound (small batches) -- copied into pinned memory, one sync.
 int readback_all(hvws_ctx* c) {
+    if (int rc = run_materialize(c)) return rc;
     const uint32_t nseg = c->nseg;
     // c->nfr is the exact count or its bound; copy at most a prefix of the
     // table with the rest, and the remainder after the sync if needed.
@@ -2356,7 +2460,9 @@ int hvws_step_resident(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_s
     if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
     c->cs = c->sstream;
     bool unmasked = false;
+    c->run_call = true;
     rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked);
+    c->run_call = false;
     if (rc == HVWS_OK && !unmasked) rc = unmask_impl(c, d_rx, rx_len);
     c->cs = c->stream;
     return rc;
@@ -2370,7 +2476,10 @@ int hvws_step(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* s
     if (((uintptr_t)d_rx & 15u) != 0) return set_err(HVWS_EINVAL, "rx buffer must be 16-byte aligned");
     if ((rc = upload_segments(c, segs, carry_in, nseg, rx_len)) != HVWS_OK) return rc;
     bool unmasked = false;
-    if ((rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked)) != HVWS_OK) return rc;
+    c->run_call = true;
+    rc = scan_device_carry(c, d_rx, rx_len, nseg, d_rx, &unmasked);
+    c->run_call = false;
+    if (rc != HVWS_OK) return rc;
     return unmasked ? HVWS_OK : unmask_impl(c, d_rx, rx_len);
 }
 
@@ -2423,6 +2532,7 @@ int hvws_get_segment_frames(hvws_ctx* c, uint64_t* first, uint64_t* count) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    if ((rc = run_materialize(c)) != HVWS_OK) return rc;
     if (c->hcache_valid) {
         if (first) memcpy(first, c->hfirst.data(), (uint64_t)c->nseg * 8);
         if (count) memcpy(count, c->hcount.data(), (uint64_t)c->nseg * 8);
@@ -2442,6 +2552,7 @@ int hvws_get_carry(hvws_ctx* c, websocket_parser* out, int* started) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (!c->have_scan) return set_err(HVWS_EINVAL, "no scan");
+    if ((rc = run_materialize(c)) != HVWS_OK) return rc;
     std::vector<dcarry> h;
     const dcarry* src;
     if (c->hcache_valid) {
@@ -2743,7 +2854,10 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     static const bool uni_ok = !getenv("HVWS_BUILD_UNI") || atoi(getenv("HVWS_BUILD_UNI")) != 0;
     // (payload steps shorter than a payload would make a tile's pieces
     // overlap out of order: the index handles those)
-    const bool uniform = uni_ok && h[2] == 0 && total % n == 0 && (n == 1 || h[4] >= h[5]);
+    // (small frames only, the lean form: at 64 KiB frames the index is ~0.1 %
+    // of the call and the position-derived form measured slower at the rx
+    // layout, 21.3 against 20.2 ms at c3, profiles/r5b_raw)
+    const bool uniform = uni_ok && v == 5 && h[2] == 0 && total % n == 0 && (n == 1 || h[4] >= h[5]);
     const uint64_t uni[4] = {uniform ? total / n : 0, uniform ? total / n - h[5] : 0, h[3], h[4]};
     c->tx_uniform = uniform;
     if (!uniform) {
@@ -2929,6 +3043,21 @@ int hvws_set_walk_verify(hvws_ctx* c, int mode) {
     if (!c) return HVWS_ENODEV;
     const int old = c->verify_mode;
     c->verify_mode = mode < 0 ? -1 : (mode ? 1 : 0);
+    return old;
+}
+
+int64_t hvws_last_run_repairs(hvws_ctx* c) {
+    if (check_ctx(c) != HVWS_OK || c->scan_path != HVWS_PATH_RUN) return -1;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    const dspec_status* st = c->h_status.as<dspec_status>();
+    return __atomic_load_n(&st->pad3[0], __ATOMIC_ACQUIRE) == c->run_seq ? (int64_t)st->pad3[1] : -1;
+}
+
+int hvws_set_run(hvws_ctx* c, int mode) {
+    if (!c) c = thread_ctx();
+    if (!c) return HVWS_ENODEV;
+    const int old = c->run_mode;
+    c->run_mode = mode < 0 ? -1 : (mode ? 1 : 0);
     return old;
 }
 

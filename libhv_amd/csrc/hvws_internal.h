@@ -120,6 +120,52 @@ enum : uint32_t {
 
 struct sieve_bufs;
 
+// RUN path (round 5): a batch whose segments each hold one run of equal
+// frames (the last check saw uniform counts) is unmasked from per-segment
+// descriptors alone -- no per-frame records, no second pass over the header
+// lines.  k_head writes the descriptor (the carried-in frame and the frame cut
+// by the segment end exactly, the run in between as a hypothesis: the first
+// whole frame's size repeated); k_unmask_run parses every run header from
+// the tile bytes it loads anyway, checks it against the hypothesis and takes
+// its key from it; k_run_fix, queued behind on the same stream, undoes and
+// redoes exactly any segment whose hypothesis failed, so work queued after a
+// step always sees the reference's bytes.  Frame records are built on demand
+// (an exact scan of the unchanged headers) when a reader asks for them.
+struct drun {
+    uint64_t seg_lo, seg_hi;   // the segment's absolute byte range
+    uint64_t p0;               // absolute offset of the run's first header
+    uint64_t stride;           // bytes per frame of the run (0: no run)
+    uint64_t len;              // payload bytes per frame of the run
+    double   inv;              // 1 / stride
+    uint32_t cnt, hlen;        // frames in the run, header bytes of each
+    uint32_t masked, flags;    // run frames carry a key (the first's mask bit); RUN_*
+    uint64_t a_off, a_end;     // carried-in frame's payload piece [a_off, a_end), absolute
+    uint64_t t_off, t_end;     // payload piece of the frame cut by the segment end
+    uint32_t a_kw, t_kw;       // their key words for 4-byte aligned words (0: nothing to XOR)
+    uint64_t pad;
+    dcarry   cin;              // the segment's carry-in (the repair's exact path; the shared
+                               // carry table belongs to the next scan by then)
+};
+static_assert(sizeof(drun) == 160, "drun layout");
+enum : uint32_t { RUN_BAD = 1u };   // the segment is not one run (k_head saw it): exact repair only
+constexpr uint32_t RUN_MAXS = 8;      // segments per unmask tile staged in LDS (more: the tile's slow path)
+constexpr uint32_t RUN_KEYS = 1024;   // run frames per tile whose keys are staged (more: slow path)
+constexpr uint64_t RUN_MAX_FRAME = 8192;   // frames at most this size take the RUN path (bigger: SPEC)
+// k_head<false> writes runs[s] when given; k_run_tiles: tseg[t] = first
+// segment ending after tile t's first byte (t <= ntiles); fail[s] is segment
+// s's failure word (zeroed by k_head), fail[nseg .. nseg + 2] the batch's
+// (any failed, failed count, repair workgroups done), zero between RUN steps
+// (the repair's last workgroup clears them; the host zeroes a new array).
+hipError_t launch_run_tiles(const dseg* segs, uint32_t nseg, uint32_t* tseg, uint32_t* fail, uint64_t ntiles,
+                            uint64_t tile, hipStream_t st);
+// The RUN unmask (geometry `variant`, as launch_unmask) and its repair pass;
+// the timing events ride on the unmask's first dispatch (start) and the
+// repair's (stop).  The repair publishes (seq, failed segments) to
+// status->pad3 when it is done.
+hipError_t launch_unmask_run(int variant, uint8_t* rx, uint64_t rx_len, const drun* runs, const uint32_t* tseg,
+                             uint32_t nseg, uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st,
+                             hipEvent_t ev_start, hipEvent_t ev_stop);
+
 struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     dmid*     mid;
     uint64_t* npred;
@@ -143,6 +189,10 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint64_t* bases_x;       // SLACK: exact bases (nseg)
     uint64_t* est_u;         // SLACK: uniform-stride estimates (nseg), for SPEC_MATCH
     uint32_t  no_verify;     // SPEC/SLACK: head + walk only (no k_verify pair, no k_head<true>)
+    drun*     runs;          // RUN: k_head writes each segment's run descriptor
+    uint32_t* run_fail;      // RUN: per-segment failure words + the batch's, zeroed by k_head / k_run_tiles
+    uint32_t* run_tseg;      // RUN: first segment of each unmask tile (run_ntiles + 1 entries)
+    uint64_t  run_ntiles, run_tile;
 };
 
 // Bijective XCD-contiguous tile order: the dispatcher deals blocks b, b+8,
@@ -225,7 +275,8 @@ hipError_t launch_sieve_emit(const uint8_t* rx, uint64_t rx_len, const dseg* seg
 // slack_cap), then a device check that every segment fit and a compaction into
 // the frame table at the exact bases; a segment that did not fit zeroes *total
 // and the host re-scans COUNT + EMIT.
-enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2, SCAN_SPEC = 3, SCAN_SLACK = 4 };
+// RUN: k_head writing run descriptors (no est, no walk) + the tile-segment index.
+enum scan_pass { SCAN_COUNT = 0, SCAN_EMIT = 1, SCAN_SINGLE = 2, SCAN_SPEC = 3, SCAN_SLACK = 4, SCAN_RUN = 5 };
 hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg,
                        const dcarry* carry_in, dcarry* carry_out, uint64_t* counts, uint64_t* bases,
                        uint64_t* total, scan_scratch sc, dframes fr, uint32_t vmask, hipStream_t st);

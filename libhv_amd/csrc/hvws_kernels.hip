@@ -229,7 +229,8 @@ __device__ __forceinline__ void head_body(const uint8_t* __restrict__ rx, uint64
                                                        const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
                                                        dcarry* __restrict__ carry_w, int probe_mixed,
                                                        uint64_t slack_cap, uint64_t* __restrict__ est_u,
-                                          uint32_t w0, uint32_t wn, uint32_t hflags) {
+                                          uint32_t w0, uint32_t wn, uint32_t hflags, drun* __restrict__ runs,
+                                          uint32_t* __restrict__ run_fail) {
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t s = w0; s < nseg; s += wn) {
         dseg sg;
@@ -260,14 +261,19 @@ __device__ __forceinline__ void head_body(const uint8_t* __restrict__ rx, uint64
         }
         const uint64_t sb = sg.off, L = sg.len;
         st.started = 0;
+        const dcarry st_in = st;
         uint64_t pos = 0, n = 0;
         frec r;
+        r.info = 0;
         if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, r, vmask)) {
             if (EMIT && lane == 0) store_frame(fr, bases[s], sb, r);
             ++n;
         }
         uint64_t stride = 0, np = 0, mixed = 0;
         hdr h;
+        h.hlen = 0;
+        h.length = 0;
+        h.flags = 0;
         if (st.state == S_START && parse_at(rx, rx_len, sb, L, pos, h)) {
             stride = (uint64_t)h.hlen + h.length;
             const uint64_t cnt = (L - pos) / stride;
@@ -314,6 +320,56 @@ __device__ __forceinline__ void head_body(const uint8_t* __restrict__ rx, uint64
                 if (hl <= rem) ++e;
             }
         }
+        if (runs && lane == 0) {
+            // RUN: the segment as one run of frames of the first whole one's
+            // size (the hypothesis k_unmask_run checks header by header), with
+            // the carried-in frame and the frame cut by the segment end exact.
+            drun d;
+            d.seg_lo = sb;
+            d.seg_hi = sb + L;
+            d.flags = 0;
+            d.a_off = d.a_end = d.t_off = d.t_end = 0;
+            d.a_kw = d.t_kw = 0;
+            d.pad = 0;
+            if (n && (r.info & I_BODY) && (r.info & F_MASK)) {   // the carried-in frame's payload here
+                d.a_off = sb + r.pay_off;
+                d.a_end = d.a_off + r.pay_len;
+                d.a_kw = key_for_aligned(r.key, d.a_off, (r.info >> 8) & 3u);
+            }
+            const uint64_t cnt = stride ? (L - pos) / stride : 0;
+            d.p0 = sb + pos;
+            d.stride = stride;
+            d.len = h.length;
+            d.inv = stride ? 1.0 / (double)stride : 0.0;
+            d.cnt = (uint32_t)cnt;
+            d.hlen = h.hlen;
+            d.masked = (h.flags & F_MASK) ? 1u : 0u;
+            if (cnt > 0xFFFFFFFFull) d.flags |= RUN_BAD;
+            if (st.state == S_START) {
+                // the frame after the run: cut by the segment end (its payload
+                // piece here), or it must end exactly there -- anything after
+                // it means the segment is not one run
+                const uint64_t q = pos + cnt * stride;
+                if (q < L && L - q >= 2) {
+                    uint64_t lo, hi;
+                    ld16(rx, rx_len, sb + q, lo, hi);
+                    const hdr ht = parse_hdr(lo, hi);
+                    if (ht.hlen <= L - q) {
+                        const uint64_t ps = q + ht.hlen, rem = L - ps;
+                        if (ht.length < rem) d.flags |= RUN_BAD;
+                        if ((ht.flags & F_MASK) && rem && ht.length) {
+                            d.t_off = sb + ps;
+                            d.t_end = sb + ps + (ht.length < rem ? ht.length : rem);
+                            d.t_kw = key_for_aligned(ht.key, d.t_off, 0);
+                        }
+                    }
+                }
+            }
+            d.cin = st_in;
+            runs[s] = d;
+            run_fail[s] = 0;
+            if (d.flags & RUN_BAD) atomicOr(&run_fail[nseg], 1u);   // the repair pass must look
+        }
         if (lane == 0) {
             // SLACK (mixed sizes): the segment's region of the slack table --
             // its record bound, at most slack_cap records
@@ -347,11 +403,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_head(const uint8_t* __restrict
                                                        const dcarry* __restrict__ src_carry, dseg* __restrict__ segs_w,
                                                        dcarry* __restrict__ carry_w, int probe_mixed,
                                                        uint64_t slack_cap, uint64_t* __restrict__ est_u,
-                                                       uint32_t hflags) {
+                                                       uint32_t hflags, drun* __restrict__ runs,
+                                                       uint32_t* __restrict__ run_fail) {
     const uint32_t wpb = SCAN_THREADS / 64;
     head_body<EMIT>(rx, rx_len, segs, nseg, carry_in, mid, npred, first_fail, last_masked, bases, fr, vmask, spec_min, est,
                     src_segs, src_carry, segs_w, carry_w, probe_mixed, slack_cap, est_u,
-                    blockIdx.x * wpb + (threadIdx.x >> 6), gridDim.x * wpb, hflags);
+                    blockIdx.x * wpb + (threadIdx.x >> 6), gridDim.x * wpb, hflags, runs, run_fail);
 }
 
 // --------------------------------------------------------------- k_verify
@@ -2021,6 +2078,325 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
     }
 }
 
+// ------------------------------------------------------------ RUN unmask
+//
+// A batch whose segments are each one run of equal frames (hvws_internal.h,
+// drun).  k_unmask_run loads its tile as k_unmask does, stages it in LDS,
+// parses the header of every run frame that starts in the tile (one thread per
+// frame), checks it against the run's hypothesis (header length, payload
+// length, mask bit) and keeps its key in LDS; then every chunk XORs the pieces
+// that meet it: the carried-in frame's, the run frames' (position by division
+// by the stride), the cut frame's.  The header lines are read once, as part
+// of the tile -- the scan beside the previous unmask is k_head alone.  A
+// failed check marks the segment; k_run_fix (behind, on the same stream)
+// XORs that segment's hypothesis back -- the same keys from the same,
+// unchanged header positions -- and unmasks it exactly.
+
+// tseg[t] = first segment whose end lies after tile t's first byte (nseg if
+// none).
+__global__ void k_run_tiles(const dseg* __restrict__ segs, uint32_t nseg, uint32_t* __restrict__ tseg,
+                            uint64_t ntiles, uint64_t tile) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t x = t * tile;
+    uint32_t lo = 0, hi = nseg;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segs[mid].off + segs[mid].len > x) hi = mid;
+        else lo = mid + 1;
+    }
+    tseg[t] = lo;
+}
+
+// floor((x - p0) / stride) for x >= p0, exact (double estimate, corrected)
+__device__ __forceinline__ uint64_t run_frame_of(const drun& r, uint64_t x) {
+    const uint64_t d = x - r.p0;
+    uint64_t j = (uint64_t)((double)d * r.inv);
+    while (j && j * r.stride > d) --j;
+    while ((j + 1) * r.stride <= d) ++j;
+    return j;
+}
+
+// OR key word kw (for 4-byte aligned words) into the chunk mask for bytes
+// [lo, hi) of the chunk at c (absolute), clamped to the chunk
+__device__ __forceinline__ void run_piece(uint64_t& mlo, uint64_t& mhi, uint64_t c, uint64_t lo, uint64_t hi,
+                                          uint32_t kw) {
+    const uint64_t a = lo > c ? lo : c, b = hi < c + 16 ? hi : c + 16;
+    if (a >= b || !kw) return;
+    const uint32_t l = (uint32_t)(a - c), h = (uint32_t)(b - c);
+    const uint64_t kk = (uint64_t)kw | ((uint64_t)kw << 32);
+    const uint64_t keep_lo = (l >= 8 ? 0ull : (~0ull << (8 * l))) & (h >= 8 ? ~0ull : ((1ull << (8 * h)) - 1));
+    const uint64_t keep_hi = (l <= 8 ? ~0ull : (~0ull << (8 * (l - 8)))) &
+                             (h <= 8 ? 0ull : (h >= 16 ? ~0ull : ((1ull << (8 * (h - 8))) - 1)));
+    mlo |= kk & keep_lo;
+    mhi |= kk & keep_hi;
+}
+
+// The run's hypothesis for header bytes (lo, hi): same header length,
+// payload length and mask bit as the run's first frame.
+__device__ __forceinline__ bool run_header_ok(const drun& r, const hdr& h) {
+    return h.hlen == r.hlen && h.length == r.len && ((h.flags & F_MASK) ? 1u : 0u) == r.masked;
+}
+
+// The mask of chunk c from segment r's pieces; key(j) gives run frame j's key.
+template <typename KEY>
+__device__ __forceinline__ void run_chunk_mask(const drun& r, uint64_t c, uint64_t& mlo, uint64_t& mhi, KEY key) {
+    if (c + 16 <= r.seg_lo || c >= r.seg_hi || (r.flags & RUN_BAD)) return;   // BAD: the repair alone
+    run_piece(mlo, mhi, c, r.a_off, r.a_end, r.a_kw);
+    run_piece(mlo, mhi, c, r.t_off, r.t_end, r.t_kw);
+    if (!r.cnt || !r.masked) return;
+    const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;   // the run's end
+    const uint64_t a = c > r.p0 ? c : r.p0, b = c + 16 < re ? c + 16 : re;
+    if (a >= b) return;
+    for (uint64_t j = run_frame_of(r, a); j < r.cnt; ++j) {
+        const uint64_t fo = r.p0 + j * r.stride;
+        if (fo >= b) break;
+        const uint64_t ps = fo + r.hlen, pe = fo + r.stride;
+        if (pe > c && ps < c + 16) run_piece(mlo, mhi, c, ps, pe, rotr32(key(j), 8u * ((0u - (uint32_t)ps) & 3u)));
+    }
+}
+
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
+                                                  const uint32_t* __restrict__ tseg, uint32_t nseg,
+                                                  uint32_t* __restrict__ fail, uint64_t tile0, uint64_t ntiles) {
+    constexpr uint64_t TILE = (uint64_t)T * U * 16u;
+    __shared__ u32x4 s_tile[TILE / 16 + 1];   // + the next tile's first chunk (a header may run into it)
+    __shared__ drun s_run[RUN_MAXS];
+    __shared__ uint32_t s_key[RUN_KEYS];
+    __shared__ uint32_t s_jlo[RUN_MAXS], s_kb[RUN_MAXS + 1];
+    const uint64_t t = tile0 + blockIdx.x;
+    const uint64_t base = t * TILE;
+    const uint32_t tid = threadIdx.x;
+    const bool full = base + TILE <= rx_len;
+    u32x4 v[U];
+    if (full) {
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rx + base + ((uint64_t)i * T + tid) * 16u));
+    } else {
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int b = 0; b < 16; ++b)
+                if (c + b < rx_len) w[b >> 2] |= (uint32_t)rx[c + b] << (8 * (b & 3));
+            v[i] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+    }
+    const uint32_t s0 = tseg[t];
+    if (s0 >= nseg) return;   // no segment reaches this tile: no byte to unmask
+    const uint32_t s1 = tseg[t + 1] < nseg ? tseg[t + 1] : nseg - 1;
+    const uint32_t ns = s1 - s0 + 1;
+    const bool staged = ns <= RUN_MAXS;
+    if (staged && tid < ns) s_run[tid] = runs[s0 + tid];
+#pragma unroll
+    for (int i = 0; i < U; ++i) s_tile[(uint32_t)i * T + tid] = v[i];
+    if (tid == 0) {
+        uint64_t lo, hi;
+        ld16(rx, rx_len, base + TILE, lo, hi);
+        s_tile[TILE / 16] = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    }
+    __syncthreads();
+    // run frames of each staged segment whose header or payload meets the tile
+    if (staged && tid < ns) {
+        const drun& r = s_run[tid];
+        uint32_t nk = 0, jlo = 0;
+        if (r.cnt) {
+            const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
+            const uint64_t a = base > r.p0 ? base : r.p0, b = base + TILE < re ? base + TILE : re;
+            if (a < b) {
+                jlo = (uint32_t)run_frame_of(r, a);
+                nk = (uint32_t)run_frame_of(r, b - 1) + 1u - jlo;
+            }
+        }
+        s_jlo[tid] = jlo;
+        s_kb[tid + 1] = nk;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        s_kb[0] = 0;
+        for (uint32_t k = 0; k < (staged ? ns : 0u); ++k) s_kb[k + 1] += s_kb[k];
+    }
+    __syncthreads();
+    const uint32_t nkeys = staged ? s_kb[ns] : 0u;
+    const bool keyed = staged && nkeys <= RUN_KEYS;
+    if (keyed) {
+        // one thread per run frame: its header from the staged tile (or, for a
+        // frame begun before the tile, from HBM), checked, its key kept
+        const uint8_t* lt = reinterpret_cast<const uint8_t*>(s_tile);
+        for (uint32_t f = tid; f < nkeys; f += T) {
+            uint32_t k = 0;
+            while (k + 1 < ns && s_kb[k + 1] <= f) ++k;
+            const drun& r = s_run[k];
+            const uint64_t hs = r.p0 + (uint64_t)(s_jlo[k] + (f - s_kb[k])) * r.stride;
+            uint64_t lo, hi;
+            if (hs >= base) {
+                const uint32_t q = (uint32_t)(hs - base);
+                const uint32_t w = q >> 2, sh = q & 3u;
+                const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lt);
+                const uint32_t d0 = l32[w], d1 = l32[w + 1], d2 = l32[w + 2], d3 = l32[w + 3], d4 = l32[w + 4];
+                lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+                hi = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32);
+            } else {
+                ld16(rx, rx_len, hs, lo, hi);
+            }
+            const hdr h = parse_hdr(lo, hi);
+            if (hs >= base && !run_header_ok(r, h)) {   // each header is checked by the tile it starts in
+                atomicOr(&fail[s0 + k], 1u);
+                atomicOr(&fail[nseg], 1u);
+            }
+            s_key[f] = r.masked ? h.key : 0u;
+        }
+    } else {
+        // slow path (more segments or run frames than staged): every header
+        // starting in the tile checked from HBM
+        for (uint32_t s = s0; s <= s1; ++s) {
+            const drun r = runs[s];
+            if (!r.cnt) continue;
+            const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
+            const uint64_t a = base > r.p0 ? base : r.p0, b = base + TILE < re ? base + TILE : re;
+            if (a >= b) continue;
+            const uint64_t j0 = run_frame_of(r, a), j1 = run_frame_of(r, b - 1);
+            for (uint64_t j = j0 + tid; j <= j1; j += T) {
+                const uint64_t hs = r.p0 + j * r.stride;
+                if (hs < base) continue;
+                uint64_t lo, hi;
+                ld16(rx, rx_len, hs, lo, hi);
+                if (!run_header_ok(r, parse_hdr(lo, hi))) {
+                    atomicOr(&fail[s], 1u);
+                    atomicOr(&fail[nseg], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // XOR: each chunk's pieces from every segment meeting it
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+        const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+        if (c >= rx_len) continue;
+        uint64_t mlo = 0, mhi = 0;
+        if (keyed) {
+            for (uint32_t k = 0; k < ns; ++k)
+                run_chunk_mask(s_run[k], c, mlo, mhi, [&](uint64_t j) { return s_key[s_kb[k] + (uint32_t)(j - s_jlo[k])]; });
+        } else {
+            for (uint32_t s = s0; s <= s1; ++s) {
+                const drun r = runs[s];
+                run_chunk_mask(r, c, mlo, mhi, [&](uint64_t j) {
+                    uint64_t lo, hi;
+                    ld16(rx, rx_len, r.p0 + j * r.stride, lo, hi);
+                    return r.masked ? parse_hdr(lo, hi).key : 0u;
+                });
+            }
+        }
+        if (!(mlo | mhi)) continue;
+        const u32x4 m = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
+        const u32x4 o = v[i] ^ m;
+        if (full) {
+            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(rx + c));
+        } else {
+            const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+            for (int b = 0; b < 16; ++b)
+                if (c + b < rx_len) rx[c + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+// XOR [lo, hi) of HBM with key word kw (for 4-byte aligned words), one wave
+__device__ __forceinline__ void wave_xor_range(uint8_t* rx, uint64_t lo, uint64_t hi, uint32_t kw) {
+    if (lo >= hi || !kw) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t a = (lo + 15) & ~15ull, b = hi & ~15ull;
+    if (a >= b) {
+        for (uint64_t x = lo + lane; x < hi; x += 64) rx[x] ^= (uint8_t)(kw >> (8 * (x & 3u)));
+        return;
+    }
+    for (uint64_t x = lo + lane; x < a; x += 64) rx[x] ^= (uint8_t)(kw >> (8 * (x & 3u)));
+    for (uint64_t x = b + lane; x < hi; x += 64) rx[x] ^= (uint8_t)(kw >> (8 * (x & 3u)));
+    for (uint64_t x = a + (uint64_t)lane * 16u; x < b; x += 64u * 16u) {
+        u32x4* q = reinterpret_cast<u32x4*>(rx + x);
+        *q = *q ^ u32x4{kw, kw, kw, kw};
+    }
+}
+
+// Repair after k_unmask_run: nothing unless a segment failed (one word read
+// per workgroup).  A failed segment is put back -- its hypothesis XORed again
+// with the same keys, read from the same header positions, which no unmask
+// changes -- and unmasked exactly (the carried-in frame, then walk_frames over
+// HBM, each record's payload XORed by its lane).  A segment k_head found not
+// to be one run (RUN_BAD) had nothing applied: exact only.  The last
+// workgroup to finish publishes (seq, failed segments) to the status block.
+// fail[nseg] = any failed, [nseg + 1] = failed count, [nseg + 2] = workgroups done.
+constexpr uint32_t RUN_FIX_BLOCKS = 32;
+
+__global__ __launch_bounds__(256) void k_run_fix(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
+                                                 uint32_t nseg, uint32_t* __restrict__ fail,
+                                                 dspec_status* __restrict__ status, uint64_t seq) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (__hip_atomic_load(&fail[nseg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        const uint32_t w0 = blockIdx.x * 4u + wave, wn = gridDim.x * 4u;
+        for (uint32_t s = w0; s < nseg; s += wn) {
+            const drun r = runs[s];
+            const bool bad = (r.flags & RUN_BAD) != 0;
+            if (!bad && !fail[s]) continue;
+            if (lane == 0) atomicAdd(&fail[nseg + 1], 1u);
+            if (!bad) {   // undo the hypothesis
+                wave_xor_range(rx, r.a_off, r.a_end, r.a_kw);
+                wave_xor_range(rx, r.t_off, r.t_end, r.t_kw);
+                if (r.masked)
+                    for (uint64_t j = 0; j < r.cnt; ++j) {
+                        const uint64_t fo = r.p0 + j * r.stride;
+                        uint64_t lo, hi;
+                        ld16(rx, rx_len, fo, lo, hi);
+                        const uint64_t ps = fo + r.hlen;
+                        wave_xor_range(rx, ps, fo + r.stride,
+                                       rotr32(parse_hdr(lo, hi).key, 8u * ((0u - (uint32_t)ps) & 3u)));
+                    }
+                __threadfence();
+            }
+            // the exact path over the segment's bytes
+            const uint64_t sb = r.seg_lo, L = r.seg_hi - r.seg_lo;
+            dcarry st = r.cin;
+            uint64_t pos = 0, n = 0;
+            frec fr0;
+            if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, fr0, 0u) && (fr0.info & I_BODY) &&
+                (fr0.info & F_MASK)) {
+                const uint64_t po = sb + fr0.pay_off;
+                wave_xor_range(rx, po, po + fr0.pay_len, key_for_aligned(fr0.key, po, (fr0.info >> 8) & 3u));
+            }
+            __threadfence();
+            // walk_frames calls emit from every lane owning a record (the
+            // whole frames of one round) or from lane 0 (the cut frame)
+            walk_frames<true>(rx, rx_len, sb, L, st, pos, n, 0u, [&](uint64_t, const frec& v) {
+                if (!(v.info & I_BODY) || !(v.info & F_MASK)) return;
+                const uint64_t po = sb + v.pay_off, pe = po + v.pay_len;
+                const uint32_t kw = key_for_aligned(v.key, po, (v.info >> 8) & 3u);
+                for (uint64_t x = po; x < pe; ++x) rx[x] ^= (uint8_t)(kw >> (8 * (x & 3u)));
+            });
+            __threadfence();
+        }
+    }
+    // the last workgroup publishes
+    __shared__ uint32_t s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(&fail[nseg + 2], 1u) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x == 0) {
+        __threadfence();
+        status->pad3[1] = __hip_atomic_load(&fail[nseg + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&status->pad3[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the batch's words clean for this table set's next RUN step (k_head
+        // sets the first for a segment that is not one run)
+        fail[nseg] = 0;
+        fail[nseg + 1] = 0;
+        fail[nseg + 2] = 0;
+    }
+}
+
 // ---------------------------------------------------------- k_stream_xor
 // The same geometry with no frame table: the measured in-place ceiling.
 template <int T, int U, bool SWZ>
@@ -2099,7 +2475,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
                            sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, (int)(pass == SCAN_SINGLE && sieve),
                            pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
-                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, 0u);
+                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, 0u, (drun*)nullptr, (uint32_t*)nullptr);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, sc.npred, sc.pbase, nseg, sc.total_pred);
         hipLaunchKernelGGL(k_verify<false>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
@@ -2108,7 +2484,7 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         hipLaunchKernelGGL(k_head<true>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
                            (uint64_t*)nullptr, (const dseg*)nullptr, (const dcarry*)nullptr, (dseg*)nullptr,
-                           (dcarry*)nullptr, 0, (uint64_t)0, (uint64_t*)nullptr, 0u);
+                           (dcarry*)nullptr, 0, (uint64_t)0, (uint64_t*)nullptr, 0u, (drun*)nullptr, (uint32_t*)nullptr);
         hipLaunchKernelGGL(k_verify<true>, dim3(vb), dim3(256), 0, st, rx, rx_len, segs, nseg, sc.mid, sc.pbase,
                            sc.total_pred, sc.first_fail, sc.last_masked, bases, fr, vmask);
         if (sieve) {
@@ -2129,7 +2505,8 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(), est,
                            sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0,
                            pass == SCAN_SLACK ? sc.slack_cap : (uint64_t)0,
-                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY);
+                           pass == SCAN_SLACK ? sc.est_u : (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY,
+                           (drun*)nullptr, (uint32_t*)nullptr);
         hipLaunchKernelGGL(k_offsets, dim3(1), dim3(ONE_BLOCK), 0, st, est, bases, nseg, total);
         hipLaunchKernelGGL(k_walk<true>, dim3(wwb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, sc.mid,
                            sc.npred, sc.first_fail, sc.last_masked, carry_out, counts, bases, fr, vmask, 1,
@@ -2161,6 +2538,14 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
         if (sc.status)
             hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(ONE_BLOCK), 0, st, counts, sc.est, sc.npred, nseg, total,
                                fr.cap, sc.status, sc.seq);
+    } else if (pass == SCAN_RUN) {
+        hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+                           sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
+                           (uint64_t*)nullptr, sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0, (uint64_t)0,
+                           (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY, sc.runs, sc.run_fail);
+        if (hipError_t e = launch_run_tiles(segs, nseg, sc.run_tseg, sc.run_fail, sc.run_ntiles, sc.run_tile, st);
+            e != hipSuccess)
+            return e;
     } else if (pass == SCAN_SLACK) {
         if (sc.no_verify) {
             head_walk(sc.est, sc.slack);
@@ -2371,6 +2756,48 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_run_tiles(const dseg* segs, uint32_t nseg, uint32_t* tseg, uint32_t* fail, uint64_t ntiles,
+                            uint64_t tile, hipStream_t st) {
+    const uint64_t nb = (ntiles + 1 + 255) / 256;
+    (void)fail;
+    hipLaunchKernelGGL(k_run_tiles, dim3((uint32_t)nb), dim3(256), 0, st, segs, nseg, tseg, ntiles, tile);
+    return hipGetLastError();
+}
+
+hipError_t launch_unmask_run(int variant, uint8_t* rx, uint64_t rx_len, const drun* runs, const uint32_t* tseg,
+                             uint32_t nseg, uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st,
+                             hipEvent_t ev_start, hipEvent_t ev_stop) {
+    if (rx_len == 0 || nseg == 0) return hipSuccess;
+    if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
+    const uint64_t tile = unmask_tile(variant);
+    const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
+    const int threads = kGeoms[variant].threads;
+    const uint64_t cap = max_tiles_per_launch(threads);
+    for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
+        const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
+        const hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
+#define HVWS_RUN_CASE(i, t, u, s)                                                                                    \
+    case i:                                                                                                          \
+        if (e0)                                                                                                      \
+            hipExtLaunchKernelGGL((k_unmask_run<t, u>), dim3((uint32_t)ntiles), dim3(t), 0, st, e0, nullptr, 0u, rx,  \
+                                  rx_len, runs, tseg, nseg, fail, tile0, ntiles);                                    \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_unmask_run<t, u>), dim3((uint32_t)ntiles), dim3(t), 0, st, rx, rx_len, runs, tseg, \
+                               nseg, fail, tile0, ntiles);                                                           \
+        break;
+        switch (variant) { HVWS_UNMASK_GEOMS(HVWS_RUN_CASE) default: return hipErrorInvalidValue; }
+#undef HVWS_RUN_CASE
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (ev_stop)
+        hipExtLaunchKernelGGL(k_run_fix, dim3(RUN_FIX_BLOCKS), dim3(256), 0, st, nullptr, ev_stop, 0u, rx, rx_len, runs,
+                              nseg, fail, status, seq);
+    else
+        hipLaunchKernelGGL(k_run_fix, dim3(RUN_FIX_BLOCKS), dim3(256), 0, st, rx, rx_len, runs, nseg, fail, status, seq);
+    return hipGetLastError();
 }
 
 hipError_t launch_stream_xor(int variant, uint8_t* d, uint64_t n, uint32_t pattern, hipStream_t st) {

@@ -194,20 +194,26 @@ def _oracle_batch(buf: np.ndarray, segs, carries):
 # The one-walk passes (SPEC, SLACK) run adaptively (default), with the
 # k_verify pair forced ("_verify", fourth field 1) and without it
 # ("_noverify", 0: head + walk, the walk records the carried-in frame).
+# The RUN path (fifth field 1: hvws_set_run forced) takes every multi-segment
+# batch of a step, uniform or not: a segment that is not one run of equal
+# frames fails its check in the unmask and is repaired exactly on the device,
+# so these modes also run the repair pass on every mixed batch.
 SCAN_MODES = [("default", 0, -1), ("count_read", 1, 0), ("speculate", 1, 1),
               ("speculate_verify", 1, 1, 1), ("speculate_noverify", 1, 1, 0),
               ("pipelined", 0, -1), ("pipelined_speculate", 1, 1),
               ("slack", 1, 2), ("slack_noverify", 1, 2, 0), ("pipelined_slack", 1, 2),
-              ("pipelined_slack_verify", 1, 2, 1)]
+              ("pipelined_slack_verify", 1, 2, 1), ("run", 1, 1, -1, 1), ("pipelined_run", 1, 1, -1, 1)]
 
 
 def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp, mode):
     L = libhv_amd.lib()
     bound, spec = mode[1], mode[2]
     verify = mode[3] if len(mode) > 3 else -1
+    run = mode[4] if len(mode) > 4 else 0   # RUN only where a mode asks for it (test_gpu_run.py: automatic)
     old_b = L.hvws_set_fast_bound(eng.ctx, bound)
     old_s = L.hvws_set_speculation(eng.ctx, spec)
     old_v = L.hvws_set_walk_verify(eng.ctx, verify)
+    old_r = L.hvws_set_run(eng.ctx, run)
     try:
         rx = eng.to_device(buf)
         if mode[0].startswith("pipelined"):
@@ -223,6 +229,9 @@ def _step_checked(eng, buf, segs, carries, exp_recs, exp_carry, exp_started, exp
         L.hvws_set_fast_bound(eng.ctx, 0 if old_b == 1 << 24 else old_b)
         L.hvws_set_speculation(eng.ctx, old_s)
         L.hvws_set_walk_verify(eng.ctx, old_v)
+        L.hvws_set_run(eng.ctx, old_r)
+    if run == 1 and len(segs) > 1:
+        assert path == 7, (mode, path)   # HVWS_PATH_RUN
     assert len(frames) == len(exp_recs), mode
     for f in ("hdr_off", "pay_off", "pay_len", "length", "key", "info"):
         assert np.array_equal(frames[f], exp_recs[f]), (mode, f)
