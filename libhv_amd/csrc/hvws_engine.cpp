@@ -130,7 +130,7 @@ struct tset {
     dbuf sc_mid, sc_npred, sc_pbase, sc_fail, sc_masked, sc_total, sc_est;
     dbuf f_hdr, f_off, f_len, f_length, f_key, f_keyrot, f_info;
     dbuf tile_first, tile_key, tile_kind;
-    dbuf runs, run_fail, run_tseg;   // RUN path: per-segment run descriptors, failure words, tile -> segment
+    dbuf runs, run_fail, run_trun;   // RUN path: per-segment run descriptors, failure words, per-tile records
     uint64_t frame_cap = 0;
     hipEvent_t free_ev = nullptr;   // recorded after the last kernel reading the set (pipelined steps)
     hipEvent_t free_wait = nullptr; // what the next scan into the set waits for: free_ev, or the stop
@@ -139,7 +139,7 @@ struct tset {
     void release() {
         for (dbuf* b : {&carry_out, &counts, &bases, &total, &sc_mid, &sc_npred, &sc_pbase, &sc_fail, &sc_masked,
                         &sc_total, &sc_est, &f_hdr, &f_off, &f_len, &f_length, &f_key, &f_keyrot, &f_info,
-                        &tile_first, &tile_key, &tile_kind, &runs, &run_fail, &run_tseg})
+                        &tile_first, &tile_key, &tile_kind, &runs, &run_fail, &run_trun})
             b->release();
         frame_cap = 0;
     }
@@ -622,7 +622,7 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
-        if ((e = launch_unmask_run(c->variant, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_tseg.as<uint32_t>(),
+        if ((e = launch_unmask_run(d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
                                    c->run_seq, c->stream, timed ? c->tev[c->t_cur][2] : nullptr,
                                    timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess)
@@ -703,7 +703,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     sc.no_verify = 0;
     sc.runs = nullptr;
     sc.run_fail = nullptr;
-    sc.run_tseg = nullptr;
+    sc.run_trun = nullptr;
     sc.run_ntiles = sc.run_tile = 0;
     dspec_status* status_d = mapped<dspec_status>(c->h_status);
     const dspec_status* status_h = c->h_status.as<dspec_status>();
@@ -895,8 +895,10 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         // RUN: a step's batch of small uniform frames (the last exact or SPEC
         // scan matched the uniform estimates): discovery is k_head alone, the
         // unmask checks every header it loads (hvws_internal.h, drun).
+        // Segments of RUN_MIN_SEG bytes or more on average: k_unmask_run
+        // takes two segments per tile and leaves any between to the repair.
         const bool run_auto = c->run_mode < 0 && c->spec_ok && c->spec_mode != 0 && !c->run_skip && c->last_mean &&
-                              c->last_mean <= RUN_MAX_FRAME && run_env();
+                              c->last_mean <= RUN_MAX_FRAME && rx_len / nseg >= RUN_MIN_SEG && run_env();
         if (c->run_skip) --c->run_skip;
         if (unmask_into && c->run_call && c->vmask == 0 && (run_auto || c->run_mode == 1)) {
             c->scan_path = HVWS_PATH_RUN;
@@ -908,12 +910,13 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 if (c->T().run_fail.p != was || c->T().run_fail.cap != had)
                     HIP_OR(hipMemsetAsync(c->T().run_fail.p, 0, c->T().run_fail.cap, c->cs), HVWS_EHIP);
             }
-            HIP_OR(c->T().run_tseg.ensure((ntiles + 2) * 4), HVWS_ENOMEM);
+            const uint64_t rtiles = (rx_len + RUN_TILE - 1) / RUN_TILE;
+            HIP_OR(c->T().run_trun.ensure((rtiles + 1) * sizeof(dtrun)), HVWS_ENOMEM);
             sc.runs = c->T().runs.as<drun>();
             sc.run_fail = c->T().run_fail.as<uint32_t>();
-            sc.run_tseg = c->T().run_tseg.as<uint32_t>();
-            sc.run_ntiles = ntiles;
-            sc.run_tile = tile;
+            sc.run_trun = c->T().run_trun.as<dtrun>();
+            sc.run_ntiles = rtiles;
+            sc.run_tile = RUN_TILE;
             HIP_OR(pass(SCAN_RUN), HVWS_EHIP);
             c->run_seq = ++c->scan_seq;
             c->run_active = true;
@@ -1487,14 +1490,6 @@ int door_cap() {
     return cap;
 }
 
-// EXPERIMENT (round 5, to be removed): $HVWS_DOOR_LEGACY_RELEASE = 1: round
-// 4's r4k park/release waits (unbounded hipStreamSynchronize, stream pooled);
-// 2: the same plus hipStreamDestroy of the CU-masked stream (r4k as it was).
-int door_legacy() {
-    static const int v = getenv("HVWS_DOOR_LEGACY_RELEASE") ? atoi(getenv("HVWS_DOOR_LEGACY_RELEASE")) : 0;
-    return v;
-}
-
 // Marks the runtime call a context is in for the wedge report and
 // hvws_debug_dump (a hang then names its call, not only its thread).
 struct in_call {
@@ -1705,12 +1700,6 @@ void door_park(hvws_ctx* c) {
                 __builtin_ia32_pause();
         }
     }
-    if (door_legacy()) {   // EXPERIMENT (round 5): r4k's unbounded wait
-        in_call ic(c, "hipStreamSynchronize(worker stream) in park");
-        hipStreamSynchronize(c->door_stream);
-        c->door_live = false;
-        return;
-    }
     if (door_drain(c, 5000, "park")) c->door_live = false;
 }
 
@@ -1776,23 +1765,7 @@ void door_release(hvws_ctx* c) {
         g_doors.erase(std::remove(g_doors.begin(), g_doors.end(), c), g_doors.end());
         g_door_count.store((int)g_doors.size(), std::memory_order_release);
     }
-    // EXPERIMENT (round 5, to be removed): round 4's r4k release -- unbounded
-    // hipStreamSynchronize + hipStreamDestroy of the CU-masked stream -- to
-    // find which call the r4k/r4n hang blocked in (scripts/probe/door_first.cpp).
-    const int legacy = door_legacy();
-    if (legacy && !c->door_wedged) {
-        {
-            in_call ic(c, "hipStreamSynchronize(worker stream)");
-            hipStreamSynchronize(c->door_stream);
-        }
-        if (legacy == 2) {
-            in_call ic(c, "hipStreamDestroy(worker stream)");
-            hipStreamDestroy(c->door_stream);
-        } else {
-            std::lock_guard<std::mutex> lk(g_door_m);
-            g_door_pool.emplace_back(c->device, c->door_stream);
-        }
-    } else if (c->door_wedged || !door_drain(c, 5000, "release")) {
+    if (c->door_wedged || !door_drain(c, 5000, "release")) {
         // a worker that may still run: its stream and the memory it writes stay
         fprintf(stderr, "[hvws] k_door: ctx %p released with its worker stream wedged; stream and mailbox leaked\n",
                 (void*)c);
@@ -1801,10 +1774,14 @@ void door_release(hvws_ctx* c) {
         c->d_door_slot.p = nullptr;
         c->d_door_req = nullptr;
         return;
-    } else {
+    }
+    {
         // drained: the next context's worker takes it.  A CU-masked stream is
-        // never destroyed (destroying one is what the r4k /
-        // r4n hangs and the round-3 exit hang have in common).
+        // never destroyed: destroying one is the cause of the r4k / r4n hangs
+        // (after hipStreamDestroy of the worker stream the
+        // context's own hipStreamDestroy blocked for good, reproduced 2 of 2
+        // times by scripts/probe/door_first at commit 605ad80, never in 300
+        // processes that kept the stream).
         std::lock_guard<std::mutex> lk(g_door_m);
         g_door_pool.emplace_back(c->device, c->door_stream);
     }

@@ -147,24 +147,42 @@ struct drun {
                                // carry table belongs to the next scan by then)
 };
 static_assert(sizeof(drun) == 160, "drun layout");
+// Per unmask tile (one 128-byte line, k_run_tiles): the first segment
+// meeting the tile (s0) with its descriptor's unmask fields copied (the drun
+// prefix up to t_kw), the last one (s1), and k0 -- the key of s0's run frame
+// whose header lies before the tile start (0 if none): a tile of one segment
+// needs no other load before its unmask.
+struct dtrun {
+    uint64_t seg_lo, seg_hi, p0, stride, len;
+    double   inv;
+    uint32_t cnt, hlen, masked, flags;
+    uint64_t a_off, a_end, t_off, t_end;
+    uint32_t a_kw, t_kw;
+    uint32_t s0, s1, k0, pad;
+    int32_t  h0;                // s0's first run frame meeting the tile: its header, tile-relative (>= -stride)
+    uint32_t nj;                // s0's run frames meeting the tile
+};
+static_assert(sizeof(dtrun) == 128, "dtrun layout");
 enum : uint32_t { RUN_BAD = 1u };   // the segment is not one run (k_head saw it): exact repair only
-constexpr uint32_t RUN_MAXS = 8;      // segments per unmask tile staged in LDS (more: the tile's slow path)
-constexpr uint32_t RUN_KEYS = 1024;   // run frames per tile whose keys are staged (more: slow path)
 constexpr uint64_t RUN_MAX_FRAME = 8192;   // frames at most this size take the RUN path (bigger: SPEC)
-// k_head<false> writes runs[s] when given; k_run_tiles: tseg[t] = first
-// segment ending after tile t's first byte (t <= ntiles); fail[s] is segment
-// s's failure word (zeroed by k_head), fail[nseg .. nseg + 2] the batch's
+constexpr uint64_t RUN_MIN_SEG = 65536;    // and segments of at least this size on average
+// k_head<false> writes runs[s] when given; k_run_tiles: trun[t] for every
+// unmask tile (t < ntiles, dtrun); fail[s] is segment
+// s's failure word (zeroed by k_head; k_run_tiles sets bit 2 for a segment
+// k_unmask_run leaves to the repair), fail[nseg .. nseg + 2] the batch's
 // (any failed, failed count, repair workgroups done), zero between RUN steps
-// (the repair's last workgroup clears them; the host zeroes a new array).
-hipError_t launch_run_tiles(const dseg* segs, uint32_t nseg, uint32_t* tseg, uint32_t* fail, uint64_t ntiles,
-                            uint64_t tile, hipStream_t st);
-// The RUN unmask (geometry `variant`, as launch_unmask) and its repair pass;
+// (the repair clears them all; the host zeroes a new array).
+hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg, const drun* runs,
+                            dtrun* trun, uint64_t ntiles, uint64_t tile, uint32_t* fail, hipStream_t st);
+// The RUN unmask (512 x 2 geometry, RUN_TILE tiles) and its repair pass;
 // the timing events ride on the unmask's first dispatch (start) and the
 // repair's (stop).  The repair publishes (seq, failed segments) to
 // status->pad3 when it is done.
-hipError_t launch_unmask_run(int variant, uint8_t* rx, uint64_t rx_len, const drun* runs, const uint32_t* tseg,
-                             uint32_t nseg, uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st,
-                             hipEvent_t ev_start, hipEvent_t ev_stop);
+hipError_t launch_unmask_run(uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
+                             uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
+                             hipEvent_t ev_stop);
+constexpr uint64_t RUN_TILE = 16384;   // bytes per k_unmask_run tile (512 threads x 2 chunks)
+constexpr uint64_t RUN_FAST_STRIDE = 1u << 20;   // run strides up to this take k_unmask_run's one-segment path
 
 struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     dmid*     mid;
@@ -191,7 +209,7 @@ struct scan_scratch {   // per-segment arrays (nseg entries) + one total
     uint32_t  no_verify;     // SPEC/SLACK: head + walk only (no k_verify pair, no k_head<true>)
     drun*     runs;          // RUN: k_head writes each segment's run descriptor
     uint32_t* run_fail;      // RUN: per-segment failure words + the batch's, zeroed by k_head / k_run_tiles
-    uint32_t* run_tseg;      // RUN: first segment of each unmask tile (run_ntiles + 1 entries)
+    dtrun*    run_trun;      // RUN: per unmask tile (run_ntiles entries)
     uint64_t  run_ntiles, run_tile;
 };
 

@@ -2092,20 +2092,14 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
 // XORs that segment's hypothesis back -- the same keys from the same,
 // unchanged header positions -- and unmasks it exactly.
 
-// tseg[t] = first segment whose end lies after tile t's first byte (nseg if
-// none).
-__global__ void k_run_tiles(const dseg* __restrict__ segs, uint32_t nseg, uint32_t* __restrict__ tseg,
-                            uint64_t ntiles, uint64_t tile) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    const uint64_t x = t * tile;
+__device__ __forceinline__ uint32_t first_seg_ending_after(const dseg* __restrict__ segs, uint32_t nseg, uint64_t x) {
     uint32_t lo = 0, hi = nseg;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (segs[mid].off + segs[mid].len > x) hi = mid;
         else lo = mid + 1;
     }
-    tseg[t] = lo;
+    return lo;
 }
 
 // floor((x - p0) / stride) for x >= p0, exact (double estimate, corrected)
@@ -2132,43 +2126,242 @@ __device__ __forceinline__ void run_piece(uint64_t& mlo, uint64_t& mhi, uint64_t
     mhi |= kk & keep_hi;
 }
 
-// The run's hypothesis for header bytes (lo, hi): same header length,
-// payload length and mask bit as the run's first frame.
-__device__ __forceinline__ bool run_header_ok(const drun& r, const hdr& h) {
-    return h.hlen == r.hlen && h.length == r.len && ((h.flags & F_MASK) ? 1u : 0u) == r.masked;
+// A run frame's key as the hypothesis lays its header out: the 4 bytes before
+// its payload (bytes hlen-4 .. hlen-1 of the 16 at the header).  Only bytes
+// inside the hypothesised header are used, which no piece of the hypothesis
+// XORs -- so the repair pass reads the same key the unmask used even where
+// the hypothesis is wrong (a key parsed by the header's own length field
+// could lie in bytes the unmask changed).
+__device__ __forceinline__ uint32_t run_key(const drun& r, uint64_t lo, uint64_t hi) {
+    if (!r.masked || r.hlen < 6) return 0u;
+    const uint32_t b = r.hlen - 4u;   // 2, 4 or 10
+    return b == 2 ? (uint32_t)(lo >> 16) : (b == 4 ? (uint32_t)(lo >> 32) : (uint32_t)(hi >> 16));
 }
 
-// The mask of chunk c from segment r's pieces; key(j) gives run frame j's key.
-template <typename KEY>
-__device__ __forceinline__ void run_chunk_mask(const drun& r, uint64_t c, uint64_t& mlo, uint64_t& mhi, KEY key) {
-    if (c + 16 <= r.seg_lo || c >= r.seg_hi || (r.flags & RUN_BAD)) return;   // BAD: the repair alone
-    run_piece(mlo, mhi, c, r.a_off, r.a_end, r.a_kw);
-    run_piece(mlo, mhi, c, r.t_off, r.t_end, r.t_kw);
-    if (!r.cnt || !r.masked) return;
-    const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;   // the run's end
-    const uint64_t a = c > r.p0 ? c : r.p0, b = c + 16 < re ? c + 16 : re;
+// Unmask entries of segment r meeting [x0, x1): the carried-in piece, the run
+// frames, the cut frame's piece (in stream order); cnt_only: just count them.
+// Run frame j's entry is [its payload start, end) with the key word of its
+// header (written by the caller, which parses the header).
+__device__ __forceinline__ void run_tile_frames(const drun& r, uint64_t x0, uint64_t x1, uint32_t& jlo, uint32_t& nj) {
+    jlo = 0;
+    nj = 0;
+    if (!r.cnt || (r.flags & RUN_BAD)) return;
+    const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
+    const uint64_t a = x0 > r.p0 ? x0 : r.p0, b = x1 < re ? x1 : re;
     if (a >= b) return;
-    for (uint64_t j = run_frame_of(r, a); j < r.cnt; ++j) {
-        const uint64_t fo = r.p0 + j * r.stride;
-        if (fo >= b) break;
-        const uint64_t ps = fo + r.hlen, pe = fo + r.stride;
-        if (pe > c && ps < c + 16) run_piece(mlo, mhi, c, ps, pe, rotr32(key(j), 8u * ((0u - (uint32_t)ps) & 3u)));
+    jlo = (uint32_t)run_frame_of(r, a);
+    nj = (uint32_t)run_frame_of(r, b - 1) + 1u - jlo;
+}
+
+// trun[t] for every unmask tile: its first and last segment (s0 = first
+// ending after the tile start, nseg if none; s1 = the one holding the tile's
+// last byte), s0's descriptor fields, and the key of s0's run frame begun
+// before the tile (its header read here, beside the previous unmask, instead
+// of on the unmask's critical path).  k_unmask_run takes a tile's first and
+// last segment; the segments between (when the tile holds more than two,
+// each wholly inside it) are marked for the repair's exact path (fail bit 2),
+// as is -- by the repair itself -- a segment whose run k_unmask_run does not
+// take (run_fast_ok).
+__device__ __forceinline__ bool run_fast_ok(const drun& r) {
+    return !(r.flags & RUN_BAD) && (!r.cnt || (r.stride >= 32 && r.stride <= RUN_FAST_STRIDE));
+}
+
+__global__ void k_run_tiles(const uint8_t* __restrict__ rx, uint64_t rx_len, const dseg* __restrict__ segs,
+                            uint32_t nseg, const drun* __restrict__ runs, dtrun* __restrict__ trun, uint64_t ntiles,
+                            uint64_t tile, uint32_t* __restrict__ fail) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint64_t x = t * tile;
+    dtrun o;
+    o.s0 = first_seg_ending_after(segs, nseg, x);
+    o.s1 = o.s0 < nseg ? first_seg_ending_after(segs, nseg, x + tile - 1) : nseg;
+    if (o.s1 >= nseg) o.s1 = nseg ? nseg - 1 : 0;
+    o.k0 = 0;
+    o.pad = 0;
+    o.h0 = 0;
+    o.nj = 0;
+    if (o.s0 < nseg) {
+        const drun r = runs[o.s0];
+        o.seg_lo = r.seg_lo, o.seg_hi = r.seg_hi, o.p0 = r.p0, o.stride = r.stride, o.len = r.len, o.inv = r.inv;
+        o.cnt = r.cnt, o.hlen = r.hlen, o.masked = r.masked, o.flags = r.flags;
+        o.a_off = r.a_off, o.a_end = r.a_end, o.t_off = r.t_off, o.t_end = r.t_end, o.a_kw = r.a_kw, o.t_kw = r.t_kw;
+        const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
+        if (r.cnt && r.masked && !(r.flags & RUN_BAD) && x > r.p0 && x < re) {
+            const uint64_t hs = r.p0 + run_frame_of(r, x) * r.stride;
+            if (hs < x) {
+                uint64_t lo, hi;
+                ld16(rx, rx_len, hs, lo, hi);
+                o.k0 = run_key(r, lo, hi);
+            }
+        }
+        uint32_t jlo, nj;
+        run_tile_frames(r, x, x + tile, jlo, nj);
+        o.nj = nj;
+        o.h0 = nj ? (int32_t)((int64_t)(r.p0 + (uint64_t)jlo * r.stride) - (int64_t)x) : 0;
+        bool exact = !run_fast_ok(r) || (o.s1 != o.s0 && !run_fast_ok(runs[o.s1]));
+        for (uint32_t s = o.s0 + 1; s < o.s1; ++s) {
+            atomicOr(&fail[s], 2u);
+            exact = true;
+        }
+        if (exact) atomicOr(&fail[nseg], 1u);   // the repair pass must look
+    } else {
+        o.seg_lo = o.seg_hi = o.p0 = o.stride = o.len = 0;
+        o.inv = 0.0;
+        o.cnt = o.hlen = o.masked = o.flags = 0;
+        o.a_off = o.a_end = o.t_off = o.t_end = 0;
+        o.a_kw = o.t_kw = 0;
+    }
+    trun[t] = o;
+}
+
+// The run hypothesis' header bytes 1 .. 1 + ext (MASK bit + 7-bit length,
+// then the extended length, big-endian) as a 16-byte pattern and its byte
+// mask, relative to the header's first byte; byte 0 (FIN, RSV, opcode) is
+// free, as is the key.
+__device__ __forceinline__ void run_pattern(uint32_t masked, uint32_t hlen, uint64_t len, uint64_t& plo, uint64_t& phi,
+                                            uint64_t& mlo, uint64_t& mhi) {
+    const uint32_t ext = hlen - 2u - (masked ? 4u : 0u);   // 0, 2 or 8
+    const uint64_t b1 = (masked ? 0x80u : 0u) | (ext == 0 ? len : (ext == 2 ? 126u : 127u));
+    plo = b1 << 8;
+    phi = 0;
+    mlo = 0xFFull << 8;
+    mhi = 0;
+    if (ext == 2) {
+        plo |= ((len >> 8) & 0xFFu) << 16 | (len & 0xFFu) << 24;
+        mlo |= 0xFFFFull << 16;
+    } else if (ext == 8) {
+        const uint64_t be = __builtin_bswap64(len);   // bytes 2..9
+        plo |= be << 16;
+        phi = be >> 48;
+        mlo |= ~0ull << 16;
+        mhi = 0xFFFFull;
     }
 }
 
+// The unmask of a RUN step.  Every tile takes at most two runs, its first
+// and last segment's (the segments between, each wholly inside the tile,
+// are left to the repair's exact path; so is a run of a stride outside
+// [32, RUN_FAST_STRIDE] or one k_head found is not one run), in 32-bit
+// tile-relative arithmetic.  An earlier form (v3: an entry table per tile
+// in LDS, as k_unmask's, plus each lane taking header bytes from its chunks)
+// took 73 VGPRs and twice k_unmask's VALU instructions per byte and ran at
+// half the stream rate (profiles/r5g_raw).
+
+// One run of a fast tile, tile-relative (32-bit positions): its frames
+// meeting the tile are g = 0 .. nj-1, g's header at h0 + g * S; their keys
+// in LDS slots slot + g + 1 (slot + 0 and the two past the run: 0).
+struct fast_run {
+    int32_t S, hl, h0;
+    uint32_t nj, slot, masked, seg, k0;
+    uint64_t len;
+    bool pieces;   // the carried-in or the cut frame's payload meets the tile
+    uint64_t a_off, a_end, t_off, t_end;
+    uint32_t a_kw, t_kw;
+};
+
+// R from a run's unmask fields, its frames meeting the tile given (h0, nj)
+template <typename D>
+__device__ __forceinline__ void fast_run_init(fast_run& R, const D& r, int32_t h0, uint32_t nj, uint32_t seg,
+                                              uint32_t k0, uint64_t base, uint64_t te, uint32_t slot) {
+    R.S = (int32_t)r.stride;
+    R.hl = (int32_t)r.hlen;
+    R.masked = r.masked;
+    R.len = r.len;
+    R.nj = nj;
+    R.slot = slot;
+    R.seg = seg;
+    R.k0 = k0;
+    R.h0 = h0;
+    R.a_off = r.a_off, R.a_end = r.a_end, R.t_off = r.t_off, R.t_end = r.t_end;
+    R.a_kw = r.a_kw, R.t_kw = r.t_kw;
+    R.pieces = (r.a_kw && r.a_off < te && r.a_end > base) || (r.t_kw && r.t_off < te && r.t_end > base);
+}
+
+// One thread per slot: the header of each run frame that starts in the tile
+// (16 bytes from HBM, issued behind the tile's loads; no unmask changes a
+// byte the hypothesis calls header) checked against the hypothesis (header
+// length, payload length, mask bit); the frame's key word, rotated to its
+// payload's phase, into its slot.
+__device__ __forceinline__ void fast_run_keys(const fast_run& R, const uint8_t* rx, uint64_t rx_len, uint64_t base,
+                                              uint32_t* s_fk, uint32_t* __restrict__ fail, uint32_t nseg, uint32_t tid,
+                                              uint32_t T) {
+    uint64_t plo, phi, mlo, mhi;
+    run_pattern(R.masked, (uint32_t)R.hl, R.len, plo, phi, mlo, mhi);
+    const uint32_t kb = (uint32_t)R.hl - 4u;   // the key's first byte in a masked header: 2, 4 or 10
+    for (uint32_t s = tid; s < R.nj + 3; s += T) {
+        const int32_t g = (int32_t)s - 1;
+        uint32_t key = 0;
+        if (g >= 0 && g < (int32_t)R.nj) {
+            const int32_t hs = R.h0 + g * R.S;
+            if (hs < 0) {
+                key = R.k0;   // begun before the tile: its header is checked where it starts
+            } else {
+                uint64_t lo, hi;
+                ld16(rx, rx_len, base + (uint64_t)hs, lo, hi);
+                if (((lo ^ plo) & mlo) | ((hi ^ phi) & mhi)) {
+                    atomicOr(&fail[R.seg], 1u);
+                    atomicOr(&fail[nseg], 1u);
+                }
+                if (R.masked) key = kb < 8 ? (uint32_t)(lo >> (8 * kb)) : (uint32_t)(hi >> (8 * (kb - 8)));
+            }
+            key = rotr32(key, 8u * ((0u - (uint32_t)(hs + R.hl)) & 3u));
+        }
+        s_fk[R.slot + s] = R.masked ? key : 0u;
+    }
+}
+
+// The key bytes run R lays on the chunk at tile-relative x, ORed into m[4]:
+// x's frame g by a float reciprocal; g's payload [t1, t2) takes slot g + 1,
+// g + 1's from t3 slot g + 2 (S >= 32: no third frame meets 16 bytes); each
+// word's bytes picked by one v_perm whose selector s_sel gives for the two
+// 4-bit byte masks.  The carried-in and cut pieces, when they meet the tile.
+__device__ __forceinline__ void fast_run_mask(const fast_run& R, const uint32_t* s_fk, const uint32_t* s_sel,
+                                              int32_t x, uint64_t base, uint32_t m[4]) {
+    if (R.nj) {
+        const int32_t S = R.S;
+        int32_t r = x - R.h0 + S;
+        r = r < 0 ? 0 : r;
+        int32_t q = (int32_t)((float)r * __builtin_amdgcn_rcpf((float)S));   // g + 1, within one
+        const int32_t qs = (int32_t)__umul24((uint32_t)q, (uint32_t)S);
+        if (qs > r) --q;
+        else if (qs + S <= r) ++q;
+        q = q < (int32_t)R.nj + 1 ? q : (int32_t)R.nj + 1;
+        const int32_t hs = R.h0 + (int32_t)__umul24((uint32_t)q, (uint32_t)S) - S;
+        const int32_t t1 = hs + R.hl - x, t2 = hs + S - x, t3 = t2 + R.hl;
+        const uint32_t a1 = (uint32_t)(t1 < 0 ? 0 : (t1 > 16 ? 16 : t1));
+        const uint32_t a2 = (uint32_t)(t2 < 0 ? 0 : (t2 > 16 ? 16 : t2));
+        const uint32_t a3 = (uint32_t)(t3 < 0 ? 0 : (t3 > 16 ? 16 : t3));
+        const uint32_t pm = ((((1u << (a2 - a1)) - 1u) << a1) & 0xFFFFu) | (((0xFFFFu << a3) & 0xFFFFu) << 16);
+        const uint32_t kf = s_fk[R.slot + (uint32_t)q], kf1 = s_fk[R.slot + (uint32_t)q + 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            m[j] |= __builtin_amdgcn_perm(kf, kf1, s_sel[((pm >> (4 * j)) & 15u) | ((pm >> (12 + 4 * j)) & 0xF0u)]);
+    }
+    if (R.pieces) {
+        uint64_t klo = 0, khi = 0;
+        const uint64_t c = base + (uint64_t)(uint32_t)x;
+        run_piece(klo, khi, c, R.a_off, R.a_end, R.a_kw);
+        run_piece(klo, khi, c, R.t_off, R.t_end, R.t_kw);
+        m[0] |= (uint32_t)klo, m[1] |= (uint32_t)(klo >> 32), m[2] |= (uint32_t)khi, m[3] |= (uint32_t)(khi >> 32);
+    }
+}
+
+// The tiles.  The tile's loads are issued first; behind them one thread per
+// run frame reads its header and keeps its key (fast_run_keys) while the
+// selector table is built; one barrier; each chunk XORs what the runs lay on
+// it.
 template <int T, int U>
 __global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
-                                                  const uint32_t* __restrict__ tseg, uint32_t nseg,
-                                                  uint32_t* __restrict__ fail, uint64_t tile0, uint64_t ntiles) {
+                                                  const dtrun* __restrict__ trun, uint32_t nseg,
+                                                  uint32_t* __restrict__ fail, uint64_t tile0) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
-    __shared__ u32x4 s_tile[TILE / 16 + 1];   // + the next tile's first chunk (a header may run into it)
-    __shared__ drun s_run[RUN_MAXS];
-    __shared__ uint32_t s_key[RUN_KEYS];
-    __shared__ uint32_t s_jlo[RUN_MAXS], s_kb[RUN_MAXS + 1];
+    static_assert(TILE == RUN_TILE, "RUN tile");
+    __shared__ uint32_t s_fk[RUN_TILE / 32 + 16];   // 2 runs: sum of (nj + 3) <= TILE / 32 + 8
+    __shared__ uint32_t s_sel[256];
     const uint64_t t = tile0 + blockIdx.x;
-    const uint64_t base = t * TILE;
+    const uint64_t base = t * TILE, te = base + TILE;
     const uint32_t tid = threadIdx.x;
-    const bool full = base + TILE <= rx_len;
+    const bool full = te <= rx_len;
     u32x4 v[U];
     if (full) {
 #pragma unroll
@@ -2184,119 +2377,67 @@ __global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint
             v[i] = u32x4{w[0], w[1], w[2], w[3]};
         }
     }
-    const uint32_t s0 = tseg[t];
-    if (s0 >= nseg) return;   // no segment reaches this tile: no byte to unmask
-    const uint32_t s1 = tseg[t + 1] < nseg ? tseg[t + 1] : nseg - 1;
-    const uint32_t ns = s1 - s0 + 1;
-    const bool staged = ns <= RUN_MAXS;
-    if (staged && tid < ns) s_run[tid] = runs[s0 + tid];
+    // the record after the data loads (it is not in any cache by now)
+    const dtrun& tr = trun[t];   // wave-uniform: scalar loads
+    const uint32_t s0 = tr.s0;
+    if (s0 >= nseg) return;   // no segment reaches this tile
+    fast_run R0, R1;
+    const bool ok0 = !(tr.flags & RUN_BAD) && (!tr.cnt || (tr.stride >= 32 && tr.stride <= RUN_FAST_STRIDE));
+    fast_run_init(R0, tr, tr.h0, ok0 ? tr.nj : 0u, s0, tr.k0, base, te, 0);
+    R0.pieces = R0.pieces && ok0;
+    const uint32_t s1 = tr.s1;
+    const bool two = s1 != s0;
+    if (two) {   // s1 starts inside the tile: its run frames from its first, no k0
+        const drun r1 = runs[s1];
+        uint32_t nj1 = 0;
+        const int64_t h1 = (int64_t)r1.p0 - (int64_t)base;
+        const bool ok1 = run_fast_ok(r1);
+        if (ok1 && r1.cnt && h1 < (int64_t)TILE) {
+            const uint64_t meet = ((uint64_t)TILE - (uint64_t)h1 + r1.stride - 1) / r1.stride;
+            nj1 = meet < r1.cnt ? (uint32_t)meet : r1.cnt;
+        }
+        fast_run_init(R1, r1, nj1 ? (int32_t)h1 : 0, nj1, s1, 0u, base, te, R0.nj + 3);
+        R1.pieces = R1.pieces && ok1;
+    }
+    fast_run_keys(R0, rx, rx_len, base, s_fk, fail, nseg, tid, T);
+    if (two) fast_run_keys(R1, rx, rx_len, base, s_fk, fail, nseg, tid, T);
+    for (uint32_t e = tid; e < 256; e += T) {
+        // selector byte b: 4 + b picks byte b of the first operand (slot g + 1),
+        // b of the second (slot g + 2), 12 gives 0
+        uint32_t sel = 0;
 #pragma unroll
-    for (int i = 0; i < U; ++i) s_tile[(uint32_t)i * T + tid] = v[i];
-    if (tid == 0) {
-        uint64_t lo, hi;
-        ld16(rx, rx_len, base + TILE, lo, hi);
-        s_tile[TILE / 16] = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-    }
-    __syncthreads();
-    // run frames of each staged segment whose header or payload meets the tile
-    if (staged && tid < ns) {
-        const drun& r = s_run[tid];
-        uint32_t nk = 0, jlo = 0;
-        if (r.cnt) {
-            const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
-            const uint64_t a = base > r.p0 ? base : r.p0, b = base + TILE < re ? base + TILE : re;
-            if (a < b) {
-                jlo = (uint32_t)run_frame_of(r, a);
-                nk = (uint32_t)run_frame_of(r, b - 1) + 1u - jlo;
-            }
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t s = ((e >> b) & 1u) ? 4u + b : (((e >> (4 + b)) & 1u) ? b : 12u);
+            sel |= s << (8 * b);
         }
-        s_jlo[tid] = jlo;
-        s_kb[tid + 1] = nk;
+        s_sel[e] = sel;
     }
     __syncthreads();
-    if (tid == 0) {
-        s_kb[0] = 0;
-        for (uint32_t k = 0; k < (staged ? ns : 0u); ++k) s_kb[k + 1] += s_kb[k];
-    }
-    __syncthreads();
-    const uint32_t nkeys = staged ? s_kb[ns] : 0u;
-    const bool keyed = staged && nkeys <= RUN_KEYS;
-    if (keyed) {
-        // one thread per run frame: its header from the staged tile (or, for a
-        // frame begun before the tile, from HBM), checked, its key kept
-        const uint8_t* lt = reinterpret_cast<const uint8_t*>(s_tile);
-        for (uint32_t f = tid; f < nkeys; f += T) {
-            uint32_t k = 0;
-            while (k + 1 < ns && s_kb[k + 1] <= f) ++k;
-            const drun& r = s_run[k];
-            const uint64_t hs = r.p0 + (uint64_t)(s_jlo[k] + (f - s_kb[k])) * r.stride;
-            uint64_t lo, hi;
-            if (hs >= base) {
-                const uint32_t q = (uint32_t)(hs - base);
-                const uint32_t w = q >> 2, sh = q & 3u;
-                const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lt);
-                const uint32_t d0 = l32[w], d1 = l32[w + 1], d2 = l32[w + 2], d3 = l32[w + 3], d4 = l32[w + 4];
-                lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
-                hi = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32);
-            } else {
-                ld16(rx, rx_len, hs, lo, hi);
-            }
-            const hdr h = parse_hdr(lo, hi);
-            if (hs >= base && !run_header_ok(r, h)) {   // each header is checked by the tile it starts in
-                atomicOr(&fail[s0 + k], 1u);
-                atomicOr(&fail[nseg], 1u);
-            }
-            s_key[f] = r.masked ? h.key : 0u;
-        }
-    } else {
-        // slow path (more segments or run frames than staged): every header
-        // starting in the tile checked from HBM
-        for (uint32_t s = s0; s <= s1; ++s) {
-            const drun r = runs[s];
-            if (!r.cnt) continue;
-            const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
-            const uint64_t a = base > r.p0 ? base : r.p0, b = base + TILE < re ? base + TILE : re;
-            if (a >= b) continue;
-            const uint64_t j0 = run_frame_of(r, a), j1 = run_frame_of(r, b - 1);
-            for (uint64_t j = j0 + tid; j <= j1; j += T) {
-                const uint64_t hs = r.p0 + j * r.stride;
-                if (hs < base) continue;
-                uint64_t lo, hi;
-                ld16(rx, rx_len, hs, lo, hi);
-                if (!run_header_ok(r, parse_hdr(lo, hi))) {
-                    atomicOr(&fail[s], 1u);
-                    atomicOr(&fail[nseg], 1u);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // XOR: each chunk's pieces from every segment meeting it
+    bool dirty[U];
 #pragma unroll
     for (int i = 0; i < U; ++i) {
-        const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
-        if (c >= rx_len) continue;
-        uint64_t mlo = 0, mhi = 0;
-        if (keyed) {
-            for (uint32_t k = 0; k < ns; ++k)
-                run_chunk_mask(s_run[k], c, mlo, mhi, [&](uint64_t j) { return s_key[s_kb[k] + (uint32_t)(j - s_jlo[k])]; });
-        } else {
-            for (uint32_t s = s0; s <= s1; ++s) {
-                const drun r = runs[s];
-                run_chunk_mask(r, c, mlo, mhi, [&](uint64_t j) {
-                    uint64_t lo, hi;
-                    ld16(rx, rx_len, r.p0 + j * r.stride, lo, hi);
-                    return r.masked ? parse_hdr(lo, hi).key : 0u;
-                });
-            }
+        const int32_t x = (int32_t)(((uint32_t)i * T + tid) * 16u);
+        dirty[i] = false;
+        if (!full && base + (uint64_t)x >= rx_len) continue;
+        uint32_t m[4] = {0u, 0u, 0u, 0u};
+        fast_run_mask(R0, s_fk, s_sel, x, base, m);
+        if (two) fast_run_mask(R1, s_fk, s_sel, x, base, m);
+        if (m[0] | m[1] | m[2] | m[3]) {
+            v[i] ^= u32x4{m[0], m[1], m[2], m[3]};
+            dirty[i] = true;
         }
-        if (!(mlo | mhi)) continue;
-        const u32x4 m = u32x4{(uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi, (uint32_t)(mhi >> 32)};
-        const u32x4 o = v[i] ^ m;
-        if (full) {
-            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(rx + c));
-        } else {
-            const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+    }
+    if (full) {
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            if (dirty[i])
+                __builtin_nontemporal_store(v[i], reinterpret_cast<u32x4*>(rx + base + ((uint64_t)i * T + tid) * 16u));
+    } else {
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            if (!dirty[i]) continue;
+            const uint64_t c = base + ((uint64_t)i * T + tid) * 16u;
+            const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
             for (int b = 0; b < 16; ++b)
                 if (c + b < rx_len) rx[c + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
         }
@@ -2325,9 +2466,13 @@ __device__ __forceinline__ void wave_xor_range(uint8_t* rx, uint64_t lo, uint64_
 // with the same keys, read from the same header positions, which no unmask
 // changes -- and unmasked exactly (the carried-in frame, then walk_frames over
 // HBM, each record's payload XORed by its lane).  A segment k_head found not
-// to be one run (RUN_BAD) had nothing applied: exact only.  The last
+// to be one run (RUN_BAD), or that k_unmask_run left (fail bit 2, or a
+// stride it does not take), had nothing applied: exact only.  The last
 // workgroup to finish publishes (seq, failed segments) to the status block.
-// fail[nseg] = any failed, [nseg + 1] = failed count, [nseg + 2] = workgroups done.
+// fail[s]: 1 = s's hypothesis failed (undo, then exact), 2 = left to this
+// pass (exact); fail[nseg] = any, [nseg + 1] = repaired count, [nseg + 2] =
+// workgroups done; all of them, and every segment's word, are zero when the
+// pass ends.
 constexpr uint32_t RUN_FIX_BLOCKS = 32;
 
 __global__ __launch_bounds__(256) void k_run_fix(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
@@ -2338,8 +2483,12 @@ __global__ __launch_bounds__(256) void k_run_fix(uint8_t* __restrict__ rx, uint6
         const uint32_t w0 = blockIdx.x * 4u + wave, wn = gridDim.x * 4u;
         for (uint32_t s = w0; s < nseg; s += wn) {
             const drun r = runs[s];
-            const bool bad = (r.flags & RUN_BAD) != 0;
-            if (!bad && !fail[s]) continue;
+            const uint32_t fs = fail[s];
+            const bool bad = !run_fast_ok(r) || (fs & 2u);   // nothing applied: the exact path only
+            // zero again for the set's next RUN step: a later batch of fewer
+            // segments has its batch words (nseg ..) where this one had these
+            if (fs && lane == 0) fail[s] = 0;
+            if (!bad && !fs) continue;
             if (lane == 0) atomicAdd(&fail[nseg + 1], 1u);
             if (!bad) {   // undo the hypothesis
                 wave_xor_range(rx, r.a_off, r.a_end, r.a_kw);
@@ -2350,8 +2499,7 @@ __global__ __launch_bounds__(256) void k_run_fix(uint8_t* __restrict__ rx, uint6
                         uint64_t lo, hi;
                         ld16(rx, rx_len, fo, lo, hi);
                         const uint64_t ps = fo + r.hlen;
-                        wave_xor_range(rx, ps, fo + r.stride,
-                                       rotr32(parse_hdr(lo, hi).key, 8u * ((0u - (uint32_t)ps) & 3u)));
+                        wave_xor_range(rx, ps, fo + r.stride, rotr32(run_key(r, lo, hi), 8u * ((0u - (uint32_t)ps) & 3u)));
                     }
                 __threadfence();
             }
@@ -2543,7 +2691,8 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
                            (uint64_t*)nullptr, sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0, (uint64_t)0,
                            (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY, sc.runs, sc.run_fail);
-        if (hipError_t e = launch_run_tiles(segs, nseg, sc.run_tseg, sc.run_fail, sc.run_ntiles, sc.run_tile, st);
+        if (hipError_t e = launch_run_tiles(rx, rx_len, segs, nseg, sc.runs, sc.run_trun, sc.run_ntiles, sc.run_tile,
+                                            sc.run_fail, st);
             e != hipSuccess)
             return e;
     } else if (pass == SCAN_SLACK) {
@@ -2758,37 +2907,29 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
     return hipSuccess;
 }
 
-hipError_t launch_run_tiles(const dseg* segs, uint32_t nseg, uint32_t* tseg, uint32_t* fail, uint64_t ntiles,
-                            uint64_t tile, hipStream_t st) {
-    const uint64_t nb = (ntiles + 1 + 255) / 256;
-    (void)fail;
-    hipLaunchKernelGGL(k_run_tiles, dim3((uint32_t)nb), dim3(256), 0, st, segs, nseg, tseg, ntiles, tile);
+hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg, const drun* runs,
+                            dtrun* trun, uint64_t ntiles, uint64_t tile, uint32_t* fail, hipStream_t st) {
+    const uint64_t nb = (ntiles + 255) / 256;
+    if (nb) hipLaunchKernelGGL(k_run_tiles, dim3((uint32_t)nb), dim3(256), 0, st, rx, rx_len, segs, nseg, runs, trun,
+                               ntiles, tile, fail);
     return hipGetLastError();
 }
 
-hipError_t launch_unmask_run(int variant, uint8_t* rx, uint64_t rx_len, const drun* runs, const uint32_t* tseg,
-                             uint32_t nseg, uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st,
-                             hipEvent_t ev_start, hipEvent_t ev_stop) {
+hipError_t launch_unmask_run(uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
+                             uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
+                             hipEvent_t ev_stop) {
     if (rx_len == 0 || nseg == 0) return hipSuccess;
-    if (variant < 0 || variant >= unmask_variant_count()) return hipErrorInvalidValue;
-    const uint64_t tile = unmask_tile(variant);
-    const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
-    const int threads = kGeoms[variant].threads;
-    const uint64_t cap = max_tiles_per_launch(threads);
+    constexpr int T = 512, U = 2;   // the small-batch geometry (512 x 2, linear): RUN_TILE bytes per tile
+    const uint64_t ntiles_all = (rx_len + RUN_TILE - 1) / RUN_TILE;
+    const uint64_t cap = max_tiles_per_launch(T);
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
-        const hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
-#define HVWS_RUN_CASE(i, t, u, s)                                                                                    \
-    case i:                                                                                                          \
-        if (e0)                                                                                                      \
-            hipExtLaunchKernelGGL((k_unmask_run<t, u>), dim3((uint32_t)ntiles), dim3(t), 0, st, e0, nullptr, 0u, rx,  \
-                                  rx_len, runs, tseg, nseg, fail, tile0, ntiles);                                    \
-        else                                                                                                         \
-            hipLaunchKernelGGL((k_unmask_run<t, u>), dim3((uint32_t)ntiles), dim3(t), 0, st, rx, rx_len, runs, tseg, \
-                               nseg, fail, tile0, ntiles);                                                           \
-        break;
-        switch (variant) { HVWS_UNMASK_GEOMS(HVWS_RUN_CASE) default: return hipErrorInvalidValue; }
-#undef HVWS_RUN_CASE
+        if (tile0 == 0 && ev_start)
+            hipExtLaunchKernelGGL((k_unmask_run<T, U>), dim3((uint32_t)ntiles), dim3(T), 0, st, ev_start, nullptr, 0u, rx,
+                                  rx_len, runs, trun, nseg, fail, tile0);
+        else
+            hipLaunchKernelGGL((k_unmask_run<T, U>), dim3((uint32_t)ntiles), dim3(T), 0, st, rx, rx_len, runs, trun, nseg,
+                               fail, tile0);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

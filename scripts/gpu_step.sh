@@ -1,7 +1,8 @@
 #!/bin/bash
 # Run one GPU step under its own time limit; record its status; refuse to go
-# on after a crash/timeout (exit codes 124/134/137/139) so no further GPU work
-# starts in the same gpurun call.
+# on after any failure (a crash, a time limit, a failed test -- which may be a
+# GPU fault reported as an exception) so no further GPU work starts in the
+# same gpurun call.
 #   scripts/gpu_step.sh NAME SECONDS cmd...
 name=$1; secs=$2; shift 2
 mkdir -p gpurun_out
@@ -11,7 +12,5 @@ timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
 rc=$?
 echo "[$name] rc=$rc $(date +%T)"
 tail -5 "gpurun_out/$name.log"
-case $rc in
-  124|134|137|139) touch gpurun_out/.stop ;;
-esac
+[ $rc -ne 0 ] && touch gpurun_out/.stop
 exit 0
