@@ -226,7 +226,7 @@ int hvws_set_table_checks(int on);
  * segment fit and compacts the records to the exact offsets (and whether the
  * uniform estimates would have held: SPEC next time).  A failed check
  * re-scans exactly (COUNT, wait, EMIT).  mode -1 = that automatic choice
- * (default, or $HVWS_SPEC unset), 0 = never speculate, 1 = try SPEC first,
+ * (default, or $HVWS_EXPERIMENT spec unset), 0 = never speculate, 1 = try SPEC first,
  * 2 = try SLACK first (tests).  Results never depend on it.  ctx NULL = the
  * calling thread's context.  Returns the previous mode. */
 int hvws_set_speculation(hvws_ctx* ctx, int mode);
@@ -314,7 +314,7 @@ int hvws_last_kernel_ms(hvws_ctx* ctx, float* ms);
 const char* hvws_build_kernel_name(void);
 /* The k_build geometry the last hvws_build_frames on ctx ran: one-wave
  * workgroups of 4 KiB tiles, in a lean-LDS form for batches of small frames
- * (mean frame < 4 KiB), or $HVWS_BUILD's.  Results never
+ * (mean frame < 4 KiB), or $HVWS_EXPERIMENT build's.  Results never
  * depend on it. */
 const char* hvws_last_build_kernel(hvws_ctx* ctx);
 /* 1 when the last hvws_build_frames on ctx found a uniform layout (every frame

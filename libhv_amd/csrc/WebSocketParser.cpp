@@ -236,11 +236,11 @@ int hvws_feed_many(WebSocketParser* const* parsers, const char* const* data, con
 }
 
 namespace {
-// $HVWS_FEED_TIMES=1: per-phase host time of feed_distinct, printed at exit (diagnostic)
+// $HVWS_EXPERIMENT feed_times=1: per-phase host time of feed_distinct, printed at exit (diagnostic)
 struct feed_times {
     double ph[6] = {0, 0, 0, 0, 0, 0};   // carry, gather, gpu, scatter, replay, feeder wait
     long calls = 0;
-    bool on = getenv("HVWS_FEED_TIMES") && atoi(getenv("HVWS_FEED_TIMES"));
+    bool on = hvws::experiment("feed_times") && atoi(hvws::experiment("feed_times"));
     std::mutex m;   // the loop thread and feeder workers add to the same counters
     void add(int k, double us) {
         std::lock_guard<std::mutex> lk(m);
@@ -342,12 +342,12 @@ void gpu_part(feed_batch& b) {
 
 // The host half, on the loop thread: the reference's message logic and
 // onMessage callbacks, connection by connection in submission order.
-// $HVWS_REPLAY_PREFETCH (bytes, default 64 KiB; 0 = off): while connection i
+// $HVWS_EXPERIMENT replay_prefetch (bytes, default 64 KiB; 0 = off): while connection i
 // replays, the next connections' read bytes -- just written by the device
 // across PCIe, so in DRAM, not in any cache -- are prefetched up to this far
 // ahead; the appends otherwise wait on DRAM a few cache lines at a time.
 const uint64_t g_replay_prefetch =
-    getenv("HVWS_REPLAY_PREFETCH") ? strtoull(getenv("HVWS_REPLAY_PREFETCH"), nullptr, 0) : (64u << 10);
+    hvws::experiment("replay_prefetch") ? strtoull(hvws::experiment("replay_prefetch"), nullptr, 0) : (64u << 10);
 
 // Replays running on this thread (nested when an onMessage feeds again).
 // While one runs, the states of its parsers after the one being replayed --
@@ -463,7 +463,7 @@ struct hvws_feeder {
     bool stop = false;
     bool in_replay = false;
     bool free_requested = false;     // hvws_feeder_free from one of its callbacks: freed when the replay returns
-    uint64_t inline_bytes = 0;      // runs up to this size skip the worker ($HVWS_FEEDER_INLINE)
+    uint64_t inline_bytes = 0;      // runs up to this size skip the worker ($HVWS_EXPERIMENT feeder_inline)
     ptr_index pend_idx;              // parser -> index in *pending (valid while pending is set)
 };
 
@@ -562,7 +562,7 @@ void feeder_run(hvws_feeder* f, WebSocketParser* const* parsers, const char* con
 
 extern "C" hvws_feeder* hvws_feeder_new(void) {
     hvws_feeder* f = new hvws_feeder();
-    if (const char* e = getenv("HVWS_FEEDER_INLINE")) f->inline_bytes = strtoull(e, nullptr, 0);
+    if (const char* e = hvws::experiment("feeder_inline")) f->inline_bytes = strtoull(e, nullptr, 0);
     f->src = hvws::thread_ctx();
     f->device = hvws_ctx_device(f->src);
     f->worker = std::thread(feeder_main, f);

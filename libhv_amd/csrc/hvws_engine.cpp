@@ -187,7 +187,7 @@ struct hvws_ctx {
     // next one-walk pass keeps the grid-wide k_verify pair (else head + walk).
     bool verify_hint = true;
     int verify_mode = -1;   // hvws_set_walk_verify: -1 adaptive (the hint), 0 never, 1 always
-    int spec_mode = -1;   // -1 auto, 0 never, 1 SPEC first, 2 SLACK first ($HVWS_SPEC / hvws_set_speculation)
+    int spec_mode = -1;   // -1 auto, 0 never, 1 SPEC first, 2 SLACK first ($HVWS_EXPERIMENT spec / hvws_set_speculation)
     // SLACK (mixed sizes, several segments): scratch table, exact bases, and
     // the per-segment region cap from the last exact scan's largest segment
     dbuf sl_hdr, sl_off, sl_len, sl_length, sl_key, sl_keyrot, sl_info, sl_bx;
@@ -234,7 +234,7 @@ struct hvws_ctx {
     hbuf h_small_in, h_small_out;
     hbuf h_small_done;             // per-segment completion words k_small writes last
     uint64_t small_seq = 0;        // value the current call's completion words carry
-    int small_poll = 1;            // $HVWS_SMALL_POLL: poll those words instead of syncing the stream
+    int small_poll = 1;            // $HVWS_EXPERIMENT small_poll: poll those words instead of syncing the stream
     bool small_quiet = false;      // the last small call saw all its words: its kernel no longer touches the pinned buffers
     hbuf h_feed;   // hvws_feed_many's gather buffer (reference-API thread contexts)
     dbuf d_small_in, d_small_slots;
@@ -244,8 +244,8 @@ struct hvws_ctx {
     dbuf d_small_ctr;
     uint64_t small_ctr_base = 0;
     bool small_ctr_dirty = true;   // unknown value (first use, failed call): zero it
-    int small_zc = 1;              // $HVWS_SMALL_ZC / hvws_set_small_zero_copy
-    uint64_t zc_batch = kZcBatch;  // largest zero-copy batch ($HVWS_ZC_BATCH)
+    int small_zc = 1;              // $HVWS_EXPERIMENT small_zc / hvws_set_small_zero_copy
+    uint64_t zc_batch = kZcBatch;  // largest zero-copy batch ($HVWS_EXPERIMENT zc_batch)
     uint32_t vmask = 0;         // protocol validation classes (V_*); 0 = reference behaviour
     // transmit side (hvws_build_frames)
     dbuf tx_size, tx_off, tx_scan, tx_tiles, tx_stat, tx_span;
@@ -403,10 +403,10 @@ T* mapped(hbuf& b) {
 // the command processor runs between kernels, and the scan-side pair cost a
 // pipelined c2 step ~9 us (0.465 -> 0.456 ms, profiles/r2d_raw); a pipelined
 // scan's span includes its wait for the previous unmask anyway.
-// $HVWS_STEP_EVENTS forces a mode.
+// $HVWS_EXPERIMENT step_events forces a mode.
 int step_events(const hvws_ctx* c) {
     static const int v = [] {
-        const char* e = getenv("HVWS_STEP_EVENTS");
+        const char* e = experiment("step_events");
         return e ? atoi(e) : -1;
     }();
     return v >= 0 ? v : (c->cs != c->stream ? 1 : 2);
@@ -454,7 +454,7 @@ int step_times_at(hvws_ctx* c, int slot, float* out) {
 // costs ~10 us of device idle between the check and the tile kernels).  A
 // stream that drains without publishing is an error, never a hang.
 // Pipelined SPEC steps queue the unmask after the host has seen the scan
-// finish instead of behind a cross-stream event ($HVWS_HOST_ORDER=0: the
+// finish instead of behind a cross-stream event ($HVWS_EXPERIMENT host_order=0: the
 // event, as in round 3).
 // $HVWS_RUN=0: the RUN path off (A/B runs); hvws_set_run overrides per context.
 bool run_env() {
@@ -462,8 +462,17 @@ bool run_env() {
     return v != 0;
 }
 
+// The RUN unmask's geometry (kRunGeoms, hvws_kernels.hip); $HVWS_EXPERIMENT run_geom for a sweep.
+int run_geom() {
+    static const int v = [] {
+        const int g = experiment("run_geom") ? atoi(experiment("run_geom")) : 0;
+        return g >= 0 && g < run_geom_count() ? g : 0;
+    }();
+    return v;
+}
+
 bool host_order() {
-    static const int v = getenv("HVWS_HOST_ORDER") ? atoi(getenv("HVWS_HOST_ORDER")) : 1;
+    static const int v = experiment("host_order") ? atoi(experiment("host_order")) : 1;
     return v != 0;
 }
 
@@ -615,14 +624,14 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
     // 1.73 -> 1.55 ms, but c3 21.3 -> 22.4 ms and c2 flat, so uniform batches
     // (SPEC: a short scan) keep one launch.  With the 512 x 2 linear geometry
     // (round 2, profiles/r2n_raw) c4 ran 1.429 / 1.405 / 1.377 / 1.366 ms at
-    // 1 / 2 / 4 / 8 pieces: 8.  $HVWS_UNMASK_PIECES overrides.
-    static const int env_pieces = getenv("HVWS_UNMASK_PIECES") ? atoi(getenv("HVWS_UNMASK_PIECES")) : -1;
+    // 1 / 2 / 4 / 8 pieces: 8.  $HVWS_EXPERIMENT unmask_pieces overrides.
+    static const int env_pieces = experiment("unmask_pieces") ? atoi(experiment("unmask_pieces")) : -1;
     const int path = c->prev_path;   // the current scan's path may not be settled yet
     const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED || path == HVWS_PATH_SPEC_FAILED ||
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
-        if ((e = launch_unmask_run(d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
+        if ((e = launch_unmask_run(run_geom(), d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
                                    c->run_seq, c->stream, timed ? c->tev[c->t_cur][2] : nullptr,
                                    timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess)
@@ -910,13 +919,14 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 if (c->T().run_fail.p != was || c->T().run_fail.cap != had)
                     HIP_OR(hipMemsetAsync(c->T().run_fail.p, 0, c->T().run_fail.cap, c->cs), HVWS_EHIP);
             }
-            const uint64_t rtiles = (rx_len + RUN_TILE - 1) / RUN_TILE;
+            const uint64_t rtile = run_tile_bytes(run_geom());
+            const uint64_t rtiles = (rx_len + rtile - 1) / rtile;
             HIP_OR(c->T().run_trun.ensure((rtiles + 1) * sizeof(dtrun)), HVWS_ENOMEM);
             sc.runs = c->T().runs.as<drun>();
             sc.run_fail = c->T().run_fail.as<uint32_t>();
             sc.run_trun = c->T().run_trun.as<dtrun>();
             sc.run_ntiles = rtiles;
-            sc.run_tile = RUN_TILE;
+            sc.run_tile = rtile;
             HIP_OR(pass(SCAN_RUN), HVWS_EHIP);
             c->run_seq = ++c->scan_seq;
             c->run_active = true;
@@ -1329,9 +1339,9 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
             HIP_OR(hipMemcpyAsync(d + o_data, h_rx, len, hipMemcpyHostToDevice, c->stream), HVWS_EHIP);
     }
     const uint8_t* d_rx = zc ? (user_mapped ? user_mapped : hp_d + o_data) : d + o_data;
-    // No timing events unless $HVWS_STEP_EVENTS >= 2 asks for them: an
+    // No timing events unless $HVWS_EXPERIMENT step_events >= 2 asks for them: an
     // event-carrying launch costs a per-read call ~10 us of ~38 (r2an).
-    static const bool timed_env = getenv("HVWS_STEP_EVENTS") && atoi(getenv("HVWS_STEP_EVENTS")) >= 2;
+    static const bool timed_env = experiment("step_events") && atoi(experiment("step_events")) >= 2;
     const bool timed = timed_env;
     // Completion: each wave releases its stores to system scope and then
     // writes its segment's word with this call's sequence number; the host
@@ -1439,14 +1449,14 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
 // from a mailbox in fine-grained pinned memory: no launch, no dispatch and no
 // end-of-kernel signal per call.
 
-// Idle time after which a worker parks ($HVWS_DOOR_IDLE_US, default 5 ms),
+// Idle time after which a worker parks ($HVWS_EXPERIMENT door_idle_us, default 5 ms),
 // in ticks of the 100 MHz realtime clock.
 std::atomic<uint64_t> g_door_idle_us{0};   // 0: not yet read from the environment
 
 uint64_t door_idle_us() {
     uint64_t us = g_door_idle_us.load(std::memory_order_relaxed);
     if (!us) {
-        const char* e = getenv("HVWS_DOOR_IDLE_US");
+        const char* e = experiment("door_idle_us");
         us = e && strtoull(e, nullptr, 0) ? strtoull(e, nullptr, 0) : 5000;
         g_door_idle_us.store(us, std::memory_order_relaxed);
     }
@@ -1504,7 +1514,7 @@ struct in_call {
 constexpr uint64_t kDoorReqBytes = 256 + kDoorMax + 256;
 
 bool door_vram_enabled() {
-    static const int v = getenv("HVWS_DOOR_VRAM") ? atoi(getenv("HVWS_DOOR_VRAM")) : 1;
+    static const int v = experiment("door_vram") ? atoi(experiment("door_vram")) : 1;
     return v != 0;
 }
 
@@ -2082,18 +2092,18 @@ hvws_ctx* hvws_ctx_create(int device) {
     for (hbuf& b : c->h_up) b.flags = hipHostMallocCoherent;
     c->h_status.flags = hipHostMallocCoherent;
     c->h_small_done.flags = hipHostMallocCoherent;
-    if (const char* sp = getenv("HVWS_SMALL_POLL")) c->small_poll = atoi(sp) ? 1 : 0;
-    if (const char* zc = getenv("HVWS_SMALL_ZC")) c->small_zc = atoi(zc) ? 1 : 0;
-    if (const char* zb = getenv("HVWS_ZC_BATCH")) c->zc_batch = strtoull(zb, nullptr, 0);
-    if (const char* sp = getenv("HVWS_SPEC")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
-    if (const char* wv = getenv("HVWS_WALK_VERIFY")) c->verify_mode = atoi(wv) < 0 ? -1 : (atoi(wv) ? 1 : 0);
+    if (const char* sp = experiment("small_poll")) c->small_poll = atoi(sp) ? 1 : 0;
+    if (const char* zc = experiment("small_zc")) c->small_zc = atoi(zc) ? 1 : 0;
+    if (const char* zb = experiment("zc_batch")) c->zc_batch = strtoull(zb, nullptr, 0);
+    if (const char* sp = experiment("spec")) c->spec_mode = atoi(sp) == 0 ? 0 : (atoi(sp) == 1 ? 1 : (atoi(sp) == 2 ? 2 : -1));
+    if (const char* wv = experiment("walk_verify")) c->verify_mode = atoi(wv) < 0 ? -1 : (atoi(wv) ? 1 : 0);
     // The pipelined scan stream at the highest priority: a scan kernel of
     // ~1000 workgroups queued while an unmask grid is being dispatched waits
     // for that whole grid at normal priority, but is dispatched beside it at
-    // high priority (scripts/dispatch_probe.hip).  $HVWS_SCAN_PRIORITY=0: normal.
+    // high priority (scripts/dispatch_probe.hip).  $HVWS_EXPERIMENT scan_priority=0: normal.
     int prio_least = 0, prio_greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-    const char* sp_env = getenv("HVWS_SCAN_PRIORITY");
+    const char* sp_env = experiment("scan_priority");
     const int scan_prio = sp_env && atoi(sp_env) == 0 ? prio_least : prio_greatest;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
@@ -2820,15 +2830,15 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     // k_build_id, which is gone, profiles/r4v_raw)
     const int v = tx_variant(total, n);
     c->tx_variant = v;
-    // each tile's source span first ($HVWS_BUILD_SPANS=0: the records-first tiles)
-    const char* sp_env = getenv("HVWS_BUILD_SPANS");
+    // each tile's source span first ($HVWS_EXPERIMENT build_spans=0: the records-first tiles)
+    const char* sp_env = experiment("build_spans");
     const bool spans_ok = !sp_env || atoi(sp_env) != 0;
     const uint64_t tile = tx_tile(v);
     const uint64_t ntiles = (total + tile - 1) / tile;
     // A uniform layout (every frame the same size and length, payload offsets
     // a + k * b, b >= 0) needs no tile index: each tile finds its frames and
-    // source span from its position ($HVWS_BUILD_UNI=0: the index anyway).
-    static const bool uni_ok = !getenv("HVWS_BUILD_UNI") || atoi(getenv("HVWS_BUILD_UNI")) != 0;
+    // source span from its position ($HVWS_EXPERIMENT build_uni=0: the index anyway).
+    static const bool uni_ok = !experiment("build_uni") || atoi(experiment("build_uni")) != 0;
     // (payload steps shorter than a payload would make a tile's pieces
     // overlap out of order: the index handles those)
     // (small frames only, the lean form: at 64 KiB frames the index is ~0.1 %

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -11,6 +12,19 @@
 #include "websocket_parser.h"
 
 namespace hvws {
+
+// $HVWS_EXPERIMENT="name=value,name=value": the A/B switches of the on-device
+// sweeps (DESIGN.md sec. 9 lists them).  The text of `name`'s value (up to
+// the next ','; atoi / strtoull stop there) or nullptr; read from the
+// environment on every call (callers that keep a value cache it themselves).
+inline const char* experiment(const char* name) {
+    const char* e = getenv("HVWS_EXPERIMENT");
+    if (!e) return nullptr;
+    const size_t n = strlen(name);
+    for (const char* p = e; p && *p; p = strchr(p, ',') ? strchr(p, ',') + 1 : nullptr)
+        if (!strncmp(p, name, n) && p[n] == '=') return p + n + 1;
+    return nullptr;
+}
 
 // With validation on, the state of a header split across reads lives in the
 // padding byte after websocket_parser.mask_offset (the reference never reads
@@ -147,22 +161,22 @@ struct drun {
                                // carry table belongs to the next scan by then)
 };
 static_assert(sizeof(drun) == 160, "drun layout");
-// Per unmask tile (one 128-byte line, k_run_tiles): the first segment
-// meeting the tile (s0) with its descriptor's unmask fields copied (the drun
-// prefix up to t_kw), the last one (s1), and k0 -- the key of s0's run frame
-// whose header lies before the tile start (0 if none): a tile of one segment
-// needs no other load before its unmask.
+// Per unmask tile (64 bytes, k_run_tiles): the first segment meeting the
+// tile (s0, nseg if none) and the last (s1), and s0's run as it meets the
+// tile, tile-relative: its first run frame's header h0 (>= -S), the run
+// frames meeting the tile (nj; 0 if s0 is left to the repair), k0 -- the key
+// of the run frame begun before the tile (its header read beside the previous
+// unmask) -- and the carried-in / cut frame's payload pieces clipped to the
+// tile.  A tile of one segment needs no other load before its unmask.
 struct dtrun {
-    uint64_t seg_lo, seg_hi, p0, stride, len;
-    double   inv;
-    uint32_t cnt, hlen, masked, flags;
-    uint64_t a_off, a_end, t_off, t_end;
-    uint32_t a_kw, t_kw;
-    uint32_t s0, s1, k0, pad;
-    int32_t  h0;                // s0's first run frame meeting the tile: its header, tile-relative (>= -stride)
-    uint32_t nj;                // s0's run frames meeting the tile
+    uint32_t s0, s1, k0;
+    int32_t  h0;
+    uint32_t nj, S, len, hm;    // run frames meeting the tile, stride, payload bytes, header bytes | masked << 8
+    int32_t  a_lo, a_hi, t_lo, t_hi;
+    uint32_t a_kw, t_kw;        // 0: no piece
+    uint32_t pad[2];
 };
-static_assert(sizeof(dtrun) == 128, "dtrun layout");
+static_assert(sizeof(dtrun) == 64, "dtrun layout");
 enum : uint32_t { RUN_BAD = 1u };   // the segment is not one run (k_head saw it): exact repair only
 constexpr uint64_t RUN_MAX_FRAME = 8192;   // frames at most this size take the RUN path (bigger: SPEC)
 constexpr uint64_t RUN_MIN_SEG = 65536;    // and segments of at least this size on average
@@ -174,14 +188,16 @@ constexpr uint64_t RUN_MIN_SEG = 65536;    // and segments of at least this size
 // (the repair clears them all; the host zeroes a new array).
 hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg, const drun* runs,
                             dtrun* trun, uint64_t ntiles, uint64_t tile, uint32_t* fail, hipStream_t st);
-// The RUN unmask (512 x 2 geometry, RUN_TILE tiles) and its repair pass;
+// The RUN unmask (geometry geom < run_geom_count(): run_tile_bytes(geom)
+// bytes per tile, the tiles k_run_tiles described) and its repair pass;
 // the timing events ride on the unmask's first dispatch (start) and the
 // repair's (stop).  The repair publishes (seq, failed segments) to
 // status->pad3 when it is done.
-hipError_t launch_unmask_run(uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
+int run_geom_count();
+uint64_t run_tile_bytes(int geom);
+hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
                              uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
                              hipEvent_t ev_stop);
-constexpr uint64_t RUN_TILE = 16384;   // bytes per k_unmask_run tile (512 threads x 2 chunks)
 constexpr uint64_t RUN_FAST_STRIDE = 1u << 20;   // run strides up to this take k_unmask_run's one-segment path
 
 struct scan_scratch {   // per-segment arrays (nseg entries) + one total
@@ -442,7 +458,7 @@ hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, 
 hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const uint8_t* flags, const uint32_t* mask,
                            const uint64_t* size, uint64_t n, uint64_t plen, uint64_t* stat, hipStream_t st);
 // k_build geometry for a batch of out_len output bytes in n frames
-// ($HVWS_BUILD, else by the mean frame size), its tile and its name
+// ($HVWS_EXPERIMENT build, else by the mean frame size), its tile and its name
 int tx_variant(uint64_t out_len, uint64_t n);
 uint64_t tx_tile(int v);   // output bytes per k_build workgroup
 const char* build_kernel_name(int v);

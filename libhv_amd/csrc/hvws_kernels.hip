@@ -193,13 +193,13 @@ __device__ bool scalar_frame(const uint8_t* seg, uint64_t L, dcarry& st, uint64_
 
 // Predicted frames that make a segment "long" (grid-wide k_verify); shorter
 // uniform runs are verified by k_walk's wave-wide speculation, 256 frames
-// per round, all segments in parallel.  $HVWS_SPEC_MIN overrides (tuning).
+// per round, all segments in parallel.  $HVWS_EXPERIMENT spec_min overrides (tuning).
 constexpr uint64_t SPEC_MIN_DEFAULT = 4096;
 static uint64_t g_spec_min = 0;   // 0: not yet read from the environment
 
 uint64_t spec_min() {
     if (!g_spec_min) {
-        const char* e = getenv("HVWS_SPEC_MIN");
+        const char* e = experiment("spec_min");
         const long long x = e ? atoll(e) : 0;
         g_spec_min = x > 0 ? (uint64_t)x : SPEC_MIN_DEFAULT;
     }
@@ -2081,26 +2081,15 @@ __global__ __launch_bounds__(T) void k_unmask(uint8_t* __restrict__ rx, uint64_t
 // ------------------------------------------------------------ RUN unmask
 //
 // A batch whose segments are each one run of equal frames (hvws_internal.h,
-// drun).  k_unmask_run loads its tile as k_unmask does, stages it in LDS,
-// parses the header of every run frame that starts in the tile (one thread per
-// frame), checks it against the run's hypothesis (header length, payload
-// length, mask bit) and keeps its key in LDS; then every chunk XORs the pieces
-// that meet it: the carried-in frame's, the run frames' (position by division
-// by the stride), the cut frame's.  The header lines are read once, as part
-// of the tile -- the scan beside the previous unmask is k_head alone.  A
-// failed check marks the segment; k_run_fix (behind, on the same stream)
-// XORs that segment's hypothesis back -- the same keys from the same,
-// unchanged header positions -- and unmasks it exactly.
-
-__device__ __forceinline__ uint32_t first_seg_ending_after(const dseg* __restrict__ segs, uint32_t nseg, uint64_t x) {
-    uint32_t lo = 0, hi = nseg;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (segs[mid].off + segs[mid].len > x) hi = mid;
-        else lo = mid + 1;
-    }
-    return lo;
-}
+// drun).  k_unmask_run loads its tile as k_unmask does; behind the loads one
+// thread per run frame starting in the tile reads its header, checks it
+// against the run's hypothesis (header length, payload length, mask bit) and
+// keeps its key in LDS; then every chunk XORs the pieces that meet it: the
+// carried-in frame's, the run frames' (position by division by the stride),
+// the cut frame's.  The scan beside the previous unmask is k_head and
+// k_run_tiles.  A failed check marks the segment; k_run_fix (behind, on the
+// same stream) XORs that segment's hypothesis back -- the same keys from the
+// same, unchanged header positions -- and unmasks it exactly.
 
 // floor((x - p0) / stride) for x >= p0, exact (double estimate, corrected)
 __device__ __forceinline__ uint64_t run_frame_of(const drun& r, uint64_t x) {
@@ -2153,40 +2142,78 @@ __device__ __forceinline__ void run_tile_frames(const drun& r, uint64_t x0, uint
     nj = (uint32_t)run_frame_of(r, b - 1) + 1u - jlo;
 }
 
-// trun[t] for every unmask tile: its first and last segment (s0 = first
-// ending after the tile start, nseg if none; s1 = the one holding the tile's
-// last byte), s0's descriptor fields, and the key of s0's run frame begun
-// before the tile (its header read here, beside the previous unmask, instead
-// of on the unmask's critical path).  k_unmask_run takes a tile's first and
-// last segment; the segments between (when the tile holds more than two,
-// each wholly inside it) are marked for the repair's exact path (fail bit 2),
-// as is -- by the repair itself -- a segment whose run k_unmask_run does not
-// take (run_fast_ok).
 __device__ __forceinline__ bool run_fast_ok(const drun& r) {
     return !(r.flags & RUN_BAD) && (!r.cnt || (r.stride >= 32 && r.stride <= RUN_FAST_STRIDE));
 }
 
-__global__ void k_run_tiles(const uint8_t* __restrict__ rx, uint64_t rx_len, const dseg* __restrict__ segs,
-                            uint32_t nseg, const drun* __restrict__ runs, dtrun* __restrict__ trun, uint64_t ntiles,
-                            uint64_t tile, uint32_t* __restrict__ fail) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles) return;
-    const uint64_t x = t * tile;
-    dtrun o;
-    o.s0 = first_seg_ending_after(segs, nseg, x);
-    o.s1 = o.s0 < nseg ? first_seg_ending_after(segs, nseg, x + tile - 1) : nseg;
-    if (o.s1 >= nseg) o.s1 = nseg ? nseg - 1 : 0;
-    o.k0 = 0;
-    o.pad = 0;
-    o.h0 = 0;
+// Run r as it meets the tile [x, x + tile) (dtrun's fields after k0); a run
+// k_unmask_run does not take (ok false) meets it with nothing.
+__device__ __forceinline__ void tile_run(dtrun& o, const drun& r, bool ok, uint64_t x, uint64_t tile) {
+    o.S = (uint32_t)r.stride;
+    o.len = (uint32_t)r.len;
+    o.hm = r.hlen | (r.masked << 8);
     o.nj = 0;
-    if (o.s0 < nseg) {
-        const drun r = runs[o.s0];
-        o.seg_lo = r.seg_lo, o.seg_hi = r.seg_hi, o.p0 = r.p0, o.stride = r.stride, o.len = r.len, o.inv = r.inv;
-        o.cnt = r.cnt, o.hlen = r.hlen, o.masked = r.masked, o.flags = r.flags;
-        o.a_off = r.a_off, o.a_end = r.a_end, o.t_off = r.t_off, o.t_end = r.t_end, o.a_kw = r.a_kw, o.t_kw = r.t_kw;
-        const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
-        if (r.cnt && r.masked && !(r.flags & RUN_BAD) && x > r.p0 && x < re) {
+    o.h0 = 0;
+    o.a_lo = o.a_hi = o.t_lo = o.t_hi = 0;
+    o.a_kw = o.t_kw = 0;
+    if (!ok) return;
+    uint32_t jlo, nj;
+    run_tile_frames(r, x, x + tile, jlo, nj);
+    o.nj = nj;
+    o.h0 = nj ? (int32_t)((int64_t)(r.p0 + (uint64_t)jlo * r.stride) - (int64_t)x) : 0;
+    const uint64_t te = x + tile;
+    if (r.a_kw && r.a_off < te && r.a_end > x) {
+        o.a_lo = (int32_t)((r.a_off > x ? r.a_off : x) - x);
+        o.a_hi = (int32_t)((r.a_end < te ? r.a_end : te) - x);
+        o.a_kw = r.a_kw;
+    }
+    if (r.t_kw && r.t_off < te && r.t_end > x) {
+        o.t_lo = (int32_t)((r.t_off > x ? r.t_off : x) - x);
+        o.t_hi = (int32_t)((r.t_end < te ? r.t_end : te) - x);
+        o.t_kw = r.t_kw;
+    }
+}
+
+// trun[t] for every unmask tile, one wave per segment s writing the tiles
+// whose first byte lies in [end of s - 1, end of s) (s0 = s; the last
+// segment's wave also the tiles past every segment: s0 = nseg).  s1 = the
+// first segment ending after the tile's last byte (clamped to the last).
+// k_unmask_run takes a tile's s0 and s1; the segments between (each wholly
+// inside the tile) are marked for the repair's exact path (fail bit 2), as
+// is -- by the repair itself -- a segment whose run it does not take
+// (run_fast_ok).  The key of s0's run frame begun before the tile is read
+// here, beside the previous unmask, not on the unmask's critical path.
+__global__ __launch_bounds__(256) void k_run_tiles(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                   const dseg* __restrict__ segs, uint32_t nseg,
+                                                   const drun* __restrict__ runs, dtrun* __restrict__ trun,
+                                                   uint64_t ntiles, uint64_t tile, uint32_t* __restrict__ fail) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (s >= nseg) return;
+    const uint64_t e0 = s ? segs[s - 1].off + segs[s - 1].len : 0;
+    const uint64_t e1 = segs[s].off + segs[s].len;
+    const uint64_t ta = (e0 + tile - 1) / tile, tb = (e1 + tile - 1) / tile;
+    const uint64_t tz = s + 1 == nseg ? ntiles : tb;
+    const drun r = runs[s];
+    const bool ok = run_fast_ok(r);
+    const uint64_t re = r.p0 + (uint64_t)r.cnt * r.stride;
+    for (uint64_t t = ta + lane; t < tz; t += 64) {
+        const uint64_t x = t * tile;
+        dtrun o;
+        o.pad[0] = o.pad[1] = 0;
+        o.k0 = 0;
+        if (t >= tb) {   // past every segment
+            o.s0 = o.s1 = nseg;
+            tile_run(o, r, false, x, tile);
+            trun[t] = o;
+            continue;
+        }
+        o.s0 = s;
+        uint32_t s1 = s;
+        while (s1 + 1 < nseg && segs[s1].off + segs[s1].len <= x + tile - 1) ++s1;
+        o.s1 = s1;
+        tile_run(o, r, ok, x, tile);
+        if (ok && r.cnt && r.masked && x > r.p0 && x < re) {
             const uint64_t hs = r.p0 + run_frame_of(r, x) * r.stride;
             if (hs < x) {
                 uint64_t lo, hi;
@@ -2194,24 +2221,14 @@ __global__ void k_run_tiles(const uint8_t* __restrict__ rx, uint64_t rx_len, con
                 o.k0 = run_key(r, lo, hi);
             }
         }
-        uint32_t jlo, nj;
-        run_tile_frames(r, x, x + tile, jlo, nj);
-        o.nj = nj;
-        o.h0 = nj ? (int32_t)((int64_t)(r.p0 + (uint64_t)jlo * r.stride) - (int64_t)x) : 0;
-        bool exact = !run_fast_ok(r) || (o.s1 != o.s0 && !run_fast_ok(runs[o.s1]));
-        for (uint32_t s = o.s0 + 1; s < o.s1; ++s) {
-            atomicOr(&fail[s], 2u);
+        bool exact = !ok || (s1 != s && !run_fast_ok(runs[s1]));
+        for (uint32_t m = s + 1; m < s1; ++m) {
+            atomicOr(&fail[m], 2u);
             exact = true;
         }
         if (exact) atomicOr(&fail[nseg], 1u);   // the repair pass must look
-    } else {
-        o.seg_lo = o.seg_hi = o.p0 = o.stride = o.len = 0;
-        o.inv = 0.0;
-        o.cnt = o.hlen = o.masked = o.flags = 0;
-        o.a_off = o.a_end = o.t_off = o.t_end = 0;
-        o.a_kw = o.t_kw = 0;
+        trun[t] = o;
     }
-    trun[t] = o;
 }
 
 // The run hypothesis' header bytes 1 .. 1 + ext (MASK bit + 7-bit length,
@@ -2247,34 +2264,44 @@ __device__ __forceinline__ void run_pattern(uint32_t masked, uint32_t hlen, uint
 // took 73 VGPRs and twice k_unmask's VALU instructions per byte and ran at
 // half the stream rate (profiles/r5g_raw).
 
+// v_perm selectors by the two 4-bit byte masks of a word (e = g's | g + 1's
+// << 4): byte b takes 4 + b (byte b of the first operand, slot g + 1), b (of
+// the second, slot g + 2) or 12 (zero).
+struct run_sel_table {
+    uint32_t v[256];
+    constexpr run_sel_table() : v() {
+        for (uint32_t e = 0; e < 256; ++e) {
+            uint32_t sel = 0;
+            for (uint32_t b = 0; b < 4; ++b)
+                sel |= (((e >> b) & 1u) ? 4u + b : (((e >> (4 + b)) & 1u) ? b : 12u)) << (8 * b);
+            v[e] = sel;
+        }
+    }
+};
+__device__ constexpr run_sel_table kRunSel{};
+
 // One run of a fast tile, tile-relative (32-bit positions): its frames
 // meeting the tile are g = 0 .. nj-1, g's header at h0 + g * S; their keys
 // in LDS slots slot + g + 1 (slot + 0 and the two past the run: 0).
 struct fast_run {
     int32_t S, hl, h0;
-    uint32_t nj, slot, masked, seg, k0;
-    uint64_t len;
-    bool pieces;   // the carried-in or the cut frame's payload meets the tile
-    uint64_t a_off, a_end, t_off, t_end;
-    uint32_t a_kw, t_kw;
+    uint32_t nj, slot, masked, seg, k0, len;
+    int32_t a_lo, a_hi, t_lo, t_hi;   // the carried-in / cut frame's payload pieces in the tile
+    uint32_t a_kw, t_kw;              // (0: none)
 };
 
-// R from a run's unmask fields, its frames meeting the tile given (h0, nj)
-template <typename D>
-__device__ __forceinline__ void fast_run_init(fast_run& R, const D& r, int32_t h0, uint32_t nj, uint32_t seg,
-                                              uint32_t k0, uint64_t base, uint64_t te, uint32_t slot) {
-    R.S = (int32_t)r.stride;
-    R.hl = (int32_t)r.hlen;
-    R.masked = r.masked;
-    R.len = r.len;
-    R.nj = nj;
+__device__ __forceinline__ void fast_run_init(fast_run& R, const dtrun& o, uint32_t seg, uint32_t slot) {
+    R.S = (int32_t)o.S;
+    R.hl = (int32_t)(o.hm & 0xFFu);
+    R.masked = (o.hm >> 8) & 1u;
+    R.len = o.len;
+    R.h0 = o.h0;
+    R.nj = o.nj;
     R.slot = slot;
     R.seg = seg;
-    R.k0 = k0;
-    R.h0 = h0;
-    R.a_off = r.a_off, R.a_end = r.a_end, R.t_off = r.t_off, R.t_end = r.t_end;
-    R.a_kw = r.a_kw, R.t_kw = r.t_kw;
-    R.pieces = (r.a_kw && r.a_off < te && r.a_end > base) || (r.t_kw && r.t_off < te && r.t_end > base);
+    R.k0 = o.k0;
+    R.a_lo = o.a_lo, R.a_hi = o.a_hi, R.t_lo = o.t_lo, R.t_hi = o.t_hi;
+    R.a_kw = o.a_kw, R.t_kw = o.t_kw;
 }
 
 // One thread per slot: the header of each run frame that starts in the tile
@@ -2316,7 +2343,7 @@ __device__ __forceinline__ void fast_run_keys(const fast_run& R, const uint8_t* 
 // word's bytes picked by one v_perm whose selector s_sel gives for the two
 // 4-bit byte masks.  The carried-in and cut pieces, when they meet the tile.
 __device__ __forceinline__ void fast_run_mask(const fast_run& R, const uint32_t* s_fk, const uint32_t* s_sel,
-                                              int32_t x, uint64_t base, uint32_t m[4]) {
+                                              int32_t x, uint32_t m[4]) {
     if (R.nj) {
         const int32_t S = R.S;
         int32_t r = x - R.h0 + S;
@@ -2337,12 +2364,16 @@ __device__ __forceinline__ void fast_run_mask(const fast_run& R, const uint32_t*
         for (int j = 0; j < 4; ++j)
             m[j] |= __builtin_amdgcn_perm(kf, kf1, s_sel[((pm >> (4 * j)) & 15u) | ((pm >> (12 + 4 * j)) & 0xF0u)]);
     }
-    if (R.pieces) {
-        uint64_t klo = 0, khi = 0;
-        const uint64_t c = base + (uint64_t)(uint32_t)x;
-        run_piece(klo, khi, c, R.a_off, R.a_end, R.a_kw);
-        run_piece(klo, khi, c, R.t_off, R.t_end, R.t_kw);
-        m[0] |= (uint32_t)klo, m[1] |= (uint32_t)(klo >> 32), m[2] |= (uint32_t)khi, m[3] |= (uint32_t)(khi >> 32);
+    if (R.a_kw | R.t_kw) {   // bytes [lo, hi) of the chunk: the 4-bit byte masks of the selector table
+        const int32_t al = R.a_lo - x, ah = R.a_hi - x, tl = R.t_lo - x, th = R.t_hi - x;
+        const uint32_t b1 = (uint32_t)(al < 0 ? 0 : (al > 16 ? 16 : al)), b2 = (uint32_t)(ah < 0 ? 0 : (ah > 16 ? 16 : ah));
+        const uint32_t c1 = (uint32_t)(tl < 0 ? 0 : (tl > 16 ? 16 : tl)), c2 = (uint32_t)(th < 0 ? 0 : (th > 16 ? 16 : th));
+        const uint32_t pa = b2 > b1 ? ((1u << (b2 - b1)) - 1u) << b1 : 0u;
+        const uint32_t pt = c2 > c1 ? ((1u << (c2 - c1)) - 1u) << c1 : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            m[j] |= __builtin_amdgcn_perm(R.a_kw, R.t_kw,
+                                          s_sel[((pa >> (4 * j)) & 15u) | (((pt >> (4 * j)) & 15u) << 4)]);
     }
 }
 
@@ -2351,14 +2382,11 @@ __device__ __forceinline__ void fast_run_mask(const fast_run& R, const uint32_t*
 // selector table is built; one barrier; each chunk XORs what the runs lay on
 // it.
 template <int T, int U>
-__global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
-                                                  const dtrun* __restrict__ trun, uint32_t nseg,
-                                                  uint32_t* __restrict__ fail, uint64_t tile0) {
+__device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
+                                                const dtrun* __restrict__ trun, uint32_t nseg,
+                                                uint32_t* __restrict__ fail, uint64_t t, uint32_t* s_fk,
+                                                uint32_t* s_sel) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
-    static_assert(TILE == RUN_TILE, "RUN tile");
-    __shared__ uint32_t s_fk[RUN_TILE / 32 + 16];   // 2 runs: sum of (nj + 3) <= TILE / 32 + 8
-    __shared__ uint32_t s_sel[256];
-    const uint64_t t = tile0 + blockIdx.x;
     const uint64_t base = t * TILE, te = base + TILE;
     const uint32_t tid = threadIdx.x;
     const bool full = te <= rx_len;
@@ -2382,36 +2410,19 @@ __global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint
     const uint32_t s0 = tr.s0;
     if (s0 >= nseg) return;   // no segment reaches this tile
     fast_run R0, R1;
-    const bool ok0 = !(tr.flags & RUN_BAD) && (!tr.cnt || (tr.stride >= 32 && tr.stride <= RUN_FAST_STRIDE));
-    fast_run_init(R0, tr, tr.h0, ok0 ? tr.nj : 0u, s0, tr.k0, base, te, 0);
-    R0.pieces = R0.pieces && ok0;
+    fast_run_init(R0, tr, s0, 0);
     const uint32_t s1 = tr.s1;
     const bool two = s1 != s0;
     if (two) {   // s1 starts inside the tile: its run frames from its first, no k0
         const drun r1 = runs[s1];
-        uint32_t nj1 = 0;
-        const int64_t h1 = (int64_t)r1.p0 - (int64_t)base;
-        const bool ok1 = run_fast_ok(r1);
-        if (ok1 && r1.cnt && h1 < (int64_t)TILE) {
-            const uint64_t meet = ((uint64_t)TILE - (uint64_t)h1 + r1.stride - 1) / r1.stride;
-            nj1 = meet < r1.cnt ? (uint32_t)meet : r1.cnt;
-        }
-        fast_run_init(R1, r1, nj1 ? (int32_t)h1 : 0, nj1, s1, 0u, base, te, R0.nj + 3);
-        R1.pieces = R1.pieces && ok1;
+        dtrun o1;
+        o1.k0 = 0;
+        tile_run(o1, r1, run_fast_ok(r1), base, TILE);
+        fast_run_init(R1, o1, s1, R0.nj + 3);
     }
     fast_run_keys(R0, rx, rx_len, base, s_fk, fail, nseg, tid, T);
     if (two) fast_run_keys(R1, rx, rx_len, base, s_fk, fail, nseg, tid, T);
-    for (uint32_t e = tid; e < 256; e += T) {
-        // selector byte b: 4 + b picks byte b of the first operand (slot g + 1),
-        // b of the second (slot g + 2), 12 gives 0
-        uint32_t sel = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t s = ((e >> b) & 1u) ? 4u + b : (((e >> (4 + b)) & 1u) ? b : 12u);
-            sel |= s << (8 * b);
-        }
-        s_sel[e] = sel;
-    }
+    for (uint32_t e = tid; e < 256; e += T) s_sel[e] = kRunSel.v[e];
     __syncthreads();
     bool dirty[U];
 #pragma unroll
@@ -2420,8 +2431,8 @@ __global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint
         dirty[i] = false;
         if (!full && base + (uint64_t)x >= rx_len) continue;
         uint32_t m[4] = {0u, 0u, 0u, 0u};
-        fast_run_mask(R0, s_fk, s_sel, x, base, m);
-        if (two) fast_run_mask(R1, s_fk, s_sel, x, base, m);
+        fast_run_mask(R0, s_fk, s_sel, x, m);
+        if (two) fast_run_mask(R1, s_fk, s_sel, x, m);
         if (m[0] | m[1] | m[2] | m[3]) {
             v[i] ^= u32x4{m[0], m[1], m[2], m[3]};
             dirty[i] = true;
@@ -2461,70 +2472,96 @@ __device__ __forceinline__ void wave_xor_range(uint8_t* rx, uint64_t lo, uint64_
     }
 }
 
-// Repair after k_unmask_run: nothing unless a segment failed (one word read
-// per workgroup).  A failed segment is put back -- its hypothesis XORed again
+// The repair: nothing unless a segment failed (one word read per
+// workgroup).  A failed segment is put back -- its hypothesis XORed again
 // with the same keys, read from the same header positions, which no unmask
 // changes -- and unmasked exactly (the carried-in frame, then walk_frames over
 // HBM, each record's payload XORed by its lane).  A segment k_head found not
-// to be one run (RUN_BAD), or that k_unmask_run left (fail bit 2, or a
-// stride it does not take), had nothing applied: exact only.  The last
-// workgroup to finish publishes (seq, failed segments) to the status block.
-// fail[s]: 1 = s's hypothesis failed (undo, then exact), 2 = left to this
-// pass (exact); fail[nseg] = any, [nseg + 1] = repaired count, [nseg + 2] =
-// workgroups done; all of them, and every segment's word, are zero when the
-// pass ends.
+// to be one run (RUN_BAD), or that the tiles left (fail bit 2, or a stride
+// they do not take), had nothing applied: exact only.  Waves w0, w0 + wn, ...
+// take the segments.
+// fail[s]: 1 = s's hypothesis failed (undo, then exact), 2 = left to the
+// repair (exact); fail[nseg] = any, [nseg + 1] = repaired count, [nseg + 2]
+// = repair workgroups done; all of them, and every segment's word, are zero
+// when the repair ends.
+__device__ __forceinline__ void run_repair(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
+                                           uint32_t nseg, uint32_t* __restrict__ fail, uint32_t w0, uint32_t wn) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (__hip_atomic_load(&fail[nseg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    for (uint32_t s = w0; s < nseg; s += wn) {
+        const drun r = runs[s];
+        const uint32_t fs = fail[s];
+        const bool bad = !run_fast_ok(r) || (fs & 2u);   // nothing applied: the exact path only
+        // zero again for the set's next RUN step: a later batch of fewer
+        // segments has its batch words (nseg ..) where this one had these
+        if (fs && lane == 0) fail[s] = 0;
+        if (!bad && !fs) continue;
+        if (lane == 0) atomicAdd(&fail[nseg + 1], 1u);
+        if (!bad) {   // undo the hypothesis
+            wave_xor_range(rx, r.a_off, r.a_end, r.a_kw);
+            wave_xor_range(rx, r.t_off, r.t_end, r.t_kw);
+            if (r.masked)
+                for (uint64_t j = 0; j < r.cnt; ++j) {
+                    const uint64_t fo = r.p0 + j * r.stride;
+                    uint64_t lo, hi;
+                    ld16(rx, rx_len, fo, lo, hi);
+                    const uint64_t ps = fo + r.hlen;
+                    wave_xor_range(rx, ps, fo + r.stride, rotr32(run_key(r, lo, hi), 8u * ((0u - (uint32_t)ps) & 3u)));
+                }
+            __threadfence();
+        }
+        // the exact path over the segment's bytes
+        const uint64_t sb = r.seg_lo, L = r.seg_hi - r.seg_lo;
+        dcarry st = r.cin;
+        uint64_t pos = 0, n = 0;
+        frec fr0;
+        if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, fr0, 0u) && (fr0.info & I_BODY) &&
+            (fr0.info & F_MASK)) {
+            const uint64_t po = sb + fr0.pay_off;
+            wave_xor_range(rx, po, po + fr0.pay_len, key_for_aligned(fr0.key, po, (fr0.info >> 8) & 3u));
+        }
+        __threadfence();
+        // walk_frames calls emit from every lane owning a record (the
+        // whole frames of one round) or from lane 0 (the cut frame)
+        walk_frames<true>(rx, rx_len, sb, L, st, pos, n, 0u, [&](uint64_t, const frec& v) {
+            if (!(v.info & I_BODY) || !(v.info & F_MASK)) return;
+            const uint64_t po = sb + v.pay_off, pe = po + v.pay_len;
+            const uint32_t kw = key_for_aligned(v.key, po, (v.info >> 8) & 3u);
+            for (uint64_t x = po; x < pe; ++x) rx[x] ^= (uint8_t)(kw >> (8 * (x & 3u)));
+        });
+        __threadfence();
+    }
+}
+
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
+                                                  const dtrun* __restrict__ trun, uint32_t nseg,
+                                                  uint32_t* __restrict__ fail, uint64_t tile0) {
+    constexpr uint64_t TILE = (uint64_t)T * U * 16u;
+    __shared__ uint32_t s_fk[TILE / 32 + 16];   // 2 runs: sum of (nj + 3) <= TILE / 32 + 8
+    __shared__ uint32_t s_sel[256];
+    run_unmask_tile<T, U>(rx, rx_len, runs, trun, nseg, fail, tile0 + blockIdx.x, s_fk, s_sel);
+}
+
+// The repair kernel behind the unmask on the same stream (a kernel boundary
+// is the one cheap grid-wide barrier: the repair workgroups folded into the
+// unmask grid needed a release fence per tile workgroup to hand over its
+// bytes, 11.7 ms a step at c2, profiles/r5r_raw).  With no failure -- the
+// common case, one word read -- workgroup 0 publishes (seq, 0) at once.
 constexpr uint32_t RUN_FIX_BLOCKS = 32;
 
 __global__ __launch_bounds__(256) void k_run_fix(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
                                                  uint32_t nseg, uint32_t* __restrict__ fail,
                                                  dspec_status* __restrict__ status, uint64_t seq) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (__hip_atomic_load(&fail[nseg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-        const uint32_t w0 = blockIdx.x * 4u + wave, wn = gridDim.x * 4u;
-        for (uint32_t s = w0; s < nseg; s += wn) {
-            const drun r = runs[s];
-            const uint32_t fs = fail[s];
-            const bool bad = !run_fast_ok(r) || (fs & 2u);   // nothing applied: the exact path only
-            // zero again for the set's next RUN step: a later batch of fewer
-            // segments has its batch words (nseg ..) where this one had these
-            if (fs && lane == 0) fail[s] = 0;
-            if (!bad && !fs) continue;
-            if (lane == 0) atomicAdd(&fail[nseg + 1], 1u);
-            if (!bad) {   // undo the hypothesis
-                wave_xor_range(rx, r.a_off, r.a_end, r.a_kw);
-                wave_xor_range(rx, r.t_off, r.t_end, r.t_kw);
-                if (r.masked)
-                    for (uint64_t j = 0; j < r.cnt; ++j) {
-                        const uint64_t fo = r.p0 + j * r.stride;
-                        uint64_t lo, hi;
-                        ld16(rx, rx_len, fo, lo, hi);
-                        const uint64_t ps = fo + r.hlen;
-                        wave_xor_range(rx, ps, fo + r.stride, rotr32(run_key(r, lo, hi), 8u * ((0u - (uint32_t)ps) & 3u)));
-                    }
-                __threadfence();
-            }
-            // the exact path over the segment's bytes
-            const uint64_t sb = r.seg_lo, L = r.seg_hi - r.seg_lo;
-            dcarry st = r.cin;
-            uint64_t pos = 0, n = 0;
-            frec fr0;
-            if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, fr0, 0u) && (fr0.info & I_BODY) &&
-                (fr0.info & F_MASK)) {
-                const uint64_t po = sb + fr0.pay_off;
-                wave_xor_range(rx, po, po + fr0.pay_len, key_for_aligned(fr0.key, po, (fr0.info >> 8) & 3u));
-            }
-            __threadfence();
-            // walk_frames calls emit from every lane owning a record (the
-            // whole frames of one round) or from lane 0 (the cut frame)
-            walk_frames<true>(rx, rx_len, sb, L, st, pos, n, 0u, [&](uint64_t, const frec& v) {
-                if (!(v.info & I_BODY) || !(v.info & F_MASK)) return;
-                const uint64_t po = sb + v.pay_off, pe = po + v.pay_len;
-                const uint32_t kw = key_for_aligned(v.key, po, (v.info >> 8) & 3u);
-                for (uint64_t x = po; x < pe; ++x) rx[x] ^= (uint8_t)(kw >> (8 * (x & 3u)));
-            });
-            __threadfence();
+    const bool any = __hip_atomic_load(&fail[nseg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (!any) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            status->pad3[1] = 0;
+            __hip_atomic_store(&status->pad3[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        return;
     }
+    run_repair(rx, rx_len, runs, nseg, fail, blockIdx.x * 4u + (threadIdx.x >> 6), gridDim.x * 4u);
     // the last workgroup publishes
     __shared__ uint32_t s_last;
     __syncthreads();
@@ -2537,8 +2574,7 @@ __global__ __launch_bounds__(256) void k_run_fix(uint8_t* __restrict__ rx, uint6
         __threadfence();
         status->pad3[1] = __hip_atomic_load(&fail[nseg + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&status->pad3[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        // the batch's words clean for this table set's next RUN step (k_head
-        // sets the first for a segment that is not one run)
+        // the batch's words clean for this table set's next RUN step
         fail[nseg] = 0;
         fail[nseg + 1] = 0;
         fail[nseg + 2] = 0;
@@ -2598,10 +2634,10 @@ static uint32_t wave_blocks(uint32_t nseg) {
     return blocks > 65536u ? 65536u : (blocks ? blocks : 1u);
 }
 
-// $HVWS_WALK_BLOCKS (experiment): cap the walk's grid; each wave then walks
+// $HVWS_EXPERIMENT walk_blocks (experiment): cap the walk's grid; each wave then walks
 // several segments in turn (fewer wave slots taken beside a running unmask).
 static uint32_t walk_blocks(uint32_t nseg) {
-    static const long cap = getenv("HVWS_WALK_BLOCKS") ? atol(getenv("HVWS_WALK_BLOCKS")) : 0;
+    static const long cap = experiment("walk_blocks") ? atol(experiment("walk_blocks")) : 0;
     const uint32_t b = wave_blocks(nseg);
     return cap > 0 && (uint32_t)cap < b ? (uint32_t)cap : b;
 }
@@ -2763,7 +2799,7 @@ hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uin
 }
 
 // Unmask geometries (threads, chunks per thread, XCD order).  Default from the
-// on-device sweep; HVWS_UNMASK=<index> selects another for experiments.
+// on-device sweep; $HVWS_EXPERIMENT unmask=<index> selects another for experiments.
 struct unmask_geom {
     int threads, unroll;
     bool swz;
@@ -2781,14 +2817,11 @@ struct unmask_geom {
     X(8, 64, 8, true)                                                                     \
     X(9, 256, 4, false)                                                                   \
     X(10, 256, 2, false)                                                                  \
-    X(11, 512, 2, false)                                                                  \
-    X(12, 64, 4, false)                                                                   \
-    X(13, 64, 8, false)                                                                   \
-    X(14, 64, 16, false)
+    X(11, 512, 2, false)
 #define HVWS_GEOM_ENTRY(i, t, u, s) {t, u, s},
 static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
 
-// Geometry by batch size unless one is chosen ($HVWS_UNMASK, or
+// Geometry by batch size unless one is chosen ($HVWS_EXPERIMENT unmask, or
 // hvws_set_unmask_variant; -1 = back to this choice).  Pipelined steps,
 // interleaved runs on one box (profiles/r2l_raw): 512 x 2 in linear tile
 // order against the XCD-contiguous 256 x 4 -- c2 (1 GiB) 0.4195 vs 0.425
@@ -2804,7 +2837,7 @@ static int g_geom_forced = -2;   // -2: not yet read from the environment; -1: b
 
 static int forced_geom() {
     if (g_geom_forced == -2) {
-        const char* e = getenv("HVWS_UNMASK");
+        const char* e = experiment("unmask");
         int v = e ? atoi(e) : -1;
         if (v < -1 || v >= (int)(sizeof(kGeoms) / sizeof(kGeoms[0]))) v = -1;
         g_geom_forced = v;
@@ -2858,7 +2891,7 @@ static uint64_t max_tiles_per_launch(int threads) {
     case i: hipExtLaunchKernelGGL((HVWS_K<t, u, s>), HVWS_EXT_ARGS); break;
 
 static uint32_t unmask_lds() {
-    static const uint32_t b = getenv("HVWS_UNMASK_LDS") ? (uint32_t)atoi(getenv("HVWS_UNMASK_LDS")) : 0u;
+    static const uint32_t b = experiment("unmask_lds") ? (uint32_t)atoi(experiment("unmask_lds")) : 0u;
     return b;
 }
 
@@ -2886,7 +2919,7 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
         const hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
         const hipEvent_t e1 = tile0 + ntiles >= ntiles_all ? ev_stop : nullptr;
-// $HVWS_UNMASK_LDS (experiments): dynamic LDS bytes per workgroup, to cap how
+// $HVWS_EXPERIMENT unmask_lds (experiments): dynamic LDS bytes per workgroup, to cap how
 // many unmask workgroups a CU holds beside the next batch's scan
 #define HVWS_K k_unmask
 #define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), unmask_lds(), st, rx, rx_len, fr.pay_off, fr.pay_len, \
@@ -2909,27 +2942,45 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
 
 hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg, const drun* runs,
                             dtrun* trun, uint64_t ntiles, uint64_t tile, uint32_t* fail, hipStream_t st) {
-    const uint64_t nb = (ntiles + 255) / 256;
-    if (nb) hipLaunchKernelGGL(k_run_tiles, dim3((uint32_t)nb), dim3(256), 0, st, rx, rx_len, segs, nseg, runs, trun,
-                               ntiles, tile, fail);
+    const uint32_t nb = (nseg + 3) / 4;   // one wave per segment
+    if (nb && ntiles) hipLaunchKernelGGL(k_run_tiles, dim3(nb), dim3(256), 0, st, rx, rx_len, segs, nseg, runs, trun,
+                                         ntiles, tile, fail);
     return hipGetLastError();
 }
 
-hipError_t launch_unmask_run(uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
+// RUN unmask geometries (threads x chunks per thread); $HVWS_EXPERIMENT run_geom picks
+// one for an on-device sweep (run_geom, hvws_engine.cpp)
+static constexpr struct { int threads, chunks; } kRunGeoms[] = {{256, 4}, {512, 2}, {256, 2}, {128, 4}, {64, 4}};
+int run_geom_count() { return (int)(sizeof kRunGeoms / sizeof kRunGeoms[0]); }
+uint64_t run_tile_bytes(int g) { return (uint64_t)kRunGeoms[g].threads * kRunGeoms[g].chunks * 16u; }
+
+hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
                              uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
                              hipEvent_t ev_stop) {
     if (rx_len == 0 || nseg == 0) return hipSuccess;
-    constexpr int T = 512, U = 2;   // the small-batch geometry (512 x 2, linear): RUN_TILE bytes per tile
-    const uint64_t ntiles_all = (rx_len + RUN_TILE - 1) / RUN_TILE;
+    if (geom < 0 || geom >= run_geom_count()) return hipErrorInvalidValue;
+    const uint64_t tile = run_tile_bytes(geom);
+    const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
+    const int T = kRunGeoms[geom].threads;
     const uint64_t cap = max_tiles_per_launch(T);
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
-        if (tile0 == 0 && ev_start)
-            hipExtLaunchKernelGGL((k_unmask_run<T, U>), dim3((uint32_t)ntiles), dim3(T), 0, st, ev_start, nullptr, 0u, rx,
-                                  rx_len, runs, trun, nseg, fail, tile0);
-        else
-            hipLaunchKernelGGL((k_unmask_run<T, U>), dim3((uint32_t)ntiles), dim3(T), 0, st, rx, rx_len, runs, trun, nseg,
-                               fail, tile0);
+        hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
+#define HVWS_RUN_K(TT, UU)                                                                                              \
+    if (e0)                                                                                                           \
+        hipExtLaunchKernelGGL((k_unmask_run<TT, UU>), dim3((uint32_t)ntiles), dim3(TT), 0, st, e0, nullptr, 0u, rx,     \
+                              rx_len, runs, trun, nseg, fail, tile0);                                                 \
+    else                                                                                                              \
+        hipLaunchKernelGGL((k_unmask_run<TT, UU>), dim3((uint32_t)ntiles), dim3(TT), 0, st, rx, rx_len, runs, trun,     \
+                           nseg, fail, tile0);
+        switch (geom) {
+            case 0: HVWS_RUN_K(256, 4) break;
+            case 1: HVWS_RUN_K(512, 2) break;
+            case 2: HVWS_RUN_K(256, 2) break;
+            case 3: HVWS_RUN_K(128, 4) break;
+            default: HVWS_RUN_K(64, 4) break;
+        }
+#undef HVWS_RUN_K
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

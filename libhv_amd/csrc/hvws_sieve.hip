@@ -732,7 +732,7 @@ constexpr uint64_t SIEVE_MIN_DEFAULT = 8ull << 20;
 
 uint64_t sieve_min() {
     if (!g_sieve_min) {
-        const char* e = getenv("HVWS_SIEVE_MIN");
+        const char* e = experiment("sieve_min");
         const long long x = e ? atoll(e) : 0;
         g_sieve_min = x > 0 ? (uint64_t)x : SIEVE_MIN_DEFAULT;
     }
@@ -750,8 +750,8 @@ uint64_t set_sieve_min(uint64_t v) {
 
 uint64_t sieve_generation() { return g_sieve_gen; }
 
-// Windows: regions of about $HVWS_SIEVE_HOPS (default 256) mean-sized frames,
-// each sieved over its first $HVWS_SIEVE_WINDOW bytes (default 1 MiB + 16 KiB:
+// Windows: regions of about $HVWS_EXPERIMENT sieve_hops (default 256) mean-sized frames,
+// each sieved over its first $HVWS_EXPERIMENT sieve_window bytes (default 1 MiB + 16 KiB:
 // past the largest frame of config 4, so a walk entering a region almost
 // always lands on a survivor of its window).  Regions shorter than two
 // windows, or no count yet: every tile.  Results never depend on it.
@@ -760,11 +760,11 @@ static uint64_t g_sv_hops = ~0ull, g_sv_win = 0;   // ~0 / 0: not yet read from 
 
 static void sieve_windows_init() {
     if (g_sv_hops == ~0ull) {
-        const char* e = getenv("HVWS_SIEVE_HOPS");
+        const char* e = experiment("sieve_hops");
         g_sv_hops = e ? (uint64_t)atoll(e) : SIEVE_HOPS_DEFAULT;
     }
     if (!g_sv_win) {
-        const char* e = getenv("HVWS_SIEVE_WINDOW");
+        const char* e = experiment("sieve_window");
         const long long x = e ? atoll(e) : 0;
         g_sv_win = x > 0 ? (uint64_t)x : SIEVE_WINDOW_DEFAULT;
     }
@@ -811,11 +811,11 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     dsieve* sv = reinterpret_cast<dsieve*>(b.state);
     hipError_t e = hipMemsetAsync(b.pool_n, 0, 8, st);
     if (e != hipSuccess) return e;
-    // $HVWS_SIEVE_MODE (timing experiments only): 1 lists without checks,
+    // $HVWS_EXPERIMENT sieve_mode (timing experiments only): 1 lists without checks,
     // 2 staging + candidate words, 3 loads alone -- these find no survivors,
     // so the chain is empty and the exact walk does everything (results stay
     // exact, only slow); 4 = without the next tile's register prefetch.
-    static const int mode = getenv("HVWS_SIEVE_MODE") ? atoi(getenv("HVWS_SIEVE_MODE")) : 0;
+    static const int mode = experiment("sieve_mode") ? atoi(experiment("sieve_mode")) : 0;
 #define HVWS_SIEVE_COUNT(M)                                                                                     \
     hipLaunchKernelGGL(k_sieve_count<M>, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,    \
                        sieve_min(), b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), \

@@ -959,14 +959,17 @@ hipError_t launch_tx_check(const uint64_t* pay_off, const uint64_t* len, const u
     X(5, 64, 4, false, false, true, 2)
 
 namespace {
-// $HVWS_BUILD: a fixed geometry (A/B runs); else by the batch's mean frame:
-// the lean one-wave form below 4 KiB per frame (c2: 0.43 against 0.46 ms),
-// the default above it (c3: 20.2-20.7 against 22.3 ms; profiles/r4v_raw)
+// $HVWS_EXPERIMENT build: a fixed geometry (A/B runs); else by the batch's mean frame:
+// the lean one-wave form from 256 B to 4 KiB per frame (c2: 0.43 against
+// 0.46 ms), the default above it (c3: 20.2-20.7 against 22.3 ms;
+// profiles/r4v_raw) and below it -- the lean form stages 16 frames per 4 KiB
+// tile, so under ~256 B most of its tiles would take the per-chunk search.
 int build_pick(uint64_t out_len, uint64_t n) {
-    const char* e = getenv("HVWS_BUILD");   // read per call (tests switch it)
+    const char* e = experiment("build");   // read per call (tests switch it)
     const int forced = e ? atoi(e) : -1;
     if (forced >= 0 && forced < 6) return forced;
-    return n && out_len / n < 4096 ? 5 : 0;
+    const uint64_t mean = n ? out_len / n : 0;
+    return mean >= 256 && mean < 4096 ? 5 : 0;
 }
 uint64_t build_tile(int v) {
     switch (v) {

@@ -109,7 +109,7 @@ def main():
                     ds[i] = scratch[i].ctypes.data
                 warm = [L.hvws_wsp_new() for _ in range(n)]
                 # gpu_pipe_inline: runs <= 256 KiB do their device half on the loop thread
-                os.environ["HVWS_FEEDER_INLINE"] = str(256 << 10) if mode == "gpu_pipe_inline" else "0"
+                os.environ["HVWS_EXPERIMENT"] = "feeder_inline=" + (str(256 << 10) if mode == "gpu_pipe_inline" else "0")
                 feeder = L.hvws_feeder_new() if mode.startswith("gpu_pipe") else None
                 if feeder:
                     L.hvws_wsp_feeder_submit(feeder, (ctypes.c_void_p * n)(*warm), ds, lens, n, rets)

@@ -74,11 +74,11 @@ def _loop(rng, conns, max_batch=None, dup=False, feeder=False):
     f = None
     if feeder:
         # "inline": every submission's device half on the loop thread (the
-        # $HVWS_FEEDER_INLINE path, read when the feeder is made)
+        # $HVWS_EXPERIMENT feeder_inline path, read when the feeder is made)
         if feeder == "inline":
-            os.environ["HVWS_FEEDER_INLINE"] = str(1 << 40)
+            os.environ["HVWS_EXPERIMENT"] = f"feeder_inline={1 << 40}"
         f = L.hvws_feeder_new()
-        os.environ.pop("HVWS_FEEDER_INLINE", None)
+        os.environ.pop("HVWS_EXPERIMENT", None)
     subs = []
     pending = [c for c in conns if c.chunks]
     while pending:

@@ -234,10 +234,10 @@ def test_build_one_moved_payload(eng):
 
 @pytest.mark.parametrize("v", ["0", "1", "2", "3", "4", "5"])
 def test_build_every_geometry(eng, v, monkeypatch):
-    """Every k_build geometry ($HVWS_BUILD) builds small frames, edge lengths
+    """Every k_build geometry ($HVWS_EXPERIMENT build=) builds small frames, edge lengths
     and misaligned payloads byte for byte like the reference and reports its
     name; unset, the pick follows the mean frame size."""
-    monkeypatch.setenv("HVWS_BUILD", v)
+    monkeypatch.setenv("HVWS_EXPERIMENT", f"build={v}")
     L = libhv_amd.lib()
     rng = np.random.default_rng(3)
     lens = np.concatenate([rng.integers(0, 20, 200), rng.integers(1000, 2019, 300), np.array(EDGE_LENS)])
@@ -248,7 +248,7 @@ def test_build_every_geometry(eng, v, monkeypatch):
 
 
 def test_build_geometry_by_frame_size(eng, monkeypatch):
-    monkeypatch.delenv("HVWS_BUILD", raising=False)
+    monkeypatch.delenv("HVWS_EXPERIMENT", raising=False)
     L = libhv_amd.lib()
     rng = np.random.default_rng(4)
     small = _frames(rng, 300, lens=[1000] * 300)
@@ -265,11 +265,11 @@ def test_build_geometry_by_frame_size(eng, monkeypatch):
 @pytest.mark.parametrize("order", ["packed", "gaps", "shuffled"])
 def test_build_boundary_tiles_span_staged(eng, spans, order, monkeypatch):
     """Boundary tiles of the general layout stage their source span in LDS
-    together with the frame records (k_tx_index; $HVWS_BUILD_SPANS=0: the
+    together with the frame records (k_tx_index; $HVWS_EXPERIMENT build_spans=0: the
     records-first tiles).  Small frames packed back to back, with gaps, and
     with payloads in shuffled order (spans past the LDS area fall back to the
     records-first path); every byte against the reference."""
-    monkeypatch.setenv("HVWS_BUILD_SPANS", spans)
+    monkeypatch.setenv("HVWS_EXPERIMENT", f"build_spans={spans}")
     rng = np.random.default_rng(31)
     lens = np.concatenate([rng.integers(900, 1100, 1500), rng.integers(0, 130, 300)])
     rng.shuffle(lens)
@@ -324,7 +324,7 @@ def _build_at(eng, frames, offs, pay: bytes):
 @pytest.mark.parametrize("layout", ["packed", "gap", "rx", "shared", "one"])
 def test_build_uniform_layouts(eng, ln, layout):
     """Uniform layouts of small frames (every frame the same size and payload
-    length, under 4 KiB, payload offsets a + k*b with b >= the payload length)
+    length, 256 B to 4 KiB, payload offsets a + k*b with b >= the payload length)
     build without a tile index
     -- each tile finds its frames and source span from its position -- frame by
     frame equal to the reference's websocket_build_frame: payloads packed, with
@@ -347,9 +347,9 @@ def test_build_uniform_layouts(eng, ln, layout):
     assert got == H.build_frames_ref(frames)
     # one payload shared by every frame (a step shorter than a payload), or
     # frames of 4 KiB and more (the default form, where the index costs ~0.1 %
-    # of the call): the index
+    # of the call) or under 256 B (the default form too: build_pick): the index
     size = len(H.build_frames_ref([frames[0]]))
-    assert uni == (0 if (layout == "shared" and ln) or size >= 4096 else 1)
+    assert uni == (0 if (layout == "shared" and ln) or size >= 4096 or size < 256 else 1)
 
 
 @pytest.mark.parametrize("kind", ["same_size_other_lengths", "descending", "one_longer", "shuffled"])
