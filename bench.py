@@ -938,7 +938,7 @@ def main():
     alg_bytes = 2 * P + HB
     achieved = alg_bytes / (mean_unmask * 1e-3) / 1e9
 
-    kname = L.hvws_unmask_kernel_name_for(plan.total).decode()
+    kname = (L.hvws_run_kernel_name() if scan_path == 7 else L.hvws_unmask_kernel_name_for(plan.total)).decode()
     traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):

@@ -168,6 +168,8 @@ int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
  * batch of rx_len bytes runs with (e.g. "k_unmask<256,4,xcd>"). */
 const char* hvws_unmask_kernel_name(void);
 const char* hvws_unmask_kernel_name_for(uint64_t rx_len);
+/* The RUN path's unmask kernel (HVWS_PATH_RUN steps), e.g. "k_unmask_run<256,4>". */
+const char* hvws_run_kernel_name(void);
 /* Force a k_unmask geometry for later scans (tuning; process-wide); -1 =
  * back to the choice by batch size. */
 int hvws_set_unmask_variant(int variant);

@@ -2978,6 +2978,8 @@ const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant())
 
 const char* hvws_unmask_kernel_name_for(uint64_t rx_len) { return unmask_name(unmask_variant_for(rx_len)); }
 
+const char* hvws_run_kernel_name(void) { return run_geom_name(run_geom()); }
+
 uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
 
 uint64_t hvws_set_sieve_min(uint64_t bytes) { return set_sieve_min(bytes); }

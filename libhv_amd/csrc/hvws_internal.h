@@ -195,6 +195,7 @@ hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs
 // status->pad3 when it is done.
 int run_geom_count();
 uint64_t run_tile_bytes(int geom);
+const char* run_geom_name(int geom);
 hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
                              uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
                              hipEvent_t ev_stop);

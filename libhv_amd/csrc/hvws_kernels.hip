@@ -2953,6 +2953,12 @@ hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs
 static constexpr struct { int threads, chunks; } kRunGeoms[] = {{256, 4}, {512, 2}, {256, 2}, {128, 4}, {64, 4}};
 int run_geom_count() { return (int)(sizeof kRunGeoms / sizeof kRunGeoms[0]); }
 uint64_t run_tile_bytes(int g) { return (uint64_t)kRunGeoms[g].threads * kRunGeoms[g].chunks * 16u; }
+const char* run_geom_name(int g) {
+    static const char* const names[] = {"k_unmask_run<256,4>", "k_unmask_run<512,2>", "k_unmask_run<256,2>",
+                                        "k_unmask_run<128,4>", "k_unmask_run<64,4>"};
+    static_assert(sizeof names / sizeof names[0] == sizeof kRunGeoms / sizeof kRunGeoms[0], "one name per geometry");
+    return g >= 0 && g < run_geom_count() ? names[g] : "";
+}
 
 hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
                              uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,

@@ -8,6 +8,11 @@ access of k_unmask and k_sieve_count, MI355X_MICROARCH.md HBM section),
 write bytes = WRITE_SIZE x 1024.
 
   scripts/step_traffic.py FETCH_DIR WRITE_DIR --alg-bytes N [--out FILE]
+      [--steps-by k_unmask_run --drop k_unmask<,k_walk,...]
+
+--steps-by counts steps by the dispatches of one unmask kernel (a RUN run's
+first steps take the exact path); --drop leaves out the kernels of those
+other steps (name prefixes).
 """
 import argparse
 import csv
@@ -19,7 +24,7 @@ from collections import defaultdict
 SETUP = ("k_synth", "k_stream_xor", "k_digest", "k_frame_sizes")   # the bench's own setup and checks
 
 
-def load(d, counter):
+def load(d, counter, steps_by="k_unmask", drop=()):
     per = defaultdict(float)
     n_unmask = 0
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -27,9 +32,9 @@ def load(d, counter):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("hvws::", "")
-            if "k_unmask" in name:
+            if name.startswith(steps_by):
                 n_unmask += 1
-            if any(s in name for s in SETUP):
+            if any(s in name for s in SETUP) or any(name.startswith(p) for p in drop):
                 continue
             per[name] += float(r["Counter_Value"])
     return per, n_unmask
@@ -41,9 +46,12 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--alg-bytes", type=float, required=True)
     ap.add_argument("--out")
+    ap.add_argument("--steps-by", default="k_unmask")
+    ap.add_argument("--drop", default="", help="comma-separated kernel name prefixes left out")
     a = ap.parse_args()
-    fe, nu_f = load(a.fetch_dir, "FETCH_SIZE")
-    wr, nu_w = load(a.write_dir, "WRITE_SIZE")
+    drop = tuple(x for x in a.drop.split(",") if x)
+    fe, nu_f = load(a.fetch_dir, "FETCH_SIZE", a.steps_by, drop)
+    wr, nu_w = load(a.write_dir, "WRITE_SIZE", a.steps_by, drop)
     steps = max(nu_f, 1)
     rd = {k: 2 * v * 1024 / steps for k, v in fe.items()}
     wb = {k: v * 1024 / max(nu_w, 1) for k, v in wr.items()}
