@@ -2311,7 +2311,7 @@ __device__ __forceinline__ void fast_run_init(fast_run& R, const dtrun& o, uint3
 // payload's phase, into its slot.
 __device__ __forceinline__ void fast_run_keys(const fast_run& R, const uint8_t* rx, uint64_t rx_len, uint64_t base,
                                               uint32_t* s_fk, uint32_t* __restrict__ fail, uint32_t nseg, uint32_t tid,
-                                              uint32_t T) {
+                                              uint32_t T, const uint32_t* s_tile = nullptr, int32_t tile_bytes = 0) {
     uint64_t plo, phi, mlo, mhi;
     run_pattern(R.masked, (uint32_t)R.hl, R.len, plo, phi, mlo, mhi);
     const uint32_t kb = (uint32_t)R.hl - 4u;   // the key's first byte in a masked header: 2, 4 or 10
@@ -2324,7 +2324,8 @@ __device__ __forceinline__ void fast_run_keys(const fast_run& R, const uint8_t* 
                 key = R.k0;   // begun before the tile: its header is checked where it starts
             } else {
                 uint64_t lo, hi;
-                ld16(rx, rx_len, base + (uint64_t)hs, lo, hi);
+                if (s_tile && hs + 16 <= tile_bytes) lds_hdr16(s_tile, (uint32_t)hs, lo, hi);   // staged tile
+                else ld16(rx, rx_len, base + (uint64_t)hs, lo, hi);
                 if (((lo ^ plo) & mlo) | ((hi ^ phi) & mhi)) {
                     atomicOr(&fail[R.seg], 1u);
                     atomicOr(&fail[nseg], 1u);
@@ -2381,11 +2382,11 @@ __device__ __forceinline__ void fast_run_mask(const fast_run& R, const uint32_t*
 // run frame reads its header and keeps its key (fast_run_keys) while the
 // selector table is built; one barrier; each chunk XORs what the runs lay on
 // it.
-template <int T, int U>
+template <int T, int U, bool STAGE>
 __device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
                                                 const dtrun* __restrict__ trun, uint32_t nseg,
                                                 uint32_t* __restrict__ fail, uint64_t t, uint32_t* s_fk,
-                                                uint32_t* s_sel) {
+                                                uint32_t* s_sel, uint32_t* s_tile) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     const uint64_t base = t * TILE, te = base + TILE;
     const uint32_t tid = threadIdx.x;
@@ -2409,6 +2410,11 @@ __device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64
     const dtrun& tr = trun[t];   // wave-uniform: scalar loads
     const uint32_t s0 = tr.s0;
     if (s0 >= nseg) return;   // no segment reaches this tile
+    if (STAGE) {   // the headers from the tile's own bytes: staged in LDS, one more barrier
+#pragma unroll
+        for (int i = 0; i < U; ++i) *reinterpret_cast<u32x4*>(&s_tile[((uint32_t)i * T + tid) * 4u]) = v[i];
+        __syncthreads();
+    }
     fast_run R0, R1;
     fast_run_init(R0, tr, s0, 0);
     const uint32_t s1 = tr.s1;
@@ -2420,8 +2426,8 @@ __device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64
         tile_run(o1, r1, run_fast_ok(r1), base, TILE);
         fast_run_init(R1, o1, s1, R0.nj + 3);
     }
-    fast_run_keys(R0, rx, rx_len, base, s_fk, fail, nseg, tid, T);
-    if (two) fast_run_keys(R1, rx, rx_len, base, s_fk, fail, nseg, tid, T);
+    fast_run_keys(R0, rx, rx_len, base, s_fk, fail, nseg, tid, T, STAGE ? s_tile : nullptr, (int32_t)TILE);
+    if (two) fast_run_keys(R1, rx, rx_len, base, s_fk, fail, nseg, tid, T, STAGE ? s_tile : nullptr, (int32_t)TILE);
     for (uint32_t e = tid; e < 256; e += T) s_sel[e] = kRunSel.v[e];
     __syncthreads();
     bool dirty[U];
@@ -2533,14 +2539,15 @@ __device__ __forceinline__ void run_repair(uint8_t* __restrict__ rx, uint64_t rx
     }
 }
 
-template <int T, int U>
+template <int T, int U, bool STAGE>
 __global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
                                                   const dtrun* __restrict__ trun, uint32_t nseg,
                                                   uint32_t* __restrict__ fail, uint64_t tile0) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     __shared__ uint32_t s_fk[TILE / 32 + 16];   // 2 runs: sum of (nj + 3) <= TILE / 32 + 8
     __shared__ uint32_t s_sel[256];
-    run_unmask_tile<T, U>(rx, rx_len, runs, trun, nseg, fail, tile0 + blockIdx.x, s_fk, s_sel);
+    __shared__ uint32_t s_tile[STAGE ? TILE / 4 + 8 : 1];
+    run_unmask_tile<T, U, STAGE>(rx, rx_len, runs, trun, nseg, fail, tile0 + blockIdx.x, s_fk, s_sel, s_tile);
 }
 
 // The repair kernel behind the unmask on the same stream (a kernel boundary
@@ -2948,14 +2955,17 @@ hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs
     return hipGetLastError();
 }
 
-// RUN unmask geometries (threads x chunks per thread); $HVWS_EXPERIMENT run_geom picks
+// RUN unmask geometries (threads x chunks per thread; 0: the tile staged in LDS
+// for the header reads, c2 0.380-0.382 against 0.386-0.387 ms per step reading
+// them from HBM, 256 x 2 staged 0.401, profiles/r5_raw/sweeps/*_r5x.json);
+// $HVWS_EXPERIMENT run_geom picks
 // one for an on-device sweep (run_geom, hvws_engine.cpp)
-static constexpr struct { int threads, chunks; } kRunGeoms[] = {{256, 4}, {512, 2}, {256, 2}, {128, 4}, {64, 4}};
+static constexpr struct { int threads, chunks; } kRunGeoms[] = {{256, 4}, {256, 4}, {512, 2}, {256, 2}, {128, 4}, {64, 4}};
 int run_geom_count() { return (int)(sizeof kRunGeoms / sizeof kRunGeoms[0]); }
 uint64_t run_tile_bytes(int g) { return (uint64_t)kRunGeoms[g].threads * kRunGeoms[g].chunks * 16u; }
 const char* run_geom_name(int g) {
-    static const char* const names[] = {"k_unmask_run<256,4>", "k_unmask_run<512,2>", "k_unmask_run<256,2>",
-                                        "k_unmask_run<128,4>", "k_unmask_run<64,4>"};
+    static const char* const names[] = {"k_unmask_run<256,4,lds>", "k_unmask_run<256,4>", "k_unmask_run<512,2>",
+                                        "k_unmask_run<256,2>", "k_unmask_run<128,4>", "k_unmask_run<64,4>"};
     static_assert(sizeof names / sizeof names[0] == sizeof kRunGeoms / sizeof kRunGeoms[0], "one name per geometry");
     return g >= 0 && g < run_geom_count() ? names[g] : "";
 }
@@ -2972,19 +2982,20 @@ hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun*
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
         hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
-#define HVWS_RUN_K(TT, UU)                                                                                              \
+#define HVWS_RUN_K(TT, UU, SS)                                                                                          \
     if (e0)                                                                                                           \
-        hipExtLaunchKernelGGL((k_unmask_run<TT, UU>), dim3((uint32_t)ntiles), dim3(TT), 0, st, e0, nullptr, 0u, rx,     \
+        hipExtLaunchKernelGGL((k_unmask_run<TT, UU, SS>), dim3((uint32_t)ntiles), dim3(TT), 0, st, e0, nullptr, 0u, rx, \
                               rx_len, runs, trun, nseg, fail, tile0);                                                 \
     else                                                                                                              \
-        hipLaunchKernelGGL((k_unmask_run<TT, UU>), dim3((uint32_t)ntiles), dim3(TT), 0, st, rx, rx_len, runs, trun,     \
+        hipLaunchKernelGGL((k_unmask_run<TT, UU, SS>), dim3((uint32_t)ntiles), dim3(TT), 0, st, rx, rx_len, runs, trun, \
                            nseg, fail, tile0);
         switch (geom) {
-            case 0: HVWS_RUN_K(256, 4) break;
-            case 1: HVWS_RUN_K(512, 2) break;
-            case 2: HVWS_RUN_K(256, 2) break;
-            case 3: HVWS_RUN_K(128, 4) break;
-            default: HVWS_RUN_K(64, 4) break;
+            case 0: HVWS_RUN_K(256, 4, true) break;
+            case 1: HVWS_RUN_K(256, 4, false) break;
+            case 2: HVWS_RUN_K(512, 2, false) break;
+            case 3: HVWS_RUN_K(256, 2, false) break;
+            case 4: HVWS_RUN_K(128, 4, false) break;
+            default: HVWS_RUN_K(64, 4, false) break;
         }
 #undef HVWS_RUN_K
         hipError_t e = hipGetLastError();

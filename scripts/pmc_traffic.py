@@ -54,6 +54,9 @@ def main():
             parts = name[len("k_build<"):-1].split(",")
             if len(parts) == 6:
                 name = f"k_build<{parts[0]}x{parts[1]}" + {"2": ",lean", "0": ",wide"}.get(parts[5], "") + ">"
+        elif name.startswith("k_unmask_run<"):   # hvws_run_kernel_name spelling: <T,U> / <T,U,lds>
+            parts = name[len("k_unmask_run<"):-1].split(",")
+            name = "k_unmask_run<" + ",".join(parts[:2]) + (",lds" if parts[2:] == ["true"] else "") + ">"
         elif not name.startswith("k_build"):   # hvws_unmask_kernel_name spelling
             name = name.replace("true", "xcd").replace("false", "linear")
         db.setdefault(name, {})[str(a.rx_bytes)] = {
