@@ -168,8 +168,13 @@ int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
  * batch of rx_len bytes runs with (e.g. "k_unmask<256,4,xcd>"). */
 const char* hvws_unmask_kernel_name(void);
 const char* hvws_unmask_kernel_name_for(uint64_t rx_len);
-/* The RUN path's unmask kernel (HVWS_PATH_RUN steps), e.g. "k_unmask_run<256,4>". */
+/* The RUN path's unmask kernel (HVWS_PATH_RUN steps), e.g. "k_unmask_run<256,4,lds>". */
 const char* hvws_run_kernel_name(void);
+/* Force a RUN unmask geometry (0 .. hvws_run_geometry_count() - 1) for later
+ * RUN steps (tests, tuning; process-wide); -1 = the default again.  Returns
+ * the previous setting (-1: none). */
+int hvws_set_run_geometry(int geometry);
+int hvws_run_geometry_count(void);
 /* Force a k_unmask geometry for later scans (tuning; process-wide); -1 =
  * back to the choice by batch size. */
 int hvws_set_unmask_variant(int variant);

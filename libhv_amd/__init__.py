@@ -177,6 +177,8 @@ _SIGS = {
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
     "hvws_unmask_kernel_name_for": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hvws_run_kernel_name": (ctypes.c_char_p, []),
+    "hvws_set_run_geometry": (ctypes.c_int, [ctypes.c_int]),
+    "hvws_run_geometry_count": (ctypes.c_int, []),
     "hvws_set_spec_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_sieve_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_table_checks": (ctypes.c_int, [ctypes.c_int]),

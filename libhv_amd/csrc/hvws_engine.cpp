@@ -200,6 +200,7 @@ struct hvws_ctx {
     // RUN path (hvws_internal.h, drun): the last scan left no frame table (its
     // records are built on demand), its unmask is k_unmask_run + k_run_fix
     bool run_active = false;
+    int run_g = 0;             // the RUN geometry the last RUN scan cut its tiles for
     bool run_call = false;     // the scan belongs to a step call (the only callers RUN serves)
     int run_mode = -1;         // hvws_set_run: -1 auto, 0 never, 1 whenever a step's batch allows it
     uint32_t run_skip = 0;     // steps left before RUN is tried again after a failed hypothesis
@@ -463,12 +464,17 @@ bool run_env() {
 }
 
 // The RUN unmask's geometry (kRunGeoms, hvws_kernels.hip); $HVWS_EXPERIMENT run_geom for a sweep.
+// hvws_set_run_geometry (tests: every compiled geometry) overrides it; a
+// step's scan records the geometry its tiles were cut for (ctx run_g) and its
+// unmask uses that one.
+std::atomic<int> g_run_geom_forced{-1};
 int run_geom() {
     static const int v = [] {
         const int g = experiment("run_geom") ? atoi(experiment("run_geom")) : 0;
         return g >= 0 && g < run_geom_count() ? g : 0;
     }();
-    return v;
+    const int f = g_run_geom_forced.load(std::memory_order_relaxed);
+    return f >= 0 && f < run_geom_count() ? f : v;
 }
 
 bool host_order() {
@@ -631,7 +637,7 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
-        if ((e = launch_unmask_run(run_geom(), d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
+        if ((e = launch_unmask_run(c->run_g, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
                                    c->run_seq, c->stream, timed ? c->tev[c->t_cur][2] : nullptr,
                                    timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess)
@@ -919,7 +925,8 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 if (c->T().run_fail.p != was || c->T().run_fail.cap != had)
                     HIP_OR(hipMemsetAsync(c->T().run_fail.p, 0, c->T().run_fail.cap, c->cs), HVWS_EHIP);
             }
-            const uint64_t rtile = run_tile_bytes(run_geom());
+            c->run_g = run_geom();
+            const uint64_t rtile = run_tile_bytes(c->run_g);
             const uint64_t rtiles = (rx_len + rtile - 1) / rtile;
             HIP_OR(c->T().run_trun.ensure((rtiles + 1) * sizeof(dtrun)), HVWS_ENOMEM);
             sc.runs = c->T().runs.as<drun>();
@@ -2979,6 +2986,13 @@ const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant())
 const char* hvws_unmask_kernel_name_for(uint64_t rx_len) { return unmask_name(unmask_variant_for(rx_len)); }
 
 const char* hvws_run_kernel_name(void) { return run_geom_name(run_geom()); }
+
+int hvws_set_run_geometry(int g) {
+    if (g >= run_geom_count()) return set_err(HVWS_EINVAL, "RUN geometry %d of %d", g, run_geom_count());
+    return g_run_geom_forced.exchange(g < 0 ? -1 : g);
+}
+
+int hvws_run_geometry_count(void) { return run_geom_count(); }
 
 uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
 

@@ -36,6 +36,18 @@ def _check(eng, buf, segs, exp_recs, exp_carry, exp_started):
         assert started[s] == exp_started[s], s
 
 
+@pytest.fixture(params=range(6), ids=lambda g: f"geom{g}")
+def geom(request):
+    """Every compiled RUN unmask geometry (hvws_set_run_geometry), the default
+    (0: 256 x 4, tile staged in LDS) first."""
+    L = libhv_amd.lib()
+    if request.param >= L.hvws_run_geometry_count():
+        pytest.skip("geometry not compiled")
+    old = L.hvws_set_run_geometry(request.param)
+    yield request.param
+    L.hvws_set_run_geometry(old)
+
+
 @pytest.fixture
 def fresh():
     """A context of its own (what earlier tests taught the shared one does not
@@ -47,7 +59,7 @@ def fresh():
     e.close()
 
 
-def test_run_taken_for_uniform_steps_and_repairs_nothing(fresh):
+def test_run_taken_for_uniform_steps_and_repairs_nothing(geom, fresh):
     """Uniform 1 KiB frames in 24 segments: after the first exact scan sees
     them uniform, steps take RUN; nothing is repaired; every step's bytes,
     frames and carries equal the oracle's."""
@@ -91,7 +103,7 @@ def test_run_pipelined_same_buffer(fresh):
 
 
 @pytest.mark.parametrize("where", ["first", "middle", "last", "tail_then_more"])
-def test_run_hypothesis_breaks(fresh, where):
+def test_run_hypothesis_breaks(geom, fresh, where):
     """One segment that is not one run -- a frame of another size at its
     start, middle or end, or a whole frame after the cut one -- under RUN
     forced: that segment alone is repaired, and bytes, frames and carries
@@ -159,7 +171,7 @@ def test_run_auto_falls_back_on_mixed_traffic(fresh):
     rx.free()
 
 
-def test_run_carried_and_cut_frames(fresh):
+def test_run_carried_and_cut_frames(geom, fresh):
     """Segments that start inside a frame (payload or header carried in) and
     end inside one (payload, header, or a single byte of it), every frame of
     one size between: the carried-in and cut frames are exact in k_head's
@@ -189,7 +201,7 @@ def test_run_carried_and_cut_frames(fresh):
     rx.free()
 
 
-def test_run_random_streams_forced(fresh):
+def test_run_random_streams_forced(geom, fresh):
     """Random streams (every opcode, masked and unmasked, all length classes)
     cut into segments, under RUN forced: mostly repaired, always exact."""
     eng, L = fresh, libhv_amd.lib()
