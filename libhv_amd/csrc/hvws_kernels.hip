@@ -2978,7 +2978,14 @@ hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun*
     const uint64_t tile = run_tile_bytes(geom);
     const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
     const int T = kRunGeoms[geom].threads;
-    const uint64_t cap = max_tiles_per_launch(T);
+    // The grid in two launches: c2 0.375-0.376 ms per step against 0.377-0.379
+    // in one, 0.378-0.379 in three, 0.383-0.385 in four (interleaved on one box,
+    // profiles/r5_raw/sweeps/*_r5za.json); 64 x 4 lost with every split
+    // ($HVWS_EXPERIMENT run_pieces=<n> overrides).
+    static const uint64_t pieces = experiment("run_pieces") && atoi(experiment("run_pieces")) > 0
+                                       ? (uint64_t)atoi(experiment("run_pieces")) : 2;
+    uint64_t cap = max_tiles_per_launch(T);
+    if (pieces > 1) cap = std::min<uint64_t>(cap, (ntiles_all + pieces - 1) / pieces);
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
         hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
