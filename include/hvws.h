@@ -161,6 +161,26 @@ int hvws_last_times(hvws_ctx* ctx, float out[2]);
  * error).  Lets a caller time a run of asynchronous steps afterwards. */
 int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
 
+/* Lagged steps: two scan chains in flight.  A lagged
+ * stepper runs consecutive hvws_step_resident steps on two contexts of one
+ * device from two worker threads, so batch k+1's discovery is launched while
+ * batch k's is still running; unmasks stay in call order.  hvws_lagged_step
+ * copies the segment and carry tables and returns once the step is handed
+ * over: the batch is unmasked by the time hvws_lagged_sync (or a later
+ * step's return, two calls on) says so.  Errors stick: every later call
+ * returns the first one (hvws_lagged_error names it).  hvws_lagged_context(i)
+ * gives the two contexts (i = 0, 1) for timing and diagnostics.  Opt-in:
+ * for one 4.3 GB mixed stream it measured slower than hvws_step_resident
+ * (1.70-1.78 against 1.58 ms per step). */
+typedef struct hvws_lagged hvws_lagged;
+hvws_lagged* hvws_lagged_new(int device);   /* NULL on failure */
+int hvws_lagged_step(hvws_lagged* lag, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
+                     const websocket_parser* carry_in, uint32_t nseg);
+int hvws_lagged_sync(hvws_lagged* lag);
+hvws_ctx* hvws_lagged_context(hvws_lagged* lag, int i);
+const char* hvws_lagged_error(hvws_lagged* lag);
+void hvws_lagged_free(hvws_lagged* lag);
+
 /* k_unmask geometry.  By default it follows the batch size: 512 threads x 2
  * chunks in linear tile order below 16 GiB, 256 x 4 in XCD-contiguous order
  * from there (measured).  hvws_unmask_kernel_name: the name

@@ -201,6 +201,11 @@ struct hvws_ctx {
     // records are built on demand), its unmask is k_unmask_run + k_run_fix
     bool run_active = false;
     int run_g = 0;             // the RUN geometry the last RUN scan cut its tiles for
+    // Lagged steps (hvws_lagged_*, hvws_lagged.cpp): called once before the
+    // step's first unmask is queued (the previous lagged step's unmask, on
+    // another context, is ordered before it there); armed per step.
+    std::function<void()> lag_before;
+    bool lag_armed = false;
     bool run_call = false;     // the scan belongs to a step call (the only callers RUN serves)
     int run_mode = -1;         // hvws_set_run: -1 auto, 0 never, 1 whenever a step's batch allows it
     uint32_t run_skip = 0;     // steps left before RUN is tried again after a failed hypothesis
@@ -616,6 +621,10 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
 // (host_order), so the unmask needs no cross-stream wait packet.
 hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined = false) {
     hipError_t e;
+    if (c->lag_armed) {
+        c->lag_armed = false;
+        if (c->lag_before) c->lag_before();
+    }
     const bool piped = c->cs != c->stream;
     if (piped && !joined) {   // the scan ran on the side stream: join it
         if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
@@ -3205,5 +3214,20 @@ void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask,
     copy_parser(carry_out, cin);
     started = st;
 }
+
+// Lagged steps (hvws_lagged.cpp)
+void ctx_arm_lag(hvws_ctx* c, std::function<void()> before) {
+    c->lag_before = std::move(before);
+    c->lag_armed = true;
+}
+bool ctx_lag_fire(hvws_ctx* c) {   // runs the hook if the step queued no unmask; true if it ran here
+    if (!c->lag_armed) return false;
+    c->lag_armed = false;
+    if (c->lag_before) c->lag_before();
+    return true;
+}
+hipStream_t ctx_stream(hvws_ctx* c) { return c->stream; }
+hipStream_t ctx_scan_stream(hvws_ctx* c) { return c->sstream; }
+int ctx_device(hvws_ctx* c) { return c->device; }
 
 }  // namespace hvws

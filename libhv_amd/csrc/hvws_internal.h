@@ -11,6 +11,8 @@
 
 #include "websocket_parser.h"
 
+struct hvws_ctx;
+
 namespace hvws {
 
 // $HVWS_EXPERIMENT="name=value,name=value": the A/B switches of the on-device
@@ -478,5 +480,13 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                         const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,
                         hipStream_t st, const uint64_t* uni = nullptr);
+
+// Lagged steps (hvws_lagged.cpp): the hook a context calls once before its
+// step's first unmask is queued, and what it needs of the context.
+void ctx_arm_lag(hvws_ctx* c, std::function<void()> before);
+bool ctx_lag_fire(hvws_ctx* c);
+hipStream_t ctx_stream(hvws_ctx* c);
+hipStream_t ctx_scan_stream(hvws_ctx* c);
+int ctx_device(hvws_ctx* c);
 
 }  // namespace hvws
