@@ -639,11 +639,15 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
     // 1.73 -> 1.55 ms, but c3 21.3 -> 22.4 ms and c2 flat, so uniform batches
     // (SPEC: a short scan) keep one launch.  With the 512 x 2 linear geometry
     // (round 2, profiles/r2n_raw) c4 ran 1.429 / 1.405 / 1.377 / 1.366 ms at
-    // 1 / 2 / 4 / 8 pieces: 8.  $HVWS_EXPERIMENT unmask_pieces overrides.
+    // 1 / 2 / 4 / 8 pieces: 8.  One sieved stream (c4 as one segment, its
+    // ~25 chain kernels beside the unmask) likewise: 1 / 2 / 4 / 8 / 12 / 16 /
+    // 32 pieces 1.58 / 1.56 / 1.54 / 1.52 / 1.525 / 1.535 / 1.59 ms
+    // (profiles/r5_raw/pieces).  $HVWS_EXPERIMENT unmask_pieces overrides.
     static const int env_pieces = experiment("unmask_pieces") ? atoi(experiment("unmask_pieces")) : -1;
     const int path = c->prev_path;   // the current scan's path may not be settled yet
     const bool mixed = path == HVWS_PATH_SLACK || path == HVWS_PATH_SLACK_FAILED || path == HVWS_PATH_SPEC_FAILED ||
-                       (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok);   // an exact scan that saw mixed counts
+                       (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok) ||   // an exact scan that saw mixed counts
+                       (path == HVWS_PATH_SINGLE && c->sv_ran);                 // a sieved stream
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
         if ((e = launch_unmask_run(c->run_g, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
