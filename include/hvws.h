@@ -433,7 +433,9 @@ int hvws_debug_backtraces(int fd);
  * or through pinned host memory (0), the context has a worker stream}. */
 int hvws_door_info(hvws_ctx* ctx, uint64_t out[2]);
 /* Diagnostics: 100 MHz device-clock stamps of the worker's last read request
- * -- seen, staged, walked, XORed, records written (before the release). */
+ * -- seen, staged, walked, XORed, records written (before the release), and
+ * the previous request's release.  Written only under $HVWS_EXPERIMENT
+ * door_stamps=1 (each stamp costs the worker a clock round trip); else 0. */
 int hvws_door_stamps(hvws_ctx* ctx, uint64_t out[12]);
 
 /* Small batches whose segments are all <= 32 KiB (total <= 1 MiB; an event

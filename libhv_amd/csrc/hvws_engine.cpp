@@ -1840,12 +1840,30 @@ void door_fail(hvws_ctx* c, const char* what) {
     if (c->door_live && !c->door_wedged && door_drain(c, 1000, "failed request")) c->door_live = false;
 }
 
+// $HVWS_EXPERIMENT feed_times=1: host time per phase of door_feed (request
+// written, answered, results copied back), printed at exit (diagnostic).
+struct door_times {
+    bool on = experiment("feed_times") && atoi(experiment("feed_times"));
+    std::atomic<uint64_t> calls{0}, ns[3] = {};
+    ~door_times() {
+        const uint64_t n = calls.load();
+        if (on && n)
+            fprintf(stderr, "[door_times] calls=%llu us/call: request %.2f answer %.2f results %.2f\n",
+                    (unsigned long long)n, ns[0].load() / 1e3 / n, ns[1].load() / 1e3 / n, ns[2].load() / 1e3 / n);
+    }
+};
+door_times g_door_times;
+
 // One read through the worker (gpu_feed's fast path): false when the worker
 // does not take it (off, or longer than kDoorMax).
 bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry, bool unmask,
                std::vector<hvws_frame>& frames, websocket_parser& carry_out, int& started) {
     if (!door_on(c) || len > kDoorMax || door_ensure(c) != HVWS_OK) return false;
     std::lock_guard<std::mutex> cl(c->door_m);
+    using clk = std::chrono::steady_clock;
+    const bool timed = g_door_times.on;
+    clk::time_point t0, t1, t2;
+    if (timed) t0 = clk::now();
     ddoor* b = c->h_door.as<ddoor>();
     ddoor* rq = door_req(c);
     uint8_t* data = c->h_door_data.as<uint8_t>();
@@ -1857,10 +1875,12 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
     dcarry cin;
     to_dcarry(carry, cin);
     memcpy(&rq->carry, &cin, sizeof(dcarry));
+    if (timed) t1 = clk::now();
     if (door_call(c) != HVWS_OK) {
         door_fail(c, "read");
         return false;
     }
+    if (timed) t2 = clk::now();
     const uint64_t n = b->count;
     frames.resize((size_t)n);
     if (n) memcpy(frames.data(), c->h_door_rec.p, (size_t)n * sizeof(drec));
@@ -1869,6 +1889,13 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
     const dcarry out = b->out;
     from_dcarry(out, carry_out);
     started = (int)out.started;
+    if (timed) {
+        const auto t3 = clk::now();
+        g_door_times.calls.fetch_add(1, std::memory_order_relaxed);
+        g_door_times.ns[0].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
+        g_door_times.ns[1].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count());
+        g_door_times.ns[2].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count());
+    }
     return true;
 }
 

@@ -387,9 +387,9 @@ struct ddoor {
     uint64_t exited;    // epoch of the last worker that has ended (its last store before it returns)
     uint64_t pad2[1];
     // realtime-clock stamps of the last request (100 MHz): seen, staged,
-    // walked, xored, stored (before the release), and the sum of ticks spent
-    // polling; read by hvws_door_stats' diagnostics
-    uint64_t stamp[12];   // [8..10]: door_walk's chase, parallel parse, tail ends
+    // walked, xored, stored (before the release); read by hvws_door_stamps'
+    // diagnostics (scripts/probe/door_phases.py)
+    uint64_t stamp[12];   // [6]: the previous request's release, ticks; [8..10]: door_walk's chase, parse, tail ends
 };
 static_assert(sizeof(dcarry) == 48, "dcarry layout");
 static_assert(offsetof(ddoor, done) == 128, "ddoor: device fields on their own lines");

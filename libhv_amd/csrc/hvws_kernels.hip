@@ -1092,9 +1092,16 @@ __device__ __forceinline__ void door_size(const uint32_t* l, uint32_t q, uint32_
 }
 
 // k_door's flags (launch_door reads them from the environment once)
-constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames (HVWS_DOOR_WALK, default on)
-constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (HVWS_DOOR_NT)
-constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (HVWS_DOOR_PRELOAD)
+constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames ($HVWS_EXPERIMENT door_walk, default on)
+constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (door_nt)
+constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (door_preload)
+constexpr uint32_t DOOR_F_STAMPS = 8u;   // realtime stamps per phase (door_stamps; scripts/probe/door_phases.py)
+
+// A phase stamp (DOOR_F_STAMPS): each realtime-clock read is a scalar
+// memory round trip that the wave waits for, so stamps are off by default.
+__device__ __forceinline__ uint64_t door_now(uint32_t flags) {
+    return (flags & DOOR_F_STAMPS) ? (uint64_t)wall_clock64() : 0ull;
+}
 
 // Chunks [c_lo, c_hi) of the data area (both multiples of 64) into LDS at the
 // same offsets by LDS-DMA: no registers (an array of 16-byte values per
@@ -1152,7 +1159,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             cnt += f;
             q += f * stride;
         }
-        if (threadIdx.x == 0) stamps[0] = wall_clock64();
+        if (threadIdx.x == 0 && stamps) stamps[0] = wall_clock64();
         if (!cnt) break;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1202,7 +1209,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
         }
         if (best) st.mask = bkey;
         n += cnt;
-        if (threadIdx.x == 0) stamps[1] = wall_clock64();
+        if (threadIdx.x == 0 && stamps) stamps[1] = wall_clock64();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // s_fpos is rewritten by the next round
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1250,7 +1257,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             }
         }
     }
-    if (threadIdx.x == 0) stamps[2] = wall_clock64();
+    if (threadIdx.x == 0 && stamps) stamps[2] = wall_clock64();
 }
 
 __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__ req, ddoor* __restrict__ box,
@@ -1272,7 +1279,8 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     // request's own round trip, as many as the previous request had (up to one
     // per thread); the data area follows the request block in device memory.
     uint32_t guess = 0;
-    __shared__ uint64_t s_t[7], s_m[2];
+    __shared__ uint64_t s_t[7];
+    uint64_t rel_prev = 0;   // thread 0: realtime ticks of the previous request's release
     __shared__ uint64_t s_req[16];
     __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
     __shared__ uint64_t s_w[3];               // door_walk's stamps
@@ -1280,11 +1288,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         if (tid == 0) {
             uint64_t t0 = wall_clock64();
             uint64_t s;
-            uint32_t ex = 0;
+            uint32_t ex = 0, polls = 0;
             for (;;) {
                 s = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (s != last) break;
-                if (wall_clock64() - t0 > idle_ticks) {
+                // the clock every 32 polls: each read is a round trip the poll would wait for
+                if ((++polls & 31u) == 0 && wall_clock64() - t0 > idle_ticks) {
                     __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     __threadfence_system();
                     s = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1299,7 +1308,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             }
             s_exit = ex;
             s_seq = s;
-            s_t[0] = wall_clock64();
+            s_t[0] = door_now(flags);
             // The request fields were written before seq; the acquire also
             // invalidates this CU's L1 and the L2 for the data loaded next.
             if (!ex) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -1326,8 +1335,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             dcarry cin;
             memcpy(&cin, &q[4], sizeof(dcarry));
             s_carry = cin;
-            s_t[5] = wall_clock64();
-            s_m[0] = __builtin_amdgcn_s_memtime();
+            s_t[5] = door_now(flags);
         }
         __syncthreads();
         const uint64_t seq = s_seq;
@@ -1359,7 +1367,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 *reinterpret_cast<u32x4*>(dout + c * 16u) = *reinterpret_cast<const u32x4*>(lds + c * 16u) ^ k4;
         } else {
             __syncthreads();
-            if (tid == 0) s_t[1] = wall_clock64();
+            if (tid == 0) s_t[1] = door_now(flags);
             if (tid < 64) {   // wave 0: carried-in frame, walk, tail (k_small's code)
                 dcarry st = s_carry;
                 st.started = 0;
@@ -1406,9 +1414,9 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                         n = 1;
                     }
                 }
-                if (tid == 0) s_t[4] = wall_clock64();
+                if (tid == 0) s_t[4] = door_now(flags);
                 if (walk)
-                    door_walk(lds, L, st, pos, n, vmask, s_fpos, s_w, emit);
+                    door_walk(lds, L, st, pos, n, vmask, s_fpos, (flags & DOOR_F_STAMPS) ? s_w : nullptr, emit);
                 else
                     walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
                 if (tid == 0) {
@@ -1418,10 +1426,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             }
             __threadfence_block();
             __syncthreads();
-            if (tid == 0) {
-                s_t[2] = wall_clock64();
-                s_m[1] = __builtin_amdgcn_s_memtime();
-            }
+            if (tid == 0) s_t[2] = door_now(flags);
             const uint64_t n = s_n;
             // records [0, nl) sit in LDS, the rest in d_slot: separate loops,
             // so LDS records are read with ds loads (a select between the two
@@ -1469,48 +1474,54 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 for (uint64_t k = wave; k < nl; k += kDoorThreads / 64u) unmask_rec(lrec[k]);
                 for (uint64_t k = nl + wave; k < n; k += kDoorThreads / 64u) unmask_rec(d_slot[k]);
                 __syncthreads();
-                if (tid == 0) s_t[6] = wall_clock64();
+                if (tid == 0) s_t[6] = door_now(flags);
                 for (uint64_t c = (uint64_t)tid * 16u; c < L; c += (uint64_t)kDoorThreads * 16u)
                     *reinterpret_cast<u32x4*>(dout + c) = *reinterpret_cast<const u32x4*>(lds + c);
             } else if (tid == 0) {
                 s_t[6] = s_t[2];
             }
-            if (tid == 0) s_t[3] = wall_clock64();
+            if (tid == 0) s_t[3] = door_now(flags);
             for (uint64_t i = tid; i < nl; i += kDoorThreads) h_rec[i] = lrec[i];
             for (uint64_t i = nl + tid; i < n; i += kDoorThreads) h_rec[i] = d_slot[i];
             if (tid == 0) {
                 box->count = n;
                 box->out = s_carry;
                 box->served = ++served;
-                box->stamp[0] = s_t[0];
-                box->stamp[1] = s_t[1];
-                box->stamp[2] = s_t[2];
-                box->stamp[3] = s_t[3];
-                box->stamp[4] = wall_clock64();
-                box->stamp[5] = s_t[5];
-                box->stamp[6] = s_m[1] - s_m[0];   // shader clocks from the request read to the walk's end
-                box->stamp[7] = s_t[4];            // carried-in frame done, the walk starts
-                box->stamp[8] = s_w[0];
-                box->stamp[9] = s_w[1];
-                box->stamp[10] = s_w[2];
-                box->stamp[11] = s_t[6];           // the XOR's barrier: stores to dout start
+                if (flags & DOOR_F_STAMPS) {
+                    box->stamp[0] = s_t[0];
+                    box->stamp[1] = s_t[1];
+                    box->stamp[2] = s_t[2];
+                    box->stamp[3] = s_t[3];
+                    box->stamp[4] = wall_clock64();
+                    box->stamp[5] = s_t[5];
+                    box->stamp[6] = rel_prev;   // the previous request's release (its fence and barrier)
+                    box->stamp[7] = s_t[4];     // carried-in frame done, the walk starts
+                    box->stamp[8] = s_w[0];
+                    box->stamp[9] = s_w[1];
+                    box->stamp[10] = s_w[2];
+                    box->stamp[11] = s_t[6];    // the XOR's barrier: stores to dout start
+                }
             }
         }
         // every thread's stores reach host memory before `done` says so
+        const uint64_t tr = tid == 0 ? door_now(flags) : 0;
         __threadfence_system();
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(&box->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) {
+            rel_prev = door_now(flags) - tr;
+            __hip_atomic_store(&box->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         last = seq;
     }
 }
 
 hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
                        uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st) {
-    // $HVWS_DOOR_WALK=0: the speculative wave-wide walk (k_small's) instead of door_walk
-    auto knob = [](const char* name, uint32_t dflt) { return getenv(name) ? (uint32_t)atoi(getenv(name)) : dflt; };
-    static const uint32_t flags = (knob("HVWS_DOOR_WALK", 1) ? DOOR_F_WALK : 0u) |
-                                  (knob("HVWS_DOOR_NT", 0) ? DOOR_F_NT : 0u) |
-                                  (knob("HVWS_DOOR_PRELOAD", 0) ? DOOR_F_PRELOAD : 0u);
+    // $HVWS_EXPERIMENT door_walk=0: the speculative wave-wide walk (k_small's)
+    // instead of door_walk; door_nt, door_preload, door_stamps
+    auto knob = [](const char* name, uint32_t dflt) { return experiment(name) ? (uint32_t)atoi(experiment(name)) : dflt; };
+    static const uint32_t flags = (knob("door_walk", 1) ? DOOR_F_WALK : 0u) | (knob("door_nt", 0) ? DOOR_F_NT : 0u) |
+                                  (knob("door_preload", 0) ? DOOR_F_PRELOAD : 0u) | (knob("door_stamps", 0) ? DOOR_F_STAMPS : 0u);
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
                        idle_ticks, first_seq, epoch, flags);
     return hipGetLastError();

@@ -11,6 +11,8 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the worker writes its phase stamps only when asked ($HVWS_EXPERIMENT door_stamps=1)
+os.environ["HVWS_EXPERIMENT"] = ",".join(x for x in (os.environ.get("HVWS_EXPERIMENT", ""), "door_stamps=1") if x)
 sys.path.insert(0, ROOT)
 import libhv_amd  # noqa: E402
 from libhv_amd import synth  # noqa: E402
@@ -59,11 +61,11 @@ if busy:
     stop.append(1)
     th.join()
 rows = np.array(rows[n // 10:], dtype=np.float64)
-t0, t1, t2, t3, t4, t5, clk, tw, tc, tp, tt, tx = (rows[:, i] for i in range(12))
+t0, t1, t2, t3, t4, t5, rel, tw, tc, tp, tt, tx = (rows[:, i] for i in range(12))
 us = lambda a, b: round(float(np.median((b - a) * 0.01)), 2)   # noqa: E731  (ticks of 10 ns)
 info = (ctypes.c_uint64 * 2)()
 L.hvws_door_info(None, info)
-out = {"reads": n, "busy_chip": busy, "request_in_device_memory": bool(info[0]), "door_walk": os.environ.get("HVWS_DOOR_WALK", "1"), "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
+out = {"reads": n, "busy_chip": busy, "request_in_device_memory": bool(info[0]), "experiment": os.environ.get("HVWS_EXPERIMENT", ""), "host_us_per_call_median": round(float(np.median(wall[n // 10:])) * 1e6, 2),
        "device_us_median": {"request_read": us(t0, t5), "stage": us(t5, t1), "carried_in_frame": us(t1, tw),
                             "walk": us(tw, t2),
                             "walk_parts": {"chase": us(tw, tc), "parse": us(tc, tp), "tail": us(tp, tt),
@@ -71,6 +73,6 @@ out = {"reads": n, "busy_chip": busy, "request_in_device_memory": bool(info[0]),
                             "xor_and_stores": us(t2, t3), "xor_parts": {"xor": us(t2, tx), "stores": us(tx, t3)},
                             "records": us(t3, t4)},
        "device_us_total_median": us(t0, t4),
-       "shader_clock_MHz_median": round(float(np.median(clk / ((t2 - t5) * 0.01))), 1)}
+       "release_us_median": round(float(np.median(rel * 0.01)), 2)}   # the previous request's fence + barrier
 print(json.dumps(out))
 L.hvws_wsp_free(h)
