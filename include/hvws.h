@@ -227,8 +227,8 @@ int hvws_last_sieve(hvws_ctx* ctx, uint64_t out[4]);
  * mean from the context's last exact count of a one-segment scan); the chain's
  * link walks cross the rest of each region frame by frame, so the sieve reads
  * window / region of the bytes instead of all of them.  hops = 0 sieves every
- * position (the round-2 behaviour).  Process-wide tuning (default 256 and
- * 1 MiB + 16 KiB; $HVWS_SIEVE_HOPS, $HVWS_SIEVE_WINDOW; window 0 = default);
+ * position (the round-2 behaviour).  Process-wide tuning (default 320 and
+ * 1 MiB + 16 KiB; $HVWS_EXPERIMENT sieve_hops, sieve_window; window 0 = default);
  * results never depend on it.  prev (may be NULL) receives the old values. */
 void hvws_set_sieve_windows(uint64_t hops, uint64_t window_bytes, uint64_t prev[2]);
 

@@ -15,7 +15,8 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhvws.so")
+# $HVWS_LIB: another build of the library, for A/B runs on one box
+LIB_PATH = os.environ.get("HVWS_LIB") or os.path.join(_HERE, "libhvws.so")
 
 # enum websocket_flags (include/websocket_parser.h; reference http/websocket_parser.h:30-45)
 WS_OP_CONTINUE, WS_OP_TEXT, WS_OP_BINARY = 0x0, 0x1, 0x2

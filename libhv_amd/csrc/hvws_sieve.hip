@@ -60,6 +60,13 @@ constexpr uint32_t SV_SLOT = 16;                       // survivors kept per til
 constexpr int SV_DEPTH = 3;                            // hops a survivor's chain must stay plausible
 constexpr uint32_t SV_TERM = 0xFFFFFFFFu;
 constexpr uint32_t SV_GRID = 4096;
+// k_sieve_count's grid when windows are on (~37 000 tiles at c4): its
+// workgroups run beside the unmask at high priority, and 4096 of them held
+// the device -- the unmask pieces beside them ran at ~40 %.  c4 as one stream,
+// ms per step by grid (sieve_hops 256): 4096 1.52, 2048 1.519, 1024 1.506,
+// 512 1.58 (the chain then bounds the step), 256 1.727; with 320 frames per
+// region 1024 1.488-1.496, 1280 1.494 (profiles/r5_raw/pieces, sg*/sgh*).
+constexpr uint32_t SV_GRID_WINDOWS = 1024;
 constexpr uint32_t SV_HOP_CAP = 4096;                  // frames one link walk may cross
 
 // Tiles of the segment that are sieved (the first wt of every rt of the NT
@@ -750,12 +757,14 @@ uint64_t set_sieve_min(uint64_t v) {
 
 uint64_t sieve_generation() { return g_sieve_gen; }
 
-// Windows: regions of about $HVWS_EXPERIMENT sieve_hops (default 256) mean-sized frames,
+// Windows: regions of about $HVWS_EXPERIMENT sieve_hops (default 320) mean-sized frames,
 // each sieved over its first $HVWS_EXPERIMENT sieve_window bytes (default 1 MiB + 16 KiB:
 // past the largest frame of config 4, so a walk entering a region almost
 // always lands on a survivor of its window).  Regions shorter than two
 // windows, or no count yet: every tile.  Results never depend on it.
-constexpr uint64_t SIEVE_HOPS_DEFAULT = 256, SIEVE_WINDOW_DEFAULT = (1 << 20) + (16 << 10);
+// 320: with the count grid of SV_GRID_WINDOWS and the faster link hops (ld16),
+// c4 as one stream 1.488-1.496 ms per step against 1.51 at 256 (r5zs, r5zt).
+constexpr uint64_t SIEVE_HOPS_DEFAULT = 320, SIEVE_WINDOW_DEFAULT = (1 << 20) + (16 << 10);
 static uint64_t g_sv_hops = ~0ull, g_sv_win = 0;   // ~0 / 0: not yet read from the environment
 
 static void sieve_windows_init() {
@@ -807,7 +816,9 @@ static uint32_t jump_rounds(uint64_t capS) {
 hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, const dmid* mid, const uint64_t* npred,
                         const sieve_bufs& b, hipStream_t st) {
     const uint64_t ntm = sieve_tiles_max(rx_len);
-    const uint32_t grid = (uint32_t)(ntm < SV_GRID ? ntm : SV_GRID);
+    static const uint32_t grid_env = experiment("sieve_grid") ? (uint32_t)atoi(experiment("sieve_grid")) : 0u;
+    const uint32_t grid_cap = grid_env ? grid_env : (b.rt != b.wt ? SV_GRID_WINDOWS : SV_GRID);
+    const uint32_t grid = (uint32_t)(ntm < grid_cap ? ntm : grid_cap);
     dsieve* sv = reinterpret_cast<dsieve*>(b.state);
     hipError_t e = hipMemsetAsync(b.pool_n, 0, 8, st);
     if (e != hipSuccess) return e;
