@@ -1108,10 +1108,13 @@ __device__ __forceinline__ uint64_t door_now(uint32_t flags) {
 // thread cost the worker ~1000 register moves, ~2 us per read); a wave
 // writes 64 consecutive chunks per instruction (lane-linear destination).
 // The caller waits for vmcnt(0) before a barrier.
+// w0: the first wave that stages (the preload leaves wave 0 to the request
+// block: its request load would otherwise wait behind these in vmcnt order).
 __device__ __forceinline__ void door_stage(const uint8_t* din, uint8_t* lds, uint32_t c_lo, uint32_t c_hi,
-                                           uint32_t flags) {
+                                           uint32_t flags, uint32_t w0 = 0) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    for (uint32_t cb = c_lo + wave * 64u; cb < c_hi; cb += kDoorThreads) {
+    if (wave < w0) return;
+    for (uint32_t cb = c_lo + (wave - w0) * 64u; cb < c_hi; cb += kDoorThreads - 64u * w0) {
         const auto* g = (const __attribute__((address_space(1))) void*)(din + (uint64_t)(cb + lane) * 16u);
         auto* l = (__attribute__((address_space(3))) void*)(lds + (uint64_t)cb * 16u);
         if (flags & DOOR_F_NT)
@@ -1275,9 +1278,9 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     uint64_t last = first_seq;
     uint64_t served = 0;
     const uint32_t walk = flags & DOOR_F_WALK;
-    // DOOR_F_PRELOAD: the first chunks of the data area are loaded in the
-    // request's own round trip, as many as the previous request had (up to one
-    // per thread); the data area follows the request block in device memory.
+    // DOOR_F_PRELOAD: waves 1-3 load the data area's first chunks in the
+    // request's own round trip, as many as the previous request had (wave 0
+    // reads the request block); the data area follows it in device memory.
     uint32_t guess = 0;
     __shared__ uint64_t s_t[7];
     uint64_t rel_prev = 0;   // thread 0: realtime ticks of the previous request's release
@@ -1318,7 +1321,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             if (tid == 0) __hip_atomic_store(&box->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        if (guess) door_stage(din, lds, 0, guess, flags);   // beside the request's own load
+        if (guess) door_stage(din, lds, 0, guess, flags, 1);   // waves 1-3, beside the request's own load
         if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
             const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(req) + tid);
             reinterpret_cast<u32x4*>(s_req)[tid] = piece;
@@ -1355,7 +1358,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         const uint32_t ngr = (uint32_t)((nch + 63u) & ~63ull);   // whole wave groups of 64 chunks (<= kDoorMax)
         // the rest of the data area into LDS (all in flight), then wait
         door_stage(din, lds, guess, ngr, flags);
-        if (flags & DOOR_F_PRELOAD) guess = ngr < kDoorThreads ? ngr : kDoorThreads;
+        if (flags & DOOR_F_PRELOAD) guess = ngr;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (op == DOOR_XOR) {
             // websocket_decode over the data area (16-byte aligned): byte i
