@@ -894,6 +894,14 @@ def main():
     # markers on the context's streams (hvws_span_*); across devices: the
     # host's CLOCK_MONOTONIC (time.perf_counter), common to all ranks of the
     # node -- value = all payload / (latest end - earliest start).
+    # Kernel times come from HIP events on sampled steps of the timed region:
+    # each event-carrying step costs device time between kernels (~15 us of a
+    # 0.38 ms config-2 step, profiles/r5_raw/events), so long runs carry them
+    # on every 8th step only (hvws_set_step_event_interval); all launches of a
+    # run are the same work.
+    ev_every = 8 if args.steps >= 32 else 1
+    if lagged is None:
+        eng.set_step_event_interval(ev_every)
     t0 = time.perf_counter()
     span_ms = ctypes.c_float(0)
     if lagged is None:
@@ -916,10 +924,14 @@ def main():
     check_distinct_devices([bus_name(int(b)) for b in trows[:, 5]], rank)
     scan_path = L.hvws_last_scan_path(eng.ctx if lagged is None else lagged.context(0))
     times = eng.step_times(min(args.steps, 32)) if lagged is None else lagged.step_times(min(args.steps, 16))
-    if lagged is not None:
+    if lagged is None:
+        eng.set_step_event_interval(1)
+    else:
         lagged.close()
     scan_ms = [t[0] for t in times]
-    unmask_ms = [t[1] for t in times]
+    unmask_ms = [t[1] for t in times if t[1] >= 0]   # the sampled steps
+    if not unmask_ms:
+        raise SystemExit(f"rank {rank}: no unmask timing events in the last {len(times)} steps")
 
     # The same number of steps through the other step call, for the record
     # (pipelined vs serial); an even count keeps the parity of passes.
@@ -1039,6 +1051,9 @@ def main():
             extra["stream_sweep_GBps"] = {n: round(2 * (plan.total & ~15) / float(np.median(t)) / 1e9, 1)
                                           for n, t in stimes.items()}
         extra["unmask_ms_mean"] = round(mean_unmask, 3)
+        extra["unmask_events"] = ((f"HIP events on every {ev_every}th timed step" if ev_every > 1 else
+                                   "HIP events on every timed step") +
+                                  f" ({len(unmask_ms)} sampled of the last {len(times)})")
 
         # event loop, before the legs that allocate and
         # free large buffers: host-side rates measured after them ran slower

@@ -160,6 +160,12 @@ int hvws_last_times(hvws_ctx* ctx, float out[2]);
  * Waits for those steps only; returns the number of steps written (< 0 on
  * error).  Lets a caller time a run of asynchronous steps afterwards. */
 int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
+/* Record those timing events on every `every`-th scan only (1, the default:
+ * every scan; 0: none).  Each event-carrying step costs device time between
+ * kernels -- ~15 us of a 0.38 ms pipelined config-2 step -- so a caller that
+ * times a long run samples it (bench.py: every 8th step); unsampled steps
+ * read -1.  Returns the previous interval (< 0 on error). */
+int hvws_set_step_event_interval(hvws_ctx* ctx, uint32_t every);
 
 /* Lagged steps: two scan chains in flight.  A lagged
  * stepper runs consecutive hvws_step_resident steps on two contexts of one

@@ -124,6 +124,7 @@ _SIGS = {
     "hvws_get_carry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "hvws_last_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "hvws_step_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    "hvws_set_step_event_interval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     "hvws_set_speculation": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_set_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hvws_last_run_repairs": (ctypes.c_int64, [ctypes.c_void_p]),
@@ -410,6 +411,13 @@ class Engine:
         if n < 0:
             _check(n, "hvws_step_times")
         return [(float(out[2 * i]), float(out[2 * i + 1])) for i in range(n)]
+
+    def set_step_event_interval(self, every: int) -> int:
+        """Timing events on every `every`-th step only (hvws_set_step_event_interval); returns the old interval."""
+        r = lib().hvws_set_step_event_interval(self.ctx, every)
+        if r < 0:
+            _check(r, "hvws_set_step_event_interval")
+        return r
 
     def lagged(self) -> "Lagged":
         """A lagged stepper on this engine's device (hvws_lagged_*)."""

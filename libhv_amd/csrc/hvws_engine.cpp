@@ -275,6 +275,8 @@ struct hvws_ctx {
     uint8_t t_rec[kTimeRing] = {};      // which of the slot's 4 events were recorded (bit i)
     uint64_t t_seq = 0;   // scans recorded so far
     int t_cur = 0;        // ring slot of the last scan
+    uint32_t t_every = 1; // hvws_set_step_event_interval: events on every t_every-th scan (0: none)
+    bool t_on = true;     // the current scan is one of them
     // resident small-path worker (k_door): its own stream (a dedicated
     // hardware queue, so the resident kernel never holds up other work), the
     // mailbox, the data and record areas (fine-grained pinned) and a device
@@ -422,7 +424,7 @@ int step_events(const hvws_ctx* c) {
 // end) of the current ring slot if this mode keeps it.
 hipError_t tev_record(hvws_ctx* c, int i, hipStream_t st) {
     const int m = step_events(c);
-    if (m <= 0 || (m == 1 && i < 2)) return hipSuccess;
+    if (!c->t_on || m <= 0 || (m == 1 && i < 2)) return hipSuccess;
     c->t_rec[c->t_cur] |= (uint8_t)(1u << i);
     return hipEventRecord(c->tev[c->t_cur][i], st);
 }
@@ -433,6 +435,7 @@ hipError_t begin_timed_scan(hvws_ctx* c, bool record = true) {
     c->t_cur = (int)(c->t_seq % hvws_ctx::kTimeRing);
     c->t_unmask[c->t_cur] = false;
     c->t_rec[c->t_cur] = 0;
+    c->t_on = c->t_every != 0 && c->t_seq % c->t_every == 0;
     ++c->t_seq;
     return record ? tev_record(c, 0, c->cs) : hipSuccess;
 }
@@ -630,7 +633,7 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
         if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(c->stream, c->scan_done, 0)) != hipSuccess) return e;
     }
-    const bool timed = step_events(c) >= 1;
+    const bool timed = step_events(c) >= 1 && c->t_on;
     // Pipelined steps of mixed multi-segment batches: the unmask in pieces.
     // The hardware dispatches a kernel queued on the second stream (the next
     // batch's discovery) only once the unmask grid is fully launched, so its
@@ -1362,7 +1365,7 @@ int rx_batch_small(hvws_ctx* c, uint8_t* h_rx, uint64_t len, const hvws_segment*
     // No timing events unless $HVWS_EXPERIMENT step_events >= 2 asks for them: an
     // event-carrying launch costs a per-read call ~10 us of ~38 (r2an).
     static const bool timed_env = experiment("step_events") && atoi(experiment("step_events")) >= 2;
-    const bool timed = timed_env;
+    const bool timed = timed_env && c->t_on;
     // Completion: each wave releases its stores to system scope and then
     // writes its segment's word with this call's sequence number; the host
     // polls the words (in segment order) instead of waiting for the stream,
@@ -2646,6 +2649,14 @@ int hvws_span_end(hvws_ctx* c, float* ms) {
         }
     *ms = best;
     return HVWS_OK;
+}
+
+int hvws_set_step_event_interval(hvws_ctx* c, uint32_t every) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    const int old = (int)c->t_every;
+    c->t_every = every;
+    return old;
 }
 
 int hvws_step_times(hvws_ctx* c, float* out, int max_steps) {

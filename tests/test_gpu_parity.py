@@ -596,6 +596,31 @@ def test_pipelined_steps_back_to_back(eng):
             assert cout[k].fields() == exp_carry[k].fields(), k
 
 
+def test_step_event_interval(eng):
+    """hvws_set_step_event_interval: pipelined steps carry their timing events
+    on every n-th scan only (unsampled steps read -1; 0 = none), and the bytes
+    do not depend on it (12 passes: the batch is masked again)."""
+    rng = random.Random(77)
+    buf, segs, carries = _cut_uniform(rng, 3000, 1024, 16)
+    d = eng.to_device(buf)
+    try:
+        for every, want in ((3, 4), (0, 0), (1, 12)):
+            assert eng.set_step_event_interval(every) >= 0
+            for _ in range(12):
+                eng.step_resident(d, len(buf), segs, carries)
+            eng.sync()
+            times = eng.step_times(12)
+            got = [i for i, (_, u) in enumerate(times) if u >= 0]
+            assert len(times) == 12 and len(got) == want, (every, times)
+            assert all(times[i][1] > 0 for i in got)
+            if every > 1:
+                assert all(b - a == every for a, b in zip(got, got[1:])), got
+            assert np.array_equal(d.download(len(buf)), buf), every
+    finally:
+        eng.set_step_event_interval(1)
+        d.free()
+
+
 def _piped_after_stall(eng, learn, target, spec_learn, spec_target, bound=1, stall_us=150_000):
     """Pipelined step of `learn`, then a host stall on the context stream (a
     stand-in for a long previous unmask: everything queued there after it
