@@ -6,9 +6,10 @@ against the library's host ws_encode_key.  CPU baseline: the reference
 ws_encode_key (oracle/_ref, one core) over a bounded sample.
 
 The kernel is integer-VALU-bound (two SHA-1 blocks + base64 per key); its
-VALU instruction count per launch comes from the rocprofv3 SQ_INSTS_VALU pass
-(scripts/measure_*.sh) and is reported against the gfx950 issue peak by
-DESIGN.md, not here.  Prints one JSON line.
+VALU instruction count per launch comes from a separate rocprofv3 pass
+(`--pmc SQ_INSTS_VALU ... --kernel-include-regex k_encode_keys -- python
+scripts/bench_keys.py`, profiles/r5_raw/keys/) and is reported against the
+gfx950 issue peak by DESIGN.md, not here.  Prints one JSON line.
 """
 from __future__ import annotations
 
