@@ -1096,6 +1096,13 @@ constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames ($HVWS_E
 constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (door_nt)
 constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (door_preload)
 constexpr uint32_t DOOR_F_STAMPS = 8u;   // realtime stamps per phase (door_stamps; scripts/probe/door_phases.py)
+// DOOR_XOR (a masked websocket_build_frame payload, websocket_decode) in
+// registers, its result written through the L2 (sc0 sc1), and `done` after
+// those stores' acks: no LDS staging, no barrier between the two, no L2
+// writeback.  A masked 125 B build: 3.41-3.46 us per call against 4.49-4.90
+// (profiles/r5_raw/door, r5x2).  $HVWS_EXPERIMENT door_xor_direct=0: the LDS path.
+// (For a read's ~500 result stores the same trade lost: 13-14 us per call.)
+constexpr uint32_t DOOR_F_XDIRECT = 16u;
 
 // A phase stamp (DOOR_F_STAMPS): each realtime-clock read is a scalar
 // memory round trip that the wave waits for, so stamps are off by default.
@@ -1356,11 +1363,22 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         const uint64_t L = s_len;
         const uint64_t nch = (L + 15u) / 16u;   // the data area has slack past L: whole chunks throughout
         const uint32_t ngr = (uint32_t)((nch + 63u) & ~63ull);   // whole wave groups of 64 chunks (<= kDoorMax)
+        const bool xdirect = op == DOOR_XOR && (flags & DOOR_F_XDIRECT);
+        if (xdirect) {
+            const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
+            const u32x4 k4 = u32x4{kw, kw, kw, kw};
+            for (uint64_t c = tid; c < nch; c += kDoorThreads) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(din + c * 16u) ^ k4;
+                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dout + c * 16u), "v"(v) : "memory");
+            }
+        } else {
         // the rest of the data area into LDS (all in flight), then wait
         door_stage(din, lds, guess, ngr, flags);
         if (flags & DOOR_F_PRELOAD) guess = ngr;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (op == DOOR_XOR) {
+        }
+        if (xdirect) {
+        } else if (op == DOOR_XOR) {
             // websocket_decode over the data area (16-byte aligned): byte i
             // uses mask[(i + phase) & 3]
             __syncthreads();
@@ -1508,7 +1526,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         }
         // every thread's stores reach host memory before `done` says so
         const uint64_t tr = tid == 0 ? door_now(flags) : 0;
-        __threadfence_system();
+        if (xdirect)   // its only results were written through the L2: their acks suffice
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else
+            __threadfence_system();
         __syncthreads();
         if (tid == 0) {
             rel_prev = door_now(flags) - tr;
@@ -1524,7 +1545,8 @@ hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t
     // instead of door_walk; door_nt, door_preload, door_stamps
     auto knob = [](const char* name, uint32_t dflt) { return experiment(name) ? (uint32_t)atoi(experiment(name)) : dflt; };
     static const uint32_t flags = (knob("door_walk", 1) ? DOOR_F_WALK : 0u) | (knob("door_nt", 0) ? DOOR_F_NT : 0u) |
-                                  (knob("door_preload", 0) ? DOOR_F_PRELOAD : 0u) | (knob("door_stamps", 0) ? DOOR_F_STAMPS : 0u);
+                                  (knob("door_preload", 0) ? DOOR_F_PRELOAD : 0u) | (knob("door_stamps", 0) ? DOOR_F_STAMPS : 0u) |
+                                  (knob("door_xor_direct", 1) ? DOOR_F_XDIRECT : 0u);
     hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
                        idle_ticks, first_seq, epoch, flags);
     return hipGetLastError();
