@@ -2,12 +2,13 @@
 //
 // hvws_step_resident waits in the host for its own scan's verdict before it
 // returns, so only one scan chain is ever in flight beside one unmask and a
-// step takes max(chain, unmask).  For one long connection of mixed frame
-// sizes (config 4 as one stream) the chain -- the frame sieve's link walks,
-// ~3 us per hop under the unmask's load -- is the longer one (DESIGN.md sec.
-// 4.3).  A lagged stepper runs consecutive steps on two contexts of the same
-// device from two worker threads: step k's scan is issued while step k-1's
-// is still running, so each chain has two unmask periods.  Unmasks stay in
+// step takes max(chain, unmask).  A lagged stepper runs consecutive steps on
+// two contexts of the same device from two worker threads, so two chains can
+// be in flight.  Measured for config 4 as one stream (DESIGN.md sec. 9.1,
+// profiles/r5_raw/lagged): 1.70-1.78 ms per step against 1.58 resident --
+// the resident chain already fits beside the unmask, each context's chain
+// runs beside its own context's unmask only, and the second chain's link
+// walks slow the unmask -- so this stays an opt-in API.  Unmasks stay in
 // step order: before its first unmask is queued, step k waits in the host
 // until step k-1 has queued all of its own, and its context's stream waits
 // on the event recorded behind them.  The batch passed to hvws_lagged_step is
