@@ -1133,6 +1133,10 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": alg_bytes,
+                # boxes differ (in-place ceilings 5.4-6.6 TB/s across the pool): the
+                # same kernel against this box's own STREAM-style ceiling, same buffer
+                "frac_of_box_ceiling": (round(achieved / extra["stream_ceiling_GBps"], 4)
+                                        if extra.get("stream_ceiling_GBps") else None),
             },
             "cpu_baseline": cpu,
         }
