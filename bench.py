@@ -22,6 +22,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -487,6 +488,22 @@ def dropin_leg(eng, device: int, seed: int, reads: int = 2000, builds: int = 400
                 "connection) and masked websocket_build_frame of 125 B, per call, timed in C; median of "
                 f"{passes} interleaved passes",
     }
+
+
+def dropin_leg_child(device: int, seed: int, reads: int) -> dict:
+    """dropin_leg in a child process of its own (scripts/bench_dropin.py), as a
+    libhv server process would call the drop-in: in this process -- after the
+    workload legs, with torch and the rank's other contexts loaded -- the same
+    calls measured ~0.7 us slower each (builds 4.1-4.2 vs 3.4-3.8 us on one
+    box, profiles/r5_raw/door).  A child is started, not exec'd."""
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "bench_dropin.py"), str(reads), str(device), str(seed)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        raise SystemExit(f"drop-in leg: child exited {r.returncode}: {r.stderr[-2000:]}")
+    res = json.loads(lines[-1])
+    res["process"] = "a child process of its own (scripts/bench_dropin.py), like a libhv server process"
+    return res
 
 
 def cpu_event_loop(streams: np.ndarray, iters: int, pay: float):
@@ -1061,7 +1078,7 @@ def main():
             extra["event_loop"], feed_streams, feed_pay = event_loop_leg(eng, device, args.feed_conns,
                                                                          args.feed_iters, plan.seed + 7)
         if args.dropin_reads > 0:
-            extra["drop_in"] = dropin_leg(eng, device, plan.seed + 11, args.dropin_reads)
+            extra["drop_in"] = dropin_leg_child(device, plan.seed + 11, args.dropin_reads)
 
     rx_plain = passes % 2 == 1   # payloads currently unmasked
     # host-inclusive: pinned host rx -> device -> scan+unmask -> host, every
