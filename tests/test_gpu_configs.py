@@ -100,12 +100,14 @@ def test_config5_rank_batches(eng, rank):
     _run(eng, synth.config_plan("c3", seed=1000 + rank), 4096, GOLD[f"c5_rank{rank}"])
 
 
-@pytest.mark.parametrize("nseg", [1, 1024])
+@pytest.mark.parametrize("nseg", [1, 1024, 4096])
 def test_config4_mixed(eng, nseg):
-    """One stream: the frame sieve discovers all 74 701 frames; 1024
-    connections: the second step takes the SLACK table (one walk)."""
+    """One stream: the frame sieve discovers all 74 701 frames; 1024 and 4096
+    connections (4096: bench.py's default): the second step takes the SLACK
+    table, whose walk then runs several segments per wave (the grid cap of a
+    SLACK scan, hvws_engine.cpp)."""
     _run(eng, synth.config_plan("c4", seed=1), nseg, GOLD["c4"], sieve=nseg == 1,
-         path2=5 if nseg == 1024 else None)
+         path2=5 if nseg > 1 else None)
 
 
 def test_config1_through_websocketparser_8k_chunks():
