@@ -2219,13 +2219,11 @@ __device__ __forceinline__ void tile_run(dtrun& o, const drun& r, bool ok, uint6
 // is -- by the repair itself -- a segment whose run it does not take
 // (run_fast_ok).  The key of s0's run frame begun before the tile is read
 // here, beside the previous unmask, not on the unmask's critical path.
-__global__ __launch_bounds__(256) void k_run_tiles(const uint8_t* __restrict__ rx, uint64_t rx_len,
-                                                   const dseg* __restrict__ segs, uint32_t nseg,
-                                                   const drun* __restrict__ runs, dtrun* __restrict__ trun,
-                                                   uint64_t ntiles, uint64_t tile, uint32_t* __restrict__ fail) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (s >= nseg) return;
+__device__ __forceinline__ void run_tiles_seg(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                              const dseg* __restrict__ segs, uint32_t nseg,
+                                              const drun* __restrict__ runs, dtrun* __restrict__ trun,
+                                              uint64_t ntiles, uint64_t tile, uint32_t* __restrict__ fail,
+                                              uint32_t s, uint32_t lane) {
     const uint64_t e0 = s ? segs[s - 1].off + segs[s - 1].len : 0;
     const uint64_t e1 = segs[s].off + segs[s].len;
     const uint64_t ta = (e0 + tile - 1) / tile, tb = (e1 + tile - 1) / tile;
@@ -2265,6 +2263,15 @@ __global__ __launch_bounds__(256) void k_run_tiles(const uint8_t* __restrict__ r
         if (exact) atomicOr(&fail[nseg], 1u);   // the repair pass must look
         trun[t] = o;
     }
+}
+
+__global__ __launch_bounds__(256) void k_run_tiles(const uint8_t* __restrict__ rx, uint64_t rx_len,
+                                                   const dseg* __restrict__ segs, uint32_t nseg,
+                                                   const drun* __restrict__ runs, dtrun* __restrict__ trun,
+                                                   uint64_t ntiles, uint64_t tile, uint32_t* __restrict__ fail) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < nseg; s += gridDim.x * (blockDim.x >> 6))
+        run_tiles_seg(rx, rx_len, segs, nseg, runs, trun, ntiles, tile, fail, s, lane);
 }
 
 // The run hypothesis' header bytes 1 .. 1 + ext (MASK bit + 7-bit length,
@@ -2671,6 +2678,19 @@ __global__ void k_xor_span(uint8_t* __restrict__ d, uint64_t n, uint32_t key, ui
 
 // --------------------------------------------------------------- launchers
 
+// A RUN scan's k_head and k_run_tiles grids at most this many blocks (512
+// waves, each taking segments in turn; $HVWS_EXPERIMENT run_scan_grid, 0: one
+// wave per segment).  They run beside the previous step's unmask at high
+// priority, and one wave per segment (1024 blocks at c2) slowed the unmask
+// piece beside them: c2 ms per step by cap, none 0.367-0.369, 512 0.367,
+// 256 0.363, 128 0.357-0.358, 64 0.357 (profiles/r5_raw/events, rg_*).  A RUN
+// segment holds >= 64 KiB (RUN_MIN_SEG), so 512 waves still scan segments
+// faster than the unmask consumes them.
+static uint32_t run_scan_grid() {
+    static const uint32_t v = experiment("run_scan_grid") ? (uint32_t)atoi(experiment("run_scan_grid")) : 128u;
+    return v;
+}
+
 static uint32_t wave_blocks(uint32_t nseg) {
     const uint32_t wpb = SCAN_THREADS / 64;
     uint32_t blocks = (nseg + wpb - 1) / wpb;
@@ -2766,7 +2786,9 @@ hipError_t launch_scan(int pass, const uint8_t* rx, uint64_t rx_len, const dseg*
             hipLaunchKernelGGL(k_spec_check<false>, dim3(1), dim3(ONE_BLOCK), 0, st, counts, sc.est, sc.npred, nseg, total,
                                fr.cap, sc.status, sc.seq);
     } else if (pass == SCAN_RUN) {
-        hipLaunchKernelGGL(k_head<false>, dim3(wb), dim3(SCAN_THREADS), 0, st, rx, rx_len, segs, nseg, carry_in,
+        const uint32_t rcap = run_scan_grid();
+        hipLaunchKernelGGL(k_head<false>, dim3(rcap && rcap < wb ? rcap : wb), dim3(SCAN_THREADS), 0, st, rx, rx_len,
+                           segs, nseg, carry_in,
                            sc.mid, sc.npred, sc.first_fail, sc.last_masked, bases, fr, vmask, spec_min(),
                            (uint64_t*)nullptr, sc.src_segs, sc.src_carry, sc.segs_w, sc.carry_w, 0, (uint64_t)0,
                            (uint64_t*)nullptr, HEAD_ZERO_LM | HEAD_NO_VERIFY, sc.runs, sc.run_fail);
@@ -2985,7 +3007,9 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
 
 hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg, const drun* runs,
                             dtrun* trun, uint64_t ntiles, uint64_t tile, uint32_t* fail, hipStream_t st) {
-    const uint32_t nb = (nseg + 3) / 4;   // one wave per segment
+    const uint32_t rcap = run_scan_grid();
+    const uint32_t nb1 = (nseg + 3) / 4;   // one wave per segment
+    const uint32_t nb = rcap && rcap < nb1 ? rcap : nb1;
     if (nb && ntiles) hipLaunchKernelGGL(k_run_tiles, dim3(nb), dim3(256), 0, st, rx, rx_len, segs, nseg, runs, trun,
                                          ntiles, tile, fail);
     return hipGetLastError();
