@@ -652,11 +652,18 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok) ||   // an exact scan that saw mixed counts
                        (path == HVWS_PATH_SINGLE && c->sv_ran);                 // a sieved stream
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
+    // An untimed pipelined RUN step attaches its set's free event to the
+    // repair's dispatch instead of recording it in a marker packet after it:
+    // c2 0.355-0.356 vs 0.358 ms per step (profiles/r5_raw/events, fa*).
+    // $HVWS_EXPERIMENT free_attach=0: the marker.
+    static const bool free_attach = !(experiment("free_attach") && atoi(experiment("free_attach")) == 0);
+    const bool attach_free = c->run_active && piped && !timed && free_attach;
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
         if ((e = launch_unmask_run(c->run_g, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
                                    c->run_seq, c->stream, timed ? c->tev[c->t_cur][2] : nullptr,
-                                   timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess)
+                                   timed ? c->tev[c->t_cur][3] : (attach_free ? c->T().free_ev : nullptr))) !=
+            hipSuccess)
             return e;
     } else if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
                                   c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(),
@@ -672,6 +679,8 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
         // pipelined c2 step (0.4215 -> 0.416 ms, profiles/r2r_raw).
         if (timed) {
             c->T().free_wait = c->tev[c->t_cur][3];
+        } else if (attach_free) {   // recorded by the repair's dispatch
+            c->T().free_wait = c->T().free_ev;
         } else {
             if ((e = hipEventRecord(c->T().free_ev, c->stream)) != hipSuccess) return e;
             c->T().free_wait = c->T().free_ev;
