@@ -652,12 +652,12 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
                        (path == HVWS_PATH_COUNT_READ_EMIT && !c->spec_ok) ||   // an exact scan that saw mixed counts
                        (path == HVWS_PATH_SINGLE && c->sv_ran);                 // a sieved stream
     const uint32_t pieces = !piped ? 1u : env_pieces > 0 ? (uint32_t)env_pieces : (mixed ? 8u : 1u);
-    // An untimed pipelined RUN step attaches its set's free event to the
-    // repair's dispatch instead of recording it in a marker packet after it:
+    // An untimed pipelined step attaches its set's free event to its last
+    // dispatch (RUN: the repair) instead of recording it in a marker packet after it:
     // c2 0.355-0.356 vs 0.358 ms per step (profiles/r5_raw/events, fa*).
     // $HVWS_EXPERIMENT free_attach=0: the marker.
     static const bool free_attach = !(experiment("free_attach") && atoi(experiment("free_attach")) == 0);
-    const bool attach_free = c->run_active && piped && !timed && free_attach;
+    const bool attach_free = piped && !timed && free_attach;
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
         if ((e = launch_unmask_run(c->run_g, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
@@ -668,7 +668,8 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
     } else if ((e = launch_unmask(c->variant, d_rx, rx_len, frames_of(c), c->T().tile_first.as<uint32_t>(),
                                   c->T().tile_key.as<uint32_t>(), c->T().tile_kind.as<uint8_t>(),
                                   c->T().total.as<uint64_t>(), c->stream, pieces, timed ? c->tev[c->t_cur][2] : nullptr,
-                                  timed ? c->tev[c->t_cur][3] : nullptr)) != hipSuccess) {
+                                  timed ? c->tev[c->t_cur][3] : (attach_free ? c->T().free_ev : nullptr))) !=
+               hipSuccess) {
         return e;
     }
     if (timed) c->t_rec[c->t_cur] |= (uint8_t)(4u | 8u);
