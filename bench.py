@@ -597,11 +597,18 @@ def init_dist():
     return rank, world, local, dist
 
 
+def rank_seed(cfg: str, rank: int) -> int:
+    """This rank's batch seed: c3 ranks take config 5's shards (seed 1000 + r,
+    fixtures c5_rank<r>); c1 / c2 / c4 ranks take seed 1 + r, so rank 0's batch
+    is the one tests/golden/configs.json holds the reference digests of."""
+    return 1000 + rank if cfg == "c3" else 1 + rank
+
+
 def rank_plan(cfg: str, rank: int, segments: int):
     """This rank's disjoint batch: same shape on every rank, distinct seed."""
     from libhv_amd import synth
 
-    return synth.config_plan(cfg, seed=1000 + rank).split(segments)
+    return synth.config_plan(cfg, seed=rank_seed(cfg, rank)).split(segments)
 
 
 def max_over_ranks(dist, seconds: float) -> float:
@@ -758,14 +765,20 @@ def check_distinct_devices(bus_ids, rank: int) -> None:
 
 
 def fixture_for(cfg: str, rank: int):
-    """(name, entry) of the committed reference digests for this rank's batch
-    (tests/golden/configs.json: c5_rank<r> = the c3-shaped batch of seed
-    1000 + r, streamed through the reference by make_golden.py --big)."""
+    """(name, entry) of the committed reference digests for this rank's batch,
+    streamed through the reference by make_golden.py --big
+    (tests/golden/configs.json): c5_rank<r> = the c3-shaped batch of seed
+    1000 + r; c1 / c2 / c4 = that config's batch of seed 1 (rank 0's)."""
     path = os.path.join(ROOT, "tests", "golden", "configs.json")
-    if cfg != "c3" or not os.path.exists(path):
+    if not os.path.exists(path):
         return None, None
-    name = f"c5_rank{rank}"
-    return name, json.load(open(path)).get(name)
+    name = f"c5_rank{rank}" if cfg == "c3" else (cfg if rank == 0 else None)
+    if name is None:
+        return None, None
+    ent = json.load(open(path)).get(name)
+    if ent is not None and cfg != "c3" and f"seed={rank_seed(cfg, rank)})" not in ent["plan"]["fn"]:
+        return None, None
+    return name, ent
 
 
 def start_watchdog(period: float) -> None:
@@ -797,6 +810,16 @@ def start_watchdog(period: float) -> None:
     threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
 
 
+def per_rank_roofline(row) -> dict:
+    """One rank's own unmask time, its fraction of 8 TB/s and of its card's
+    in-place ceiling (row = [unmask ms mean, achieved GB/s, ceiling GB/s])."""
+    ms, achieved, ceiling = (float(x) for x in row)
+    return {"unmask_ms_mean": round(ms, 3),
+            "roofline_frac": round(achieved / HBM_PEAK_GBS, 4),
+            "stream_ceiling_GBps": round(ceiling, 1),
+            "frac_of_box_ceiling": round(achieved / ceiling, 4) if ceiling > 0 else None}
+
+
 def dry_run(args, rank: int, world: int, local: int, dist) -> None:
     """--dry-run: the rank plumbing of a real run with the GPU legs stubbed --
     every rank builds its disjoint batch plan (CPU), the timing rows and the
@@ -816,6 +839,11 @@ def dry_run(args, rank: int, world: int, local: int, dist) -> None:
     check_distinct_devices([bus_name(int(b)) for b in trows[:, 5]], rank)
     fx_name, fx = fixture_for("c3", rank)
     vrows = gather_rows(dist, [rank, local, int(plan.seed), -1 if fx is None else 1])
+    # stand-in per-rank unmask times and ceilings ($HVWS_BENCH_DRYRUN_SLOW_RANK
+    # makes one rank's card slow), through the same gather as a real run
+    slow = os.environ.get("HVWS_BENCH_DRYRUN_SLOW_RANK") == str(rank)
+    ms = 21.3 * (1.5 if slow else 1.0)
+    prows = gather_rows(dist, [ms, 137.4536e9 / (ms * 1e-3) / 1e9, 6460.0])
     if rank == 0:
         print(json.dumps({
             "metric": "device-resident WS unmask GiB/s, 64 KiB masked frames, 1/2/4/8 MI355X",
@@ -823,7 +851,8 @@ def dry_run(args, rank: int, world: int, local: int, dist) -> None:
             "timing": {"elapsed_s": span_of(trows),
                        "per_rank": [{"rank": int(r), "device": int(trows[r, 3]), "hip_device": int(trows[r, 4]),
                                      "pci_bus_id": bus_name(int(trows[r, 5])),
-                                     "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3)}
+                                     "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3),
+                                     **per_rank_roofline(prows[r])}
                                     for r in range(trows.shape[0])]},
             "verified": {"ranks": [{"rank": int(v[0]), "local_rank": int(v[1]), "seed": int(v[2]),
                                     "fixture": f"c5_rank{int(v[0])}" if v[3] >= 0 else None} for v in vrows]},
@@ -992,18 +1021,23 @@ def main():
         if ent:
             traffic, traffic_src = ent["hbm_bytes"], f"profiles/traffic.json ({ent['method']})"
 
+    # Every rank: the STREAM-style in-place ceiling (read+write every byte) of
+    # its own card on the same buffer (an even number of passes: no net
+    # change), so an N-rank line shows each card's unmask time, its fraction
+    # of 8 TB/s and of its own ceiling -- one slow card stands out.
+    eng.sync()
+    t = time.perf_counter()
+    reps = 4
+    for _ in range(reps):
+        eng.stream_xor(rx, plan.total & ~15, 0x5A5A5A5A)
+    eng.sync()
+    ceiling = 2 * (plan.total & ~15) * reps / (time.perf_counter() - t) / 1e9
+    prows = gather_rows(dist, [mean_unmask, achieved, ceiling])
+
     extra = {}
     sample = None
     feed_streams = feed_pay = None
     if rank == 0:
-        # STREAM-style in-place ceiling (read+write every byte) on the same buffer
-        eng.sync()
-        t = time.perf_counter()
-        reps = 4
-        for _ in range(reps):
-            eng.stream_xor(rx, plan.total & ~15, 0x5A5A5A5A)
-        eng.sync()
-        ceiling = 2 * (plan.total & ~15) * reps / (time.perf_counter() - t) / 1e9
         extra["stream_ceiling_GBps"] = round(ceiling, 1)
         # pipelined steps record no scan-side timing markers (-1; include/hvws.h)
         scan_rec = [t for t in scan_ms if t >= 0]
@@ -1026,15 +1060,17 @@ def main():
                           "pci_bus_id": bus_name(int(trows[r, 5])),
                           "device_span_ms": round(float(trows[r, 2]), 3),
                           "start_offset_ms": round(float(trows[r, 0] - trows[:, 0].min()) * 1e3, 3),
-                          "end_offset_ms": round(float(trows[r, 1] - trows[:, 0].min()) * 1e3, 3)}
+                          "end_offset_ms": round(float(trows[r, 1] - trows[:, 0].min()) * 1e3, 3),
+                          **per_rank_roofline(prows[r])}
                          for r in range(trows.shape[0])],
             "device_span_ms_max": round(float(trows[:, 2].max()), 3),
         }
         extra["verified"] = {
             "method": "every payload byte vs its plaintext (device synth VERIFY) after the run; digest of the "
-                      "whole rx buffer vs the reference's (tests/golden/configs.json c5_rank<r>) before and after",
+                      "whole rx buffer vs the reference's (tests/golden/configs.json: c5_rank<r> for c3, the "
+                      "config's own entry for rank 0 of c1/c2/c4) before and after",
             "ranks": [{"rank": int(v[0]), "device": int(v[1]),
-                       "fixture": (f"c5_rank{int(v[0])}" if v[2] >= 0 else None),
+                       "fixture": (fixture_for(cfg, int(v[0]))[0] if v[2] >= 0 else None),
                        "digest_match": (bool(v[2]) if v[2] >= 0 else None)} for v in vrows],
         }
         if args.sweep_unmask:

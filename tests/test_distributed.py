@@ -96,6 +96,35 @@ def test_bench_launcher_two_ranks():
     v = out["verified"]["ranks"]
     assert [r["fixture"] for r in v] == ["c5_rank0", "c5_rank1"]
     assert [r["local_rank"] for r in v] == [0, 1] and v[0]["seed"] != v[1]["seed"]
+    # each card's own unmask time, fraction of 8 TB/s and of its own ceiling
+    for r in pr:
+        assert {"unmask_ms_mean", "roofline_frac", "stream_ceiling_GBps", "frac_of_box_ceiling"} <= set(r)
+        assert r["roofline_frac"] == round(137.4536e9 / (r["unmask_ms_mean"] * 1e-3) / 1e9 / 8000.0, 4)
+
+
+def test_bench_per_rank_roofline_shows_a_slow_card():
+    """an N-rank line exposes one slow card -- its unmask
+    time and HBM fractions arrive through the gloo gather in its own row."""
+    import json
+
+    p = _bench(["--gpus", "2", "--dry-run"], {"HVWS_BENCH_DRYRUN_SLOW_RANK": "1"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    pr = out["timing"]["per_rank"]
+    assert pr[1]["unmask_ms_mean"] > pr[0]["unmask_ms_mean"] * 1.4
+    assert pr[1]["roofline_frac"] < pr[0]["roofline_frac"] and pr[1]["frac_of_box_ceiling"] < pr[0]["frac_of_box_ceiling"]
+
+
+def test_bench_fixture_per_config():
+    """Rank 0's c2 / c4 batch is the one the reference digests were taken of
+    (seed 1), c3 ranks take config 5's shards; other ranks of c2 / c4 have none."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.fixture_for("c3", 3)[0] == "c5_rank3"
+    assert bench.fixture_for("c2", 0)[0] == "c2" and bench.fixture_for("c4", 0)[0] == "c4"
+    assert bench.fixture_for("c2", 1) == (None, None)
+    assert bench.rank_seed("c2", 0) == 1 and bench.rank_seed("c3", 0) == 1000
 
 
 def test_bench_launcher_fails_with_a_rank():
