@@ -66,9 +66,6 @@ def parse():
                          "against a launch per call (0: skip; scripts/bench_dropin.py runs it alone)")
     ap.add_argument("--serial", action="store_true",
                     help="hvws_step (discovery after the previous unmask) instead of hvws_step_resident")
-    ap.add_argument("--lagged", action="store_true",
-                    help="hvws_lagged_step (two scan chains in flight, two contexts; a batch is unmasked by the "
-                         "next calls / sync) instead of hvws_step_resident")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the rank launcher and the timing reductions: no GPU call, "
                          "no measurement (tests/test_distributed.py)")
@@ -924,15 +921,10 @@ def main():
     # batch (the same buffer: headers are never modified, payloads toggle).
     step = eng.step if args.serial else eng.step_resident
     L = libhv_amd.lib()
-    lagged = eng.lagged() if args.lagged else None
-    if lagged is not None:
-        step = lagged.step
     if args.validate:
         L.hvws_set_validation(eng.ctx, 0x3F)   # HVWS_V_ALL
     for _ in range(args.warmup):
         step(rx, plan.total, segs)
-    if lagged is not None:
-        lagged.sync()
     barrier()
     # Steps are issued back to back (each still synchronises once inside its
     # scan to size the frame table); the per-launch kernel times are read
@@ -946,34 +938,23 @@ def main():
     # on every 8th step only (hvws_set_step_event_interval); all launches of a
     # run are the same work.
     ev_every = 8 if args.steps >= 32 else 1
-    if lagged is None:
-        eng.set_step_event_interval(ev_every)
+    eng.set_step_event_interval(ev_every)
     t0 = time.perf_counter()
     span_ms = ctypes.c_float(0)
-    if lagged is None:
-        libhv_amd._check(L.hvws_span_begin(eng.ctx), "span_begin")
-        for _ in range(args.steps):
-            step(rx, plan.total, segs)
-        libhv_amd._check(L.hvws_span_end(eng.ctx, ctypes.byref(span_ms)), "span_end")
-        eng.sync()
-        t1 = time.perf_counter()
-    else:   # two contexts: the host clock around the steps and the final sync
-        for _ in range(args.steps):
-            step(rx, plan.total, segs)
-        lagged.sync()
-        t1 = time.perf_counter()
-        span_ms.value = (t1 - t0) * 1e3
+    libhv_amd._check(L.hvws_span_begin(eng.ctx), "span_begin")
+    for _ in range(args.steps):
+        step(rx, plan.total, segs)
+    libhv_amd._check(L.hvws_span_end(eng.ctx, ctypes.byref(span_ms)), "span_end")
+    eng.sync()
+    t1 = time.perf_counter()
     barrier()
     trows = gather_rows(dist, [t0, t1, span_ms.value, device, hip_device, bus_number(bus_id)])
     elapsed = span_of(trows)
     # every rank on its own card (a rehearsal under HVWS_BENCH_DEVICE excepted)
     check_distinct_devices([bus_name(int(b)) for b in trows[:, 5]], rank)
-    scan_path = L.hvws_last_scan_path(eng.ctx if lagged is None else lagged.context(0))
-    times = eng.step_times(min(args.steps, 32)) if lagged is None else lagged.step_times(min(args.steps, 16))
-    if lagged is None:
-        eng.set_step_event_interval(1)
-    else:
-        lagged.close()
+    scan_path = L.hvws_last_scan_path(eng.ctx)
+    times = eng.step_times(min(args.steps, 32))
+    eng.set_step_event_interval(1)
     scan_ms = [t[0] for t in times]
     unmask_ms = [t[1] for t in times if t[1] >= 0]   # the sampled steps
     if not unmask_ms:
@@ -1043,7 +1024,6 @@ def main():
         scan_rec = [t for t in scan_ms if t >= 0]
         extra["scan_ms_mean"] = round(float(np.mean(scan_rec)), 3) if scan_rec else None
         extra["step_call"] = ("hvws_step" if args.serial else
-                              "hvws_lagged_step (two scan chains in flight on two contexts)" if args.lagged else
                               "hvws_step_resident (discovery overlaps the previous unmask)")
         if args.validate:
             extra["validation"] = "HVWS_V_ALL"
@@ -1051,10 +1031,8 @@ def main():
         extra["scan_path"] = {0: "count_emit", 1: "count_read_emit", 2: "single", 3: "speculative",
                               4: "speculative_rejected", 5: "slack", 6: "slack_rejected", 7: "run"}.get(scan_path, scan_path)
         extra["timing"] = {
-            "method": ("per device: the host clock around the lagged steps and their final sync (two contexts); "
-                       if args.lagged else
-                       "per device: hvws_span_begin/end markers on the context's streams (HIP events); ")
-                      + "across devices: latest end - earliest start on the host CLOCK_MONOTONIC after a barrier",
+            "method": "per device: hvws_span_begin/end markers on the context's streams (HIP events); "
+                      "across devices: latest end - earliest start on the host CLOCK_MONOTONIC after a barrier",
             "elapsed_s": round(elapsed, 6),
             "per_rank": [{"rank": int(r), "device": int(trows[r, 3]), "hip_device": int(trows[r, 4]),
                           "pci_bus_id": bus_name(int(trows[r, 5])),

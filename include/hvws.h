@@ -134,7 +134,12 @@ int hvws_step(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len, const hvws_segment*
  * previous step, whose tables are kept in the other of two table sets; the
  * unmask is queued on the context stream after it, as with hvws_step.  Frames
  * and carry of the call are readable (hvws_get_*) until the next scan; work
- * queued on the context stream afterwards sees the unmasked bytes. */
+ * queued on the context stream afterwards sees the unmasked bytes.
+ * A step that took the RUN path (hvws_set_run; hvws_step too) builds its
+ * frames and carry when hvws_get_* / hvws_frame_count first asks, from the
+ * batch's header bytes: those bytes must not change until then (reading them
+ * before the next receive into the buffer, or calling hvws_frame_count right
+ * after the step, fixes them).  Payload bytes may change freely. */
 int hvws_step_resident(hvws_ctx* ctx, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
                        const websocket_parser* carry_in, uint32_t nseg);
 
@@ -167,28 +172,6 @@ int hvws_step_times(hvws_ctx* ctx, float* out, int max_steps);
  * read -1.  Returns the previous interval (< 0 on error). */
 int hvws_set_step_event_interval(hvws_ctx* ctx, uint32_t every);
 
-/* Lagged steps: two scan chains in flight.  A lagged
- * stepper runs consecutive hvws_step_resident steps on two contexts of one
- * device from two worker threads, so batch k+1's discovery is launched while
- * batch k's is still running; unmasks stay in call order.  hvws_lagged_step
- * copies the segment and carry tables and returns once the step is handed
- * over: the batch is unmasked by the time hvws_lagged_sync (or a later
- * step's return, two calls on) says so.  Errors stick: every later call
- * returns the first one (hvws_lagged_error names it).  hvws_lagged_context(i)
- * gives the two contexts (i = 0, 1) for timing and diagnostics.  Steps,
- * sync and free come from one thread (the stepper's own two workers run the
- * steps).  Opt-in:
- * for one 4.3 GB mixed stream it measured slower than hvws_step_resident
- * (1.70-1.78 against 1.58 ms per step). */
-typedef struct hvws_lagged hvws_lagged;
-hvws_lagged* hvws_lagged_new(int device);   /* NULL on failure */
-int hvws_lagged_step(hvws_lagged* lag, uint8_t* d_rx, uint64_t rx_len, const hvws_segment* segs,
-                     const websocket_parser* carry_in, uint32_t nseg);
-int hvws_lagged_sync(hvws_lagged* lag);
-hvws_ctx* hvws_lagged_context(hvws_lagged* lag, int i);
-const char* hvws_lagged_error(hvws_lagged* lag);
-void hvws_lagged_free(hvws_lagged* lag);
-
 /* k_unmask geometry.  By default it follows the batch size: 512 threads x 2
  * chunks in linear tile order below 16 GiB, 256 x 4 in XCD-contiguous order
  * from there (measured).  hvws_unmask_kernel_name: the name
@@ -198,11 +181,6 @@ const char* hvws_unmask_kernel_name(void);
 const char* hvws_unmask_kernel_name_for(uint64_t rx_len);
 /* The RUN path's unmask kernel (HVWS_PATH_RUN steps), e.g. "k_unmask_run<256,4,lds>". */
 const char* hvws_run_kernel_name(void);
-/* Force a RUN unmask geometry (0 .. hvws_run_geometry_count() - 1) for later
- * RUN steps (tests, tuning; process-wide); -1 = the default again.  Returns
- * the previous setting (-1: none). */
-int hvws_set_run_geometry(int geometry);
-int hvws_run_geometry_count(void);
 /* Force a k_unmask geometry for later scans (tuning; process-wide); -1 =
  * back to the choice by batch size. */
 int hvws_set_unmask_variant(int variant);
@@ -298,7 +276,10 @@ int hvws_last_scan_path(hvws_ctx* ctx);
  * hypothesis failed, so work queued after the step sees the reference's bytes
  * either way; the next steps then scan exactly until a check sees uniform
  * frames again.  The frame records, counts and carry of a RUN step are built
- * (an exact scan of the unchanged headers) when hvws_get_* first asks.  mode
+ * (an exact scan of the unchanged headers) when hvws_get_* first asks: the
+ * header bytes must stay as they were until then (hvws_step_resident).  An
+ * hvws_unmask after a RUN step builds them first and XORs by that exact
+ * table.  mode
  * -1 = automatic (default; $HVWS_RUN=0 turns it off), 0 = never, 1 = every
  * step batch of several segments, whatever the last scan saw (tests).  ctx
  * NULL = the calling thread's context.  Returns the previous mode. */

@@ -109,15 +109,6 @@ _SIGS = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32],
     ),
-    "hvws_lagged_new": (ctypes.c_void_p, [ctypes.c_int]),
-    "hvws_lagged_step": (
-        ctypes.c_int,
-        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32],
-    ),
-    "hvws_lagged_sync": (ctypes.c_int, [ctypes.c_void_p]),
-    "hvws_lagged_context": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
-    "hvws_lagged_error": (ctypes.c_char_p, [ctypes.c_void_p]),
-    "hvws_lagged_free": (None, [ctypes.c_void_p]),
     "hvws_frame_count": (ctypes.c_int64, [ctypes.c_void_p]),
     "hvws_get_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "hvws_get_segment_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -188,8 +179,6 @@ _SIGS = {
     "hvws_unmask_kernel_name": (ctypes.c_char_p, []),
     "hvws_unmask_kernel_name_for": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hvws_run_kernel_name": (ctypes.c_char_p, []),
-    "hvws_set_run_geometry": (ctypes.c_int, [ctypes.c_int]),
-    "hvws_run_geometry_count": (ctypes.c_int, []),
     "hvws_set_spec_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_sieve_min": (ctypes.c_uint64, [ctypes.c_uint64]),
     "hvws_set_table_checks": (ctypes.c_int, [ctypes.c_int]),
@@ -419,10 +408,6 @@ class Engine:
             _check(r, "hvws_set_step_event_interval")
         return r
 
-    def lagged(self) -> "Lagged":
-        """A lagged stepper on this engine's device (hvws_lagged_*)."""
-        return Lagged(self.device)
-
     def stream_xor(self, buf: DeviceBuffer, n: int, pattern: int) -> None:
         _check(lib().hvws_stream_xor(self.ctx, buf.ptr, n, pattern), "hvws_stream_xor")
 
@@ -537,51 +522,3 @@ def device_identity(device: int) -> tuple:
     _check(lib().hvws_device_identity(device, buf, 64, ctypes.byref(cur)), "hvws_device_identity")
     return buf.value.decode(), int(cur.value)
 
-
-class Lagged:
-    """hvws_lagged_*: consecutive steps on two contexts from two worker threads,
-    two scan chains in flight; a batch is unmasked by the time sync() returns."""
-
-    def __init__(self, device: int = 0):
-        self.h = lib().hvws_lagged_new(device)
-        if not self.h:
-            raise HvwsError("hvws_lagged_new failed")
-
-    def _check(self, rc: int, what: str) -> None:
-        if rc != 0:
-            raise HvwsError(f"{what} failed ({rc}): {lib().hvws_lagged_error(self.h).decode(errors='replace')}")
-
-    def step(self, rx: "DeviceBuffer", rx_len: int, segs, carry=None) -> None:
-        if isinstance(segs, Prepared):
-            s, c, n = segs.segs, segs.carry, segs.n
-        else:
-            s, c, n = Engine._segs(segs), Engine._carry(len(segs), carry), len(segs)
-        self._check(lib().hvws_lagged_step(self.h, rx.ptr, rx_len, s, c, n), "hvws_lagged_step")
-
-    def sync(self) -> None:
-        self._check(lib().hvws_lagged_sync(self.h), "hvws_lagged_sync")
-
-    def context(self, i: int):
-        return lib().hvws_lagged_context(self.h, i)
-
-    def step_times(self, max_steps: int = 32):
-        """(scan ms, unmask ms) of the last steps of both contexts."""
-        res = []
-        for i in range(2):
-            out = (ctypes.c_float * (2 * max_steps))()
-            n = lib().hvws_step_times(self.context(i), out, max_steps)
-            if n < 0:
-                _check(n, "hvws_step_times")
-            res += [(float(out[2 * k]), float(out[2 * k + 1])) for k in range(n)]
-        return res
-
-    def close(self) -> None:
-        if self.h:
-            lib().hvws_lagged_free(self.h)
-            self.h = None
-
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *exc):
-        self.close()

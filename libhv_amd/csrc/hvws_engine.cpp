@@ -200,12 +200,7 @@ struct hvws_ctx {
     // RUN path (hvws_internal.h, drun): the last scan left no frame table (its
     // records are built on demand), its unmask is k_unmask_run + k_run_fix
     bool run_active = false;
-    int run_g = 0;             // the RUN geometry the last RUN scan cut its tiles for
-    // Lagged steps (hvws_lagged_*, hvws_lagged.cpp): called once before the
-    // step's first unmask is queued (the previous lagged step's unmask, on
-    // another context, is ordered before it there); armed per step.
-    std::function<void()> lag_before;
-    bool lag_armed = false;
+    bool materializing = false;   // run_materialize's exact scan: no timing slot, no RUN bookkeeping
     bool run_call = false;     // the scan belongs to a step call (the only callers RUN serves)
     int run_mode = -1;         // hvws_set_run: -1 auto, 0 never, 1 whenever a step's batch allows it
     uint32_t run_skip = 0;     // steps left before RUN is tried again after a failed hypothesis
@@ -471,19 +466,6 @@ bool run_env() {
     return v != 0;
 }
 
-// The RUN unmask's geometry (kRunGeoms, hvws_kernels.hip); $HVWS_EXPERIMENT run_geom for a sweep.
-// hvws_set_run_geometry (tests: every compiled geometry) overrides it; a
-// step's scan records the geometry its tiles were cut for (ctx run_g) and its
-// unmask uses that one.
-std::atomic<int> g_run_geom_forced{-1};
-int run_geom() {
-    static const int v = [] {
-        const int g = experiment("run_geom") ? atoi(experiment("run_geom")) : 0;
-        return g >= 0 && g < run_geom_count() ? g : 0;
-    }();
-    const int f = g_run_geom_forced.load(std::memory_order_relaxed);
-    return f >= 0 && f < run_geom_count() ? f : v;
-}
 
 bool host_order() {
     static const int v = experiment("host_order") ? atoi(experiment("host_order")) : 1;
@@ -624,10 +606,6 @@ int ensure_sieve(hvws_ctx* c, uint64_t rx_len, sieve_bufs& b) {
 // (host_order), so the unmask needs no cross-stream wait packet.
 hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined = false) {
     hipError_t e;
-    if (c->lag_armed) {
-        c->lag_armed = false;
-        if (c->lag_before) c->lag_before();
-    }
     const bool piped = c->cs != c->stream;
     if (piped && !joined) {   // the scan ran on the side stream: join it
         if ((e = hipEventRecord(c->scan_done, c->cs)) != hipSuccess) return e;
@@ -659,7 +637,7 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
     static const bool free_attach = !(experiment("free_attach") && atoi(experiment("free_attach")) == 0);
     const bool attach_free = piped && !timed && free_attach;
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
-        if ((e = launch_unmask_run(c->run_g, d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
+        if ((e = launch_unmask_run(d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
                                    c->run_seq, c->stream, timed ? c->tev[c->t_cur][2] : nullptr,
                                    timed ? c->tev[c->t_cur][3] : (attach_free ? c->T().free_ev : nullptr))) !=
@@ -751,7 +729,9 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
     if (!status_d) return set_err(HVWS_EHIP, "pinned status not device-mapped");
     const dseg* segs = c->segs.as<dseg>();
     const dcarry* cin = c->carry_in.as<dcarry>();
-    HIP_OR(begin_timed_scan(c), HVWS_EHIP);
+    // (run_materialize's rebuild of a RUN step's records keeps that step's
+    // timing slot: no new slot, no events)
+    if (!c->materializing) HIP_OR(begin_timed_scan(c), HVWS_EHIP);
     // After the first pass the device tables hold the uploaded segments; the
     // pinned slot is free once that pass's first kernel has run.
     const int up_slot = c->up_slot;
@@ -940,7 +920,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
         // takes two segments per tile and leaves any between to the repair.
         const bool run_auto = c->run_mode < 0 && c->spec_ok && c->spec_mode != 0 && !c->run_skip && c->last_mean &&
                               c->last_mean <= RUN_MAX_FRAME && rx_len / nseg >= RUN_MIN_SEG && run_env();
-        if (c->run_skip) --c->run_skip;
+        if (c->run_skip && !c->materializing) --c->run_skip;
         if (unmask_into && c->run_call && c->vmask == 0 && (run_auto || c->run_mode == 1)) {
             c->scan_path = HVWS_PATH_RUN;
             HIP_OR(c->T().runs.ensure((uint64_t)nseg * sizeof(drun) + 64), HVWS_ENOMEM);
@@ -951,8 +931,7 @@ int scan_device_carry(hvws_ctx* c, const uint8_t* d_rx, uint64_t rx_len, uint32_
                 if (c->T().run_fail.p != was || c->T().run_fail.cap != had)
                     HIP_OR(hipMemsetAsync(c->T().run_fail.p, 0, c->T().run_fail.cap, c->cs), HVWS_EHIP);
             }
-            c->run_g = run_geom();
-            const uint64_t rtile = run_tile_bytes(c->run_g);
+            const uint64_t rtile = RUN_TILE;
             const uint64_t rtiles = (rx_len + rtile - 1) / rtile;
             HIP_OR(c->T().run_trun.ensure((rtiles + 1) * sizeof(dtrun)), HVWS_ENOMEM);
             sc.runs = c->T().runs.as<drun>();
@@ -1128,9 +1107,13 @@ int run_materialize(hvws_ctx* c) {
     const int path = c->scan_path;
     hipStream_t cs = c->cs;
     c->cs = c->stream;
-    const bool call = c->run_call;
+    const bool call = c->run_call, t_on = c->t_on;
     c->run_call = false;
+    c->t_on = false;   // the RUN step's events stay in its slot (hvws_last_times / hvws_step_times)
+    c->materializing = true;
     const int rc = scan_device_carry(c, c->rx, c->rx_len, c->nseg);
+    c->materializing = false;
+    c->t_on = t_on;
     c->run_call = call;
     c->cs = cs;
     c->scan_path = path;
@@ -1563,8 +1546,20 @@ uint8_t* door_din(hvws_ctx* c) {
     return c->d_door_req ? (uint8_t*)c->d_door_req + 256 : c->h_door_data.as<uint8_t>();
 }
 
+// A context that gets no worker serves its calls with a launch each (its
+// callers fall back on any failure here), so the thread's last-error text is
+// left as it was: the call itself succeeds.
+int door_ensure_impl(hvws_ctx* c);
 int door_ensure(hvws_ctx* c) {
     if (c->door_stream) return HVWS_OK;
+    char saved[sizeof g_err];
+    memcpy(saved, g_err, sizeof g_err);
+    const int rc = door_ensure_impl(c);
+    if (rc != HVWS_OK) memcpy(g_err, saved, sizeof g_err);
+    return rc;
+}
+
+int door_ensure_impl(hvws_ctx* c) {
     {
         std::lock_guard<std::mutex> lk(g_door_m);
         int same = 0;
@@ -1991,6 +1986,10 @@ int unmask_impl(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len) {
     if (!c->have_scan) return set_err(HVWS_EINVAL, "hvws_unmask without a preceding hvws_scan");
     if (d_rx != c->rx || rx_len != c->rx_len)
         return set_err(HVWS_EINVAL, "hvws_unmask buffer differs from the scanned one");
+    // After a RUN step its descriptors are spent (the repair cleared the
+    // failure words): a further unmask of the batch goes through the exact
+    // frame table, built now, so every frame is XORed again.
+    if (c->run_active && (rc = run_materialize(c)) != HVWS_OK) return rc;
     HIP_OR(issue_unmask(c, d_rx, rx_len), HVWS_EHIP);
     return HVWS_OK;
 }
@@ -3046,14 +3045,7 @@ const char* hvws_unmask_kernel_name(void) { return unmask_name(unmask_variant())
 
 const char* hvws_unmask_kernel_name_for(uint64_t rx_len) { return unmask_name(unmask_variant_for(rx_len)); }
 
-const char* hvws_run_kernel_name(void) { return run_geom_name(run_geom()); }
-
-int hvws_set_run_geometry(int g) {
-    if (g >= run_geom_count()) return set_err(HVWS_EINVAL, "RUN geometry %d of %d", g, run_geom_count());
-    return g_run_geom_forced.exchange(g < 0 ? -1 : g);
-}
-
-int hvws_run_geometry_count(void) { return run_geom_count(); }
+const char* hvws_run_kernel_name(void) { return run_kernel_name(); }
 
 uint64_t hvws_set_spec_min(uint64_t frames) { return set_spec_min(frames); }
 
@@ -3266,20 +3258,5 @@ void gpu_feed(char* buf, size_t len, const websocket_parser& carry, bool unmask,
     copy_parser(carry_out, cin);
     started = st;
 }
-
-// Lagged steps (hvws_lagged.cpp)
-void ctx_arm_lag(hvws_ctx* c, std::function<void()> before) {
-    c->lag_before = std::move(before);
-    c->lag_armed = true;
-}
-bool ctx_lag_fire(hvws_ctx* c) {   // runs the hook if the step queued no unmask; true if it ran here
-    if (!c->lag_armed) return false;
-    c->lag_armed = false;
-    if (c->lag_before) c->lag_before();
-    return true;
-}
-hipStream_t ctx_stream(hvws_ctx* c) { return c->stream; }
-hipStream_t ctx_scan_stream(hvws_ctx* c) { return c->sstream; }
-int ctx_device(hvws_ctx* c) { return c->device; }
 
 }  // namespace hvws

@@ -190,15 +190,13 @@ constexpr uint64_t RUN_MIN_SEG = 65536;    // and segments of at least this size
 // (the repair clears them all; the host zeroes a new array).
 hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs, uint32_t nseg, const drun* runs,
                             dtrun* trun, uint64_t ntiles, uint64_t tile, uint32_t* fail, hipStream_t st);
-// The RUN unmask (geometry geom < run_geom_count(): run_tile_bytes(geom)
-// bytes per tile, the tiles k_run_tiles described) and its repair pass;
-// the timing events ride on the unmask's first dispatch (start) and the
-// repair's (stop).  The repair publishes (seq, failed segments) to
-// status->pad3 when it is done.
-int run_geom_count();
-uint64_t run_tile_bytes(int geom);
-const char* run_geom_name(int geom);
-hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
+// The RUN unmask (RUN_TILE bytes per tile, the tiles k_run_tiles described)
+// and its repair pass; the timing events ride on the unmask's first dispatch
+// (start) and the repair's (stop).  The repair publishes (seq, failed
+// segments) to status->pad3 when it is done.
+constexpr uint64_t RUN_TILE = 16384;   // 256 threads x 4 chunks of 16 B
+const char* run_kernel_name();
+hipError_t launch_unmask_run(uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
                              uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
                              hipEvent_t ev_stop);
 constexpr uint64_t RUN_FAST_STRIDE = 1u << 20;   // run strides up to this take k_unmask_run's one-segment path
@@ -480,13 +478,5 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
                         const uint64_t* len, const uint8_t* flags, const uint32_t* mask, const uint64_t* out_off,
                         const uint64_t* size, const uint32_t* tile_first, const uint64_t* span, uint64_t n, int v,
                         hipStream_t st, const uint64_t* uni = nullptr);
-
-// Lagged steps (hvws_lagged.cpp): the hook a context calls once before its
-// step's first unmask is queued, and what it needs of the context.
-void ctx_arm_lag(hvws_ctx* c, std::function<void()> before);
-bool ctx_lag_fire(hvws_ctx* c);
-hipStream_t ctx_stream(hvws_ctx* c);
-hipStream_t ctx_scan_stream(hvws_ctx* c);
-int ctx_device(hvws_ctx* c);
 
 }  // namespace hvws

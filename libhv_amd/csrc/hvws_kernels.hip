@@ -2178,8 +2178,18 @@ __device__ __forceinline__ void run_tile_frames(const drun& r, uint64_t x0, uint
     nj = (uint32_t)run_frame_of(r, b - 1) + 1u - jlo;
 }
 
+// Runs k_unmask_run takes: strides of at least RUN_MIN_STRIDE bytes, so the
+// frames of a tile's two runs need at most TILE / RUN_MIN_STRIDE + 8 key
+// slots (s_fk, sized by run_key_slots); a run of smaller frames (2-31 B:
+// thousands per tile) is left to the repair's exact path.
+constexpr uint32_t RUN_MIN_STRIDE = 32;
+__host__ __device__ constexpr uint32_t run_key_slots(uint64_t tile) { return (uint32_t)(tile / RUN_MIN_STRIDE) + 16u; }
+// frames of one run meeting a tile: at most (tile + stride - 1) / stride + 1;
+// two runs, each with 3 extra slots, fit with room to spare
+static_assert((16384 + RUN_MIN_STRIDE - 1) / RUN_MIN_STRIDE + 1 + 3 + 3 + 3 <= run_key_slots(16384), "RUN key slots");
+
 __device__ __forceinline__ bool run_fast_ok(const drun& r) {
-    return !(r.flags & RUN_BAD) && (!r.cnt || (r.stride >= 32 && r.stride <= RUN_FAST_STRIDE));
+    return !(r.flags & RUN_BAD) && (!r.cnt || (r.stride >= RUN_MIN_STRIDE && r.stride <= RUN_FAST_STRIDE));
 }
 
 // Run r as it meets the tile [x, x + tile) (dtrun's fields after k0); a run
@@ -2354,7 +2364,7 @@ __device__ __forceinline__ void fast_run_init(fast_run& R, const dtrun& o, uint3
 // payload's phase, into its slot.
 __device__ __forceinline__ void fast_run_keys(const fast_run& R, const uint8_t* rx, uint64_t rx_len, uint64_t base,
                                               uint32_t* s_fk, uint32_t* __restrict__ fail, uint32_t nseg, uint32_t tid,
-                                              uint32_t T, const uint32_t* s_tile = nullptr, int32_t tile_bytes = 0) {
+                                              uint32_t T, const uint32_t* s_tile, int32_t tile_bytes) {
     uint64_t plo, phi, mlo, mhi;
     run_pattern(R.masked, (uint32_t)R.hl, R.len, plo, phi, mlo, mhi);
     const uint32_t kb = (uint32_t)R.hl - 4u;   // the key's first byte in a masked header: 2, 4 or 10
@@ -2367,7 +2377,7 @@ __device__ __forceinline__ void fast_run_keys(const fast_run& R, const uint8_t* 
                 key = R.k0;   // begun before the tile: its header is checked where it starts
             } else {
                 uint64_t lo, hi;
-                if (s_tile && hs + 16 <= tile_bytes) lds_hdr16(s_tile, (uint32_t)hs, lo, hi);   // staged tile
+                if (hs + 16 <= tile_bytes) lds_hdr16(s_tile, (uint32_t)hs, lo, hi);   // staged tile
                 else ld16(rx, rx_len, base + (uint64_t)hs, lo, hi);
                 if (((lo ^ plo) & mlo) | ((hi ^ phi) & mhi)) {
                     atomicOr(&fail[R.seg], 1u);
@@ -2425,7 +2435,7 @@ __device__ __forceinline__ void fast_run_mask(const fast_run& R, const uint32_t*
 // run frame reads its header and keeps its key (fast_run_keys) while the
 // selector table is built; one barrier; each chunk XORs what the runs lay on
 // it.
-template <int T, int U, bool STAGE>
+template <int T, int U>
 __device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
                                                 const dtrun* __restrict__ trun, uint32_t nseg,
                                                 uint32_t* __restrict__ fail, uint64_t t, uint32_t* s_fk,
@@ -2453,11 +2463,10 @@ __device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64
     const dtrun& tr = trun[t];   // wave-uniform: scalar loads
     const uint32_t s0 = tr.s0;
     if (s0 >= nseg) return;   // no segment reaches this tile
-    if (STAGE) {   // the headers from the tile's own bytes: staged in LDS, one more barrier
+    // the headers from the tile's own bytes: staged in LDS, one more barrier
 #pragma unroll
-        for (int i = 0; i < U; ++i) *reinterpret_cast<u32x4*>(&s_tile[((uint32_t)i * T + tid) * 4u]) = v[i];
-        __syncthreads();
-    }
+    for (int i = 0; i < U; ++i) *reinterpret_cast<u32x4*>(&s_tile[((uint32_t)i * T + tid) * 4u]) = v[i];
+    __syncthreads();
     fast_run R0, R1;
     fast_run_init(R0, tr, s0, 0);
     const uint32_t s1 = tr.s1;
@@ -2469,8 +2478,8 @@ __device__ __forceinline__ void run_unmask_tile(uint8_t* __restrict__ rx, uint64
         tile_run(o1, r1, run_fast_ok(r1), base, TILE);
         fast_run_init(R1, o1, s1, R0.nj + 3);
     }
-    fast_run_keys(R0, rx, rx_len, base, s_fk, fail, nseg, tid, T, STAGE ? s_tile : nullptr, (int32_t)TILE);
-    if (two) fast_run_keys(R1, rx, rx_len, base, s_fk, fail, nseg, tid, T, STAGE ? s_tile : nullptr, (int32_t)TILE);
+    fast_run_keys(R0, rx, rx_len, base, s_fk, fail, nseg, tid, T, s_tile, (int32_t)TILE);
+    if (two) fast_run_keys(R1, rx, rx_len, base, s_fk, fail, nseg, tid, T, s_tile, (int32_t)TILE);
     for (uint32_t e = tid; e < 256; e += T) s_sel[e] = kRunSel.v[e];
     __syncthreads();
     bool dirty[U];
@@ -2533,6 +2542,14 @@ __device__ __forceinline__ void wave_xor_range(uint8_t* rx, uint64_t lo, uint64_
 // repair (exact); fail[nseg] = any, [nseg + 1] = repaired count, [nseg + 2]
 // = repair workgroups done; all of them, and every segment's word, are zero
 // when the repair ends.
+// wave_xor_range clamped to segment r's bytes: every range the repair XORs
+// from a descriptor lies inside its segment by construction (k_head), and the
+// clamp keeps it there by construction too -- the repair's XORs are the RUN
+// path's only global writes not bounded by a tile (the r5h fault).
+__device__ __forceinline__ void seg_xor_range(uint8_t* rx, const drun& r, uint64_t lo, uint64_t hi, uint32_t kw) {
+    wave_xor_range(rx, lo > r.seg_lo ? lo : r.seg_lo, hi < r.seg_hi ? hi : r.seg_hi, kw);
+}
+
 __device__ __forceinline__ void run_repair(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
                                            uint32_t nseg, uint32_t* __restrict__ fail, uint32_t w0, uint32_t wn) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -2547,15 +2564,15 @@ __device__ __forceinline__ void run_repair(uint8_t* __restrict__ rx, uint64_t rx
         if (!bad && !fs) continue;
         if (lane == 0) atomicAdd(&fail[nseg + 1], 1u);
         if (!bad) {   // undo the hypothesis
-            wave_xor_range(rx, r.a_off, r.a_end, r.a_kw);
-            wave_xor_range(rx, r.t_off, r.t_end, r.t_kw);
+            seg_xor_range(rx, r, r.a_off, r.a_end, r.a_kw);
+            seg_xor_range(rx, r, r.t_off, r.t_end, r.t_kw);
             if (r.masked)
                 for (uint64_t j = 0; j < r.cnt; ++j) {
                     const uint64_t fo = r.p0 + j * r.stride;
                     uint64_t lo, hi;
                     ld16(rx, rx_len, fo, lo, hi);
                     const uint64_t ps = fo + r.hlen;
-                    wave_xor_range(rx, ps, fo + r.stride, rotr32(run_key(r, lo, hi), 8u * ((0u - (uint32_t)ps) & 3u)));
+                    seg_xor_range(rx, r, ps, fo + r.stride, rotr32(run_key(r, lo, hi), 8u * ((0u - (uint32_t)ps) & 3u)));
                 }
             __threadfence();
         }
@@ -2567,7 +2584,7 @@ __device__ __forceinline__ void run_repair(uint8_t* __restrict__ rx, uint64_t rx
         if (st.state != S_START && scalar_frame(rx + sb, L, st, pos, fr0, 0u) && (fr0.info & I_BODY) &&
             (fr0.info & F_MASK)) {
             const uint64_t po = sb + fr0.pay_off;
-            wave_xor_range(rx, po, po + fr0.pay_len, key_for_aligned(fr0.key, po, (fr0.info >> 8) & 3u));
+            seg_xor_range(rx, r, po, po + fr0.pay_len, key_for_aligned(fr0.key, po, (fr0.info >> 8) & 3u));
         }
         __threadfence();
         // walk_frames calls emit from every lane owning a record (the
@@ -2582,15 +2599,15 @@ __device__ __forceinline__ void run_repair(uint8_t* __restrict__ rx, uint64_t rx
     }
 }
 
-template <int T, int U, bool STAGE>
+template <int T, int U>
 __global__ __launch_bounds__(T) void k_unmask_run(uint8_t* __restrict__ rx, uint64_t rx_len, const drun* __restrict__ runs,
                                                   const dtrun* __restrict__ trun, uint32_t nseg,
                                                   uint32_t* __restrict__ fail, uint64_t tile0) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
-    __shared__ uint32_t s_fk[TILE / 32 + 16];   // 2 runs: sum of (nj + 3) <= TILE / 32 + 8
+    __shared__ uint32_t s_fk[run_key_slots(TILE)];   // 2 runs: sum of (nj + 3) <= TILE / 32 + 8 (run_fast_ok)
     __shared__ uint32_t s_sel[256];
-    __shared__ uint32_t s_tile[STAGE ? TILE / 4 + 8 : 1];
-    run_unmask_tile<T, U, STAGE>(rx, rx_len, runs, trun, nseg, fail, tile0 + blockIdx.x, s_fk, s_sel, s_tile);
+    __shared__ uint32_t s_tile[TILE / 4 + 8];
+    run_unmask_tile<T, U>(rx, rx_len, runs, trun, nseg, fail, tile0 + blockIdx.x, s_fk, s_sel, s_tile);
 }
 
 // The repair kernel behind the unmask on the same stream (a kernel boundary
@@ -3015,56 +3032,33 @@ hipError_t launch_run_tiles(const uint8_t* rx, uint64_t rx_len, const dseg* segs
     return hipGetLastError();
 }
 
-// RUN unmask geometries (threads x chunks per thread; 0: the tile staged in LDS
-// for the header reads, c2 0.380-0.382 against 0.386-0.387 ms per step reading
-// them from HBM, 256 x 2 staged 0.401, profiles/r5_raw/sweeps/*_r5x.json);
-// $HVWS_EXPERIMENT run_geom picks
-// one for an on-device sweep (run_geom, hvws_engine.cpp)
-static constexpr struct { int threads, chunks; } kRunGeoms[] = {{256, 4}, {256, 4}, {512, 2}, {256, 2}, {128, 4}, {64, 4}};
-int run_geom_count() { return (int)(sizeof kRunGeoms / sizeof kRunGeoms[0]); }
-uint64_t run_tile_bytes(int g) { return (uint64_t)kRunGeoms[g].threads * kRunGeoms[g].chunks * 16u; }
-const char* run_geom_name(int g) {
-    static const char* const names[] = {"k_unmask_run<256,4,lds>", "k_unmask_run<256,4>", "k_unmask_run<512,2>",
-                                        "k_unmask_run<256,2>", "k_unmask_run<128,4>", "k_unmask_run<64,4>"};
-    static_assert(sizeof names / sizeof names[0] == sizeof kRunGeoms / sizeof kRunGeoms[0], "one name per geometry");
-    return g >= 0 && g < run_geom_count() ? names[g] : "";
-}
+// The RUN unmask: 256 threads x 4 chunks per 16 KiB tile, the tile staged
+// in LDS for the header reads (c2 0.380-0.382 ms per step against 0.386-0.387
+// reading them from HBM; 512 x 2, 256 x 2, 128 x 4 and 64 x 4 all lost,
+// profiles/r5_raw/sweeps/*_r5l-r5x.json; those geometries were removed in
+// round 6).
+const char* run_kernel_name() { return "k_unmask_run<256,4,lds>"; }
 
-hipError_t launch_unmask_run(int geom, uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
+hipError_t launch_unmask_run(uint8_t* rx, uint64_t rx_len, const drun* runs, const dtrun* trun, uint32_t nseg,
                              uint32_t* fail, dspec_status* status, uint64_t seq, hipStream_t st, hipEvent_t ev_start,
                              hipEvent_t ev_stop) {
     if (rx_len == 0 || nseg == 0) return hipSuccess;
-    if (geom < 0 || geom >= run_geom_count()) return hipErrorInvalidValue;
-    const uint64_t tile = run_tile_bytes(geom);
-    const uint64_t ntiles_all = (rx_len + tile - 1) / tile;
-    const int T = kRunGeoms[geom].threads;
+    constexpr int T = 256, U = 4;
+    static_assert((uint64_t)T * U * 16u == RUN_TILE, "RUN tile");
+    const uint64_t ntiles_all = (rx_len + RUN_TILE - 1) / RUN_TILE;
     // The grid in two launches: c2 0.375-0.376 ms per step against 0.377-0.379
     // in one, 0.378-0.379 in three, 0.383-0.385 in four (interleaved on one box,
-    // profiles/r5_raw/sweeps/*_r5za.json); 64 x 4 lost with every split
-    // ($HVWS_EXPERIMENT run_pieces=<n> overrides).
-    static const uint64_t pieces = experiment("run_pieces") && atoi(experiment("run_pieces")) > 0
-                                       ? (uint64_t)atoi(experiment("run_pieces")) : 2;
-    uint64_t cap = max_tiles_per_launch(T);
-    if (pieces > 1) cap = std::min<uint64_t>(cap, (ntiles_all + pieces - 1) / pieces);
+    // profiles/r5_raw/sweeps/*_r5za.json).
+    constexpr uint64_t pieces = 2;
+    const uint64_t cap = std::min<uint64_t>(max_tiles_per_launch(T), (ntiles_all + pieces - 1) / pieces);
     for (uint64_t tile0 = 0; tile0 < ntiles_all; tile0 += cap) {
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
-        hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
-#define HVWS_RUN_K(TT, UU, SS)                                                                                          \
-    if (e0)                                                                                                           \
-        hipExtLaunchKernelGGL((k_unmask_run<TT, UU, SS>), dim3((uint32_t)ntiles), dim3(TT), 0, st, e0, nullptr, 0u, rx, \
-                              rx_len, runs, trun, nseg, fail, tile0);                                                 \
-    else                                                                                                              \
-        hipLaunchKernelGGL((k_unmask_run<TT, UU, SS>), dim3((uint32_t)ntiles), dim3(TT), 0, st, rx, rx_len, runs, trun, \
-                           nseg, fail, tile0);
-        switch (geom) {
-            case 0: HVWS_RUN_K(256, 4, true) break;
-            case 1: HVWS_RUN_K(256, 4, false) break;
-            case 2: HVWS_RUN_K(512, 2, false) break;
-            case 3: HVWS_RUN_K(256, 2, false) break;
-            case 4: HVWS_RUN_K(128, 4, false) break;
-            default: HVWS_RUN_K(64, 4, false) break;
-        }
-#undef HVWS_RUN_K
+        if (tile0 == 0 && ev_start)
+            hipExtLaunchKernelGGL((k_unmask_run<T, U>), dim3((uint32_t)ntiles), dim3(T), 0, st, ev_start, nullptr, 0u, rx,
+                                  rx_len, runs, trun, nseg, fail, tile0);
+        else
+            hipLaunchKernelGGL((k_unmask_run<T, U>), dim3((uint32_t)ntiles), dim3(T), 0, st, rx, rx_len, runs, trun, nseg,
+                               fail, tile0);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -87,6 +87,46 @@ def test_config2_1m_x_1k(eng, nseg):
     _run(eng, synth.config_plan("c2", seed=1), nseg, GOLD["c2"])
 
 
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_config2_run_full_size(eng, pipelined):
+    """Config 2 at full size (1M x 1 KiB, 4096 connections) on the RUN path
+    (every header read once, inside the unmask), as bench.py
+    --config c2 measures it: steps until the RUN path is taken (it needs a
+    matched check first), then the reference's unmasked digest after that
+    step and its masked digest after the next RUN step, nothing repaired,
+    and the on-demand frame records of a RUN step (hvws_frame_count) exact."""
+    L = libhv_amd.lib()
+    plan = synth.config_plan("c2", seed=1)
+    plan.split(4096)
+    dp = libhv_amd.DevicePlan(eng, plan)
+    rx = _rx(eng, plan.total + 64)
+    segs = eng.prepare(plan.segments)
+    step = eng.step_resident if pipelined else eng.step
+    try:
+        eng.synth(rx, plan.total, plan.seed, dp, 0)
+        passes = 0
+        for _ in range(8):
+            step(rx, plan.total, segs)
+            passes += 1
+            if L.hvws_last_scan_path(eng.ctx) == 7:   # HVWS_PATH_RUN
+                break
+        assert L.hvws_last_scan_path(eng.ctx) == 7, "RUN was not taken on a uniform c2 batch"
+        eng.sync()
+        assert L.hvws_last_run_repairs(eng.ctx) == 0
+        want = GOLD["c2"]["digest_unmasked" if passes % 2 else "digest_masked"]
+        assert f"{eng.digest(rx, plan.total):016x}" == want
+        step(rx, plan.total, segs)
+        passes += 1
+        assert L.hvws_last_scan_path(eng.ctx) == 7
+        eng.sync()
+        want = GOLD["c2"]["digest_unmasked" if passes % 2 else "digest_masked"]
+        assert f"{eng.digest(rx, plan.total):016x}" == want
+        assert eng.synth(rx, plan.total, plan.seed, dp, 2 if passes % 2 else 1) == 0
+        assert L.hvws_frame_count(eng.ctx) == plan.n   # records built on demand (run_materialize)
+    finally:
+        dp.free()
+
+
 @pytest.mark.parametrize("nseg", [4096, 1])
 def test_config3_1m_x_64k(eng, nseg):
     _run(eng, synth.config_plan("c3", seed=1), nseg, GOLD["c3"])

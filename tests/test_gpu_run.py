@@ -36,18 +36,6 @@ def _check(eng, buf, segs, exp_recs, exp_carry, exp_started):
         assert started[s] == exp_started[s], s
 
 
-@pytest.fixture(params=range(6), ids=lambda g: f"geom{g}")
-def geom(request):
-    """Every compiled RUN unmask geometry (hvws_set_run_geometry), the default
-    (0: 256 x 4, tile staged in LDS) first."""
-    L = libhv_amd.lib()
-    if request.param >= L.hvws_run_geometry_count():
-        pytest.skip("geometry not compiled")
-    old = L.hvws_set_run_geometry(request.param)
-    yield request.param
-    L.hvws_set_run_geometry(old)
-
-
 @pytest.fixture
 def fresh():
     """A context of its own (what earlier tests taught the shared one does not
@@ -59,7 +47,7 @@ def fresh():
     e.close()
 
 
-def test_run_taken_for_uniform_steps_and_repairs_nothing(geom, fresh):
+def test_run_taken_for_uniform_steps_and_repairs_nothing(fresh):
     """Uniform 1 KiB frames in 24 segments: after the first exact scan sees
     them uniform, steps take RUN; nothing is repaired; every step's bytes,
     frames and carries equal the oracle's."""
@@ -103,7 +91,7 @@ def test_run_pipelined_same_buffer(fresh):
 
 
 @pytest.mark.parametrize("where", ["first", "middle", "last", "tail_then_more"])
-def test_run_hypothesis_breaks(geom, fresh, where):
+def test_run_hypothesis_breaks(fresh, where):
     """One segment that is not one run -- a frame of another size at its
     start, middle or end, or a whole frame after the cut one -- under RUN
     forced: that segment alone is repaired, and bytes, frames and carries
@@ -171,7 +159,7 @@ def test_run_auto_falls_back_on_mixed_traffic(fresh):
     rx.free()
 
 
-def test_run_carried_and_cut_frames(geom, fresh):
+def test_run_carried_and_cut_frames(fresh):
     """Segments that start inside a frame (payload or header carried in) and
     end inside one (payload, header, or a single byte of it), every frame of
     one size between: the carried-in and cut frames are exact in k_head's
@@ -201,7 +189,7 @@ def test_run_carried_and_cut_frames(geom, fresh):
     rx.free()
 
 
-def test_run_random_streams_forced(geom, fresh):
+def test_run_random_streams_forced(fresh):
     """Random streams (every opcode, masked and unmasked, all length classes)
     cut into segments, under RUN forced: mostly repaired, always exact."""
     eng, L = fresh, libhv_amd.lib()
@@ -221,3 +209,128 @@ def test_run_random_streams_forced(geom, fresh):
         assert np.array_equal(rx.download(len(buf)), exp), trial
         _check(eng, buf, segs, recs, carry, started)
         rx.free()
+
+
+def _segments(parts):
+    segs, at = [], 0
+    for p in parts:
+        segs.append((at, len(p)))
+        at += len(p)
+    return np.frombuffer(b"".join(parts), np.uint8).copy(), segs
+
+
+def test_run_small_strides_forced(fresh):
+    """Runs of frames of 2-31 bytes (unmasked empty frames: stride 2; masked
+    frames of 0-25 payload bytes: 6-31) under RUN forced, several 16 KiB tiles
+    each, beside runs of 32-40 B frames.  k_unmask_run's key slots hold the
+    frames of strides >= 32 only (a 16 KiB tile of 2-byte frames holds 8192);
+    smaller strides are left to the exact repair (run_fast_ok; DESIGN 4.2, the
+    round-5 fault analysis).  Bytes, frames and carries equal the oracle's."""
+    eng, L = fresh, libhv_amd.lib()
+    L.hvws_set_run(eng.ctx, 1)
+    rng = random.Random(2031)
+    key = b"\x5a\xa5\x3c\xc3"
+    parts, small = [], 0
+    for stride in [2, 6, 7, 13, 20, 26, 31, 32, 33, 40]:
+        if stride == 2:
+            frames = [(0x2 | 0x10, b"", None)] * 24000
+        else:
+            frames = [(0x2 | 0x10 | 0x20, rng.randbytes(stride - 6), key) for _ in range(40000 // stride)]
+        parts.append(H.build_frames_ref(frames))
+        small += stride < 32
+    buf, segs = _segments(parts)
+    recs, carry, started, exp = _oracle_batch(buf, segs, None)
+    rx = eng.to_device(buf)
+    eng.step(rx, len(buf), segs)
+    assert L.hvws_last_scan_path(eng.ctx) == PATH_RUN
+    assert L.hvws_last_run_repairs(eng.ctx) == small   # exact path: every run of stride < 32
+    assert np.array_equal(rx.download(len(buf)), exp)
+    _check(eng, buf, segs, recs, carry, started)
+    rx.free()
+
+
+def test_run_fewer_segments_after_more(fresh):
+    """One context, RUN forced, batches of 30, then 10, then 5 segments into
+    the same table set: a batch's words (any / count / workgroups done) sit
+    where an earlier, larger batch had segment failure words.  The repair
+    zeroes every word it reads, so a later batch sees none of them (a stale
+    'done' count published the verdict early; a stale 'any' or count said
+    segments failed that did not)."""
+    eng, L = fresh, libhv_amd.lib()
+    L.hvws_set_run(eng.ctx, 1)
+    rng = random.Random(33)
+    key = b"\x01\x23\x45\x67"
+    for nseg, bad in ((30, {3, 10, 11, 12, 20}), (10, set()), (5, {2}), (10, set())):
+        parts = []
+        for s in range(nseg):
+            lens = [1000] * 40
+            if s in bad:
+                lens[17] = 555
+            parts.append(H.build_frames_ref([(0x2 | 0x10 | 0x20, rng.randbytes(n), key) for n in lens]))
+        buf, segs = _segments(parts)
+        recs, carry, started, exp = _oracle_batch(buf, segs, None)
+        rx = eng.to_device(buf)
+        eng.step(rx, len(buf), segs)
+        assert L.hvws_last_scan_path(eng.ctx) == PATH_RUN
+        assert L.hvws_last_run_repairs(eng.ctx) == len(bad), (nseg, bad)
+        assert np.array_equal(rx.download(len(buf)), exp), nseg
+        _check(eng, buf, segs, recs, carry, started)
+        rx.free()
+
+
+def test_run_repair_key_from_hypothesis_layout(fresh):
+    """The round-5 wrong bytes (gpurun_out/pytest_run_r5c.log): a broken run
+    whose hypothesised header positions land in payload bytes that parse as a
+    longer header (byte 1 = 0xFE: 126-length, masked -> 8 header bytes
+    against the run's 6).  Parsed by its own length, that "header"'s key lies
+    in bytes the hypothesis XORed, so the repair read another key than the
+    unmask had used and the undo left bytes wrong.  Keys are taken at the
+    hypothesis' layout (run_key), inside the hypothesised header, which no
+    piece of the hypothesis changes."""
+    eng, L = fresh, libhv_amd.lib()
+    L.hvws_set_run(eng.ctx, 1)
+
+    def frame(n):   # masked binary frame, wire payload bytes all 0xFE
+        return bytes([0x82, 0x80 | n]) + b"\x9b\x17\xe2\x4d" + b"\xfe" * n
+
+    parts = []
+    for s in range(6):
+        lens = [100] * 30
+        if s % 2:
+            lens[5 + s] = 60   # the frames after it start 40 B before the hypothesis says
+        parts.append(b"".join(frame(n) for n in lens))
+    buf, segs = _segments(parts)
+    recs, carry, started, exp = _oracle_batch(buf, segs, None)
+    rx = eng.to_device(buf)
+    eng.step(rx, len(buf), segs)
+    assert L.hvws_last_scan_path(eng.ctx) == PATH_RUN
+    assert L.hvws_last_run_repairs(eng.ctx) == 3
+    assert np.array_equal(rx.download(len(buf)), exp)
+    _check(eng, buf, segs, recs, carry, started)
+    rx.free()
+
+
+def test_unmask_after_run_step(fresh):
+    """hvws_unmask after a RUN step XORs every frame again -- by
+    the exact table built on demand, not the spent run descriptors (their
+    failure words were cleared by the repair, so segments left to the repair
+    would have been skipped).  Uniform, broken and small-stride segments."""
+    eng, L = fresh, libhv_amd.lib()
+    L.hvws_set_run(eng.ctx, 1)
+    rng = random.Random(404)
+    key = b"\xde\xad\xbe\xef"
+    parts = []
+    for s in range(8):
+        lens = [700] * 30 if s != 3 else [12] * 3000
+        if s == 5:
+            lens[9] = 333
+        parts.append(H.build_frames_ref([(0x2 | 0x10 | 0x20, rng.randbytes(n), key) for n in lens]))
+    buf, segs = _segments(parts)
+    _, _, _, exp = _oracle_batch(buf, segs, None)
+    rx = eng.to_device(buf)
+    eng.step(rx, len(buf), segs)
+    assert L.hvws_last_scan_path(eng.ctx) == PATH_RUN
+    assert np.array_equal(rx.download(len(buf)), exp)
+    libhv_amd._check(L.hvws_unmask(eng.ctx, rx.ptr, len(buf)), "hvws_unmask")
+    assert np.array_equal(rx.download(len(buf)), buf)   # masked again, every byte
+    rx.free()
