@@ -272,11 +272,11 @@ struct hvws_ctx {
     int t_cur = 0;        // ring slot of the last scan
     uint32_t t_every = 1; // hvws_set_step_event_interval: events on every t_every-th scan (0: none)
     bool t_on = true;     // the current scan is one of them
-    // resident small-path worker (k_door): its own stream (a dedicated
-    // hardware queue, so the resident kernel never holds up other work), the
-    // mailbox, the data and record areas (fine-grained pinned) and a device
-    // slot for records past the worker's LDS area
-    hipStream_t door_stream = nullptr;
+    // resident small-path worker (k_door): its own HSA queue (a dedicated
+    // hardware queue, so the resident kernel never holds up other work;
+    // hvws_doorq.cpp), the mailbox, the data and record areas (fine-grained
+    // pinned) and a device slot for records past the worker's LDS area
+    door_queue* door_q = nullptr;
     hbuf h_door, h_door_data, h_door_rec;
     dbuf d_door_slot;
     // Request block + request bytes in fine-grained device memory, written by
@@ -285,7 +285,7 @@ struct hvws_ctx {
     // request and its bytes go through the pinned box and data area (round 3).
     void* d_door_req = nullptr;
     bool door_live = false;     // launched and not yet seen to have ended
-    bool door_wedged = false;   // its stream stayed busy past every bound: stream and mailbox are left alone
+    bool door_wedged = false;   // its launch ran on past every bound: queue and mailbox are left alone
     bool door_broken = false;   // a request went unanswered: this context launches per call from now on
     // The HIP runtime call this context's worker lifecycle or teardown is
     // in (nullptr: none): a wedge report or hvws_debug_dump names the call.
@@ -1488,16 +1488,14 @@ bool door_on(hvws_ctx* c) {
     return env != 0;
 }
 
-// Contexts that own a worker stream.  Lock order: g_door_m, then a
+// Contexts that own a worker queue.  Lock order: g_door_m, then a
 // context's door_m; nothing that holds a door_m takes g_door_m.
 std::mutex g_door_m;
 std::vector<hvws_ctx*> g_doors;
-// Drained worker streams of released contexts, per device, for the next
-// context's worker: a CU-masked stream is created once per concurrent worker
-// and never destroyed (its creation is the costliest step of a context's
-// first call, and destroying one hung a process's exit in round 3,
-// profiles/r3ab_raw).  Guarded by g_door_m.
-std::vector<std::pair<int, hipStream_t>> g_door_pool;
+// Idle worker queues of released contexts, for the next context's worker on
+// that device (creating one is the costliest step of a context's first call);
+// destroyed at exit.  Guarded by g_door_m.
+std::vector<door_queue*> g_door_pool;
 std::atomic<int> g_door_count{0};   // g_doors.size(): frees skip the lock when no worker exists
 void door_atexit();
 // Process-wide failure counts (hvws_door_health; the test session fails on
@@ -1551,7 +1549,7 @@ uint8_t* door_din(hvws_ctx* c) {
 // left as it was: the call itself succeeds.
 int door_ensure_impl(hvws_ctx* c);
 int door_ensure(hvws_ctx* c) {
-    if (c->door_stream) return HVWS_OK;
+    if (c->door_q) return HVWS_OK;
     char saved[sizeof g_err];
     memcpy(saved, g_err, sizeof g_err);
     const int rc = door_ensure_impl(c);
@@ -1564,16 +1562,11 @@ int door_ensure_impl(hvws_ctx* c) {
         std::lock_guard<std::mutex> lk(g_door_m);
         int same = 0;
         for (const hvws_ctx* o : g_doors) same += o->device == c->device;
-        if (same >= door_cap()) return set_err(HVWS_EINVAL, "k_door: %d worker streams on device %d already", same, c->device);
+        if (same >= door_cap()) return set_err(HVWS_EINVAL, "k_door: %d workers on device %d already", same, c->device);
     }
     HIP_OR(hipSetDevice(c->device), HVWS_EHIP);
     hipDeviceProp_t prop;
     HIP_OR(hipGetDeviceProperties(&prop, c->device), HVWS_EHIP);
-    // A CU-masked stream gets a hardware queue of its own instead of sharing
-    // one round-robin with other streams, so the resident kernel holds up no
-    // other work.  The mask names every CU.
-    std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0u);
-    for (int i = 0; i < prop.multiProcessorCount; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
     // The mailbox is fine-grained (polled, uncached); the data and record
     // areas are ordinary pinned memory: the worker's system-scope acquire on
     // each request invalidates its caches before it stages the bytes, and its
@@ -1587,7 +1580,7 @@ int door_ensure_impl(hvws_ctx* c) {
     memset(c->h_door.p, 0, sizeof(ddoor));
     if (!mapped<ddoor>(c->h_door) || !mapped<uint8_t>(c->h_door_data) || !mapped<drec>(c->h_door_rec))
         return set_err(HVWS_EHIP, "worker mailbox not device-mapped");
-    if (door_vram_enabled() && prop.isLargeBar) {
+    if (door_vram_enabled() && prop.isLargeBar && !c->d_door_req) {
         // With a large BAR, fine-grained device memory is mapped for the host
         // at its device address (profiles/r4a_raw/vram_probe.jsonl: host
         // stores and loads work, an 8 KiB memcpy into it takes 0.49 us);
@@ -1603,16 +1596,16 @@ int door_ensure_impl(hvws_ctx* c) {
     std::lock_guard<std::mutex> lk(g_door_m);
     int same = 0;   // again, under the lock that also registers this context
     for (const hvws_ctx* o : g_doors) same += o->device == c->device;
-    if (same >= door_cap()) return set_err(HVWS_EINVAL, "k_door: %d worker streams on device %d already", same, c->device);
+    if (same >= door_cap()) return set_err(HVWS_EINVAL, "k_door: %d workers on device %d already", same, c->device);
     for (size_t i = 0; i < g_door_pool.size(); ++i)
-        if (g_door_pool[i].first == c->device) {
-            c->door_stream = g_door_pool[i].second;
+        if (g_door_pool[i]->device == c->device) {
+            c->door_q = g_door_pool[i];
             g_door_pool.erase(g_door_pool.begin() + (long)i);
             break;
         }
-    if (!c->door_stream) {
-        in_call ic(c, "hipExtStreamCreateWithCUMask");
-        HIP_OR(hipExtStreamCreateWithCUMask(&c->door_stream, (uint32_t)mask.size(), mask.data()), HVWS_EHIP);
+    if (!c->door_q) {
+        in_call ic(c, "hsa_queue_create (worker queue)");
+        if (int rc = door_queue_create(c->device, &c->door_q)) return set_err(rc, "%s", door_queue_why());
     }
     // registered after the HIP runtime's own exit handlers, so it runs before them
     static const bool reg = (atexit(door_atexit), true);
@@ -1627,20 +1620,17 @@ uint64_t door_word(const hvws_ctx* c, const uint64_t& w) {
     return __atomic_load_n(&w, __ATOMIC_ACQUIRE);
 }
 
-// Wait up to `ms` for the worker stream to drain (hipStreamQuery, never an
-// unbounded hipStreamSynchronize: a worker that never ends must not hang its
-// host thread).  On a timeout the mailbox state goes to stderr and the
-// context is marked wedged: its stream and mailbox are never reused or freed.
+// Wait up to `ms` for the worker's last launch to end (its completion
+// signal: never an unbounded wait -- a worker that never ends must not hang
+// its host thread).  On a timeout the mailbox state goes to stderr and the
+// context is marked wedged: its queue and mailbox are never reused or freed.
 bool door_drain(hvws_ctx* c, int ms, const char* where) {
     const auto t0 = std::chrono::steady_clock::now();
-    in_call ic(c, "hipStreamQuery(worker stream)");
     for (;;) {
-        const hipError_t q = hipStreamQuery(c->door_stream);
-        if (q == hipSuccess) return true;
-        if (q != hipErrorNotReady) {
-            (void)hipGetLastError();
-            set_err(HVWS_EHIP, "k_door: %s", hipGetErrorString(q));
-            return true;   // the stream failed: nothing of the worker runs any more
+        if (door_queue_idle(c->door_q)) return true;
+        if (const int e = door_queue_error(c->door_q)) {
+            set_err(HVWS_EHIP, "k_door: worker queue error 0x%x", e);
+            return true;   // the queue failed: nothing of the worker runs any more
         }
         if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms)) break;
         usleep(20);
@@ -1648,7 +1638,7 @@ bool door_drain(hvws_ctx* c, int ms, const char* where) {
     const ddoor* b = c->h_door.as<ddoor>();
     const ddoor* rq = door_req(c);
     fprintf(stderr,
-            "[hvws] k_door (%s): ctx %p worker stream still busy after %d ms: seq %llu done %llu alive %llu "
+            "[hvws] k_door (%s): ctx %p worker launch still running after %d ms: seq %llu done %llu alive %llu "
             "exited %llu epoch %llu served %llu live %d\n",
             where, (void*)c, ms, (unsigned long long)__atomic_load_n(&rq->seq, __ATOMIC_ACQUIRE),
             (unsigned long long)door_word(c, b->done), (unsigned long long)door_word(c, b->alive),
@@ -1656,18 +1646,16 @@ bool door_drain(hvws_ctx* c, int ms, const char* where) {
             (unsigned long long)door_word(c, b->served), (int)c->door_live);
     c->door_wedged = true;
     g_door_wedged.fetch_add(1);
-    set_err(HVWS_EHIP, "k_door: the worker stream did not drain (%s)", where);
+    set_err(HVWS_EHIP, "k_door: the worker launch did not end (%s)", where);
     return false;
 }
 
 // Post the request already written into the mailbox and wait for it (the
 // caller holds c->door_m).  A worker is (re)launched when none is resident.
-// Whether the resident one has ended is read from the mailbox only: its last
-// store is `exited = epoch`.  Round 3 also took hipStreamQuery(door_stream)
-// == hipSuccess as "ended"; a worker that had cleared `alive` was then
-// treated as gone (its stream destroyed, its mailbox freed, or a second
-// worker queued behind it) while it could still be running.
-// The stream is asked only for errors (a kernel fault surfaces there).
+// Whether the resident one has ended is read from the mailbox: its last
+// store is `exited = epoch`; a relaunch also waits for the last launch's
+// completion signal (door_drain), so two workers never share the mailbox.
+// The queue's error state says whether a kernel fault ended it.
 int door_call(hvws_ctx* c) {
     ddoor* b = c->h_door.as<ddoor>();
     ddoor* rq = door_req(c);
@@ -1689,19 +1677,27 @@ int door_call(hvws_ctx* c) {
             ++c->door_epoch;
             const ddoor* dreq = c->d_door_req ? (const ddoor*)c->d_door_req : mapped<ddoor>(c->h_door);
             const uint8_t* ddin = c->d_door_req ? (const uint8_t*)c->d_door_req + 256 : mapped<uint8_t>(c->h_door_data);
-            in_call ic(c, "hipLaunchKernel(k_door)");
-            HIP_OR(launch_door(dreq, mapped<ddoor>(c->h_door), ddin, mapped<uint8_t>(c->h_door_data),
-                               mapped<drec>(c->h_door_rec), c->d_door_slot.as<drec>(), door_idle_ticks(),
-                               __atomic_load_n(&b->done, __ATOMIC_ACQUIRE), c->door_epoch, c->door_stream),
-                   HVWS_EHIP);
+            door_args a;
+            a.req = dreq;
+            a.box = mapped<ddoor>(c->h_door);
+            a.din = ddin;
+            a.dout = mapped<uint8_t>(c->h_door_data);
+            a.h_rec = mapped<drec>(c->h_door_rec);
+            a.d_slot = c->d_door_slot.as<drec>();
+            a.idle_ticks = door_idle_ticks();
+            a.first_seq = __atomic_load_n(&b->done, __ATOMIC_ACQUIRE);
+            a.epoch = c->door_epoch;
+            a.flags = door_flags();
+            in_call ic(c, "AQL dispatch of k_door (worker queue)");
+            if (int rc = door_queue_launch(c->door_q, &a, (uint32_t)sizeof a)) return set_err(rc, "%s", door_queue_why());
             c->door_live = true;
             ++c->door_launches;
             continue;
         }
         if (door_word(c, b->exited) == c->door_epoch) {
             // The worker has ended; its last look at seq came before this
-            // request.  The stream drains (the wave retires) before the next
-            // launch, so two workers never share the mailbox.
+            // request.  Its launch completes (the wave retires) before the
+            // next launch, so two workers never share the mailbox.
             if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) return HVWS_OK;
             if (!door_drain(c, 5000, "relaunch")) return HVWS_EHIP;
             c->door_live = false;
@@ -1711,8 +1707,7 @@ int door_call(hvws_ctx* c) {
             const auto now = std::chrono::steady_clock::now();
             if (now >= next_query) {
                 next_query = now + std::chrono::microseconds(100);
-                const hipError_t q = hipStreamQuery(c->door_stream);
-                if (q != hipSuccess && q != hipErrorNotReady) return set_err(HVWS_EHIP, "k_door: %s", hipGetErrorString(q));
+                if (const int e = door_queue_error(c->door_q)) return set_err(HVWS_EHIP, "k_door: worker queue error 0x%x", e);
                 if (now - t0 > std::chrono::seconds(10)) return set_err(HVWS_EHIP, "k_door: no answer in 10 s");
             }
         }
@@ -1724,7 +1719,7 @@ int door_call(hvws_ctx* c) {
 // holds c->door_m): context teardown, a free, a thread's exit, the door
 // switched off.
 void door_park(hvws_ctx* c) {
-    if (!c->door_stream || !c->door_live || c->door_wedged) return;
+    if (!c->door_q || !c->door_live || c->door_wedged) return;
     ddoor* b = c->h_door.as<ddoor>();
     if (door_word(c, b->exited) != c->door_epoch) {
         door_req(c)->op = DOOR_EXIT;
@@ -1766,7 +1761,7 @@ void door_park_device() {
 // say it has ended; a context whose owner holds its lock past 100 ms is left
 // as it is.
 void door_quit_nohip(hvws_ctx* c) {
-    if (!c->door_stream || !c->door_live) return;
+    if (!c->door_q || !c->door_live) return;
     ddoor* b = c->h_door.as<ddoor>();
     if (door_word(c, b->exited) != c->door_epoch) {
         ddoor* rq = door_req(c);
@@ -1782,18 +1777,38 @@ void door_quit_nohip(hvws_ctx* c) {
     c->door_live = false;
 }
 
+// At exit, once every worker has ended (its launch's completion signal),
+// the worker queues are destroyed (HSA calls only; this handler runs before
+// the HIP runtime's own, so the HSA runtime is still up).  A process that
+// ended with a worker queue alive crashed under rocprofv3; a
+// queue whose worker did not end is left alone.
 void door_atexit() {
     std::lock_guard<std::mutex> lk(g_door_m);
     for (hvws_ctx* c : g_doors) {
         std::unique_lock<std::mutex> cl(c->door_m, std::defer_lock);
         const auto t0 = std::chrono::steady_clock::now();
         while (!cl.try_lock() && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(100)) usleep(100);
-        if (cl.owns_lock()) door_quit_nohip(c);
+        if (!cl.owns_lock()) continue;
+        door_quit_nohip(c);
+        if (!c->door_q || c->door_wedged) continue;
+        const auto t1 = std::chrono::steady_clock::now();
+        while (!door_queue_idle(c->door_q) && std::chrono::steady_clock::now() - t1 < std::chrono::milliseconds(100))
+            usleep(50);
+        if (door_queue_idle(c->door_q)) {
+            c->door_q->at_exit = true;
+            door_queue_destroy(c->door_q);
+            c->door_q = nullptr;
+        }
     }
+    for (door_queue* q : g_door_pool) {
+        q->at_exit = true;
+        door_queue_destroy(q);
+    }
+    g_door_pool.clear();
 }
 
 void door_release(hvws_ctx* c) {
-    if (!c->door_stream) return;
+    if (!c->door_q) return;
     {
         std::lock_guard<std::mutex> lk(g_door_m);
         {
@@ -1804,26 +1819,21 @@ void door_release(hvws_ctx* c) {
         g_door_count.store((int)g_doors.size(), std::memory_order_release);
     }
     if (c->door_wedged || !door_drain(c, 5000, "release")) {
-        // a worker that may still run: its stream and the memory it writes stay
-        fprintf(stderr, "[hvws] k_door: ctx %p released with its worker stream wedged; stream and mailbox leaked\n",
+        // a worker that may still run: its queue and the memory it writes stay
+        fprintf(stderr, "[hvws] k_door: ctx %p released with its worker launch wedged; queue and mailbox leaked\n",
                 (void*)c);
-        c->door_stream = nullptr;
+        c->door_q = nullptr;
         c->h_door.p = c->h_door_data.p = c->h_door_rec.p = nullptr;
         c->d_door_slot.p = nullptr;
         c->d_door_req = nullptr;
         return;
     }
     {
-        // drained: the next context's worker takes it.  A CU-masked stream is
-        // never destroyed: destroying one is the cause of the r4k / r4n hangs
-        // (after hipStreamDestroy of the worker stream the
-        // context's own hipStreamDestroy blocked for good, reproduced 2 of 2
-        // times by scripts/probe/door_first at commit 605ad80, never in 300
-        // processes that kept the stream).
+        // ended: the next context's worker takes the queue (destroyed at exit)
         std::lock_guard<std::mutex> lk(g_door_m);
-        g_door_pool.emplace_back(c->device, c->door_stream);
+        g_door_pool.push_back(c->door_q);
     }
-    c->door_stream = nullptr;
+    c->door_q = nullptr;
     in_call ic(c, "hipHostFree / hipFree (worker mailbox and areas)");
     c->h_door.release();
     c->h_door_data.release();
@@ -2050,7 +2060,7 @@ int hvws_debug_dump(int fd) {
         dprintf(fd, " | wedged %d broken %d | in %s | last scan path %d, have_scan %d\n", (int)c->door_wedged,
                 (int)c->door_broken, at ? at : "-", c->scan_path, (int)c->have_scan);
     }
-    dprintf(fd, "libhvws: worker streams wedged %llu, requests unanswered %llu (process)\n",
+    dprintf(fd, "libhvws: worker launches wedged %llu, requests unanswered %llu (process)\n",
             (unsigned long long)g_door_wedged.load(), (unsigned long long)g_door_failed.load());
     for (hvws_ctx* c : all) {
         if (c->at.load()) {   // its streams may be going away under that call: not queried
@@ -2062,9 +2072,12 @@ int hvws_debug_dump(int fd) {
             const char* n;
             hipStream_t s;
         } ss[] = {{"stream", c->stream}, {"sstream", c->sstream}, {"copy_in", c->copy_in},
-                  {"copy_out", c->copy_out}, {"door", c->door_stream}};
+                  {"copy_out", c->copy_out}};
         for (const auto& x : ss)
             if (x.s) dprintf(fd, " %s=%s", x.n, qname(hipStreamQuery(x.s)));
+        if (c->door_q)
+            dprintf(fd, " worker-queue=%s error=0x%x", door_queue_idle(c->door_q) ? "idle" : "running",
+                    door_queue_error(c->door_q));
         dprintf(fd, "\n");
     }
     return (int)all.size();
@@ -2992,7 +3005,7 @@ int hvws_door_info(hvws_ctx* c, uint64_t out[2]) {
     if (!c) c = hvws::thread_ctx();
     if (!out) return set_err(HVWS_EINVAL, "null output");
     out[0] = c->d_door_req ? 1 : 0;
-    out[1] = c->door_stream ? 1 : 0;
+    out[1] = c->door_q ? 1 : 0;
     return HVWS_OK;
 }
 

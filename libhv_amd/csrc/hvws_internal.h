@@ -2,11 +2,13 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
 #include <stddef.h>
 #include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
 #include <functional>
 
 #include "websocket_parser.h"
@@ -399,8 +401,43 @@ static_assert(offsetof(ddoor, carry) == 40 && offsetof(ddoor, len) == 16 && offs
 // memory the host writes through the PCIe BAR, or the pinned box itself;
 // din: the request's bytes (same choice); dout: results (pinned host; may equal
 // din when both are the pinned area).
-hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
-                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st);
+// k_door's kernel arguments, as an AQL dispatch of it reads them (the
+// kernel's explicit arguments in order; it uses no hidden ones).
+struct door_args {
+    const ddoor* req;
+    ddoor* box;
+    const uint8_t* din;
+    uint8_t* dout;
+    drec* h_rec;
+    drec* d_slot;
+    uint64_t idle_ticks, first_seq, epoch;
+    uint32_t flags;
+};
+uint32_t door_flags();                      // k_door's flags ($HVWS_EXPERIMENT door_stamps)
+hipError_t door_anchor(void** dev_addr);    // a device symbol of k_door's code object (loads it on the device)
+const char* door_kernel_symbol_prefix();    // k_door's symbol name, up to its argument types
+
+// The worker's own HSA queue (hvws_doorq.cpp): k_door dispatched by one AQL
+// packet per launch; `done` (its completion signal) reaches 0 when the launch
+// has ended; destroyed only then.
+struct door_queue {
+    hsa_queue_t* q = nullptr;
+    hsa_signal_t done{0};
+    hsa_agent_t agent{0};
+    uint64_t object = 0;                   // k_door's kernel descriptor
+    uint32_t group = 0, priv = 0, kernarg_size = 0;
+    void* kernarg = nullptr;               // pinned host
+    void* kernarg_dev = nullptr;
+    int device = -1;
+    bool at_exit = false;                  // destroyed from the exit handler: no HIP call
+    std::atomic<int> error{0};             // queue error reported by the runtime (hsa_status_t)
+};
+int  door_queue_create(int device, door_queue** out);
+int  door_queue_launch(door_queue* q, const void* args, uint32_t nargs);
+bool door_queue_idle(door_queue* q);     // the last launch has ended (or none was made)
+int  door_queue_error(door_queue* q);    // 0, or the queue's error status
+const char* door_queue_why();            // what the last failing door_queue_* call of this thread hit
+void door_queue_destroy(door_queue* q);  // only when idle
 
 // Host copy pool (hvws_hostpool.cpp): fn(i) for i in [0, n) on up to
 // copy_width() threads (the caller included; serial when another caller

@@ -1091,18 +1091,16 @@ __device__ __forceinline__ void door_size(const uint32_t* l, uint32_t q, uint32_
     }
 }
 
-// k_door's flags (launch_door reads them from the environment once)
-constexpr uint32_t DOOR_F_WALK = 1u;      // door_walk, not walk_frames ($HVWS_EXPERIMENT door_walk, default on)
-constexpr uint32_t DOOR_F_NT = 2u;        // nontemporal loads of the data area (door_nt)
-constexpr uint32_t DOOR_F_PRELOAD = 4u;   // data loads in the request's round trip (door_preload)
+// k_door's flags (door_flags reads them from the environment once)
 constexpr uint32_t DOOR_F_STAMPS = 8u;   // realtime stamps per phase (door_stamps; scripts/probe/door_phases.py)
-// DOOR_XOR (a masked websocket_build_frame payload, websocket_decode) in
+// DOOR_XOR (a masked websocket_build_frame payload, websocket_decode) runs in
 // registers, its result written through the L2 (sc0 sc1), and `done` after
 // those stores' acks: no LDS staging, no barrier between the two, no L2
 // writeback.  A masked 125 B build: 3.41-3.46 us per call against 4.49-4.90
-// (profiles/r5_raw/door, r5x2).  $HVWS_EXPERIMENT door_xor_direct=0: the LDS path.
-// (For a read's ~500 result stores the same trade lost: 13-14 us per call.)
-constexpr uint32_t DOOR_F_XDIRECT = 16u;
+// staged in LDS (profiles/r5_raw/door, r5x2).  (For a read's ~500 result
+// stores the same trade lost: 13-14 us per call.)  Round 5's other worker
+// variants -- walk_frames instead of door_walk, non-temporal staging loads,
+// the data preload -- lost and were removed in round 6.
 
 // A phase stamp (DOOR_F_STAMPS): each realtime-clock read is a scalar
 // memory round trip that the wave waits for, so stamps are off by default.
@@ -1110,24 +1108,17 @@ __device__ __forceinline__ uint64_t door_now(uint32_t flags) {
     return (flags & DOOR_F_STAMPS) ? (uint64_t)wall_clock64() : 0ull;
 }
 
-// Chunks [c_lo, c_hi) of the data area (both multiples of 64) into LDS at the
-// same offsets by LDS-DMA: no registers (an array of 16-byte values per
-// thread cost the worker ~1000 register moves, ~2 us per read); a wave
-// writes 64 consecutive chunks per instruction (lane-linear destination).
-// The caller waits for vmcnt(0) before a barrier.
-// w0: the first wave that stages (the preload leaves wave 0 to the request
-// block: its request load would otherwise wait behind these in vmcnt order).
-__device__ __forceinline__ void door_stage(const uint8_t* din, uint8_t* lds, uint32_t c_lo, uint32_t c_hi,
-                                           uint32_t flags, uint32_t w0 = 0) {
+// Chunks [0, c_hi) of the data area (a multiple of 64) into LDS at the same
+// offsets by LDS-DMA: no registers (an array of 16-byte values per thread
+// cost the worker ~1000 register moves, ~2 us per read); a wave writes 64
+// consecutive chunks per instruction (lane-linear destination).  The caller
+// waits for vmcnt(0) before a barrier.
+__device__ __forceinline__ void door_stage(const uint8_t* din, uint8_t* lds, uint32_t c_hi) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    if (wave < w0) return;
-    for (uint32_t cb = c_lo + (wave - w0) * 64u; cb < c_hi; cb += kDoorThreads - 64u * w0) {
+    for (uint32_t cb = wave * 64u; cb < c_hi; cb += kDoorThreads) {
         const auto* g = (const __attribute__((address_space(1))) void*)(din + (uint64_t)(cb + lane) * 16u);
         auto* l = (__attribute__((address_space(3))) void*)(lds + (uint64_t)cb * 16u);
-        if (flags & DOOR_F_NT)
-            __builtin_amdgcn_global_load_lds(g, l, 16, 0, 2);
-        else
-            __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
     }
 }
 
@@ -1284,11 +1275,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     uint8_t* lds = reinterpret_cast<uint8_t*>(lds_door);
     uint64_t last = first_seq;
     uint64_t served = 0;
-    const uint32_t walk = flags & DOOR_F_WALK;
-    // DOOR_F_PRELOAD: waves 1-3 load the data area's first chunks in the
-    // request's own round trip, as many as the previous request had (wave 0
-    // reads the request block); the data area follows it in device memory.
-    uint32_t guess = 0;
     __shared__ uint64_t s_t[7];
     uint64_t rel_prev = 0;   // thread 0: realtime ticks of the previous request's release
     __shared__ uint64_t s_req[16];
@@ -1328,7 +1314,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             if (tid == 0) __hip_atomic_store(&box->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        if (guess) door_stage(din, lds, 0, guess, flags, 1);   // waves 1-3, beside the request's own load
         if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
             const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(req) + tid);
             reinterpret_cast<u32x4*>(s_req)[tid] = piece;
@@ -1363,7 +1348,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         const uint64_t L = s_len;
         const uint64_t nch = (L + 15u) / 16u;   // the data area has slack past L: whole chunks throughout
         const uint32_t ngr = (uint32_t)((nch + 63u) & ~63ull);   // whole wave groups of 64 chunks (<= kDoorMax)
-        const bool xdirect = op == DOOR_XOR && (flags & DOOR_F_XDIRECT);
+        const bool xdirect = op == DOOR_XOR;
         if (xdirect) {
             const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
             const u32x4 k4 = u32x4{kw, kw, kw, kw};
@@ -1372,21 +1357,11 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dout + c * 16u), "v"(v) : "memory");
             }
         } else {
-        // the rest of the data area into LDS (all in flight), then wait
-        door_stage(din, lds, guess, ngr, flags);
-        if (flags & DOOR_F_PRELOAD) guess = ngr;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the data area into LDS (all in flight), then wait
+            door_stage(din, lds, ngr);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (xdirect) {
-        } else if (op == DOOR_XOR) {
-            // websocket_decode over the data area (16-byte aligned): byte i
-            // uses mask[(i + phase) & 3]
-            __syncthreads();
-            const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
-            const u32x4 k4 = u32x4{kw, kw, kw, kw};
-            for (uint64_t c = tid; c < nch; c += kDoorThreads)
-                *reinterpret_cast<u32x4*>(dout + c * 16u) = *reinterpret_cast<const u32x4*>(lds + c * 16u) ^ k4;
-        } else {
+        if (!xdirect) {
             __syncthreads();
             if (tid == 0) s_t[1] = door_now(flags);
             if (tid < 64) {   // wave 0: carried-in frame, walk, tail (k_small's code)
@@ -1436,10 +1411,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     }
                 }
                 if (tid == 0) s_t[4] = door_now(flags);
-                if (walk)
-                    door_walk(lds, L, st, pos, n, vmask, s_fpos, (flags & DOOR_F_STAMPS) ? s_w : nullptr, emit);
-                else
-                    walk_frames<true>(lds, L, 0, L, st, pos, n, vmask, emit);
+                door_walk(lds, L, st, pos, n, vmask, s_fpos, (flags & DOOR_F_STAMPS) ? s_w : nullptr, emit);
                 if (tid == 0) {
                     s_n = n;
                     s_carry = st;
@@ -1539,18 +1511,19 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     }
 }
 
-hipError_t launch_door(const ddoor* req, ddoor* box, const uint8_t* din, uint8_t* dout, drec* h_rec, drec* d_slot,
-                       uint64_t idle_ticks, uint64_t first_seq, uint64_t epoch, hipStream_t st) {
-    // $HVWS_EXPERIMENT door_walk=0: the speculative wave-wide walk (k_small's)
-    // instead of door_walk; door_nt, door_preload, door_stamps
-    auto knob = [](const char* name, uint32_t dflt) { return experiment(name) ? (uint32_t)atoi(experiment(name)) : dflt; };
-    static const uint32_t flags = (knob("door_walk", 1) ? DOOR_F_WALK : 0u) | (knob("door_nt", 0) ? DOOR_F_NT : 0u) |
-                                  (knob("door_preload", 0) ? DOOR_F_PRELOAD : 0u) | (knob("door_stamps", 0) ? DOOR_F_STAMPS : 0u) |
-                                  (knob("door_xor_direct", 1) ? DOOR_F_XDIRECT : 0u);
-    hipLaunchKernelGGL(k_door, dim3(1), dim3(kDoorThreads), kDoorMax + 32, st, req, box, din, dout, h_rec, d_slot,
-                       idle_ticks, first_seq, epoch, flags);
-    return hipGetLastError();
+// k_door's flags ($HVWS_EXPERIMENT door_stamps: the worker's phase stamps,
+// scripts/probe/door_phases.py)
+uint32_t door_flags() {
+    static const uint32_t flags = experiment("door_stamps") && atoi(experiment("door_stamps")) ? DOOR_F_STAMPS : 0u;
+    return flags;
 }
+
+// A device symbol of this code object: its address names the executable the
+// HIP runtime loaded for the device, in which the worker queue finds k_door
+// (hvws_doorq.cpp); asking for it loads the code object.
+__device__ uint32_t g_door_anchor;
+hipError_t door_anchor(void** dev_addr) { return hipGetSymbolAddress(dev_addr, HIP_SYMBOL(g_door_anchor)); }
+const char* door_kernel_symbol_prefix() { return "_ZN4hvws6k_doorE"; }
 
 // ------------------------------------------------------------- k_offsets
 // Exclusive scan of counts[0..nseg) into bases[], total into *total.  One

@@ -31,7 +31,7 @@ assert H.run_messages("gpu", data, [len(data)]) == H.run_messages("oracle", data
 st = (ctypes.c_uint64 * 4)()
 L.hvws_door_stats(None, st)
 print(f"[exit_probe] door stats {list(st)} (served > 0: the read went to the worker)", flush=True)
-assert st[1] > 0, "the read did not go to the worker"
+assert st[1] > 0 or os.environ.get("HVWS_DOOR") == "0", "the read did not go to the worker"
 if os.environ.get("EXIT_PROBE_RELEASE") == "1":
     L.hvws_thread_release()
     print("[exit_probe] thread context released", flush=True)
@@ -42,4 +42,5 @@ def _maps():
     print("[exit_probe] maps written; exiting", flush=True)
 
 
-atexit.register(_maps)
+if os.environ.get("EXIT_PROBE_MAPS", "1") == "1":
+    atexit.register(_maps)

@@ -475,3 +475,22 @@ def _oracle_batch_one(buf):
     import test_gpu_parity as P
 
     return P._oracle_batch(buf, [(0, len(buf))], None)
+
+
+@pytest.mark.parametrize("release", [False, True])
+def test_child_process_with_worker_exits_cleanly(release):
+    """a process whose reference-API read went to the
+    resident worker exits with status 0 -- its worker asked home and its
+    worker queue destroyed by the exit handler (hvws_doorq.cpp), whether the
+    thread's context was released first or not (scripts/probe/exit_probe.py,
+    run as a child process as a libhv server process would run)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, EXIT_PROBE_MAPS="0", EXIT_PROBE_RELEASE="1" if release else "0")
+    env.pop("HVWS_DOOR", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "probe", "exit_probe.py"), "test"], env=env,
+                       capture_output=True, text=True, timeout=90)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
+    assert "the read went to the worker" in p.stdout

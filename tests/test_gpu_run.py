@@ -295,9 +295,9 @@ def test_run_repair_key_from_hypothesis_layout(fresh):
 
     parts = []
     for s in range(6):
-        lens = [100] * 30
+        lens = [100] * 160   # 17 KB segments: no tile holds a third segment (those go to the repair whole)
         if s % 2:
-            lens[5 + s] = 60   # the frames after it start 40 B before the hypothesis says
+            lens[5 + 20 * s] = 60   # the frames after it start 40 B before the hypothesis says
         parts.append(b"".join(frame(n) for n in lens))
     buf, segs = _segments(parts)
     recs, carry, started, exp = _oracle_batch(buf, segs, None)
