@@ -467,10 +467,10 @@ bool run_env() {
 }
 
 
-bool host_order() {
-    static const int v = experiment("host_order") ? atoi(experiment("host_order")) : 1;
-    return v != 0;
-}
+// Pipelined steps: the host queues the unmask once the scan's last kernel
+// has published (always since round 4; round 6 removed the switch back to a
+// cross-stream event).
+constexpr bool host_order() { return true; }
 
 int wait_status(hvws_ctx* c, uint64_t seq, bool tiles = false) {
     const dspec_status* st = c->h_status.as<dspec_status>();
@@ -633,9 +633,7 @@ hipError_t issue_unmask(hvws_ctx* c, uint8_t* d_rx, uint64_t rx_len, bool joined
     // An untimed pipelined step attaches its set's free event to its last
     // dispatch (RUN: the repair) instead of recording it in a marker packet after it:
     // c2 0.355-0.356 vs 0.358 ms per step (profiles/r5_raw/events, fa*).
-    // $HVWS_EXPERIMENT free_attach=0: the marker.
-    static const bool free_attach = !(experiment("free_attach") && atoi(experiment("free_attach")) == 0);
-    const bool attach_free = piped && !timed && free_attach;
+    const bool attach_free = piped && !timed;
     if (c->run_active) {   // the RUN unmask and its repair pass (the stop event rides on the repair)
         if ((e = launch_unmask_run(d_rx, rx_len, c->T().runs.as<drun>(), c->T().run_trun.as<dtrun>(),
                                    c->nseg, c->T().run_fail.as<uint32_t>(), mapped<dspec_status>(c->h_status),
@@ -2172,11 +2170,10 @@ hvws_ctx* hvws_ctx_create(int device) {
     // The pipelined scan stream at the highest priority: a scan kernel of
     // ~1000 workgroups queued while an unmask grid is being dispatched waits
     // for that whole grid at normal priority, but is dispatched beside it at
-    // high priority (scripts/dispatch_probe.hip).  $HVWS_EXPERIMENT scan_priority=0: normal.
+    // high priority (scripts/dispatch_probe.hip).
     int prio_least = 0, prio_greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-    const char* sp_env = experiment("scan_priority");
-    const int scan_prio = sp_env && atoi(sp_env) == 0 ? prio_least : prio_greatest;
+    const int scan_prio = prio_greatest;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess ||
@@ -2910,15 +2907,15 @@ int hvws_build_frames(hvws_ctx* c, uint8_t* d_out, uint64_t out_cap, const uint8
     // k_build_id, which is gone, profiles/r4v_raw)
     const int v = tx_variant(total, n);
     c->tx_variant = v;
-    // each tile's source span first ($HVWS_EXPERIMENT build_spans=0: the records-first tiles)
-    const char* sp_env = experiment("build_spans");
-    const bool spans_ok = !sp_env || atoi(sp_env) != 0;
+    // each tile's source span first (round 4: records-first tiles lost, and
+    // their switch went in round 6)
+    const bool spans_ok = true;
     const uint64_t tile = tx_tile(v);
     const uint64_t ntiles = (total + tile - 1) / tile;
     // A uniform layout (every frame the same size and length, payload offsets
     // a + k * b, b >= 0) needs no tile index: each tile finds its frames and
-    // source span from its position ($HVWS_EXPERIMENT build_uni=0: the index anyway).
-    static const bool uni_ok = !experiment("build_uni") || atoi(experiment("build_uni")) != 0;
+    // source span from its position.
+    constexpr bool uni_ok = true;
     // (payload steps shorter than a payload would make a tile's pieces
     // overlap out of order: the index handles those)
     // (small frames only, the lean form: at 64 KiB frames the index is ~0.1 %

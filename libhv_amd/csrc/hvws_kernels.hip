@@ -2853,26 +2853,19 @@ hipError_t launch_tile_class(const uint64_t* off, const uint64_t* len, const uin
     return hipGetLastError();
 }
 
-// Unmask geometries (threads, chunks per thread, XCD order).  Default from the
-// on-device sweep; $HVWS_EXPERIMENT unmask=<index> selects another for experiments.
+// Unmask geometries (threads, chunks per thread, XCD order): the two the
+// batch size picks between.  Rounds 1-5 swept ten more (128 x 2 ... 1024 x 1,
+// 64 x 8, 256 x 8, linear and XCD orders; profiles/r2c_raw, r2l_raw); none
+// won anywhere, and round 6 removed them.  hvws_set_unmask_variant (tests,
+// bench.py --sweep-unmask) or $HVWS_EXPERIMENT unmask=<index> forces one.
 struct unmask_geom {
     int threads, unroll;
     bool swz;
 };
-// X(index, threads, chunks per thread, XCD order); index 0 is the default.
+// X(index, threads, chunks per thread, XCD order)
 #define HVWS_UNMASK_GEOMS(X)                                                              \
     X(0, 256, 4, true)                                                                    \
-    X(1, 128, 2, true)                                                                    \
-    X(2, 512, 1, true)                                                                    \
-    X(3, 128, 4, true)                                                                    \
-    X(4, 1024, 1, true)                                                                   \
-    X(5, 256, 2, true)                                                                    \
-    X(6, 256, 8, true)                                                                    \
-    X(7, 256, 8, false)                                                                   \
-    X(8, 64, 8, true)                                                                     \
-    X(9, 256, 4, false)                                                                   \
-    X(10, 256, 2, false)                                                                  \
-    X(11, 512, 2, false)
+    X(1, 512, 2, false)
 #define HVWS_GEOM_ENTRY(i, t, u, s) {t, u, s},
 static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
 
@@ -2884,7 +2877,7 @@ static const unmask_geom kGeoms[] = {HVWS_UNMASK_GEOMS(HVWS_GEOM_ENTRY)};
 // XCD-contiguous order wins, 20.92 vs 22.76 ms.  The single-step sweep over
 // uniform batches (profiles/r2c_raw/size_sweep.jsonl) puts the crossover at
 // 16 GiB.
-constexpr int kGeomSmall = 11;                        // 512 x 2, linear
+constexpr int kGeomSmall = 1;                         // 512 x 2, linear
 constexpr int kGeomLarge = 0;                         // 256 x 4, XCD-contiguous
 constexpr uint64_t kGeomLinearMax = 16ull << 30;     // bytes
 
@@ -2945,11 +2938,6 @@ static uint64_t max_tiles_per_launch(int threads) {
 #define HVWS_GEOM_CASE_EXT(i, t, u, s) \
     case i: hipExtLaunchKernelGGL((HVWS_K<t, u, s>), HVWS_EXT_ARGS); break;
 
-static uint32_t unmask_lds() {
-    static const uint32_t b = experiment("unmask_lds") ? (uint32_t)atoi(experiment("unmask_lds")) : 0u;
-    return b;
-}
-
 hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, const uint32_t* tile_first,
                          const uint32_t* tile_key, const uint8_t* tile_kind, const uint64_t* nfr_dev, hipStream_t st,
                          uint32_t pieces, hipEvent_t ev_start, hipEvent_t ev_stop) {
@@ -2974,12 +2962,10 @@ hipError_t launch_unmask(int variant, uint8_t* rx, uint64_t rx_len, dframes fr, 
         const uint64_t ntiles = ntiles_all - tile0 < cap ? ntiles_all - tile0 : cap;
         const hipEvent_t e0 = tile0 == 0 ? ev_start : nullptr;
         const hipEvent_t e1 = tile0 + ntiles >= ntiles_all ? ev_stop : nullptr;
-// $HVWS_EXPERIMENT unmask_lds (experiments): dynamic LDS bytes per workgroup, to cap how
-// many unmask workgroups a CU holds beside the next batch's scan
 #define HVWS_K k_unmask
-#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), unmask_lds(), st, rx, rx_len, fr.pay_off, fr.pay_len, \
+#define HVWS_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, rx, rx_len, fr.pay_off, fr.pay_len, \
                   fr.keyrot, tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
-#define HVWS_EXT_ARGS dim3((uint32_t)ntiles), dim3(threads), unmask_lds(), st, e0, e1, 0u, rx, rx_len, fr.pay_off, \
+#define HVWS_EXT_ARGS dim3((uint32_t)ntiles), dim3(threads), 0, st, e0, e1, 0u, rx, rx_len, fr.pay_off, \
                       fr.pay_len, fr.keyrot, tile_first, tile_key, tile_kind, nfr_dev, tile0, ntiles
         if (e0 || e1) {
             switch (variant) { HVWS_UNMASK_GEOMS(HVWS_GEOM_CASE_EXT) default: return hipErrorInvalidValue; }

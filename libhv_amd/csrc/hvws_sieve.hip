@@ -268,7 +268,6 @@ struct sieve_lds {
 // each thread's 32 positions waited for the busiest lane); survivors land in
 // the tile's bitmaps.  Two block barriers per tile: tile + candidate words
 // staged, and survivors complete.
-template <int MODE>
 __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, sieve_lds& sh, tile_regs& r, int par,
                                            uint64_t T0, bool have_next, uint64_t next_T0, uint64_t sb, uint64_t L,
                                            uint64_t pos) {
@@ -281,13 +280,8 @@ __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, s
     if (halo_lane(t)) sh.cb[2 * SV_THREADS + (t >> 3)] = chunk_candidates(r.v[2], r.nx[2]);
     sh.sbits[par][t] = 0;
     sh.pbits[par][t] = 0;
-    if (MODE != 4 && have_next) load_tile(rx, rx_len, next_T0, r);   // MODE 4: no prefetch (registers)
+    if (have_next) load_tile(rx, rx_len, next_T0, r);   // the next tile's loads under this one's work
     __syncthreads();
-    if (MODE == 2) {   // timing experiment: staging and candidate words only
-        if (w0 == 0x12345678u) sh.sbits[par][0] = w1;
-        __syncthreads();
-        return;
-    }
     const uint64_t lo = sb + pos, hi = sb + L;
     const uint32_t qlo = lo > T0 ? (uint32_t)(lo - T0) : 0u;
     const uint32_t qhi = hi - T0 < SV_TILE ? (uint32_t)(hi - T0) : SV_TILE;
@@ -312,7 +306,7 @@ __device__ __forceinline__ void sieve_tile(const uint8_t* rx, uint64_t rx_len, s
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t nl = wtot - base < SV_WLIST ? wtot - base : SV_WLIST;
-        for (uint32_t e = lane; e < nl && MODE != 1; e += 64) {   // MODE 1 (timing): lists only
+        for (uint32_t e = lane; e < nl; e += 64) {
             const uint32_t q = list[e];
             if (q < qlo || q >= qhi) continue;
             uint32_t v = quick_verdict(sh.l, sh.cb, q, hrel);
@@ -373,7 +367,6 @@ __device__ __forceinline__ void record_tile(const sieve_lds& sh, int par, uint64
 }
 
 // COUNT: tcount[t] = survivors of tile t, recorded by record_tile.
-template <int MODE>
 __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_sieve_count(const uint8_t* __restrict__ rx, uint64_t rx_len,
                                                             const dseg* __restrict__ segs, const dmid* __restrict__ mid,
                                                             const uint64_t* __restrict__ npred, uint64_t sieve_min,
@@ -402,13 +395,7 @@ __global__ __launch_bounds__(SV_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     for (; t < ntiles; t += gridDim.x, par ^= 1) {
         const uint64_t tn = t + gridDim.x;
         const uint64_t T0 = A0 + sv_tile(t, rt, wt) * SV_TILE, Tn = A0 + sv_tile(tn, rt, wt) * SV_TILE;
-        if (MODE == 3) {   // timing experiment: the loads alone
-            if (tn < ntiles) load_tile(rx, rx_len, Tn, r);
-            if (threadIdx.x == 0) tcount[t] = r.v[0].x == 0x12345678u && r.v[1].y == 7u ? 1u : 0u;
-            continue;
-        }
-        if (MODE == 4 && t != blockIdx.x) load_tile(rx, rx_len, T0, r);
-        sieve_tile<MODE>(rx, rx_len, sh, r, par, T0, tn < ntiles, Tn, sb, L, pos);
+        sieve_tile(rx, rx_len, sh, r, par, T0, tn < ntiles, Tn, sb, L, pos);
         // wave 0 records while the other waves stage the next tile (the
         // bitmaps alternate by parity; the next barrier orders the rest)
         if (threadIdx.x < 64) record_tile(sh, par, t, tcount, slot, pool, pool_n, pool_cap);
@@ -822,23 +809,11 @@ hipError_t launch_sieve(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
     dsieve* sv = reinterpret_cast<dsieve*>(b.state);
     hipError_t e = hipMemsetAsync(b.pool_n, 0, 8, st);
     if (e != hipSuccess) return e;
-    // $HVWS_EXPERIMENT sieve_mode (timing experiments only): 1 lists without checks,
-    // 2 staging + candidate words, 3 loads alone -- these find no survivors,
-    // so the chain is empty and the exact walk does everything (results stay
-    // exact, only slow); 4 = without the next tile's register prefetch.
-    static const int mode = experiment("sieve_mode") ? atoi(experiment("sieve_mode")) : 0;
-#define HVWS_SIEVE_COUNT(M)                                                                                     \
-    hipLaunchKernelGGL(k_sieve_count<M>, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred,    \
-                       sieve_min(), b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), \
-                       b.capS, ntm, sv, b.rt, b.wt)
-    switch (mode) {
-        case 1: HVWS_SIEVE_COUNT(1); break;
-        case 2: HVWS_SIEVE_COUNT(2); break;
-        case 3: HVWS_SIEVE_COUNT(3); break;
-        case 4: HVWS_SIEVE_COUNT(4); break;
-        default: HVWS_SIEVE_COUNT(0); break;
-    }
-#undef HVWS_SIEVE_COUNT
+    // (round 4's timing modes -- lists without checks, staging alone, loads
+    // alone, no next-tile prefetch -- were removed in round 6; profiles/r4*_raw)
+    hipLaunchKernelGGL(k_sieve_count, dim3(grid), dim3(SV_THREADS), 0, st, rx, rx_len, segs, mid, npred, sieve_min(),
+                       b.tcount, b.slot, b.pool, reinterpret_cast<unsigned long long*>(b.pool_n), b.capS, ntm, sv, b.rt,
+                       b.wt);
     if ((e = launch_exclusive_scan(b.tcount, b.tbase, ntm, b.tmp, b.m_pre, st)) != hipSuccess) return e;
     const uint64_t fb = (ntm + 255) / 256;
     hipLaunchKernelGGL(k_sieve_fill, dim3((uint32_t)(fb < 8192 ? fb : 8192)), dim3(256), 0, st, segs, mid, b.tcount,

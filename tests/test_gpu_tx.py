@@ -261,15 +261,13 @@ def test_build_geometry_by_frame_size(eng, monkeypatch):
     assert not L.hvws_last_build_kernel(eng.ctx).decode().endswith(",lean>")
 
 
-@pytest.mark.parametrize("spans", ["1", "0"])
 @pytest.mark.parametrize("order", ["packed", "gaps", "shuffled"])
-def test_build_boundary_tiles_span_staged(eng, spans, order, monkeypatch):
+def test_build_boundary_tiles_span_staged(eng, order):
     """Boundary tiles of the general layout stage their source span in LDS
-    together with the frame records (k_tx_index; $HVWS_EXPERIMENT build_spans=0: the
-    records-first tiles).  Small frames packed back to back, with gaps, and
-    with payloads in shuffled order (spans past the LDS area fall back to the
-    records-first path); every byte against the reference."""
-    monkeypatch.setenv("HVWS_EXPERIMENT", f"build_spans={spans}")
+    together with the frame records (k_tx_index).  Small frames packed back
+    to back, with gaps, and with payloads in shuffled order (spans past the
+    LDS area fall back to the records-first path); every byte against the
+    reference."""
     rng = np.random.default_rng(31)
     lens = np.concatenate([rng.integers(900, 1100, 1500), rng.integers(0, 130, 300)])
     rng.shuffle(lens)
