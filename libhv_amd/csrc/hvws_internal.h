@@ -240,6 +240,21 @@ __device__ __forceinline__ uint64_t xcd_tile(uint64_t b, uint64_t ntiles) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// Workgroup b -> tile, runs of g adjacent tiles per XCD: within each window
+// of 8 g tiles, XCD x (= b mod 8, the hardware's round-robin placement) takes
+// tiles x g .. x g + g - 1, in order.  Neighbouring tiles that share a cache
+// line (a payload span's boundary line, a line of the per-frame tables) then
+// meet in one L2 instead of being fetched from memory by two XCDs, while the
+// eight XCDs still stream through the same window of memory (the whole-range
+// XCD order of xcd_tile halved k_build's rate).  A bijection on
+// [0, ntiles): the last partial window keeps the linear order.
+__device__ __forceinline__ uint64_t xcd_group_tile(uint64_t b, uint64_t ntiles, uint32_t g) {
+    const uint64_t win = 8ull * g, full = ntiles - ntiles % win;
+    if (g <= 1 || b >= full) return b;
+    const uint64_t w = b / win, r = b % win;
+    return w * win + (r & 7u) * g + (r >> 3);
+}
+
 // Frame sieve (hvws_sieve.hip): parallel discovery of one long mixed-size
 // stream.  State of the current scan, device side.
 struct dsieve {

@@ -1146,19 +1146,30 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             }
             const uint32_t stride = hl + len;
             const uint32_t p = q + lane * stride;   // lane * stride < 64 * 2^15
-            bool ok = lane == 0;
+            bool ok = lane == 0, whole = true;
             if (lane && p + 2 <= Lw && p - q == lane * stride) {
                 uint32_t hj, lj;
                 door_size(l, p, hj, lj);
                 const uint32_t rj = Lw - p;
-                ok = hj <= rj && lj <= rj - hj && hj + lj == stride;
+                whole = hj <= rj && lj <= rj - hj;
+                ok = whole && hj + lj == stride;
+            } else if (lane) {
+                whole = false;
             }
             const unsigned long long bad = __ballot(!ok);
+            const unsigned long long cutm = __ballot(!whole);
             uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1u : 64u;
+            // the first frame off the run is not whole: the read's cut frame
+            // (the next round's header check would find the same)
+            const bool cut_next = f < 64u && ((cutm >> f) & 1ull);
             if (f > DOOR_CHASE - cnt) f = DOOR_CHASE - cnt;
             if (lane < f) s_fpos[cnt + lane] = p;
             cnt += f;
             q += f * stride;
+            if (cut_next && f == (uint32_t)__ffsll((long long)bad) - 1u) {
+                cut = true;
+                break;
+            }
         }
         if (threadIdx.x == 0 && stamps) stamps[0] = wall_clock64();
         if (!cnt) break;
@@ -1430,7 +1441,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             // the records.  A chunk inside one payload belongs to that record
             // alone (plain read-modify-write); a payload's first and last
             // chunks may hold another record's bytes too (LDS atomic XOR per
-            // dword).  Then every chunk of the read goes to dout.
+            // dword).  Then every chunk of the read goes to dout.  (Round 6
+            // tried chunk-major instead -- a binary search of the records'
+            // payload ends per chunk, the chunk XORed and stored straight to
+            // dout: 1.52 against 1.08 us for an 8 KiB read, profiles/r6_raw/door.)
             if (s_unmask) {
                 uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
                 const uint32_t wave = tid >> 6, lane = tid & 63u;

@@ -454,7 +454,7 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                                            const uint64_t* __restrict__ out_off,
                                            const uint64_t* __restrict__ size,
                                            const unsigned long long* __restrict__ span, uint64_t n, uint64_t t,
-                                           const build_idx x) {
+                                           const build_idx x, const build_uni& uni) {
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     const uint64_t base = t * TILE;
     const uint32_t tid = threadIdx.x;
@@ -561,10 +561,15 @@ __device__ __forceinline__ void build_one_tile(uint8_t* __restrict__ out, uint64
                 // the key loads with the rest of the record, not after its
                 // flags (a second round trip per tile)
                 const uint32_t mk = mask ? mask[k] : 0u;
-                const uint64_t ln = len[k], o = out_off[k];
+                // a uniform layout's frame position, length and payload offset
+                // follow from k: only the flags and keys are read (the tables'
+                // lines, shared by neighbouring tiles, were 12 % of the lean
+                // form's reads at c2, profiles/r6_raw/tx_traffic)
+                const bool un = uni.stride != 0;
+                const uint64_t ln = un ? uni.stride - uni.hdr : len[k], o = un ? k * uni.stride : out_off[k];
                 const uint64_t ps = o + tx_hdr_len(fl, ln);
-                s_rel[r] = tx_frel_make(o, ps, ps + ln, pay_off[k], base, sa, TILE, (fl & F_MASK) ? mk : 0u, fl,
-                                          ln);
+                s_rel[r] = tx_frel_make(o, ps, ps + ln, un ? uni.pay_a + k * uni.pay_b : pay_off[k], base, sa, TILE,
+                                        (fl & F_MASK) ? mk : 0u, fl, ln);
                 if (C == 2) {
                     // the header's bytes, once per frame instead of per chunk
                     // and lane, already where they go in the two 16-byte
@@ -869,12 +874,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(C == 2 ? 7 : 
     const uint64_t* __restrict__ pay_off, const uint64_t* __restrict__ len, const uint8_t* __restrict__ flags,
     const uint32_t* __restrict__ mask, const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ size,
     const uint32_t* __restrict__ tile_first, const unsigned long long* __restrict__ span, uint64_t n, uint64_t tile0,
-    uint64_t ntiles, build_uni uni) {
-    const uint64_t t = tile0 + blockIdx.x;
+    uint64_t ntiles, build_uni uni, uint32_t xgroup) {
+    const uint64_t t = tile0 + xcd_group_tile(blockIdx.x, ntiles, xgroup);
     constexpr uint64_t TILE = (uint64_t)T * U * 16u;
     build_one_tile<T, U, NT, SF, C>(out, out_len, pay, plen, pay_off, len, flags, mask, out_off, size, span, n, t,
                                  uni.stride ? build_uni_idx(uni, t * TILE, TILE, n, out_len)
-                                            : build_load_idx(tile_first, span, t, n));
+                                            : build_load_idx(tile_first, span, t, n),
+                                 uni);
 }
 
 
@@ -1026,6 +1032,16 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
     }
     const uint64_t tile = build_tile(v);
     const uint64_t ntiles = (out_len + tile - 1) / tile;
+    // Runs of xg adjacent tiles per XCD (xcd_group_tile): a boundary line of
+    // a payload span, and a line of the flags and keys, shared by neighbouring
+    // tiles is then fetched once per run instead of once per tile.  DRAM-side
+    // reads per payload byte (profiles/r6_raw/tx_traffic): the lean form at c2
+    // 1.047 / 1.068 (rx layout / packed) at xg 1, 1.027 / 1.029 at 4, 1.021 /
+    // 1.019 at 8, at the same speed; k_build<64x4> at c3 1.027 / 1.058 at 1,
+    // 1.012 / 1.022 at 4 but 3-5 % slower there.  ($HVWS_EXPERIMENT build_xgroup)
+    static const uint32_t xg_env =
+        experiment("build_xgroup") ? (uint32_t)atoi(experiment("build_xgroup")) : 0xFFFFFFFFu;
+    const uint32_t xg = xg_env != 0xFFFFFFFFu ? xg_env : (v == 5 ? 8u : 2u);
     // a grid beyond 2^32-1 work-items is silently truncated: split the launch
     const uint64_t per_launch = 0xFFFFFFFFull / 256;
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
@@ -1034,7 +1050,7 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
 #define X(I, T, U, S, N, F, C)                                                                                 \
     case I:                                                                                                    \
         hipLaunchKernelGGL((k_build<T, U, N, F, C>), dim3((uint32_t)nt), dim3(T), 0, st, out, out_len, pay, plen, \
-                           pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt, u);           \
+                           pay_off, len, flags, mask, out_off, size, tile_first, sp, n, t0, nt, u, xg);       \
         break;
             HVWS_BUILD_GEOMS(X)
 #undef X

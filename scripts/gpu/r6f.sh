@@ -8,11 +8,6 @@ set -u
 S=scripts/gpu_step.sh
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 rm -f gpurun_out/.stop
-$S lat_r6f 60 scripts/probe/lat_probe
-[ -f gpurun_out/.stop ] && exit 1
-# negative control: round 5's repair key (605ad80) must fail the test that pins it
-HVWS_LIB=build/ab/libhvws_r5ckey.so timeout -k 10 120 python -u -m pytest tests/test_gpu_run.py -k "key_from_hypothesis or hypothesis_breaks" -v --timeout 120 --timeout-method thread > gpurun_out/negctl_r5ckey_r6f.log 2>&1
-echo "[negctl_r5ckey_r6f] rc=$? (1 expected: the test fails on round 5's key)"
 $S pytest_gpu_r6f 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 [ -f gpurun_out/.stop ] && exit 1
 for i in 1 2; do

@@ -428,7 +428,7 @@ def test_unmask_geometries(eng):
     nvar = 0
     while L.hvws_set_unmask_variant(nvar) == 0:
         nvar += 1
-    assert nvar >= 12, nvar
+    assert nvar == 2, nvar   # 256 x 4 XCD-ordered, 512 x 2 linear (round 6 removed the rest)
     try:
         for buf, segs in zip(cases, segss):
             exp_recs, _, _, exp = _oracle_batch(buf, segs, None)
