@@ -1037,11 +1037,14 @@ hipError_t launch_build(uint8_t* out, uint64_t out_len, const uint8_t* pay, uint
     // tiles is then fetched once per run instead of once per tile.  DRAM-side
     // reads per payload byte (profiles/r6_raw/tx_traffic): the lean form at c2
     // 1.047 / 1.068 (rx layout / packed) at xg 1, 1.027 / 1.029 at 4, 1.021 /
-    // 1.019 at 8, at the same speed; k_build<64x4> at c3 1.027 / 1.058 at 1,
-    // 1.012 / 1.022 at 4 but 3-5 % slower there.  ($HVWS_EXPERIMENT build_xgroup)
+    // 1.019 at 8 -- but 3-5 % slower (interleaved, r6h: 0.362-0.381 against
+    // 0.344-0.350 ms), so the lean form keeps 1; k_build<64x4> at c3 1.027 /
+    // 1.058 at 1, 1.019 / 1.036 at 2 at the same speed (20.29-20.36 / 20.72-
+    // 20.74 against 20.39-20.60 / 20.63-20.66 ms), 1.012 / 1.022 at 4 but 3-5 %
+    // slower.  ($HVWS_EXPERIMENT build_xgroup)
     static const uint32_t xg_env =
         experiment("build_xgroup") ? (uint32_t)atoi(experiment("build_xgroup")) : 0xFFFFFFFFu;
-    const uint32_t xg = xg_env != 0xFFFFFFFFu ? xg_env : (v == 5 ? 8u : 2u);
+    const uint32_t xg = xg_env != 0xFFFFFFFFu ? xg_env : (v == 5 ? 1u : 2u);
     // a grid beyond 2^32-1 work-items is silently truncated: split the launch
     const uint64_t per_launch = 0xFFFFFFFFull / 256;
     for (uint64_t t0 = 0; t0 < ntiles; t0 += per_launch) {
