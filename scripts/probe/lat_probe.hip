@@ -3,7 +3,8 @@
 // dependent LDS loads, an s_barrier of 4 waves, a wave-local fence, the
 // realtime-clock read, a system-scope fence after stores to pinned host
 // memory, a fine-grained device-memory load (the mailbox poll), a dependent
-// chain of 32-bit VALU ops and of 64-bit ones.  Cycles from s_memtime.
+// chain of 32-bit VALU ops and of 64-bit ones, and the acquire / release
+// fences alone (profiles/r6_raw/door/README.md).  Cycles from s_memtime.
 //   hipcc --offload-arch=gfx950 -O3 scripts/probe/lat_probe.hip -o scripts/probe/lat_probe
 #include <hip/hip_runtime.h>
 
@@ -111,6 +112,31 @@ __global__ __launch_bounds__(256) void k_lat(uint64_t* out, const uint32_t* fg, 
     }
     const uint64_t w1 = wall_clock64(), c1 = clock64();
     if (tid == 0) out[10] = (c1 - c0) * 100 / (w1 - w0);   // MHz
+    // 11: system-scope acquire fence (buffer_inv sc0 sc1), thread 0 alone
+    if (tid == 0) {
+        t0 = clock64();
+        for (int i = 0; i < 32; ++i) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        t1 = clock64();
+        out[11] = (t1 - t0) / 32;
+        // 12: agent-scope acquire
+        t0 = clock64();
+        for (int i = 0; i < 32; ++i) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        t1 = clock64();
+        out[12] = (t1 - t0) / 32;
+        // 13: system-scope release with nothing dirty (buffer_wbl2 sc0 sc1)
+        t0 = clock64();
+        for (int i = 0; i < 32; ++i) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        t1 = clock64();
+        out[13] = (t1 - t0) / 32;
+        // 14: one 16-B store to pinned host memory, then a system release
+        t0 = clock64();
+        for (int i = 0; i < 32; ++i) {
+            host[i * 64] = (uint32_t)i;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
+        t1 = clock64();
+        out[14] = (t1 - t0) / 32;
+    }
     if (tid == 0) out[15] = x + v + (uint32_t)w + y + z + b + acc + (uint32_t)r;
 }
 
@@ -130,9 +156,12 @@ int main() {
     printf("{\"lds_dep_load_cycles\": %llu, \"valu32_dep_cycles\": %llu, \"valu64_dep_cycles\": %llu, "
            "\"barrier_4waves_cycles\": %llu, \"realtime_read_cycles\": %llu, \"finegrained_vram_load_cycles\": %llu, "
            "\"host_store_fence_sys_barrier_cycles\": %llu, \"lds_write_read_wave_cycles\": %llu, "
-           "\"ballot_readlane_cycles\": %llu, \"branchy_size_step_cycles\": %llu, \"shader_MHz\": %llu}\n",
+           "\"ballot_readlane_cycles\": %llu, \"branchy_size_step_cycles\": %llu, \"shader_MHz\": %llu, "
+           "\"acquire_system_cycles\": %llu, \"acquire_agent_cycles\": %llu, \"release_system_clean_cycles\": %llu, "
+           "\"store_host_release_system_cycles\": %llu}\n",
            (unsigned long long)o[0], (unsigned long long)o[1], (unsigned long long)o[2], (unsigned long long)o[3],
            (unsigned long long)o[4], (unsigned long long)o[5], (unsigned long long)o[6], (unsigned long long)o[7],
-           (unsigned long long)o[8], (unsigned long long)o[9], (unsigned long long)o[10]);
+           (unsigned long long)o[8], (unsigned long long)o[9], (unsigned long long)o[10], (unsigned long long)o[11],
+           (unsigned long long)o[12], (unsigned long long)o[13], (unsigned long long)o[14]);
     return 0;
 }
