@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdint>
+#include <utility>
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -140,6 +141,45 @@ __global__ __launch_bounds__(256) void k_lat(uint64_t* out, const uint32_t* fg, 
     if (tid == 0) out[15] = x + v + (uint32_t)w + y + z + b + acc + (uint32_t)r;
 }
 
+
+// Instruction-cache probe: a straight-line block of NI distinct VALU ops
+// (each with its own 32-bit literal: 8 bytes, so NI * 8 bytes of code) timed
+// the first time this dispatch runs it, again at once, and again after ~50 us
+// of polling fine-grained memory with s_sleep, as the resident worker idles.
+constexpr int NI = 2048;
+template <uint32_t K>
+__device__ __forceinline__ void add_lit(uint32_t& v) {
+    asm volatile("v_add_u32 %0, %1, %0" : "+v"(v) : "i"(K));
+}
+template <size_t... I>
+__device__ __forceinline__ uint32_t icache_block(uint32_t v, std::index_sequence<I...>) {
+    (add_lit<(uint32_t)(I * 2654435761u + 0x10001u)>(v), ...);
+    return v;
+}
+__global__ __launch_bounds__(64) void k_icache(uint64_t* out, const uint32_t* fg, uint32_t seed) {
+    uint32_t v = seed + threadIdx.x;
+    uint64_t t0 = clock64();
+    v = icache_block(v, std::make_index_sequence<NI>{});
+    uint64_t t1 = clock64();
+    v = icache_block(v, std::make_index_sequence<NI>{});
+    uint64_t t2 = clock64();
+    const uint64_t w0 = wall_clock64();
+    uint32_t y = 0;
+    while (wall_clock64() - w0 < 5000) {
+        y += __hip_atomic_load(&fg[y & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_sleep(2);
+    }
+    uint64_t t3 = clock64();
+    v = icache_block(v + y, std::make_index_sequence<NI>{});
+    uint64_t t4 = clock64();
+    if (threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = t2 - t1;
+        out[2] = t4 - t3;
+        out[3] = v;
+    }
+}
+
 int main() {
     uint64_t* d_out;
     uint32_t *fg, *host;
@@ -153,6 +193,17 @@ int main() {
     }
     uint64_t o[T];
     CK(hipMemcpy(o, d_out, sizeof o, hipMemcpyDeviceToHost));
+    uint64_t ic[3][4];
+    for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(k_icache, dim3(1), dim3(64), 0, 0, d_out, fg, 5u + rep);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ic[rep], d_out, sizeof ic[rep], hipMemcpyDeviceToHost));
+    }
+    printf("{\"icache_block_instructions\": %d, \"icache_block_bytes\": %d, \"cycles_first\": [%llu, %llu, %llu], "
+           "\"cycles_again\": [%llu, %llu, %llu], \"cycles_after_50us_idle\": [%llu, %llu, %llu]}\n",
+           NI, NI * 8, (unsigned long long)ic[0][0], (unsigned long long)ic[1][0], (unsigned long long)ic[2][0],
+           (unsigned long long)ic[0][1], (unsigned long long)ic[1][1], (unsigned long long)ic[2][1],
+           (unsigned long long)ic[0][2], (unsigned long long)ic[1][2], (unsigned long long)ic[2][2]);
     printf("{\"lds_dep_load_cycles\": %llu, \"valu32_dep_cycles\": %llu, \"valu64_dep_cycles\": %llu, "
            "\"barrier_4waves_cycles\": %llu, \"realtime_read_cycles\": %llu, \"finegrained_vram_load_cycles\": %llu, "
            "\"host_store_fence_sys_barrier_cycles\": %llu, \"lds_write_read_wave_cycles\": %llu, "
