@@ -3,7 +3,7 @@
 # default bench line, the RUN / SPEC c2 A/B and transmit lines, and the
 # kernel-trace profile of the default bench, every step under its own limit
 # (scripts/gpu_step.sh: any failure ends the call).
-#   gpurun --timeout 1200 -- 'bash scripts/gpu/closing.sh r5z'
+#   gpurun --timeout 1200 -- 'bash scripts/gpu/closing.sh r6z'
 set -u
 S=scripts/gpu_step.sh
 TAG=${1:-closing}
@@ -23,7 +23,9 @@ for cfg in c2 c3 c4; do
   CONFIG=$cfg $S tx_${cfg}_$TAG 200 python3 scripts/bench_tx.py
   [ -f gpurun_out/.stop ] && exit 1
 done
-# traced without the drop-in leg: a process that ends with a resident-worker (CU-masked)
-# stream alive crashes in rocprofv3's exit teardown after the output is written
-$S kt_$TAG 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_kt -o kt -- python3 bench.py --dropin-reads 0
+# c4 as one stream (the frame sieve), then the traced default bench with every leg on,
+# the drop-in's resident worker included (its HSA queue is destroyed at exit)
+$S c4_one_$TAG 240 python3 bench.py --config c4 --segments 1 --steps 40 --warmup 5 --no-tx --feed-conns 0 --dropin-reads 0 --host-gib 0 --cpu-seconds 0
+[ -f gpurun_out/.stop ] && exit 1
+$S kt_$TAG 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_kt -o kt -- python3 bench.py
 exit 0
