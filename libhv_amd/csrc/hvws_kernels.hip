@@ -1510,14 +1510,23 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 }
             }
         }
-        // every thread's stores reach host memory before `done` says so
+        // Every thread's stores reach host memory before `done` says so: each
+        // thread waits for its stores' L2 acknowledgements, the barrier orders
+        // them before thread 0, and thread 0's one system-scope release writes
+        // the L2 back (an L2-wide writeback: every wave's lines).  A release in
+        // every thread meant four writebacks: 1.14 us against 0.49 for one
+        // (scripts/probe/lat_probe.hip).  DOOR_XOR's results were written
+        // through the L2: their acknowledgements suffice.
         const uint64_t tr = tid == 0 ? door_now(flags) : 0;
-        if (xdirect)   // its only results were written through the L2: their acks suffice
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else
-            __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
+            if (!xdirect) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                // the writeback's completion before `done`: the compiler
+                // drops the fence's own wait after the barrier's
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             rel_prev = door_now(flags) - tr;
             __hip_atomic_store(&box->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
