@@ -1031,22 +1031,19 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 //
 // The resident small-path worker (ddoor, hvws_internal.h): one workgroup of
 // kDoorThreads threads that stays on the device between reference-API calls.
-// Thread 0 polls the mailbox in fine-grained host memory (one relaxed
-// system-scope load, then s_sleep -- no fence per poll); on a new request
-// every wave stages the request's bytes into LDS (all loads in flight at once
-// across PCIe), wave 0 runs the carried-in frame, the walk and the tail (the
-// k_small device code), then every wave XORs its chunks chunk-major (each
-// chunk's mask from the records that overlap it, so no two threads write one
-// chunk) and stores the changed ones straight back into the mailbox's data
-// area; records, count and carry follow, each thread releases its stores at
-// system scope, and thread 0 publishes `done`.  A request costs no launch, no
-// dispatch and no end-of-kernel signal, and the segment's work is spread
-// over four waves instead of one.  Parking: idle for idle_ticks of the
-// 100 MHz realtime clock, the worker clears `alive`, takes one last look at
-// `seq` (serving a request that arrived meanwhile) and exits; its last store
-// is `exited = epoch`, and the host relaunches it on the next request once it
-// has seen that word.
-// The worker's header walk over a read staged in LDS (walk != 0).  A single
+// Thread 0 polls the mailbox (one relaxed system-scope load, then s_sleep --
+// no fence per poll); on a new read every wave stages the request's bytes
+// into LDS (all loads in flight at once), wave 0 runs the carried-in frame,
+// the header walk and the cut frame (door_walk), then the waves XOR the
+// staged bytes record by record and store every chunk to the mailbox's data
+// area; records, count and carry follow; thread 0 writes the L2 back once
+// every thread's stores are in it, and publishes `done`.  A request costs no
+// launch, no dispatch and no end-of-kernel signal.  Parking: idle for
+// idle_ticks of the 100 MHz realtime clock, the worker clears `alive`, takes
+// one last look at `seq` (serving a request that arrived meanwhile) and
+// exits; its last store is `exited = epoch`, and the host relaunches it on the
+// next request once it has seen that word.
+// The worker's header walk over a read staged in LDS.  A single
 // wave walking headers one after the other is a chain of dependent
 // instructions (~8 cycles each): round 3's walks spent ~4.5 us on the 8
 // headers of an 8 KiB read (profiles/r4c_raw).  So the chain carries only
