@@ -71,6 +71,9 @@ __device__ __forceinline__ bool reserved_opcode(uint32_t op) { return (op >= 3 &
 // Layout per websocket_build_frame (http/websocket_parser.c:207-256):
 // b0 = FIN<<7 | opcode, b1 = MASK<<7 | len7, then 0/2/8 big-endian length
 // bytes, then the 4 key bytes if MASK.  RSV bits are dropped (Q1).
+// V = false: no violation classes (viol = 0), for callers whose validation
+// mask is 0 (invalid_bits drops them there anyway).
+template <bool V = true>
 __device__ __forceinline__ hdr parse_hdr(uint64_t lo, uint64_t hi) {
     hdr h;
     uint32_t b0 = (uint32_t)lo & 0xFFu;
@@ -86,11 +89,14 @@ __device__ __forceinline__ hdr parse_hdr(uint64_t lo, uint64_t hi) {
     uint32_t k0 = (uint32_t)(lo >> 16), k2 = (uint32_t)(lo >> 32), k8 = (uint32_t)(hi >> 16);
     h.key = m ? (ext == 0 ? k0 : (ext == 2 ? k2 : k8)) : 0u;
     const uint32_t op = b0 & F_OPMASK;
-    h.viol = ((b0 & 0x70u) ? V_RSV : 0u) | (reserved_opcode(op) ? V_OPCODE : 0u) |
-             ((op & 8u) && (!(b0 & 0x80u) || h.length > 125) ? V_CONTROL : 0u) |
-             (ext == 8 && (h.length >> 63) ? V_LEN64 : 0u) |
-             ((ext == 2 && h.length < 126) || (ext == 8 && h.length <= 0xFFFFu) ? V_NONMIN : 0u) |
-             (m ? 0u : V_UNMASKED);
+    if constexpr (V)
+        h.viol = ((b0 & 0x70u) ? V_RSV : 0u) | (reserved_opcode(op) ? V_OPCODE : 0u) |
+                 ((op & 8u) && (!(b0 & 0x80u) || h.length > 125) ? V_CONTROL : 0u) |
+                 (ext == 8 && (h.length >> 63) ? V_LEN64 : 0u) |
+                 ((ext == 2 && h.length < 126) || (ext == 8 && h.length <= 0xFFFFu) ? V_NONMIN : 0u) |
+                 (m ? 0u : V_UNMASKED);
+    else
+        h.viol = 0u;
     return h;
 }
 

@@ -1178,21 +1178,27 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
         uint32_t lastm = 0, lastm_key = 0;   // 1 + index of this lane's last masked frame
         uint32_t lfl = 0;
         uint64_t llen = 0;
-        for (uint32_t k = lane; k < cnt; k += 64) {
-            const uint32_t p = s_fpos[k];
-            uint64_t lo, hi;
-            lds_hdr16(l, p, lo, hi);
-            const hdr h = parse_hdr(lo, hi);
-            frec v;
-            whole_frame_rec(v, p, h, vmask);
-            emit(n + k, v);
-            if (h.flags & F_MASK) {
-                lastm = k + 1;
-                lastm_key = h.key;
+        // without validation the headers' violation classes are not computed
+        // (invalid_bits would drop them)
+        auto parse = [&](auto valid) {
+            for (uint32_t k = lane; k < cnt; k += 64) {
+                const uint32_t p = s_fpos[k];
+                uint64_t lo, hi;
+                lds_hdr16(l, p, lo, hi);
+                const hdr h = parse_hdr<decltype(valid)::value>(lo, hi);
+                frec v;
+                whole_frame_rec(v, p, h, vmask);
+                emit(n + k, v);
+                if (h.flags & F_MASK) {
+                    lastm = k + 1;
+                    lastm_key = h.key;
+                }
+                lfl = h.flags;
+                llen = h.length;
             }
-            lfl = h.flags;
-            llen = h.length;
-        }
+        };
+        if (vmask) parse(std::true_type{});
+        else parse(std::false_type{});
         // wave-uniform lane indices: s_readlane, not an LDS-routed shuffle
         const int src = (int)((cnt - 1) & 63u);   // that lane parsed frame cnt - 1 last
         st.flags = (uint32_t)__builtin_amdgcn_readlane((int)lfl, src);
@@ -1442,6 +1448,9 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             // tried chunk-major instead -- a binary search of the records'
             // payload ends per chunk, the chunk XORed and stored straight to
             // dout: 1.52 against 1.08 us for an 8 KiB read, profiles/r6_raw/door.)
+            // the records to host memory first: their stores run beside the XOR
+            for (uint64_t i = tid; i < nl; i += kDoorThreads) h_rec[i] = lrec[i];
+            for (uint64_t i = nl + tid; i < n; i += kDoorThreads) h_rec[i] = d_slot[i];
             if (s_unmask) {
                 uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
                 const uint32_t wave = tid >> 6, lane = tid & 63u;
@@ -1485,8 +1494,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 s_t[6] = s_t[2];
             }
             if (tid == 0) s_t[3] = door_now(flags);
-            for (uint64_t i = tid; i < nl; i += kDoorThreads) h_rec[i] = lrec[i];
-            for (uint64_t i = nl + tid; i < n; i += kDoorThreads) h_rec[i] = d_slot[i];
             if (tid == 0) {
                 box->count = n;
                 box->out = s_carry;
