@@ -1658,6 +1658,7 @@ int door_call(hvws_ctx* c) {
     ddoor* b = c->h_door.as<ddoor>();
     ddoor* rq = door_req(c);
     const uint64_t seq = ++c->door_seq;
+    rq->seq_tail = seq;
     if (c->d_door_req) door_flush_wc();   // the request's bytes and fields first
     __atomic_store_n(&rq->seq, seq, __ATOMIC_RELEASE);
     if (c->d_door_req) door_flush_wc();
@@ -1764,6 +1765,7 @@ void door_quit_nohip(hvws_ctx* c) {
     if (door_word(c, b->exited) != c->door_epoch) {
         ddoor* rq = door_req(c);
         rq->op = DOOR_EXIT;
+        rq->seq_tail = c->door_seq + 1;
         if (c->d_door_req) door_flush_wc();
         __atomic_store_n(&rq->seq, ++c->door_seq, __ATOMIC_RELEASE);
         if (c->d_door_req) door_flush_wc();

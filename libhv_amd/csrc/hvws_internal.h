@@ -392,7 +392,9 @@ struct ddoor {
     uint32_t phase;     // DOOR_XOR: mask_offset of the first byte
     uint32_t pad0;
     dcarry   carry;     // DOOR_FEED: carry in
-    uint64_t pad1[5];
+    uint64_t pad1[4];
+    uint64_t seq_tail;  // seq again, written with the fields (before seq): the worker reads the
+                        // whole block with its poll and takes it when both copies agree
     // device -> host (own cache lines; `done` written last)
     uint64_t done;      // seq of the last request served
     uint64_t alive;     // 1 while a worker runs (0 once it parked)
@@ -408,6 +410,7 @@ struct ddoor {
 };
 static_assert(sizeof(dcarry) == 48, "dcarry layout");
 static_assert(offsetof(ddoor, done) == 128, "ddoor: device fields on their own lines");
+static_assert(offsetof(ddoor, seq_tail) == 120, "k_door reads seq_tail as the last 8 bytes of the request block");
 static_assert(offsetof(ddoor, carry) == 40 && offsetof(ddoor, len) == 16 && offsetof(ddoor, vmask) == 24,
               "k_door reads the request as words 1-10");
 // data areas: kDoorMax + 256 bytes (256-aligned); h_rec: kDoorRecords records

@@ -1119,6 +1119,13 @@ __device__ __forceinline__ void door_stage(const uint8_t* din, uint8_t* lds, uin
     }
 }
 
+// 16 bytes at system scope (the poll's view of the request block)
+__device__ __forceinline__ u32x4 ld16_sys(const void* p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
 template <typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
                                           uint32_t vmask, uint32_t* s_fpos, uint64_t* stamps, Emit&& emit) {
@@ -1295,44 +1302,65 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
     __shared__ uint64_t s_w[3];               // door_walk's stamps
     for (;;) {
-        if (tid == 0) {
+        if (tid < 64) {
+            // Wave 0 polls the whole 128-byte request block, lanes 0-7 16
+            // bytes each: a new request's fields arrive with its seq, so no
+            // second round trip for them.  The host writes seq_tail with the
+            // fields and seq after them; a block read straddling those writes
+            // shows the two copies differing and is read again.
+            const uint32_t lane = tid;
             uint64_t t0 = wall_clock64();
-            uint64_t s;
+            uint64_t s = last;
             uint32_t ex = 0, polls = 0;
+            u32x4 piece = u32x4{0u, 0u, 0u, 0u};
             for (;;) {
-                s = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (s != last) break;
-                // the clock every 32 polls: each read is a round trip the poll would wait for
-                if ((++polls & 31u) == 0 && wall_clock64() - t0 > idle_ticks) {
-                    __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __threadfence_system();
-                    s = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (s != last) {   // arrived while parking: serve it
-                        __hip_atomic_store(&box->alive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (lane < 8) piece = ld16_sys(reinterpret_cast<const u32x4*>(req) + lane);
+                const uint64_t head = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)piece[0], 0) |
+                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)piece[1], 0) << 32);
+                bool torn = false;   // read again at once
+                if (head != last) {
+                    const uint64_t tail = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)piece[2], 7) |
+                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)piece[3], 7) << 32);
+                    if (tail == head) {
+                        s = head;
                         break;
                     }
-                    ex = 1;
-                    break;
+                    torn = true;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                // the clock every 32 polls: each read is a round trip the poll would wait for
+                if ((++polls & 31u) == 0 && wall_clock64() - t0 > idle_ticks) {
+                    if (lane == 0) {
+                        __hip_atomic_store(&box->alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __threadfence_system();
+                    }
+                    const uint64_t again = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    const uint32_t a_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)again);
+                    const uint32_t a_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(again >> 32));
+                    if ((((uint64_t)a_hi << 32) | a_lo) == last) {
+                        ex = 1;
+                        break;
+                    }
+                    // arrived while parking: serve it (read and checked at the loop's top)
+                    if (lane == 0) __hip_atomic_store(&box->alive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    torn = true;
+                }
+                if (!torn) __builtin_amdgcn_s_sleep(2);
             }
-            s_exit = ex;
-            s_seq = s;
-            s_t[0] = door_now(flags);
-            // The request fields were written before seq; the acquire also
-            // invalidates this CU's L1 and the L2 for the data loaded next.
-            if (!ex) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            if (lane < 8) reinterpret_cast<u32x4*>(s_req)[lane] = piece;
+            if (lane == 0) {
+                s_exit = ex;
+                s_seq = s;
+                s_t[0] = door_now(flags);
+                // The acquire invalidates this CU's L1 and the L2 for the
+                // request's bytes loaded next.
+                if (!ex) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            }
         }
         __syncthreads();
         if (s_exit) {   // parked (idle): `alive` is already 0; say this launch has ended
             if (tid == 0) __hip_atomic_store(&box->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        if (tid < 8) {   // the request's 128 bytes: one round trip (the mailbox is uncached)
-            const u32x4 piece = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(req) + tid);
-            reinterpret_cast<u32x4*>(s_req)[tid] = piece;
-        }
-        __syncthreads();
         if (tid == 0) {
             const uint64_t* q = s_req + 1;   // word 0 is seq
             s_op = (uint32_t)q[0];
