@@ -1031,8 +1031,8 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 //
 // The resident small-path worker (ddoor, hvws_internal.h): one workgroup of
 // kDoorThreads threads that stays on the device between reference-API calls.
-// Thread 0 polls the mailbox (one relaxed system-scope load, then s_sleep --
-// no fence per poll); on a new read every wave stages the request's bytes
+// Wave 0 polls the mailbox's 128-byte request block (one system-scope load,
+// then s_sleep -- no fence per poll); on a new read every wave stages the request's bytes
 // into LDS (all loads in flight at once), wave 0 runs the carried-in frame,
 // the header walk and the cut frame (door_walk), then the waves XOR the
 // staged bytes record by record and store every chunk to the mailbox's data
