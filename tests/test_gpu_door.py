@@ -494,3 +494,20 @@ def test_child_process_with_worker_exits_cleanly(release):
                        capture_output=True, text=True, timeout=90)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
     assert "the read went to the worker" in p.stdout
+
+
+def test_door_request_in_pinned_host_memory():
+    """The worker's request block and bytes in pinned host memory ($HVWS_EXPERIMENT
+    door_vram=0: the layout of a box without a large BAR), polled across PCIe
+    with the block's seq_tail check: feeds, decodes and masked builds in a
+    child process equal the oracle's (tests/door_pinned_child.py)."""
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, HVWS_EXPERIMENT="door_vram=0")
+    env.pop("HVWS_DOOR", None)
+    p = subprocess.run([sys.executable, os.path.join(here, "door_pinned_child.py")], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
+    assert p.stdout.startswith("ok "), p.stdout
