@@ -293,6 +293,7 @@ int main(int argc, char** argv) {
         std::mt19937_64 rng(20261017);
         test_door(rng);
         printf("asan_driver door: %s (%d failed checks)\n", g_fail ? "FAIL" : "ok", g_fail);
+        fflush(stdout);
         return g_fail ? 1 : 0;
     }
     std::mt19937_64 rng(20261015);
@@ -307,5 +308,6 @@ int main(int argc, char** argv) {
     test_tx_and_keys(rng);
     hvws_thread_release();
     printf("asan_driver: %s (%d failed checks)\n", g_fail ? "FAIL" : "ok", g_fail);
+    fflush(stdout);   // before the runtimes' exit handlers
     return g_fail ? 1 : 0;
 }
