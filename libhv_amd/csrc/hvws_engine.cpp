@@ -1654,7 +1654,11 @@ bool door_drain(hvws_ctx* c, int ms, const char* where) {
 // store is `exited = epoch`; a relaunch also waits for the last launch's
 // completion signal (door_drain), so two workers never share the mailbox.
 // The queue's error state says whether a kernel fault ended it.
-int door_call(hvws_ctx* c) {
+// pf, pf_len: results the caller copies out once `done` is seen.  The
+// worker's stores land in host memory before `done` (its release waits for
+// them), so prefetching those lines while waiting pulls them into the cache
+// as they land instead of after `done`.
+int door_call(hvws_ctx* c, const void* pf = nullptr, size_t pf_len = 0) {
     ddoor* b = c->h_door.as<ddoor>();
     ddoor* rq = door_req(c);
     const uint64_t seq = ++c->door_seq;
@@ -1710,7 +1714,10 @@ int door_call(hvws_ctx* c) {
                 if (now - t0 > std::chrono::seconds(10)) return set_err(HVWS_EHIP, "k_door: no answer in 10 s");
             }
         }
-        __builtin_ia32_pause();
+        if (pf_len)
+            for (size_t i = 0; i < pf_len; i += 64) __builtin_prefetch(static_cast<const char*>(pf) + i);
+        else
+            __builtin_ia32_pause();
     }
 }
 
@@ -1894,7 +1901,7 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
     to_dcarry(carry, cin);
     memcpy(&rq->carry, &cin, sizeof(dcarry));
     if (timed) t1 = clk::now();
-    if (door_call(c) != HVWS_OK) {
+    if (door_call(c, data, unmask ? len : 0) != HVWS_OK) {
         door_fail(c, "read");
         return false;
     }
@@ -1927,7 +1934,7 @@ bool door_xor(hvws_ctx* c, char* dst, const char* src, size_t n, uint32_t key, u
     rq->len = n;
     rq->key = key;
     rq->phase = phase;
-    if (door_call(c) != HVWS_OK) {
+    if (door_call(c, data, n) != HVWS_OK) {
         door_fail(c, "XOR");
         return false;
     }
