@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <dirent.h>
+#include <immintrin.h>
 #include <execinfo.h>
 #include <signal.h>
 #include <sys/syscall.h>
@@ -1536,6 +1537,20 @@ bool door_vram_enabled() {
 // profiles/r4a_raw/vram_probe.jsonl).
 inline void door_flush_wc() { __builtin_ia32_sfence(); }
 
+// A request's bytes into the mailbox.  Device memory behind the BAR is
+// write-combining: with AVX-512 every store is one whole 64-byte line, a
+// non-temporal one (the sfence in door_call drains them); otherwise memcpy.
+__attribute__((target("avx512f"))) void wc_copy_avx512(uint8_t* dst, const uint8_t* src, size_t n) {
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) _mm512_stream_si512((__m512i*)(dst + i), _mm512_loadu_si512(src + i));
+    if (i < n) memcpy(dst + i, src + i, n - i);
+}
+void door_copy_in(hvws_ctx* c, uint8_t* dst, const void* src, size_t n) {
+    static const bool avx512 = __builtin_cpu_supports("avx512f");
+    if (c->d_door_req && avx512 && ((uintptr_t)dst & 63u) == 0) wc_copy_avx512(dst, static_cast<const uint8_t*>(src), n);
+    else memcpy(dst, src, n);
+}
+
 // Where the host writes a request (block and bytes) and where the worker reads it.
 ddoor* door_req(hvws_ctx* c) { return c->d_door_req ? (ddoor*)c->d_door_req : c->h_door.as<ddoor>(); }
 uint8_t* door_din(hvws_ctx* c) {
@@ -1892,7 +1907,7 @@ bool door_feed(hvws_ctx* c, char* buf, size_t len, const websocket_parser& carry
     ddoor* b = c->h_door.as<ddoor>();
     ddoor* rq = door_req(c);
     uint8_t* data = c->h_door_data.as<uint8_t>();
-    memcpy(door_din(c), buf, len);
+    door_copy_in(c, door_din(c), buf, len);
     rq->op = DOOR_FEED;
     rq->unmask = unmask ? 1u : 0u;
     rq->len = len;
@@ -1929,7 +1944,7 @@ bool door_xor(hvws_ctx* c, char* dst, const char* src, size_t n, uint32_t key, u
     std::lock_guard<std::mutex> cl(c->door_m);
     ddoor* rq = door_req(c);
     uint8_t* data = c->h_door_data.as<uint8_t>();
-    memcpy(door_din(c), src, n);
+    door_copy_in(c, door_din(c), src, n);
     rq->op = DOOR_XOR;
     rq->len = n;
     rq->key = key;
