@@ -378,7 +378,7 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // takes that word -- not the stream's status -- as the sign that the worker
 // has ended ("Resident worker").
 enum : uint32_t { DOOR_FEED = 1u, DOOR_XOR = 2u, DOOR_EXIT = 3u };
-constexpr uint32_t kDoorThreads = 256;              // 4 waves: staging and XOR in parallel, walk on wave 0
+constexpr uint32_t kDoorThreads = 512;              // 8 waves: staging and XOR in parallel, walk on wave 0
 constexpr uint64_t kDoorMax = 32ull << 10;          // largest request (bytes)
 constexpr uint64_t kDoorRecords = kDoorMax / 2 + 3; // records a kDoorMax segment can hold
 struct ddoor {

@@ -1,0 +1,20 @@
+#!/bin/bash
+# r6af: the worker as 8 waves (512 threads) instead of 4: at most 2 records per wave in the XOR of an 8 KiB read
+set -u
+S=scripts/gpu_step.sh
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+rm -f gpurun_out/.stop
+OLD=build/ab/libhvws_head.so
+i=0
+for v in old new new old old new; do
+  i=$((i+1))
+  if [ $v = old ]; then HVWS_LIB=$OLD $S dropin_${v}${i}_r6af 200 python3 scripts/bench_dropin.py
+  else $S dropin_${v}${i}_r6af 200 python3 scripts/bench_dropin.py; fi
+  [ -f gpurun_out/.stop ] && exit 1
+done
+HVWS_EXPERIMENT=feed_times=1 $S dph_new_r6af 200 python3 scripts/probe/door_phases.py 4000
+[ -f gpurun_out/.stop ] && exit 1
+HVWS_LIB=build/ab/libhvws_head.so HVWS_EXPERIMENT=feed_times=1 $S dph_old_r6af 200 python3 scripts/probe/door_phases.py 4000
+[ -f gpurun_out/.stop ] && exit 1
+$S pytest_door_r6af 300 python -u -m pytest tests/test_gpu_door.py tests/test_gpu_feed_many.py -x -q --timeout 120 --timeout-method thread
+exit 0
