@@ -1391,6 +1391,21 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         const uint64_t nch = (L + 15u) / 16u;   // the data area has slack past L: whole chunks throughout
         const uint32_t ngr = (uint32_t)((nch + 63u) & ~63ull);   // whole wave groups of 64 chunks (<= kDoorMax)
         const bool xdirect = op == DOOR_XOR;
+        dcarry st;                   // wave 0: the carry through a read
+        uint64_t pos = 0, n = 0;     // wave 0: position in the read, records so far
+        bool carried = false;        // wave 0: the carried-in payload is done
+        const uint32_t vmask = s_vmask;
+        auto emit = [&](uint64_t idx, const frec& v) {
+            drec o;
+            o.hdr_off = v.hdr_off;
+            o.pay_off = v.pay_off;
+            o.pay_len = v.pay_len;
+            o.length = v.length;
+            o.key = v.key;
+            o.info = v.info;
+            if (idx < SMALL_LREC) lrec[idx] = o;
+            else d_slot[idx] = o;
+        };
         if (xdirect) {
             const uint32_t kw = rotr32(s_key, 8u * (s_phase & 3u));
             const u32x4 k4 = u32x4{kw, kw, kw, kw};
@@ -1399,33 +1414,15 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                 asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dout + c * 16u), "v"(v) : "memory");
             }
         } else {
-            // the data area into LDS (all in flight), then wait
+            // the data area into LDS (all in flight)
             door_stage(din, lds, ngr);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (!xdirect) {
-            __syncthreads();
-            if (tid == 0) s_t[1] = door_now(flags);
-            if (tid < 64) {   // wave 0: carried-in frame, walk, tail (k_small's code)
-                dcarry st = s_carry;
+            // wave 0: the common carry, a payload that continues into this
+            // read, needs none of the staged bytes -- it runs while they land
+            // (scalar_frame's S_BODY step without its state dispatch)
+            if (tid < 64) {
+                st = s_carry;
                 st.started = 0;
-                uint64_t pos = 0, n = 0;
-                const uint32_t vmask = s_vmask;
-                auto emit = [&](uint64_t idx, const frec& v) {
-                    drec o;
-                    o.hdr_off = v.hdr_off;
-                    o.pay_off = v.pay_off;
-                    o.pay_len = v.pay_len;
-                    o.length = v.length;
-                    o.key = v.key;
-                    o.info = v.info;
-                    if (idx < SMALL_LREC) lrec[idx] = o;
-                    else d_slot[idx] = o;
-                };
                 if (st.state == S_BODY && st.require > 0 && L > 0) {
-                    // the common carry, a payload that continues into this
-                    // read: scalar_frame's S_BODY step without its state
-                    // dispatch (a chain of scalar branches, ~0.5 us)
                     const uint64_t nb = st.require < L ? st.require : L;
                     frec r;
                     r.hdr_off = -1;
@@ -1445,7 +1442,16 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     }
                     if (tid == 0) emit(0, r);
                     n = 1;
-                } else if (st.state != S_START) {
+                    carried = true;
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (!xdirect) {
+            __syncthreads();
+            if (tid == 0) s_t[1] = door_now(flags);
+            if (tid < 64) {   // wave 0: the rest of a carried-in frame, walk, tail (k_small's code)
+                if (!carried && st.state != S_START) {
                     frec r;
                     if (scalar_frame(lds, L, st, pos, r, vmask)) {
                         if (tid == 0) emit(0, r);
