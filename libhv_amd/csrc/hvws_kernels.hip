@@ -1030,14 +1030,16 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // ------------------------------------------------------------------ k_door
 //
 // The resident small-path worker (ddoor, hvws_internal.h): one workgroup of
-// kDoorThreads threads that stays on the device between reference-API calls.
-// Wave 0 polls the mailbox's 128-byte request block (one system-scope load,
-// then s_sleep -- no fence per poll); on a new read every wave stages the request's bytes
-// into LDS (all loads in flight at once), wave 0 runs the carried-in frame,
-// the header walk and the cut frame (door_walk), then the waves XOR the
-// staged bytes record by record and store every chunk to the mailbox's data
-// area; records, count and carry follow; thread 0 writes the L2 back once
-// every thread's stores are in it, and publishes `done`.  A request costs no
+// kDoorThreads threads (8 waves) that stays on the device between
+// reference-API calls.  Wave 0 polls the mailbox's 128-byte request block
+// (one system-scope load, then s_sleep -- no fence per poll); on a new read
+// every wave stages the request's bytes into LDS (all loads in flight at
+// once) while wave 0 runs a carried-in payload (it needs none of them); then
+// wave 0 walks the headers and the cut frame (door_walk), the waves XOR the
+// staged bytes record by record (8 waves: at most 2 of an 8 KiB read's 9
+// records each) beside the records' copy to host memory, and store every
+// chunk to the mailbox's data area; thread 0 writes the L2 back once every
+// thread's stores are in it, and publishes `done`.  A request costs no
 // launch, no dispatch and no end-of-kernel signal.  Parking: idle for
 // idle_ticks of the 100 MHz realtime clock, the worker clears `alive`, takes
 // one last look at `seq` (serving a request that arrived meanwhile) and
