@@ -1045,17 +1045,19 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // one last look at `seq` (serving a request that arrived meanwhile) and
 // exits; its last store is `exited = epoch`, and the host relaunches it on the
 // next request once it has seen that word.
-// The worker's header walk over a read staged in LDS.  A single
-// wave walking headers one after the other is a chain of dependent
-// instructions (~8 cycles each): round 3's walks spent ~4.5 us on the 8
-// headers of an 8 KiB read (profiles/r4c_raw).  So the chain carries only
-// what the next position needs -- byte 1, the extended length, the mask bit
-// -- in 32-bit arithmetic, and the frames' positions go to LDS; then the
-// wave's lanes parse those headers in parallel and emit the records.  Up to
-// DOOR_CHASE positions per round; the frame cut by the read's end goes
-// through the exact state machine.  Records and the carried fields (Q14) as
-// walk_frames leaves them.
-constexpr uint32_t DOOR_CHASE = 512;
+// The worker's header walk over a read staged in LDS.  A single wave walking
+// headers one after the other is a chain of dependent instructions (~8
+// cycles each): round 3's walks spent ~4.5 us on the 8 headers of an 8 KiB
+// read (profiles/r4c_raw).  So the wave takes a run of equal-size frames per
+// round: lane j parses the header at q + j * stride in full and emits its
+// record if the frames from q up to it are whole and of that size; the first
+// lane off the run gives the next round's stride, or it holds the frame cut
+// by the read's end, whose record and S_BODY carry follow from its header
+// bytes (the exact state machine only when that header itself is cut).
+// Records and the carried fields (Q14) as walk_frames leaves them.  (Until
+// round 6 a round sized the frames first, wrote their positions to LDS and
+// parsed them in a second pass, and the cut frame's header was loaded and
+// parsed once more: chase 0.56 + parse 0.48 + tail 0.52 us per 8 KiB read.)
 
 // 16 bytes at LDS byte q (dword-aligned loads, v_alignbyte realigns)
 __device__ __forceinline__ void lds_hdr16(const uint32_t* l, uint32_t q, uint64_t& lo, uint64_t& hi) {
@@ -1128,130 +1130,98 @@ __device__ __forceinline__ u32x4 ld16_sys(const void* p) {
     return v;
 }
 
-template <typename Emit>
+// readlane of a 64-bit value (wave-uniform lane index)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int src) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src) << 32);
+}
+
+template <bool V, typename Emit>
 __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry& st, uint64_t& pos, uint64_t& n,
-                                          uint32_t vmask, uint32_t* s_fpos, uint64_t* stamps, Emit&& emit) {
+                                          uint32_t vmask, uint64_t* stamps, Emit&& emit) {
     const uint32_t* l = reinterpret_cast<const uint32_t*>(lds);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t Lw = (uint32_t)L;   // reads are <= kDoorMax
-    uint32_t q = (uint32_t)pos;
+    uint32_t q = (uint32_t)pos, nn = (uint32_t)n;
     bool cut = false;
-    while (st.state == S_START && !cut && q + 2 <= Lw) {
-        // 1. positions only, a run of equal-size frames per step: every lane
-        // reads the header at q (its size is the stride), then lane j the
-        // header at q + j * stride; the first lane whose frame is not whole or
-        // not of that size ends the run, and the next step starts there.
-        uint32_t cnt = 0;
-        while (cnt < DOOR_CHASE && q + 2 <= Lw) {
+    uint64_t clo = 0, chi = 0;   // the cut frame's first 16 bytes (its header is whole)
+    if (st.state == S_START && q + 2 <= Lw) {
+        // the stride of the frame at q (0: that frame is cut by the read's end)
+        uint32_t stride;
+        {
             uint32_t hl, len;
             door_size(l, q, hl, len);
             const uint32_t rq = Lw - q;
-            if (hl > rq || len > rq - hl) {
-                cut = true;
-                break;
-            }
-            const uint32_t stride = hl + len;
-            const uint32_t p = q + lane * stride;   // lane * stride < 64 * 2^15
-            bool ok = lane == 0, whole = true;
-            if (lane && p + 2 <= Lw && p - q == lane * stride) {
-                uint32_t hj, lj;
-                door_size(l, p, hj, lj);
-                const uint32_t rj = Lw - p;
-                whole = hj <= rj && lj <= rj - hj;
-                ok = whole && hj + lj == stride;
-            } else if (lane) {
-                whole = false;
-            }
-            const unsigned long long bad = __ballot(!ok);
-            const unsigned long long cutm = __ballot(!whole);
-            uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1u : 64u;
-            // the first frame off the run is not whole: the read's cut frame
-            // (the next round's header check would find the same)
-            const bool cut_next = f < 64u && ((cutm >> f) & 1ull);
-            if (f > DOOR_CHASE - cnt) f = DOOR_CHASE - cnt;
-            if (lane < f) s_fpos[cnt + lane] = p;
-            cnt += f;
-            q += f * stride;
-            if (cut_next && f == (uint32_t)__ffsll((long long)bad) - 1u) {
-                cut = true;
-                break;
-            }
+            stride = (hl <= rq && len <= rq - hl) ? hl + len : 0u;
         }
-        if (threadIdx.x == 0 && stamps) stamps[0] = wall_clock64();
-        if (!cnt) break;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // 2. the headers in parallel: records; the round's last frame and last
-        // masked frame give the carried fields (Q14)
-        uint32_t lastm = 0, lastm_key = 0;   // 1 + index of this lane's last masked frame
-        uint32_t lfl = 0;
-        uint64_t llen = 0;
-        // without validation the headers' violation classes are not computed
-        // (invalid_bits would drop them)
-        auto parse = [&](auto valid) {
-            for (uint32_t k = lane; k < cnt; k += 64) {
-                const uint32_t p = s_fpos[k];
-                uint64_t lo, hi;
-                lds_hdr16(l, p, lo, hi);
-                const hdr h = parse_hdr<decltype(valid)::value>(lo, hi);
+        bool first = true;
+        for (;;) {
+            // lane j parses the header at q + j * stride in full; the run of
+            // whole frames of that size from lane 0 are this round's records,
+            // and the first lane off the run is the next round's start (its
+            // size the next stride) or the frame cut by the read's end
+            const uint32_t p = q + lane * stride;   // < 64 * 2^16: no overflow
+            const bool inb = lane == 0 || (stride != 0 && p + 2 <= Lw);
+            const uint32_t pp = inb ? p : q;
+            uint64_t lo, hi;
+            lds_hdr16(l, pp, lo, hi);
+            const hdr h = parse_hdr<V>(lo, hi);
+            const uint32_t rj = Lw - pp;
+            const bool whole = inb && h.hlen <= rj && h.length <= (uint64_t)(rj - h.hlen);
+            const uint32_t size = h.hlen + (uint32_t)h.length;   // whole: <= rj
+            const bool ok = whole && size == stride;
+            const unsigned long long bad = __ballot(!ok);
+            const uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1u : 64u;
+            if (lane < f) {
                 frec v;
                 whole_frame_rec(v, p, h, vmask);
-                emit(n + k, v);
-                if (h.flags & F_MASK) {
-                    lastm = k + 1;
-                    lastm_key = h.key;
-                }
-                lfl = h.flags;
-                llen = h.length;
+                emit(nn + lane, v);
             }
-        };
-        if (vmask) parse(std::true_type{});
-        else parse(std::false_type{});
-        // wave-uniform lane indices: s_readlane, not an LDS-routed shuffle
-        const int src = (int)((cnt - 1) & 63u);   // that lane parsed frame cnt - 1 last
-        st.flags = (uint32_t)__builtin_amdgcn_readlane((int)lfl, src);
-        st.length = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)llen, src) |
-                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(llen >> 32), src) << 32);
-        st.require = 0;
-        st.offset = 0;
-        st.mask_offset = (st.flags & F_MASK) ? (uint32_t)(st.length & 3u) : 0u;
-        st.started = 0;
-        uint32_t best = lastm, bkey = lastm_key;
-        if (cnt <= 64) {   // one frame per lane: the last masked frame is the highest lane with one
-            const unsigned long long mm = __ballot(lastm != 0);
-            best = mm ? 1u : 0u;
-            if (mm) bkey = (uint32_t)__builtin_amdgcn_readlane((int)lastm_key, 63 - __clzll((long long)mm));
-        } else {
-            for (int o = 32; o > 0; o >>= 1) {
-                const uint32_t ob = __shfl_xor(best, o), ok = __shfl_xor(bkey, o);
-                if (ob > best) {
-                    best = ob;
-                    bkey = ok;
-                }
+            if (f) {   // the carried fields (Q14): the run's last frame and last masked frame
+                const int last = (int)f - 1;
+                st.flags = (uint32_t)__builtin_amdgcn_readlane((int)h.flags, last);
+                st.length = readlane64(h.length, last);
+                st.require = 0;
+                st.offset = 0;
+                st.mask_offset = (st.flags & F_MASK) ? (uint32_t)(st.length & 3u) : 0u;
+                st.started = 0;
+                const unsigned long long mm = __ballot(lane < f && (h.flags & F_MASK)) ;
+                if (mm) st.mask = (uint32_t)__builtin_amdgcn_readlane((int)h.key, 63 - __clzll((long long)mm));
             }
+            nn += f;
+            q += f * stride;
+            if (stamps && first && threadIdx.x == 0) stamps[0] = wall_clock64();
+            first = false;
+            if (f == 64u) {   // the same stride again
+                if (q + 2 > Lw) break;
+                continue;
+            }
+            // lane f: a whole frame of another size, or the read's cut frame
+            if ((__ballot(whole) >> f) & 1ull) {
+                stride = (uint32_t)__builtin_amdgcn_readlane((int)size, (int)f);
+                continue;
+            }
+            // lane f's frame is cut; with at least 2 bytes of it here lane f
+            // parsed its header
+            if (q + 2 <= Lw) {
+                clo = readlane64(lo, (int)f);
+                chi = readlane64(hi, (int)f);
+                cut = true;
+            }
+            break;
         }
-        if (best) st.mask = bkey;
-        n += cnt;
-        if (threadIdx.x == 0 && stamps) stamps[1] = wall_clock64();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // s_fpos is rewritten by the next round
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (threadIdx.x == 0 && stamps) stamps[1] = wall_clock64();
+    n = nn;
     pos = q;
-    if (st.state == S_START && pos < L) {
+    if (cut) {
+        // The common cut: the header is whole, the payload runs past the
+        // read.  What scalar_frame leaves behind, in one step: a record with
+        // the payload bytes here, S_BODY with the rest to come.  (Wave-uniform
+        // values: lane f's header bytes.)
         const uint32_t rq = Lw - q;
-        uint64_t lo = 0, hi = 0;
-        hdr h;
-        h.hlen = 0xFFu;
-        if (rq >= 2) {
-            lds_hdr16(l, q, lo, hi);
-            h = parse_hdr(lo, hi);
-        }
+        const hdr h = parse_hdr(clo, chi);
         if (h.hlen <= rq) {
-            // The common cut: the header is whole, the payload runs past the
-            // read.  What scalar_frame leaves behind, in one step: a record
-            // with the payload bytes here, S_BODY with the rest to come.
             const uint32_t nb = rq - h.hlen;   // < h.length: the frame is cut
             frec r;
             r.hdr_off = (int64_t)q;
@@ -1260,7 +1230,7 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             r.length = h.length;
             r.key = (h.flags & F_MASK) ? h.key : 0u;
             r.info = I_START | (h.flags & 0xFFu) | I_HDR | invalid_bits(h.viol, vmask) | (nb ? I_BODY : 0u);
-            const uint32_t len7 = (uint32_t)(lo >> 8) & 0x7Fu;
+            const uint32_t len7 = (uint32_t)(clo >> 8) & 0x7Fu;
             st.state = S_BODY;
             st.flags = h.flags;
             st.length = h.length;
@@ -1273,12 +1243,13 @@ __device__ __forceinline__ void door_walk(const uint8_t* lds, uint64_t L, dcarry
             if (lane == 0) emit(n, r);
             ++n;
             pos = L;
-        } else {   // the header itself is cut: the exact state machine
-            frec r;
-            if (scalar_frame(lds, L, st, pos, r, vmask)) {
-                if (lane == 0) emit(n, r);
-                ++n;
-            }
+        }
+    }
+    if (st.state == S_START && pos < L) {   // the header itself is cut: the exact state machine
+        frec r;
+        if (scalar_frame(lds, L, st, pos, r, vmask)) {
+            if (lane == 0) emit(n, r);
+            ++n;
         }
     }
     if (threadIdx.x == 0 && stamps) stamps[2] = wall_clock64();
@@ -1301,7 +1272,6 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     __shared__ uint64_t s_t[7];
     uint64_t rel_prev = 0;   // thread 0: realtime ticks of the previous request's release
     __shared__ uint64_t s_req[16];
-    __shared__ uint32_t s_fpos[DOOR_CHASE];   // door_walk: frame positions of a round
     __shared__ uint64_t s_w[3];               // door_walk's stamps
     for (;;) {
         if (tid < 64) {
@@ -1461,7 +1431,9 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     }
                 }
                 if (tid == 0) s_t[4] = door_now(flags);
-                door_walk(lds, L, st, pos, n, vmask, s_fpos, (flags & DOOR_F_STAMPS) ? s_w : nullptr, emit);
+                uint64_t* const ws = (flags & DOOR_F_STAMPS) ? s_w : nullptr;
+                if (vmask) door_walk<true>(lds, L, st, pos, n, vmask, ws, emit);
+                else door_walk<false>(lds, L, st, pos, n, vmask, ws, emit);
                 if (tid == 0) {
                     s_n = n;
                     s_carry = st;
