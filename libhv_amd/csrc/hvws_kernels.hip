@@ -1273,6 +1273,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
     uint64_t rel_prev = 0;   // thread 0: realtime ticks of the previous request's release
     __shared__ uint64_t s_req[16];
     __shared__ uint64_t s_w[3];               // door_walk's stamps
+    __shared__ uint32_t s_c0;                 // record 0 is the carried-in payload (made while staging)
     for (;;) {
         if (tid < 64) {
             // Wave 0 polls the whole 128-byte request block, lanes 0-7 16
@@ -1341,6 +1342,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             s_vmask = (uint32_t)q[2];
             s_key = (uint32_t)(q[2] >> 32);
             s_phase = (uint32_t)q[3];
+            s_c0 = 0;
             dcarry cin;
             memcpy(&cin, &q[4], sizeof(dcarry));
             s_carry = cin;
@@ -1412,7 +1414,10 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     } else {
                         st.offset += L;   // http/websocket_parser.c:153
                     }
-                    if (tid == 0) emit(0, r);
+                    if (tid == 0) {
+                        emit(0, r);
+                        s_c0 = 1;
+                    }
                     n = 1;
                     carried = true;
                 }
@@ -1422,6 +1427,38 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
         if (!xdirect) {
             __syncthreads();
             if (tid == 0) s_t[1] = door_now(flags);
+            uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+            const uint32_t wave = tid >> 6, lane = tid & 63u;
+            auto unmask_rec = [&](const drec& f) {
+                // 32-bit: offsets inside one read.  Chunks start at
+                // multiples of 16, so one key word serves every chunk.
+                const uint32_t po = (uint32_t)f.pay_off, pl = (uint32_t)f.pay_len, info = f.info;
+                if (!(info & F_MASK) || pl == 0) return;
+                const uint32_t pe = po + pl;
+                const uint32_t kw = rotr32(f.key, 8u * ((((info >> 8) & 3u) - po) & 3u));
+                const uint32_t cf = (po + 15u) & ~15u, cl = pe & ~15u;   // whole chunks [cf, cl)
+                for (uint32_t c = cf + lane * 16u; c < cl; c += 64u * 16u) {
+                    u32x4* q = reinterpret_cast<u32x4*>(lds + c);
+                    *q = *q ^ u32x4{kw, kw, kw, kw};
+                }
+                // the partial chunks at either end (they may hold another
+                // record's bytes), a dword per lane: lanes 0-3 the first
+                // chunk, lanes 4-7 the last (one atomic step, not four)
+                const uint32_t c0 = po & ~15u;
+                const bool head = (po & 15u) != 0, tail = (pe & 15u) != 0 && cl >= cf;
+                const bool hl = lane < 4u;
+                if ((hl && head) || (lane - 4u < 4u && tail)) {
+                    const uint32_t cc = hl ? c0 : cl;
+                    const int32_t a = hl ? (int32_t)(po - c0) : 0;
+                    const int32_t e = (hl && cl < cf) ? (int32_t)(pe - c0) : (hl ? 16 : (int32_t)(pe - cl));
+                    const int32_t d4 = 4 * (int32_t)(lane & 3u);
+                    const int32_t lo = a - d4 < 0 ? 0 : (a - d4), hi = e - d4 > 4 ? 4 : (e - d4);
+                    if (hi > lo) {
+                        const uint32_t m = (hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+                        atomicXor(l32 + cc / 4u + (lane & 3u), kw & m);
+                    }
+                }
+            };
             if (tid < 64) {   // wave 0: the rest of a carried-in frame, walk, tail (k_small's code)
                 if (!carried && st.state != S_START) {
                     frec r;
@@ -1438,6 +1475,12 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
                     s_n = n;
                     s_carry = st;
                 }
+            } else if (tid >= kDoorThreads - 64u && s_c0 && s_unmask) {
+                // the last wave unmasks the carried-in payload while wave 0
+                // walks (wave 0 reads header bytes only, none of that
+                // payload's): the waves then share the other records, at
+                // most one each for an 8 KiB read of 1 KiB frames
+                unmask_rec(lrec[0]);
             }
             __threadfence_block();
             __syncthreads();
@@ -1460,39 +1503,7 @@ __global__ __launch_bounds__(kDoorThreads) void k_door(const ddoor* __restrict__
             for (uint64_t i = tid; i < nl; i += kDoorThreads) h_rec[i] = lrec[i];
             for (uint64_t i = nl + tid; i < n; i += kDoorThreads) h_rec[i] = d_slot[i];
             if (s_unmask) {
-                uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
-                const uint32_t wave = tid >> 6, lane = tid & 63u;
-                auto unmask_rec = [&](const drec& f) {
-                    // 32-bit: offsets inside one read.  Chunks start at
-                    // multiples of 16, so one key word serves every chunk.
-                    const uint32_t po = (uint32_t)f.pay_off, pl = (uint32_t)f.pay_len, info = f.info;
-                    if (!(info & F_MASK) || pl == 0) return;
-                    const uint32_t pe = po + pl;
-                    const uint32_t kw = rotr32(f.key, 8u * ((((info >> 8) & 3u) - po) & 3u));
-                    const uint32_t cf = (po + 15u) & ~15u, cl = pe & ~15u;   // whole chunks [cf, cl)
-                    for (uint32_t c = cf + lane * 16u; c < cl; c += 64u * 16u) {
-                        u32x4* q = reinterpret_cast<u32x4*>(lds + c);
-                        *q = *q ^ u32x4{kw, kw, kw, kw};
-                    }
-                    // the partial chunks at either end (they may hold another
-                    // record's bytes): lane 0 the first, lane 1 the last
-                    const uint32_t c0 = po & ~15u;
-                    const bool head = (po & 15u) != 0, tail = (pe & 15u) != 0 && cl >= cf;
-                    if ((lane == 0 && head) || (lane == 1 && tail)) {
-                        const uint32_t cc = lane == 0 ? c0 : cl;
-                        const int32_t a = lane == 0 ? (int32_t)(po - c0) : 0;
-                        const int32_t e = (lane == 0 && cl < cf) ? (int32_t)(pe - c0) : (lane == 0 ? 16 : (int32_t)(pe - cl));
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) {
-                            const int32_t lo = a - 4 * d < 0 ? 0 : (a - 4 * d), hi = e - 4 * d > 4 ? 4 : (e - 4 * d);
-                            if (hi > lo) {
-                                const uint32_t m = (hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
-                                atomicXor(l32 + cc / 4u + (uint32_t)d, kw & m);
-                            }
-                        }
-                    }
-                };
-                for (uint64_t k = wave; k < nl; k += kDoorThreads / 64u) unmask_rec(lrec[k]);
+                for (uint64_t k = s_c0 + wave; k < nl; k += kDoorThreads / 64u) unmask_rec(lrec[k]);
                 for (uint64_t k = nl + wave; k < n; k += kDoorThreads / 64u) unmask_rec(d_slot[k]);
                 __syncthreads();
                 if (tid == 0) s_t[6] = door_now(flags);
