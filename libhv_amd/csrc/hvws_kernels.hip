@@ -1035,10 +1035,10 @@ hipError_t launch_small(const uint8_t* rx, uint64_t rx_len, const dseg* segs, co
 // (one system-scope load, then s_sleep -- no fence per poll); on a new read
 // every wave stages the request's bytes into LDS (all loads in flight at
 // once) while wave 0 runs a carried-in payload (it needs none of them); then
-// wave 0 walks the headers and the cut frame (door_walk), the waves XOR the
-// staged bytes record by record (8 waves: at most 2 of an 8 KiB read's 9
-// records each) beside the records' copy to host memory, and store every
-// chunk to the mailbox's data area; thread 0 writes the L2 back once every
+// wave 0 walks the headers and the cut frame (door_walk) while the last wave
+// unmasks the carried-in payload, the waves XOR the other records (8 waves:
+// at most one each of an 8 KiB read's 8 others) beside the records' copy to
+// host memory, and store every chunk to the mailbox's data area; thread 0 writes the L2 back once every
 // thread's stores are in it, and publishes `done`.  A request costs no
 // launch, no dispatch and no end-of-kernel signal.  Parking: idle for
 // idle_ticks of the 100 MHz realtime clock, the worker clears `alive`, takes
