@@ -151,6 +151,25 @@ def test_door_varying_read_sizes(door):
     assert _stats()[1] > before[1], "no request reached the worker"
 
 
+def test_door_carried_payload_every_alignment(door):
+    """Reads of 8 KiB + k bytes (k = 0..15) over masked frames of 1000-1100 B:
+    almost every read starts inside a payload, which the worker unmasks while
+    its header walk reads the next frame's header, and that payload's end --
+    the chunk its last bytes share with the header -- falls at every alignment.
+    Messages, return values and the in-place buffer equal the oracle's."""
+    rng = random.Random(23)
+    frames = [(0x2 | S.FIN | S.MASK, rng.randbytes(rng.randint(1000, 1100)), rng.randbytes(4)) for _ in range(200)]
+    data = H.build_frames_ref(frames)
+    chunks, tot, k = [], 0, 0
+    while tot < len(data):
+        chunks.append(min(8192 + k % 16, len(data) - tot))
+        tot += chunks[-1]
+        k += 1
+    before = _stats()
+    assert H.run_messages("gpu", data, chunks) == H.run_messages("oracle", data, chunks)
+    assert _stats()[1] > before[1], "no request reached the worker"
+
+
 def test_door_execute_callbacks_and_early_return(door):
     """websocket_parser_execute through the worker: callback logs (with and
     without the user's in-callback decode) and early returns equal the oracle's."""
